@@ -1,0 +1,212 @@
+/* lego_loam.h — C-ABI of the MI355X-native LeGO-LOAM per-scan hot path.
+ *
+ * The reference's "plugin API" for this path is its ROS node/topic surface
+ * (SURVEY.md §8b).  Each entry point below replaces one node callback and
+ * keeps that topic's payload:
+ *
+ *   lego_ip_process   <- ImageProjection::cloudHandler
+ *                        (LeGO-LOAM/src/imageProjection.cpp:181-197)
+ *                        in : /velodyne_points        (PointCloud2, PointXYZIR)
+ *                        out: /segmented_cloud, /segmented_cloud_info
+ *                             (cloud_msgs/msg/cloud_info.msg:1-12),
+ *                             /outlier_cloud (+ gated /full_cloud_projected,
+ *                             /ground_cloud, /segmented_cloud_pure)
+ *   lego_fa_process   <- FeatureAssociation::runFeatureAssociation
+ *                        (LeGO-LOAM/src/featureAssociation.cpp:1817-1860)
+ *                        out: /laser_cloud_{sharp,less_sharp,flat,less_flat},
+ *                             /laser_odom_to_init, /laser_cloud_{corner,surf}_last,
+ *                             /outlier_cloud_last
+ *   lego_mo_process   <- mapOptimization::run scan-to-map part
+ *                        (LeGO-LOAM/src/mapOptmization.cpp:1487-1522,
+ *                         376-606, 956-1350)
+ *   lego_odom_batch   the device-resident hot path: ip+fa (incl. the two-step
+ *                        LM odometry) over K consecutive scans of one stream,
+ *                        one pose record per scan (what bench.py times).
+ *
+ * Conventions (mirroring the reference):
+ *   - all functions return a lego_status; nothing throws across the ABI;
+ *   - a non-dense input cloud is LEGO_E_NOT_DENSE (the reference ROS_ERRORs and
+ *     shuts down, imageProjection.cpp:174-177);
+ *   - output buffers are library-owned and valid until the next call on the
+ *     same context (the reference reuses member clouds the same way);
+ *   - a context is NOT thread-safe; distinct contexts are independent.
+ */
+#ifndef LEGO_LOAM_H_
+#define LEGO_LOAM_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  LEGO_OK = 0,
+  LEGO_E_NOT_DENSE = 1, /* input has non-finite xyz (imageProjection.cpp:174) */
+  LEGO_E_CAPACITY = 2,  /* more points than the context was sized for */
+  LEGO_E_DEVICE = 3,    /* HIP runtime error / no device */
+  LEGO_E_ARG = 4,       /* bad argument (null, empty cloud, bad config) */
+  LEGO_E_STATE = 5      /* call out of order (e.g. mo before any fa) */
+} lego_status;
+
+/* /velodyne_points point: the velodyne PointCloud2 wire layout, point_step 32
+ * (x@0 y@4 z@8 intensity@16 ring@20) = PointXYZIR, utility.h:153-165. */
+typedef struct lego_point_xyzir {
+  float x, y, z, _pad0;
+  float intensity;
+  uint16_t ring;
+  uint16_t _pad1;
+  uint32_t _pad2[2];
+} lego_point_xyzir;
+
+/* PointType = pcl::PointXYZI (utility.h:51), packed to 16 bytes. */
+typedef struct lego_point_xyzi {
+  float x, y, z, intensity;
+} lego_point_xyzi;
+
+/* Runtime form of the compile-time constants of utility.h:53-136. */
+typedef struct lego_sensor_cfg {
+  int32_t n_scan;            /* N_SCAN            utility.h:63 */
+  int32_t horizon_scan;      /* Horizon_SCAN      utility.h:64 */
+  float ang_res_x;           /* utility.h:65 */
+  float ang_res_y;           /* utility.h:66 */
+  float ang_bottom;          /* utility.h:67 */
+  int32_t ground_scan_ind;   /* groundScanInd     utility.h:68 */
+  int32_t use_cloud_ring;    /* utility.h:60 */
+  float sensor_minimum_range;/* utility.h:111 */
+  float sensor_mount_angle;  /* utility.h:112 */
+  float segment_theta;       /* utility.h:113 */
+  int32_t segment_valid_point_num; /* utility.h:114 */
+  int32_t segment_valid_line_num;  /* utility.h:115 */
+  float segment_alpha_x;     /* utility.h:116 (derived) */
+  float segment_alpha_y;     /* utility.h:117 (derived) */
+  float edge_threshold;      /* utility.h:123 */
+  float surf_threshold;      /* utility.h:124 */
+  float nearest_feature_search_sq_dist; /* utility.h:125 */
+  float scan_period;         /* utility.h:107 */
+  double mapping_process_interval; /* utility.h:105 */
+  float surrounding_keyframe_search_radius; /* utility.h:129 */
+  int32_t skip_frame_num;    /* featureAssociation.cpp:284 */
+} lego_sensor_cfg;
+
+/* Presets: "VLP-16" (utility.h:63-68), "HDL-32E" (:71-76), "VLS-128" (:79-84),
+ * "OS1-16" (:89-94), "OS1-64" (:97-102), and "HDL-64E" (64x2048, KITTI-shaped:
+ * no preset in the reference, README.md:86; derived in DESIGN.md). */
+int lego_sensor_preset(const char* name, lego_sensor_cfg* out);
+
+/* cloud_msgs/cloud_info (cloud_info.msg:1-12).  The three per-point arrays have
+ * length N_SCAN*Horizon_SCAN like the reference (imageProjection.cpp:128-130);
+ * only the first n_segmented entries are meaningful. */
+typedef struct lego_cloud_info {
+  double stamp;
+  const int32_t* start_ring_index; /* [n_scan] */
+  const int32_t* end_ring_index;   /* [n_scan] */
+  float start_orientation;
+  float end_orientation;
+  float orientation_diff;
+  const uint8_t* segmented_cloud_ground_flag; /* [P] */
+  const uint32_t* segmented_cloud_col_ind;    /* [P] */
+  const float* segmented_cloud_range;         /* [P] */
+} lego_cloud_info;
+
+typedef struct lego_ip_out {
+  lego_cloud_info info;                  /* /segmented_cloud_info */
+  const lego_point_xyzi* segmented_cloud;/* /segmented_cloud */
+  int32_t n_segmented;
+  const lego_point_xyzi* outlier_cloud;  /* /outlier_cloud */
+  int32_t n_outlier;
+  /* gated outputs / range-image debug view; NULL unless LEGO_IP_IMAGES set */
+  const lego_point_xyzi* full_cloud;     /* /full_cloud_projected [P] */
+  const float* range_image;              /* rangeMat  [P] */
+  const int8_t* ground_image;            /* groundMat [P] */
+  const int32_t* label_image;            /* labelMat  [P] */
+} lego_ip_out;
+
+#define LEGO_IP_IMAGES 1u
+
+typedef struct lego_fa_out {
+  double stamp;
+  /* /laser_cloud_sharp, _less_sharp, _flat, _less_flat (camera frame) */
+  const lego_point_xyzi* sharp;      int32_t n_sharp;
+  const lego_point_xyzi* less_sharp; int32_t n_less_sharp;
+  const lego_point_xyzi* flat;       int32_t n_flat;
+  const lego_point_xyzi* less_flat;  int32_t n_less_flat;
+  /* /laser_odom_to_init (featureAssociation.cpp:1727-1744) */
+  int32_t odom_valid;        /* 0 on the initialisation scan (:1846-1849) */
+  float transform_cur[6];
+  float transform_sum[6];
+  double odom_quat[4];       /* x,y,z,w exactly as published (:1731-1734) */
+  double odom_pos[3];
+  /* hand-off to mapping every (skip_frame_num+1)-th scan (:1790-1814) */
+  int32_t publish_to_mapping;
+  const lego_point_xyzi* corner_last;  int32_t n_corner_last;
+  const lego_point_xyzi* surf_last;    int32_t n_surf_last;
+  const lego_point_xyzi* outlier_last; int32_t n_outlier_last;
+} lego_fa_out;
+
+typedef struct lego_mo_out {
+  int32_t processed;          /* mapping ran this call (interval gate :1499) */
+  int32_t optimized;          /* scan2MapOptimization guard passed (:1331) */
+  int32_t iterations;
+  float transform_tobe_mapped[6];
+  float transform_aft_mapped[6];
+  float transform_bef_mapped[6];
+  int32_t n_corner_map_ds, n_surf_map_ds, n_corner_scan_ds, n_surf_scan_ds;
+  int32_t n_rows_last;        /* laserCloudOri size at the last iteration */
+} lego_mo_out;
+
+/* One record per scan from the batch path (64 bytes, also the RCCL gather
+ * unit of the multi-GPU bench). */
+typedef struct lego_pose_rec {
+  double stamp;
+  float transform_sum[6];
+  int32_t n_segmented;
+  int32_t n_sharp, n_less_sharp, n_flat, n_less_flat;
+  int32_t odom_valid;
+  int32_t flags;
+  int32_t _pad;
+} lego_pose_rec;
+
+typedef struct lego_ctx lego_ctx;
+
+/* Creates a per-stream context on HIP device `device`, sized for scans of up to
+ * max_points points and batches of up to max_batch scans. */
+int lego_create(const lego_sensor_cfg* cfg, int device, int32_t max_points,
+                int32_t max_batch, lego_ctx** out);
+int lego_destroy(lego_ctx* ctx);
+/* Resets the per-stream state (odometry, residues) to construction values. */
+int lego_reset(lego_ctx* ctx);
+
+int lego_ip_process(lego_ctx* ctx, const lego_point_xyzir* pts, int32_t n,
+                    double stamp, uint32_t flags, lego_ip_out* out);
+int lego_fa_process(lego_ctx* ctx, const lego_ip_out* in, lego_fa_out* out);
+
+/* Device-resident batch: scans k=0..nscans-1 are the points
+ * pts[offsets[k] .. offsets[k+1]).  pts/offsets are device pointers when
+ * on_device != 0, host pointers otherwise.  Runs ip + fa + odometry for every
+ * scan in stream order and writes one record per scan to recs (host). */
+int lego_odom_batch(lego_ctx* ctx, const lego_point_xyzir* pts,
+                    const int64_t* offsets, const double* stamps,
+                    int32_t nscans, int32_t on_device, lego_pose_rec* recs);
+/* After lego_odom_batch: fetch full per-scan outputs of scan k of that batch. */
+int lego_batch_fetch(lego_ctx* ctx, int32_t k, lego_ip_out* ip, lego_fa_out* fa);
+
+/* Mapping (scan-to-map).  lego_mo_set_map installs a fixed surrounding map
+ * (config 5) instead of the keyframe-built one; pass NULLs to go back to the
+ * keyframe map of mapOptmization.cpp:1001-1056. */
+int lego_mo_set_map(lego_ctx* ctx, const lego_point_xyzi* corner, int32_t n_corner,
+                    const lego_point_xyzi* surf, int32_t n_surf);
+int lego_mo_process(lego_ctx* ctx, const lego_fa_out* in, lego_mo_out* out);
+
+/* Last device error string (static storage). */
+const char* lego_last_error(void);
+
+/* Per-stage device timings of the last lego_odom_batch call (ms), for bench:
+ * names[i] / ms[i], i < *n. */
+int lego_stage_times(lego_ctx* ctx, const char** names, float* ms, int32_t cap,
+                     int32_t* n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LEGO_LOAM_H_ */

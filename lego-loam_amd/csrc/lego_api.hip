@@ -1,0 +1,606 @@
+// lego_api.hip — the C-ABI (include/lego_loam.h) over the gfx950 kernels.
+//
+// One lego_ctx = one lidar stream = one HIP stream on one device.  All
+// per-scan work is device resident; the node-shaped calls (lego_ip_process,
+// lego_fa_process) are the batch path at B = 1 followed by the copies the
+// reference's publishers would serialise.  There is no CPU fallback: every
+// entry point fails with LEGO_E_DEVICE if HIP cannot run.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "lego_device.h"
+#include "lego_kernels.h"
+#include "lego_loam.h"
+
+using namespace lego;
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+void set_err(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+#define HIPCHK(x)                                                                 \
+  do {                                                                            \
+    hipError_t e_ = (x);                                                          \
+    if (e_ != hipSuccess) {                                                       \
+      set_err("%s:%d %s: %s", __FILE__, __LINE__, #x, hipGetErrorString(e_));     \
+      return LEGO_E_DEVICE;                                                       \
+    }                                                                             \
+  } while (0)
+
+// tf::Quaternion::setRPY + publishOdometry axis shuffle (featureAssociation.cpp:1728-1737)
+void odom_quat(const float ts[6], double q[4], double pos[3]) {
+  const double roll = ts[2], pitch = -ts[0], yaw = -ts[1];
+  const double hy = yaw * 0.5, hp = pitch * 0.5, hr = roll * 0.5;
+  const double cy = std::cos(hy), sy = std::sin(hy), cp = std::cos(hp), sp = std::sin(hp);
+  const double cr = std::cos(hr), sr = std::sin(hr);
+  const double g0 = sr * cp * cy - cr * sp * sy, g1 = cr * sp * cy + sr * cp * sy;
+  const double g2 = cr * cp * sy - sr * sp * cy, g3 = cr * cp * cy + sr * sp * sy;
+  q[0] = -g1; q[1] = -g2; q[2] = g0; q[3] = g3;
+  pos[0] = ts[3]; pos[1] = ts[4]; pos[2] = ts[5];
+}
+
+template <typename T>
+hipError_t dalloc(T** p, size_t n) {
+  return hipMalloc((void**)p, sizeof(T) * (n ? n : 1));
+}
+
+}  // namespace
+
+struct lego_ctx {
+  lego_sensor_cfg cfg;
+  DevCfg dc;
+  int device = 0;
+  int maxPoints = 0, maxBatch = 0;
+  hipStream_t stream = nullptr;
+  BatchBufs bb{};
+  OdomBufs ob{};
+  FaCarry* d_carry = nullptr;
+  unsigned long long* d_gkeys = nullptr;
+  lego_point_xyzir* d_pts = nullptr;
+  int64_t* d_off = nullptr;
+  std::vector<void*> allocs;
+  StageTimer tm;
+  // last batch
+  int lastB = 0;
+  std::vector<double> stamps;
+  // host staging (library-owned outputs)
+  std::vector<lego_point_xyzi> h_seg, h_outl, h_full, h_sharp, h_lsharp, h_flat, h_lflat;
+  std::vector<lego_point_xyzi> h_cornerLast, h_surfLast, h_outlLast;
+  std::vector<int32_t> h_sri, h_eri, h_label;
+  std::vector<uint8_t> h_gflag;
+  std::vector<uint32_t> h_col;
+  std::vector<float> h_range, h_rimg;
+  std::vector<int8_t> h_gimg;
+  lego_ip_out lastIp{};
+  bool lastIpDevice = false;  // lastIp describes batch slot 0 on device
+  std::vector<std::string> tnames;
+  std::vector<float> tms;
+
+  template <typename T>
+  hipError_t alloc(T** p, size_t n) {
+    hipError_t e = dalloc(p, n);
+    if (e == hipSuccess) allocs.push_back((void*)*p);
+    return e;
+  }
+  ~lego_ctx() {
+    if (device >= 0) hipSetDevice(device);
+    for (void* p : allocs) hipFree(p);
+    if (stream) hipStreamDestroy(stream);
+  }
+};
+
+static int make_devcfg(const lego_sensor_cfg* c, DevCfg* d) {
+  if (c->n_scan <= 0 || c->n_scan > kMaxRings || c->horizon_scan <= 0 ||
+      c->horizon_scan > kMaxHorizon || c->ground_scan_ind < 0 || c->ground_scan_ind >= c->n_scan ||
+      !c->use_cloud_ring)
+    return LEGO_E_ARG;
+  d->N = c->n_scan;
+  d->H = c->horizon_scan;
+  d->P = c->n_scan * c->horizon_scan;
+  d->g = c->ground_scan_ind;
+  d->ang_res_x = c->ang_res_x;
+  d->min_range = c->sensor_minimum_range;
+  d->mount_angle = c->sensor_mount_angle;
+  d->theta = c->segment_theta;
+  // labelComponents re-evaluates sin/cos(alpha) per edge (imageProjection.cpp:421);
+  // they are per-sensor constants, evaluated with the same libm restatement.
+  d->sinAX = lego_sinf(c->segment_alpha_x);
+  d->cosAX = lego_cosf(c->segment_alpha_x);
+  d->sinAY = lego_sinf(c->segment_alpha_y);
+  d->cosAY = lego_cosf(c->segment_alpha_y);
+  d->valid_pt = c->segment_valid_point_num;
+  d->valid_line = c->segment_valid_line_num;
+  d->edge_thr = c->edge_threshold;
+  d->surf_thr = c->surf_threshold;
+  d->nn_sq = c->nearest_feature_search_sq_dist;
+  d->scan_period = c->scan_period;
+  d->skip = c->skip_frame_num;
+  return LEGO_OK;
+}
+
+static int ctx_reset(lego_ctx* x) {
+  OdomState st;
+  std::memset(&st, 0, sizeof(st));
+  st.frameCount = x->cfg.skip_frame_num;  // frameCount = skipFrameNum (:314)
+  HIPCHK(hipMemcpyAsync(x->ob.st, &st, sizeof(st), hipMemcpyHostToDevice, x->stream));
+  FaCarry cz{0, 0, 0, 0};  // fresh member arrays: phantom {0.0f, 0}, picked[0] = 0
+  HIPCHK(hipMemcpyAsync(x->d_carry, &cz, sizeof(cz), hipMemcpyHostToDevice, x->stream));
+  HIPCHK(hipStreamSynchronize(x->stream));
+  x->lastIpDevice = false;
+  x->lastB = 0;
+  return LEGO_OK;
+}
+
+extern "C" {
+
+const char* lego_last_error(void) { return g_err; }
+
+int lego_sensor_preset(const char* name, lego_sensor_cfg* o) {
+  if (!name || !o) return LEGO_E_ARG;
+  std::memset(o, 0, sizeof(*o));
+  if (!std::strcmp(name, "VLP-16")) {  // utility.h:63-68
+    o->n_scan = 16; o->horizon_scan = 1800; o->ang_res_x = 0.2f; o->ang_res_y = 2.0f;
+    o->ang_bottom = (float)(15.0 + 0.1); o->ground_scan_ind = 7;
+  } else if (!std::strcmp(name, "HDL-32E")) {  // utility.h:71-76
+    o->n_scan = 32; o->horizon_scan = 1800; o->ang_res_x = (float)(360.0 / (float)1800);
+    o->ang_res_y = (float)(41.33 / (float)(32 - 1)); o->ang_bottom = 30.67f; o->ground_scan_ind = 20;
+  } else if (!std::strcmp(name, "VLS-128")) {  // utility.h:79-84
+    o->n_scan = 128; o->horizon_scan = 1800; o->ang_res_x = 0.2f; o->ang_res_y = 0.3f;
+    o->ang_bottom = 25.0f; o->ground_scan_ind = 10;
+  } else if (!std::strcmp(name, "OS1-16")) {  // utility.h:89-94
+    o->n_scan = 16; o->horizon_scan = 1024; o->ang_res_x = (float)(360.0 / (float)1024);
+    o->ang_res_y = (float)(33.2 / (float)(16 - 1)); o->ang_bottom = (float)(16.6 + 0.1);
+    o->ground_scan_ind = 7;
+  } else if (!std::strcmp(name, "OS1-64")) {  // utility.h:97-102
+    o->n_scan = 64; o->horizon_scan = 1024; o->ang_res_x = (float)(360.0 / (float)1024);
+    o->ang_res_y = (float)(33.2 / (float)(64 - 1)); o->ang_bottom = (float)(16.6 + 0.1);
+    o->ground_scan_ind = 15;
+  } else if (!std::strcmp(name, "HDL-64E")) {  // KITTI-shaped, DESIGN.md §2
+    o->n_scan = 64; o->horizon_scan = 2048; o->ang_res_x = (float)(360.0 / (float)2048);
+    o->ang_res_y = (float)(26.8 / (float)(64 - 1)); o->ang_bottom = 24.8f;
+    o->ground_scan_ind = 55;
+  } else {
+    return LEGO_E_ARG;
+  }
+  o->use_cloud_ring = 1;
+  o->sensor_minimum_range = 1.0f;
+  o->sensor_mount_angle = 0.0f;
+  o->segment_theta = (float)(60.0 / 180.0 * M_PI);
+  o->segment_valid_point_num = 5;
+  o->segment_valid_line_num = 3;
+  o->segment_alpha_x = (float)(o->ang_res_x / 180.0 * M_PI);
+  o->segment_alpha_y = (float)(o->ang_res_y / 180.0 * M_PI);
+  o->edge_threshold = 0.1f;
+  o->surf_threshold = 0.1f;
+  o->nearest_feature_search_sq_dist = 25.f;
+  o->scan_period = 0.1f;
+  o->mapping_process_interval = 0.3;
+  o->surrounding_keyframe_search_radius = 50.0f;
+  o->skip_frame_num = 1;
+  return LEGO_OK;
+}
+
+int lego_create(const lego_sensor_cfg* cfg, int device, int32_t max_points, int32_t max_batch,
+                lego_ctx** out) {
+  if (!cfg || !out || max_points <= 0 || max_batch <= 0) return LEGO_E_ARG;
+  DevCfg dc;
+  if (make_devcfg(cfg, &dc) != LEGO_OK) {
+    set_err("unsupported sensor configuration");
+    return LEGO_E_ARG;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) {
+    set_err("no HIP device %d (count %d)", device, ndev);
+    return LEGO_E_DEVICE;
+  }
+  lego_ctx* x = new (std::nothrow) lego_ctx;
+  if (!x) return LEGO_E_CAPACITY;
+  x->cfg = *cfg;
+  x->dc = dc;
+  x->device = device;
+  x->maxPoints = max_points;
+  x->maxBatch = max_batch;
+  auto fail = [&](int st) { delete x; return st; };
+  if (hipSetDevice(device) != hipSuccess) return fail(LEGO_E_DEVICE);
+  if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess) return fail(LEGO_E_DEVICE);
+  const size_t B = max_batch, P = dc.P, N = dc.N;
+  BatchBufs& bb = x->bb;
+  bb.B = max_batch;
+  bb.Nmax = max_points;
+#define A(ptr, n)                                           \
+  if (x->alloc(&(ptr), (n)) != hipSuccess) {                \
+    set_err("hipMalloc failed for %s", #ptr);               \
+    return fail(LEGO_E_DEVICE);                             \
+  }
+  A(x->d_pts, B * max_points);
+  A(x->d_off, B + 1);
+  A(bb.owner, B * P);
+  A(bb.range, B * P);
+  A(bb.full, B * P);
+  A(bb.ground, B * P);
+  A(bb.label, B * P);
+  A(bb.parent, B * P);
+  A(bb.root, B * P);
+  A(bb.edges, B * P);
+  A(bb.csize, B * P);
+  A(bb.rowmask, B * P * 2);
+  A(bb.rawang, B * 2);
+  A(bb.seg, B * P);
+  A(bb.gflag, B * P);
+  A(bb.col, B * P);
+  A(bb.srange, B * P);
+  A(bb.outl, B * P);
+  A(bb.ns, B);
+  A(bb.nout, B);
+  A(bb.sri, B * N);
+  A(bb.eri, B * N);
+  A(bb.orient, B * 3);
+  A(bb.firsthalf, B);
+  A(bb.dsk, B * P);
+  A(bb.curv, B * P);
+  A(bb.pick0, B * P);
+  A(bb.r_sharp, B * N * kSharpPerRing);
+  A(bb.r_lsharp, B * N * kLessSharpPerRing);
+  A(bb.r_flat, B * N * kFlatPerRing);
+  A(bb.r_lflat, B * P);
+  A(bb.r_cnt, B * N * 4);
+  A(bb.spec_out, B);
+  A(bb.fa_flags, B);
+  A(bb.f_sharp, B * N * kSharpPerRing);
+  A(bb.f_lsharp, B * N * kLessSharpPerRing);
+  A(bb.f_flat, B * N * kFlatPerRing);
+  A(bb.f_lflat, B * P);
+  A(bb.f_cnt, B * 4);
+  OdomBufs& ob = x->ob;
+  ob.capLS = (int)(N * kLessSharpPerRing);
+  ob.capCorner = ob.capLS;
+  ob.capSurf = (int)P;
+  A(ob.st, 1);
+  A(ob.cornerLast, (size_t)ob.capCorner);
+  A(ob.surfLast, (size_t)ob.capSurf);
+  A(ob.nnCorner, (size_t)ob.capCorner);
+  A(ob.nnSurf, (size_t)ob.capSurf);
+  A(ob.nnCornerIdx, (size_t)ob.capCorner);
+  A(ob.nnSurfIdx, (size_t)ob.capSurf);
+  A(ob.nnCornerBox, odom_nn_box_count(ob.capCorner));
+  A(ob.nnSurfBox, odom_nn_box_count(ob.capSurf));
+  A(ob.sumOut, B * 6);
+  A(ob.curOut, B * 6);
+  A(ob.validOut, B);
+  A(ob.pubOut, B);
+  A(ob.cornerEnd, B * ob.capLS);
+  A(ob.surfEnd, B * P);
+  A(x->d_carry, 1);
+  {
+    size_t m = 1;
+    while (m < P) m <<= 1;
+    A(x->d_gkeys, m);
+  }
+#undef A
+  bb.pts = x->d_pts;
+  bb.off = x->d_off;
+  x->h_seg.resize(P); x->h_outl.resize(P); x->h_full.resize(P);
+  x->h_sharp.resize(N * kSharpPerRing); x->h_lsharp.resize(N * kLessSharpPerRing);
+  x->h_flat.resize(N * kFlatPerRing); x->h_lflat.resize(P);
+  x->h_cornerLast.resize(N * kLessSharpPerRing); x->h_surfLast.resize(P); x->h_outlLast.resize(P);
+  x->h_sri.resize(N); x->h_eri.resize(N); x->h_label.resize(P);
+  x->h_gflag.resize(P); x->h_col.resize(P); x->h_range.resize(P); x->h_rimg.resize(P);
+  x->h_gimg.resize(P);
+  int st = ctx_reset(x);
+  if (st != LEGO_OK) return fail(st);
+  *out = x;
+  return LEGO_OK;
+}
+
+int lego_destroy(lego_ctx* x) {
+  delete x;
+  return LEGO_OK;
+}
+
+int lego_reset(lego_ctx* x) {
+  if (!x) return LEGO_E_ARG;
+  HIPCHK(hipSetDevice(x->device));
+  return ctx_reset(x);
+}
+
+static int run_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offsets, int B,
+                     int on_device, int want_labels, bool with_fa) {
+  HIPCHK(hipSetDevice(x->device));
+  BatchBufs bb = x->bb;
+  if (on_device) {
+    bb.pts = pts;
+    bb.off = offsets;
+    int64_t last = 0, first = 0;
+    HIPCHK(hipMemcpyAsync(&first, offsets, sizeof(int64_t), hipMemcpyDeviceToHost, x->stream));
+    HIPCHK(hipMemcpyAsync(&last, offsets + B, sizeof(int64_t), hipMemcpyDeviceToHost, x->stream));
+    HIPCHK(hipStreamSynchronize(x->stream));
+    (void)first;
+    (void)last;
+    bb.Nmax = x->maxPoints;
+  } else {
+    int64_t total = offsets[B] - offsets[0];
+    for (int k = 0; k < B; ++k)
+      if (offsets[k + 1] - offsets[k] > x->maxPoints || offsets[k + 1] < offsets[k]) {
+        set_err("scan %d has %lld points > capacity %d", k, (long long)(offsets[k + 1] - offsets[k]),
+                x->maxPoints);
+        return LEGO_E_CAPACITY;
+      }
+    if (total > (int64_t)x->maxPoints * x->maxBatch) return LEGO_E_CAPACITY;
+    std::vector<int64_t> off(B + 1);
+    for (int k = 0; k <= B; ++k) off[k] = offsets[k] - offsets[0];
+    HIPCHK(hipMemcpyAsync(x->d_pts, pts + offsets[0], sizeof(lego_point_xyzir) * total,
+                          hipMemcpyHostToDevice, x->stream));
+    HIPCHK(hipMemcpyAsync(x->d_off, off.data(), sizeof(int64_t) * (B + 1), hipMemcpyHostToDevice,
+                          x->stream));
+    bb.pts = x->d_pts;
+    bb.off = x->d_off;
+    int mx = 0;
+    for (int k = 0; k < B; ++k) mx = std::max<int>(mx, (int)(off[k + 1] - off[k]));
+    bb.Nmax = std::max(mx, 1);
+  }
+  x->tm.begin();
+  launch_ip(bb, x->dc, B, want_labels, x->stream, &x->tm);
+  if (with_fa) {
+    launch_fa(bb, x->dc, B, x->d_carry, x->stream, &x->tm);
+    launch_odom(bb, x->ob, x->dc, B, x->stream, &x->tm, x->d_gkeys);
+  }
+  x->tm.end(x->stream);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(x->stream));
+  x->tm.collect(x->tnames, x->tms);
+  x->lastB = B;
+  return LEGO_OK;
+}
+
+// copy scan k's image-projection outputs of the last batch into host staging
+static int fetch_ip(lego_ctx* x, int k, bool images, lego_ip_out* o) {
+  const DevCfg& c = x->dc;
+  const size_t P = c.P, N = c.N;
+  int ns = 0, nout = 0;
+  float orient[3];
+  hipStream_t s = x->stream;
+  HIPCHK(hipMemcpyAsync(&ns, x->bb.ns + k, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(&nout, x->bb.nout + k, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(orient, x->bb.orient + 3 * k, sizeof(orient), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(x->h_sri.data(), x->bb.sri + k * N, sizeof(int) * N, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(x->h_eri.data(), x->bb.eri + k * N, sizeof(int) * N, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipMemcpyAsync(x->h_seg.data(), x->bb.seg + k * P, sizeof(float4) * ns, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(x->h_gflag.data(), x->bb.gflag + k * P, ns, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(x->h_col.data(), x->bb.col + k * P, sizeof(uint32_t) * ns, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(x->h_range.data(), x->bb.srange + k * P, sizeof(float) * ns, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(x->h_outl.data(), x->bb.outl + k * P, sizeof(float4) * nout, hipMemcpyDeviceToHost, s));
+  if (images) {
+    HIPCHK(hipMemcpyAsync(x->h_full.data(), x->bb.full + k * P, sizeof(float4) * P, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(x->h_rimg.data(), x->bb.range + k * P, sizeof(float) * P, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(x->h_gimg.data(), x->bb.ground + k * P, P, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(x->h_label.data(), x->bb.label + k * P, sizeof(int) * P, hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  std::memset(o, 0, sizeof(*o));
+  o->info.stamp = (k < (int)x->stamps.size()) ? x->stamps[k] : 0.0;
+  o->info.start_ring_index = x->h_sri.data();
+  o->info.end_ring_index = x->h_eri.data();
+  o->info.start_orientation = orient[0];
+  o->info.end_orientation = orient[1];
+  o->info.orientation_diff = orient[2];
+  o->info.segmented_cloud_ground_flag = x->h_gflag.data();
+  o->info.segmented_cloud_col_ind = x->h_col.data();
+  o->info.segmented_cloud_range = x->h_range.data();
+  o->segmented_cloud = x->h_seg.data();
+  o->n_segmented = ns;
+  o->outlier_cloud = x->h_outl.data();
+  o->n_outlier = nout;
+  if (images) {
+    o->full_cloud = x->h_full.data();
+    o->range_image = x->h_rimg.data();
+    o->ground_image = x->h_gimg.data();
+    o->label_image = x->h_label.data();
+  }
+  return LEGO_OK;
+}
+
+static int fetch_fa(lego_ctx* x, int k, lego_fa_out* o) {
+  const DevCfg& c = x->dc;
+  const size_t P = c.P, N = c.N;
+  hipStream_t s = x->stream;
+  int cnt[4], valid = 0, pub = 0, nout = 0;
+  float sum[6], cur[6];
+  HIPCHK(hipMemcpyAsync(cnt, x->bb.f_cnt + 4 * k, sizeof(cnt), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(&valid, x->ob.validOut + k, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(&pub, x->ob.pubOut + k, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(&nout, x->bb.nout + k, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(sum, x->ob.sumOut + 6 * k, sizeof(sum), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(cur, x->ob.curOut + 6 * k, sizeof(cur), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipMemcpyAsync(x->h_sharp.data(), x->bb.f_sharp + k * N * kSharpPerRing, sizeof(float4) * cnt[0], hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(x->h_lsharp.data(), x->bb.f_lsharp + k * N * kLessSharpPerRing, sizeof(float4) * cnt[1], hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(x->h_flat.data(), x->bb.f_flat + k * N * kFlatPerRing, sizeof(float4) * cnt[2], hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(x->h_lflat.data(), x->bb.f_lflat + k * P, sizeof(float4) * cnt[3], hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(x->h_cornerLast.data(), x->ob.cornerEnd + (size_t)k * x->ob.capLS, sizeof(float4) * cnt[1], hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(x->h_surfLast.data(), x->ob.surfEnd + k * P, sizeof(float4) * cnt[3], hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(x->h_outlLast.data(), x->bb.outl + k * P, sizeof(float4) * nout, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  // adjustOutlierCloud :1746-1757 (axis swap) on the published copy
+  for (int i = 0; i < nout; ++i) {
+    const lego_point_xyzi p = x->h_outlLast[i];
+    x->h_outlLast[i] = {p.y, p.z, p.x, p.intensity};
+  }
+  std::memset(o, 0, sizeof(*o));
+  o->stamp = (k < (int)x->stamps.size()) ? x->stamps[k] : 0.0;
+  o->sharp = x->h_sharp.data(); o->n_sharp = cnt[0];
+  o->less_sharp = x->h_lsharp.data(); o->n_less_sharp = cnt[1];
+  o->flat = x->h_flat.data(); o->n_flat = cnt[2];
+  o->less_flat = x->h_lflat.data(); o->n_less_flat = cnt[3];
+  o->odom_valid = valid;
+  for (int i = 0; i < 6; ++i) { o->transform_sum[i] = sum[i]; o->transform_cur[i] = cur[i]; }
+  odom_quat(sum, o->odom_quat, o->odom_pos);
+  o->publish_to_mapping = pub;
+  if (pub) {
+    o->corner_last = x->h_cornerLast.data(); o->n_corner_last = cnt[1];
+    o->surf_last = x->h_surfLast.data(); o->n_surf_last = cnt[3];
+    o->outlier_last = x->h_outlLast.data(); o->n_outlier_last = nout;
+  }
+  return LEGO_OK;
+}
+
+int lego_ip_process(lego_ctx* x, const lego_point_xyzir* pts, int32_t n, double stamp,
+                    uint32_t flags, lego_ip_out* out) {
+  if (!x || !pts || !out || n <= 0) return LEGO_E_ARG;
+  if (n > x->maxPoints) return LEGO_E_CAPACITY;
+  for (int i = 0; i < n; ++i)  // dense check (imageProjection.cpp:174)
+    if (!std::isfinite(pts[i].x) || !std::isfinite(pts[i].y) || !std::isfinite(pts[i].z))
+      return LEGO_E_NOT_DENSE;
+  int64_t off[2] = {0, n};
+  x->stamps.assign(1, stamp);
+  int st = run_batch(x, pts, off, 1, 0, (flags & LEGO_IP_IMAGES) ? 1 : 0, false);
+  if (st != LEGO_OK) return st;
+  st = fetch_ip(x, 0, (flags & LEGO_IP_IMAGES) != 0, out);
+  if (st != LEGO_OK) return st;
+  x->lastIp = *out;
+  x->lastIpDevice = true;
+  return LEGO_OK;
+}
+
+// Uploads a host cloud_info + segmented cloud into batch slot 0 (used when the
+// caller's input did not come from this context's lego_ip_process).
+static int upload_ip(lego_ctx* x, const lego_ip_out* in) {
+  const DevCfg& c = x->dc;
+  const int ns = in->n_segmented;
+  if (ns < 0 || ns > c.P || in->n_outlier < 0 || in->n_outlier > c.P) return LEGO_E_CAPACITY;
+  hipStream_t s = x->stream;
+  std::vector<float4> seg(ns);
+  for (int i = 0; i < ns; ++i) {
+    const lego_point_xyzi& p = in->segmented_cloud[i];
+    seg[i] = make_float4(p.x, p.y, p.z, p.intensity);
+  }
+  float orient[3] = {in->info.start_orientation, in->info.end_orientation, in->info.orientation_diff};
+  HIPCHK(hipMemcpyAsync(x->bb.seg, seg.data(), sizeof(float4) * ns, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(x->bb.gflag, in->info.segmented_cloud_ground_flag, ns, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(x->bb.col, in->info.segmented_cloud_col_ind, sizeof(uint32_t) * ns, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(x->bb.srange, in->info.segmented_cloud_range, sizeof(float) * ns, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(x->bb.outl, in->outlier_cloud, sizeof(float4) * in->n_outlier, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(x->bb.ns, &ns, sizeof(int), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(x->bb.nout, &in->n_outlier, sizeof(int), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(x->bb.sri, in->info.start_ring_index, sizeof(int) * c.N, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(x->bb.eri, in->info.end_ring_index, sizeof(int) * c.N, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(x->bb.orient, orient, sizeof(orient), hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return LEGO_OK;
+}
+
+int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
+  if (!x || !in || !out) return LEGO_E_ARG;
+  HIPCHK(hipSetDevice(x->device));
+  const bool resident = x->lastIpDevice && in->segmented_cloud == x->h_seg.data() &&
+                        in->n_segmented == x->lastIp.n_segmented;
+  if (!resident) {
+    int st = upload_ip(x, in);
+    if (st != LEGO_OK) return st;
+  }
+  x->stamps.assign(1, in->info.stamp);
+  x->tm.begin();
+  launch_fa(x->bb, x->dc, 1, x->d_carry, x->stream, &x->tm);
+  launch_odom(x->bb, x->ob, x->dc, 1, x->stream, &x->tm, x->d_gkeys);
+  x->tm.end(x->stream);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(x->stream));
+  x->lastB = 1;
+  x->lastIpDevice = false;
+  return fetch_fa(x, 0, out);
+}
+
+int lego_odom_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offsets,
+                    const double* stamps, int32_t nscans, int32_t on_device, lego_pose_rec* recs) {
+  if (!x || !pts || !offsets || nscans <= 0 || !recs) return LEGO_E_ARG;
+  if (nscans > x->maxBatch) {
+    set_err("batch of %d scans > context capacity %d", nscans, x->maxBatch);
+    return LEGO_E_CAPACITY;
+  }
+  x->stamps.assign(stamps ? stamps : nullptr, stamps ? stamps + nscans : nullptr);
+  if (!stamps) x->stamps.assign(nscans, 0.0);
+  int st = run_batch(x, pts, offsets, nscans, on_device, 0, true);
+  if (st != LEGO_OK) return st;
+  x->lastIpDevice = false;
+  std::vector<float> sum(6 * nscans);
+  std::vector<int> valid(nscans), fcnt(4 * nscans), ns(nscans), flags(nscans);
+  hipStream_t s = x->stream;
+  HIPCHK(hipMemcpyAsync(sum.data(), x->ob.sumOut, sizeof(float) * 6 * nscans, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(valid.data(), x->ob.validOut, sizeof(int) * nscans, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(fcnt.data(), x->bb.f_cnt, sizeof(int) * 4 * nscans, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(ns.data(), x->bb.ns, sizeof(int) * nscans, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(flags.data(), x->bb.fa_flags, sizeof(int) * nscans, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  for (int k = 0; k < nscans; ++k) {
+    lego_pose_rec& r = recs[k];
+    std::memset(&r, 0, sizeof(r));
+    r.stamp = x->stamps[k];
+    for (int i = 0; i < 6; ++i) r.transform_sum[i] = sum[6 * k + i];
+    r.n_segmented = ns[k];
+    r.n_sharp = fcnt[4 * k];
+    r.n_less_sharp = fcnt[4 * k + 1];
+    r.n_flat = fcnt[4 * k + 2];
+    r.n_less_flat = fcnt[4 * k + 3];
+    r.odom_valid = valid[k];
+    r.flags = flags[k];
+  }
+  return LEGO_OK;
+}
+
+int lego_batch_fetch(lego_ctx* x, int32_t k, lego_ip_out* ip, lego_fa_out* fa) {
+  if (!x || k < 0 || k >= x->lastB) return LEGO_E_ARG;
+  HIPCHK(hipSetDevice(x->device));
+  if (ip) {
+    int st = fetch_ip(x, k, false, ip);
+    if (st != LEGO_OK) return st;
+  }
+  if (fa) return fetch_fa(x, k, fa);
+  return LEGO_OK;
+}
+
+int lego_mo_set_map(lego_ctx* x, const lego_point_xyzi* corner, int32_t n_corner,
+                    const lego_point_xyzi* surf, int32_t n_surf) {
+  (void)corner; (void)n_corner; (void)surf; (void)n_surf;
+  if (!x) return LEGO_E_ARG;
+  set_err("scan-to-map is not in this build yet");
+  return LEGO_E_STATE;
+}
+
+int lego_mo_process(lego_ctx* x, const lego_fa_out* in, lego_mo_out* out) {
+  (void)in; (void)out;
+  if (!x) return LEGO_E_ARG;
+  set_err("scan-to-map is not in this build yet");
+  return LEGO_E_STATE;
+}
+
+int lego_stage_times(lego_ctx* x, const char** names, float* ms, int32_t cap, int32_t* n) {
+  if (!x || !n) return LEGO_E_ARG;
+  if (cap == 0) {  // toggle: cap 0 with names == NULL enables/disables the timer
+    x->tm.enabled = ms != nullptr;
+    *n = 0;
+    return LEGO_OK;
+  }
+  const int m = std::min<int>((int)x->tnames.size(), cap);
+  for (int i = 0; i < m; ++i) {
+    if (names) names[i] = x->tnames[i].c_str();
+    if (ms) ms[i] = x->tms[i];
+  }
+  *n = m;
+  return LEGO_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,100 @@
+// lego_device.h — shared device-side types for the gfx950 kernels.
+//
+// Data layout in HBM (one stream context, batch of B scans, P = N*H pixels):
+//   range image / label / parent / root / ground : [B][P]  (row-major pixels)
+//   full cloud                                    : [B][P]  float4 (x,y,z,I)
+//   segmented cloud + cloud_info arrays           : [B][P]  (first Ns valid)
+//   feature ring slots                            : [B][N][cap]
+//   compacted features                            : [B][cap]
+// Everything a later stage reads stays resident; nothing round-trips to host
+// inside lego_odom_batch except the 64-B pose records at the end.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lego_numerics.h"
+
+namespace lego {
+
+constexpr int kMaxRings = 128;        // rowmask = 2 x u64
+constexpr int kMaxHorizon = 4096;     // col fits u16; ring window fits LDS
+constexpr int kSharpPerRing = 12;     // 2 per sector (featureAssociation.cpp:709)
+constexpr int kLessSharpPerRing = 120;// 20 per sector (:713)
+constexpr int kFlatPerRing = 24;      // 4 per sector (:746-748)
+constexpr int kExtractThreads = 256;
+constexpr int kSortCap = 1024;        // sector sort buffer (sector <= H/6 + 2)
+constexpr int kVoxCap = 4096;         // per-ring less-flat voxel sort
+
+struct DevCfg {
+  int N, H, P, g;
+  float ang_res_x, min_range, mount_angle, theta;
+  float sinAX, cosAX, sinAY, cosAY;
+  int valid_pt, valid_line;
+  float edge_thr, surf_thr, nn_sq, scan_period;
+  int skip;  // skipFrameNum (featureAssociation.cpp:284)
+};
+
+// Per-stream feature-extraction carry: the stale
+// cloudSmoothness[4] entry (value is always 0.0f, only its index moves) and the
+// sticky cloudNeighborPicked[0].  S* = {0, 1} is the steady state.
+struct FaCarry {
+  int phantom_ind;
+  int picked0;
+  int flags;
+  int _pad;
+};
+
+// Batch-wide device pointers (filled by the host, passed by value).
+struct BatchBufs {
+  int B;
+  int Nmax;                  // max input points per scan
+  // ---- image projection
+  const void* pts;           // lego_point_xyzir [*]
+  const int64_t* off;        // [B+1]
+  int* owner;                // [B*P]
+  float* range;              // [B*P]
+  float4* full;              // [B*P]
+  int8_t* ground;            // [B*P]
+  int* label;                // [B*P]  init label, then final label image
+  int* parent;               // [B*P]
+  int* root;                 // [B*P]
+  uint8_t* edges;            // [B*P]
+  int* csize;                // [B*P]
+  unsigned long long* rowmask;  // [B*P*2]
+  float* rawang;             // [B*2]
+  // ---- segmented cloud + cloud_info
+  float4* seg;               // [B*P]
+  uint8_t* gflag;            // [B*P]
+  uint32_t* col;             // [B*P]
+  float* srange;             // [B*P]
+  float4* outl;              // [B*P]
+  int* ns;                   // [B]  segmented count
+  int* nout;                 // [B]
+  int* sri;                  // [B*N]
+  int* eri;                  // [B*N]
+  float* orient;             // [B*3]
+  // ---- feature association
+  int* firsthalf;            // [B]
+  float4* dsk;               // [B*P] deskewed segmented cloud
+  float* curv;               // [B*P]
+  uint8_t* pick0;            // [B*P] occlusion marks
+  float4* r_sharp;           // [B*N*12]
+  float4* r_lsharp;          // [B*N*120]
+  float4* r_flat;            // [B*N*24]
+  float4* r_lflat;           // [B*P]   ring r at [b*P + r*H]
+  int* r_cnt;                // [B*N*4]
+  FaCarry* spec_out;         // [B] carry produced under S*
+  int* fa_flags;             // [B]
+  float4* f_sharp;           // [B*N*12]
+  float4* f_lsharp;          // [B*N*120]
+  float4* f_flat;            // [B*N*24]
+  float4* f_lflat;           // [B*P]
+  int* f_cnt;                // [B*4]
+};
+
+// Buffer views inside the batch for scan b.
+__device__ __forceinline__ int scan_npts(const BatchBufs& bb, int b) {
+  return (int)(bb.off[b + 1] - bb.off[b]);
+}
+
+}  // namespace lego

@@ -1,0 +1,578 @@
+// lego_fa.hip — featureAssociation feature extraction on gfx950.
+//
+//   k_fa_half     1 lane / segmented point: the !halfPassed orientation test;
+//                 the first point that flips halfPassed is an atomicMin
+//                 (adjustDistortion, featureAssociation.cpp:491-523)
+//   k_fa_point    1 lane / point: deskew (axis swap + relTime), 11-tap
+//                 curvature (:621-641), occlusion marks as a gather (:643-678)
+//   k_extract     1 workgroup / (scan, ring): per sector a bitonic sort of
+//                 (curvature, index) in LDS — libstdc++ introsort port when the
+//                 sector holds ties (equal keys are ordered by std::sort's
+//                 unstable algorithm) — then the edge/flat picking scans as
+//                 wave ballots, the less-flat set and the per-ring 0.2 m
+//                 VoxelGrid (:680-784).  Rings are independent except through
+//                 the ring-0 carry: extraction runs for every
+//                 scan under the steady carry S*; k_fa_fixup walks the batch in
+//                 stream order and re-runs ring 0 where the real carry differs.
+//   k_fa_compact  concatenates the per-ring slots in ring order.
+#include <climits>
+
+#include "lego_device.h"
+#include "lego_introsort.h"
+#include "lego_kernels.h"
+
+namespace lego {
+
+// ---------------------------------------------------------------- deskew
+__device__ __forceinline__ float ori_not_half(float ori, float so) {
+  if ((double)ori < (double)so - M_PI / 2) ori = (float)((double)ori + 2 * M_PI);
+  else if ((double)ori > (double)so + M_PI * 3 / 2) ori = (float)((double)ori - 2 * M_PI);
+  return ori;
+}
+
+__global__ void k_fa_half(BatchBufs bb, DevCfg c) {
+  const int b = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= bb.ns[b]) return;
+  const float4 p = bb.seg[(size_t)b * c.P + i];
+  const float so = bb.orient[3 * b];
+  const float ori = ori_not_half(-lego_atan2f(p.y, p.x), so);        // point.x = y, point.z = x
+  if ((double)(ori - so) > M_PI) atomicMin(&bb.firsthalf[b], i);
+}
+
+__device__ __forceinline__ bool occ_fwd(const float* r, const uint32_t* col, int i, int ns) {
+  if (i < 5 || i >= ns - 6) return false;
+  const int cd = abs((int)(col[i + 1] - col[i]));
+  return cd < 10 && (double)(r[i] - r[i + 1]) > 0.3;
+}
+__device__ __forceinline__ bool occ_bwd(const float* r, const uint32_t* col, int i, int ns) {
+  if (i < 5 || i >= ns - 6) return false;
+  const int cd = abs((int)(col[i + 1] - col[i]));
+  return cd < 10 && !((double)(r[i] - r[i + 1]) > 0.3) && (double)(r[i + 1] - r[i]) > 0.3;
+}
+__device__ __forceinline__ bool occ_par(const float* r, int i, int ns) {
+  if (i < 5 || i >= ns - 6) return false;
+  const float d1 = lfabsf(r[i - 1] - r[i]), d2 = lfabsf(r[i + 1] - r[i]);
+  return (double)d1 > 0.02 * (double)r[i] && (double)d2 > 0.02 * (double)r[i];
+}
+
+__global__ void k_fa_point(BatchBufs bb, DevCfg c) {
+  const int b = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int ns = bb.ns[b];
+  if (i >= ns) return;
+  const size_t base = (size_t)b * c.P;
+  // adjustDistortion (imuPointerLast < 0): :498-523
+  const float4 p = bb.seg[base + i];
+  const float so = bb.orient[3 * b], eo = bb.orient[3 * b + 1], od = bb.orient[3 * b + 2];
+  float ori = -lego_atan2f(p.y, p.x);
+  if (i <= bb.firsthalf[b]) {
+    ori = ori_not_half(ori, so);
+  } else {
+    ori = (float)((double)ori + 2 * M_PI);
+    if ((double)ori < (double)eo - M_PI * 3 / 2) ori = (float)((double)ori + 2 * M_PI);
+    else if ((double)ori > (double)eo + M_PI / 2) ori = (float)((double)ori - 2 * M_PI);
+  }
+  const float relTime = (ori - so) / od;
+  const float inten = (float)(int)p.w + c.scan_period * relTime;
+  bb.dsk[base + i] = make_float4(p.y, p.z, p.x, inten);
+  // calculateSmoothness :624-640
+  const float* r = bb.srange + base;
+  float cv = 0.f;
+  if (i >= 5 && i < ns - 5) {
+    const float d = r[i - 5] + r[i - 4] + r[i - 3] + r[i - 2] + r[i - 1] - r[i] * 10 + r[i + 1] +
+                    r[i + 2] + r[i + 3] + r[i + 4] + r[i + 5];
+    cv = d * d;
+  }
+  bb.curv[base + i] = cv;
+  // markOccludedPoints as a gather: which i' mark index i
+  const uint32_t* col = bb.col + base;
+  bool m = occ_par(r, i, ns);
+  for (int k = i; k <= i + 5 && !m; ++k) m = occ_fwd(r, col, k, ns);
+  for (int k = i - 6; k <= i - 1 && !m; ++k) m = occ_bwd(r, col, k, ns);
+  bb.pick0[base + i] = m ? 1 : 0;
+}
+
+// ---------------------------------------------------------------- extraction
+struct ExtractLds {
+  float* curv;
+  uint16_t* col;
+  uint8_t* picked;
+  int8_t* label;
+  uint8_t* gfl;
+  int* lf;
+  SmoothEntry* srt;
+  SmoothEntry* orig;
+  unsigned long long* vox;
+  int* misc;
+  float* red;
+};
+
+__host__ __device__ inline int next_pow2(int x) {
+  int m = 1;
+  while (m < x) m <<= 1;
+  return m;
+}
+
+__host__ __device__ inline size_t extract_lds_bytes(int H) {
+  const size_t W = (size_t)H + 32;
+  const size_t vox = (size_t)next_pow2((int)W);
+  size_t s = 0;
+  s += W * 4;                 // curv
+  s += W * 4;                 // lf
+  s += 2 * kSortCap * 8;      // srt + orig
+  s += vox * 8;               // vox
+  s += 64 * 4 + 64 * 4;       // misc + red
+  s += W * 2;                 // col
+  s += W * 3;                 // picked, label, gfl
+  return (s + 15) & ~(size_t)15;
+}
+
+__device__ ExtractLds carve(unsigned char* base, int H) {
+  const size_t W = (size_t)H + 32;
+  const size_t vox = (size_t)next_pow2((int)W);
+  ExtractLds L;
+  size_t o = 0;
+  L.vox = (unsigned long long*)(base + o); o += vox * 8;
+  L.srt = (SmoothEntry*)(base + o); o += kSortCap * 8;
+  L.orig = (SmoothEntry*)(base + o); o += kSortCap * 8;
+  L.curv = (float*)(base + o); o += W * 4;
+  L.lf = (int*)(base + o); o += W * 4;
+  L.misc = (int*)(base + o); o += 64 * 4;
+  L.red = (float*)(base + o); o += 64 * 4;
+  L.col = (uint16_t*)(base + o); o += W * 2;
+  L.picked = base + o; o += W;
+  L.label = (int8_t*)(base + o); o += W;
+  L.gfl = base + o; o += W;
+  return L;
+}
+
+enum { M_TIE = 0, M_LF = 1, M_OVF = 2, M_NSH = 3, M_NLS = 4, M_NFL = 5, M_D0 = 6, M_D1 = 7,
+       M_MB0 = 8, M_MB1 = 9, M_MB2 = 10, M_WOFF = 16 };
+
+// Bitonic sort of m (power of two) entries in LDS by value, all threads.
+__device__ void bitonic_entries(SmoothEntry* a, int m) {
+  for (int k = 2; k <= m; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int t = threadIdx.x; t < m / 2; t += blockDim.x) {
+        const int i = (t / j) * 2 * j + (t % j);
+        const int l = i + j;
+        const bool up = (i & k) == 0;
+        const SmoothEntry x = a[i], y = a[l];
+        if ((x.value > y.value) == up) { a[i] = y; a[l] = x; }
+      }
+      __syncthreads();
+    }
+  }
+}
+__device__ void bitonic_u64(unsigned long long* a, int m) {
+  for (int k = 2; k <= m; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int t = threadIdx.x; t < m / 2; t += blockDim.x) {
+        const int i = (t / j) * 2 * j + (t % j);
+        const int l = i + j;
+        const bool up = (i & k) == 0;
+        const unsigned long long x = a[i], y = a[l];
+        if ((x > y) == up) { a[i] = y; a[l] = x; }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Ordered block compaction helper: returns this thread's exclusive rank among
+// flagged threads of the block and the block total (256 threads = 4 waves).
+__device__ __forceinline__ int block_rank(bool f, int* woff, int* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const unsigned long long m = __ballot(f);
+  const int r = __popcll(m & ((1ull << lane) - 1));
+  if (lane == 0) woff[wave] = __popcll(m);
+  __syncthreads();
+  int off = 0, tot = 0;
+  const int nw = blockDim.x >> 6;
+  for (int w = 0; w < nw; ++w) {
+    if (w < wave) off += woff[w];
+    tot += woff[w];
+  }
+  __syncthreads();
+  *total = tot;
+  return off + r;
+}
+
+struct RingCtx {
+  int b, ring, lo, Wn, ns;
+  size_t base;
+  float4* osh;
+  float4* ols;
+  float4* ofl;
+};
+
+// neighbour suppression (:720-732, :751-767); negative indices break (the
+// reference reads colInd[-1] there — UB; SURVEY.md §9.7 policy).
+__device__ void suppress(const RingCtx& R, volatile uint8_t* picked, const uint16_t* col, int ind) {
+  const int w = ind - R.lo;
+  picked[w] = 1;
+  for (int l = 1; l <= 5; l++) {
+    const int q = w + l;
+    if (q >= R.Wn) break;
+    if (abs((int)col[q] - (int)col[q - 1]) > 10) break;
+    picked[q] = 1;
+  }
+  for (int l = -1; l >= -5; l--) {
+    const int q = w + l;
+    if (ind + l < 0 || q < 0) break;
+    if (abs((int)col[q] - (int)col[q + 1]) > 10) break;
+    picked[q] = 1;
+  }
+}
+
+__device__ __forceinline__ int entry_ind(const SmoothEntry* srt, int sp, int ep, int k) {
+  return (k == ep) ? ep : srt[k - sp].ind;
+}
+
+__device__ __forceinline__ bool in_win(const RingCtx& R, int ind) {
+  return ind >= R.lo && ind - R.lo < R.Wn;
+}
+
+__device__ void extract_ring(const BatchBufs& bb, const DevCfg& c, int b, int ring, FaCarry* carry,
+                             const ExtractLds& L) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ns = bb.ns[b];
+  const int s = bb.sri[b * c.N + ring], e = bb.eri[b * c.N + ring];
+  RingCtx R;
+  R.b = b; R.ring = ring; R.ns = ns;
+  R.base = (size_t)b * c.P;
+  R.lo = max(0, s - 5);
+  int hi = min(ns, e + 6);
+  if (hi < R.lo) hi = R.lo;
+  R.Wn = hi - R.lo;
+  R.osh = bb.r_sharp + ((size_t)b * c.N + ring) * kSharpPerRing;
+  R.ols = bb.r_lsharp + ((size_t)b * c.N + ring) * kLessSharpPerRing;
+  R.ofl = bb.r_flat + ((size_t)b * c.N + ring) * kFlatPerRing;
+  float4* olf = bb.r_lflat + R.base + (size_t)ring * c.H;
+  volatile uint8_t* picked = L.picked;
+  volatile int8_t* label = L.label;
+  for (int t = tid; t < R.Wn; t += blockDim.x) {
+    const size_t g = R.base + R.lo + t;
+    L.curv[t] = bb.curv[g];
+    L.col[t] = (uint16_t)bb.col[g];
+    L.picked[t] = bb.pick0[g];
+    L.label[t] = 0;
+    L.gfl[t] = bb.gflag[g];
+  }
+  if (tid < 64) L.misc[tid] = 0;
+  __syncthreads();
+  int ph = 0;
+  if (ring == 0 && carry) {
+    ph = carry->phantom_ind;
+    if (tid == 0 && R.lo == 0 && R.Wn > 0 && carry->picked0) L.picked[0] = 1;
+  }
+  __syncthreads();
+  int newph = ph;
+  int flags = 0;
+  for (int j = 0; j < 6; j++) {
+    const int sp = (s * (6 - j) + e * j) / 6;
+    const int ep = (s * (5 - j) + e * (j + 1)) / 6 - 1;
+    if (sp >= ep) continue;
+    const int n = ep - sp;
+    const int m = next_pow2(n);
+    const bool phantom_here = (ring == 0 && sp <= 4 && 4 < ep);
+    for (int t = tid; t < m; t += blockDim.x) {
+      SmoothEntry en;
+      if (t < n) {
+        const int pos = sp + t;
+        if (phantom_here && pos == 4) en = {0.0f, ph};
+        else en = {L.curv[pos - R.lo], pos};
+        L.orig[t] = en;
+      } else {
+        en = {__builtin_inff(), INT_MAX};
+      }
+      L.srt[t] = en;
+    }
+    __syncthreads();
+    bitonic_entries(L.srt, m);
+    for (int t = tid; t < n - 1; t += blockDim.x)
+      if (L.srt[t].value == L.srt[t + 1].value) L.misc[M_TIE] = 1;
+    __syncthreads();
+    if (L.misc[M_TIE]) {
+      // equal curvatures: their relative order is std::sort's
+      if (tid == 0) {
+        for (int t = 0; t < n; ++t) L.srt[t] = L.orig[t];
+        std_sort_by_value(L.srt, n);
+        L.misc[M_TIE] = 0;
+      }
+      __syncthreads();
+    }
+    if (phantom_here) newph = L.srt[4 - sp].ind;
+    // ---- edge scan (wave 0), k = ep .. sp
+    if (wave == 0) {
+      int cnt = 0;
+      int nsh = L.misc[M_NSH], nls = L.misc[M_NLS];
+      bool done = false;
+      for (int base = ep; base >= sp && !done; base -= 64) {
+        const int k = base - lane;
+        bool act = k >= sp;
+        const int ind = act ? entry_ind(L.srt, sp, ep, k) : -1;
+        if (act && !in_win(R, ind)) { act = false; flags |= 1; }
+        while (true) {
+          bool el = false;
+          if (act) {
+            const int w = ind - R.lo;
+            el = picked[w] == 0 && L.curv[w] > c.edge_thr && L.gfl[w] == 0;
+          }
+          const unsigned long long msk = __ballot(el);
+          if (msk == 0) break;
+          const int l = __ffsll((long long)msk) - 1;
+          cnt++;
+          if (cnt > 20) { done = true; break; }
+          if (lane == l) {
+            const int w = ind - R.lo;
+            label[w] = cnt <= 2 ? 2 : 1;
+            const float4 pt = bb.dsk[R.base + ind];
+            if (cnt <= 2) R.osh[nsh] = pt;
+            R.ols[nls] = pt;
+            suppress(R, picked, L.col, ind);
+          }
+          if (cnt <= 2) nsh++;
+          nls++;
+          act = act && lane > l;
+        }
+      }
+      if (lane == 0) { L.misc[M_NSH] = nsh; L.misc[M_NLS] = nls; }
+    }
+    __syncthreads();
+    // ---- flat scan (wave 0), k = sp .. ep
+    if (wave == 0) {
+      int cnt = 0;
+      int nfl = L.misc[M_NFL];
+      bool done = false;
+      for (int base = sp; base <= ep && !done; base += 64) {
+        const int k = base + lane;
+        bool act = k <= ep;
+        const int ind = act ? entry_ind(L.srt, sp, ep, k) : -1;
+        if (act && !in_win(R, ind)) { act = false; flags |= 1; }
+        while (true) {
+          bool el = false;
+          if (act) {
+            const int w = ind - R.lo;
+            el = picked[w] == 0 && L.curv[w] < c.surf_thr && L.gfl[w] == 1;
+          }
+          const unsigned long long msk = __ballot(el);
+          if (msk == 0) break;
+          const int l = __ffsll((long long)msk) - 1;
+          if (lane == l) {
+            label[ind - R.lo] = -1;
+            R.ofl[nfl] = bb.dsk[R.base + ind];
+          }
+          nfl++;
+          cnt++;
+          if (cnt >= 4) { done = true; break; }
+          if (lane == l) suppress(R, picked, L.col, ind);
+          act = act && lane > l;
+        }
+      }
+      if (lane == 0) L.misc[M_NFL] = nfl;
+    }
+    __syncthreads();
+    // ---- less-flat set: positions k in [sp, ep] with label <= 0, in order (:771-775)
+    for (int k0 = sp; k0 <= ep; k0 += blockDim.x) {
+      const int k = k0 + tid;
+      const bool f = k <= ep && label[k - R.lo] <= 0;
+      int tot;
+      const int r = block_rank(f, L.misc + M_WOFF, &tot);
+      if (f) L.lf[L.misc[M_LF] + r] = k;
+      __syncthreads();
+      if (tid == 0) L.misc[M_LF] += tot;
+      __syncthreads();
+    }
+  }
+  // ---- per-ring VoxelGrid 0.2 m on the less-flat set (:778-782)
+  const int K = L.misc[M_LF];
+  const float inv = 1.0f / 0.2f;
+  float mn[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
+  float mx[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+  for (int t = tid; t < K; t += blockDim.x) {
+    const float4 p = bb.dsk[R.base + L.lf[t]];
+    mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+    mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+  }
+  for (int q = 0; q < 3; ++q) {
+    for (int o = 32; o > 0; o >>= 1) {
+      mn[q] = fminf(mn[q], __shfl_xor(mn[q], o, 64));
+      mx[q] = fmaxf(mx[q], __shfl_xor(mx[q], o, 64));
+    }
+  }
+  if (lane == 0)
+    for (int q = 0; q < 3; ++q) { L.red[wave * 6 + q] = mn[q]; L.red[wave * 6 + 3 + q] = mx[q]; }
+  __syncthreads();
+  if (tid == 0 && K > 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
+      for (int q = 0; q < 3; ++q) {
+        L.red[q] = fminf(L.red[q], L.red[w * 6 + q]);
+        L.red[3 + q] = fmaxf(L.red[3 + q], L.red[w * 6 + 3 + q]);
+      }
+    const long long dx = (long long)((L.red[3] - L.red[0]) * inv) + 1;
+    const long long dy = (long long)((L.red[4] - L.red[1]) * inv) + 1;
+    const long long dz = (long long)((L.red[5] - L.red[2]) * inv) + 1;
+    L.misc[M_OVF] = (dx * dy * dz > (long long)INT_MAX) ? 1 : 0;
+    int mb[3], xb[3];
+    for (int q = 0; q < 3; ++q) {
+      mb[q] = (int)floorf(L.red[q] * inv);
+      xb[q] = (int)floorf(L.red[3 + q] * inv);
+    }
+    L.misc[M_MB0] = mb[0]; L.misc[M_MB1] = mb[1]; L.misc[M_MB2] = mb[2];
+    L.misc[M_D0] = xb[0] - mb[0] + 1;
+    L.misc[M_D1] = xb[1] - mb[1] + 1;
+  }
+  __syncthreads();
+  int nlf = 0;
+  if (K > 0 && L.misc[M_OVF]) {
+    for (int t = tid; t < K; t += blockDim.x) olf[t] = bb.dsk[R.base + L.lf[t]];
+    nlf = K;
+  } else if (K > 0) {
+    const int m = next_pow2(K);
+    const int d0 = L.misc[M_D0], d1 = L.misc[M_D1];
+    const float fb0 = (float)L.misc[M_MB0], fb1 = (float)L.misc[M_MB1], fb2 = (float)L.misc[M_MB2];
+    for (int t = tid; t < m; t += blockDim.x) {
+      unsigned long long key = ~0ull;
+      if (t < K) {
+        const float4 p = bb.dsk[R.base + L.lf[t]];
+        const int i0 = (int)(floorf(p.x * inv) - fb0);
+        const int i1 = (int)(floorf(p.y * inv) - fb1);
+        const int i2 = (int)(floorf(p.z * inv) - fb2);
+        const int idx = i0 + i1 * d0 + i2 * d0 * d1;
+        key = ((unsigned long long)(unsigned)idx << 32) | (unsigned)t;
+      }
+      L.vox[t] = key;
+    }
+    __syncthreads();
+    bitonic_u64(L.vox, m);
+    int outc = 0;
+    for (int t0 = 0; t0 < K; t0 += blockDim.x) {
+      const int t = t0 + tid;
+      const bool head = t < K && (t == 0 || (L.vox[t] >> 32) != (L.vox[t - 1] >> 32));
+      int tot;
+      const int r = block_rank(head, L.misc + M_WOFF, &tot);
+      if (head) {
+        const unsigned key = (unsigned)(L.vox[t] >> 32);
+        float cx = 0, cy = 0, cz = 0, ci = 0;
+        int u = t;
+        for (; u < K && (unsigned)(L.vox[u] >> 32) == key; ++u) {
+          const float4 p = bb.dsk[R.base + L.lf[(unsigned)(L.vox[u] & 0xffffffffu)]];
+          cx += p.x; cy += p.y; cz += p.z; ci += p.w;
+        }
+        const float cnt = (float)(u - t);
+        olf[outc + r] = make_float4(cx / cnt, cy / cnt, cz / cnt, ci / cnt);
+      }
+      outc += tot;
+    }
+    nlf = outc;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int* cnt = bb.r_cnt + ((size_t)b * c.N + ring) * 4;
+    cnt[0] = L.misc[M_NSH];
+    cnt[1] = L.misc[M_NLS];
+    cnt[2] = L.misc[M_NFL];
+    cnt[3] = nlf;
+  }
+  if (ring == 0 && carry) {
+    // wave 0 holds the picking flags; lane values of `flags` are merged below
+    int fl = __ballot(flags != 0) ? 1 : 0;
+    if (tid == 0) {
+      carry->phantom_ind = newph;
+      carry->picked0 = (R.lo == 0 && R.Wn > 0) ? (L.picked[0] ? 1 : 0) : carry->picked0;
+      carry->flags |= fl;
+    }
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(kExtractThreads) k_extract(BatchBufs bb, DevCfg c) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  const ExtractLds L = carve(lds_raw, c.H);
+  const int ring = blockIdx.x, b = blockIdx.y;
+  if (ring == 0) {
+    __shared__ FaCarry cs;
+    if (threadIdx.x == 0) cs = FaCarry{0, 1, 0, 0};  // S*
+    __syncthreads();
+    extract_ring(bb, c, b, 0, &cs, L);
+    if (threadIdx.x == 0) bb.spec_out[b] = cs;
+  } else {
+    extract_ring(bb, c, b, ring, nullptr, L);
+  }
+}
+
+// Walks the batch in stream order; re-runs ring 0 wherever the real carry is
+// not S* (the first scan of a stream, or after a 0.0-curvature tie).
+__global__ void __launch_bounds__(kExtractThreads) k_fa_fixup(BatchBufs bb, DevCfg c, int B,
+                                                             FaCarry* carry) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  const ExtractLds L = carve(lds_raw, c.H);
+  __shared__ FaCarry cs;
+  if (threadIdx.x == 0) cs = *carry;
+  __syncthreads();
+  for (int b = 0; b < B; ++b) {
+    const bool steady = cs.phantom_ind == 0 && cs.picked0 == 1;
+    if (steady) {
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const FaCarry s = bb.spec_out[b];
+        cs.phantom_ind = s.phantom_ind;
+        cs.picked0 = s.picked0;
+        cs.flags |= s.flags;
+      }
+      __syncthreads();
+    } else {
+      extract_ring(bb, c, b, 0, &cs, L);
+      if (threadIdx.x == 0) bb.fa_flags[b] |= 2;  // ring 0 recomputed with the real carry
+    }
+  }
+  if (threadIdx.x == 0) *carry = cs;
+}
+
+__global__ void k_fa_compact(BatchBufs bb, DevCfg c) {
+  __shared__ int off[4][kMaxRings + 1];
+  const int b = blockIdx.x;
+  const int* cnt = bb.r_cnt + (size_t)b * c.N * 4;
+  if (threadIdx.x < 4) {
+    int s = 0;
+    for (int r = 0; r < c.N; ++r) {
+      off[threadIdx.x][r] = s;
+      s += cnt[r * 4 + threadIdx.x];
+    }
+    off[threadIdx.x][c.N] = s;
+    bb.f_cnt[b * 4 + threadIdx.x] = s;
+  }
+  __syncthreads();
+  for (int r = 0; r < c.N; ++r) {
+    const size_t rb = (size_t)b * c.N + r;
+    for (int t = threadIdx.x; t < cnt[r * 4 + 0]; t += blockDim.x)
+      bb.f_sharp[(size_t)b * c.N * kSharpPerRing + off[0][r] + t] = bb.r_sharp[rb * kSharpPerRing + t];
+    for (int t = threadIdx.x; t < cnt[r * 4 + 1]; t += blockDim.x)
+      bb.f_lsharp[(size_t)b * c.N * kLessSharpPerRing + off[1][r] + t] = bb.r_lsharp[rb * kLessSharpPerRing + t];
+    for (int t = threadIdx.x; t < cnt[r * 4 + 2]; t += blockDim.x)
+      bb.f_flat[(size_t)b * c.N * kFlatPerRing + off[2][r] + t] = bb.r_flat[rb * kFlatPerRing + t];
+    for (int t = threadIdx.x; t < cnt[r * 4 + 3]; t += blockDim.x)
+      bb.f_lflat[(size_t)b * c.P + off[3][r] + t] = bb.r_lflat[(size_t)b * c.P + (size_t)r * c.H + t];
+  }
+}
+
+void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, FaCarry* d_carry, hipStream_t s,
+               StageTimer* tm) {
+  tm->mark("fa.deskew", s);
+  hipMemsetAsync(bb.firsthalf, 0x7f, sizeof(int) * B, s);
+  hipMemsetAsync(bb.fa_flags, 0, sizeof(int) * B, s);
+  dim3 gpts((c.P + 255) / 256, B);
+  k_fa_half<<<gpts, 256, 0, s>>>(bb, c);
+  k_fa_point<<<gpts, 256, 0, s>>>(bb, c);
+  tm->mark("fa.extract", s);
+  const size_t lds = extract_lds_bytes(c.H);
+  k_extract<<<dim3(c.N, B), kExtractThreads, lds, s>>>(bb, c);
+  tm->mark("fa.fixup", s);
+  k_fa_fixup<<<1, kExtractThreads, lds, s>>>(bb, c, B, d_carry);
+  tm->mark("fa.compact", s);
+  k_fa_compact<<<B, 256, 0, s>>>(bb, c);
+}
+
+}  // namespace lego

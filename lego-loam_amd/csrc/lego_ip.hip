@@ -1,0 +1,313 @@
+// lego_ip.hip — imageProjection hot path on gfx950.
+//
+//   k_project   1 lane / input point: ring -> row, atan2f -> column, range;
+//               last-writer-wins through atomicMax on the point index
+//               (imageProjection.cpp:219-256)
+//   k_pixels    1 lane / pixel: rangeMat + fullCloud (:248-255)
+//   k_ground    1 lane / column: the sequential ground-pair walk (:267-301)
+//   k_ccl_*     BFS segmentation as connected components (:312-317, 370-460):
+//               symmetric edge predicate -> union-find with CAS on roots; the
+//               root is the component's minimum raster index = the BFS seed
+//   k_compact   1 workgroup / scan: component validity, label ranking,
+//               row-major compaction into segmented cloud + cloud_info,
+//               outlier cloud (:319-355)
+//
+// All float expressions mirror the reference's mixed float/double evaluation
+// (SURVEY.md §9.2); compiled with -ffp-contract=off.
+#include <cfloat>
+
+#include "lego_device.h"
+#include "lego_kernels.h"
+#include "lego_loam.h"
+
+namespace lego {
+
+__global__ void k_project(BatchBufs bb, DevCfg c) {
+  const int b = blockIdx.y;
+  const int n = scan_npts(bb, b);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const lego_point_xyzir* pp = (const lego_point_xyzir*)bb.pts + bb.off[b] + i;
+  const float4 xyz = *(const float4*)pp;
+  const uint16_t ring = pp->ring;
+  const float x = xyz.x, y = xyz.y, z = xyz.z;
+  if (i == 0) bb.rawang[2 * b] = -lego_atan2f(y, x);                   // :201
+  if (i == n - 1) bb.rawang[2 * b + 1] = -lego_atan2f(y, x);           // :202
+  const int row = ring;
+  if (row >= c.N) return;
+  const float h = (float)((double)(lego_atan2f(x, y) * 180.0f) / M_PI);  // :235
+  const double cd = -round(((double)h - 90.0) / (double)c.ang_res_x) + (double)(c.H / 2);
+  if (cd < 0) return;
+  long col = (long)cd;
+  if (col >= c.H) col -= c.H;
+  if (col >= c.H) return;
+  const float range = __builtin_sqrtf(x * x + y * y + z * z);          // :244
+  if (range < c.min_range) return;
+  atomicMax(&bb.owner[(size_t)b * c.P + row * c.H + col], i);
+}
+
+__global__ void k_pixels(BatchBufs bb, DevCfg c) {
+  const int b = blockIdx.y;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= c.P) return;
+  const size_t gp = (size_t)b * c.P + p;
+  const int o = bb.owner[gp];
+  if (o < 0) {
+    bb.range[gp] = FLT_MAX;
+    const float qn = __builtin_nanf("");
+    bb.full[gp] = make_float4(qn, qn, qn, -1.0f);
+    return;
+  }
+  const int row = p / c.H, col = p - row * c.H;
+  const float4 xyz = *(const float4*)((const lego_point_xyzir*)bb.pts + bb.off[b] + o);
+  const float range = __builtin_sqrtf(xyz.x * xyz.x + xyz.y * xyz.y + xyz.z * xyz.z);
+  const float inten = (float)((double)(float)row + (double)(float)col / 10000.0);  // :250
+  bb.range[gp] = range;
+  bb.full[gp] = make_float4(xyz.x, xyz.y, xyz.z, inten);
+}
+
+// groundMat column walk.  Carry form of the overwrite semantics:
+// G[i] is final once pair (i, i+1) has been examined.
+__global__ void k_ground(BatchBufs bb, DevCfg c) {
+  const int b = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= c.H) return;
+  const size_t base = (size_t)b * c.P;
+  int cur = 0;  // value G[i] holds before pair i is examined
+  for (int i = 0; i < c.N; ++i) {
+    int G;
+    int next = 0;
+    if (i < c.g) {
+      const float4 lo = bb.full[base + i * c.H + j];
+      const float4 up = bb.full[base + (i + 1) * c.H + j];
+      if (lo.w == -1.0f || up.w == -1.0f) {
+        G = -1;
+      } else {
+        const float dX = up.x - lo.x, dY = up.y - lo.y, dZ = up.z - lo.z;
+        const float angle =
+            (float)((double)(lego_atan2f(dZ, __builtin_sqrtf(dX * dX + dY * dY)) * 180.0f) / M_PI);
+        if (lfabsf(angle - c.mount_angle) <= 10) {
+          G = 1;
+          next = 1;
+        } else {
+          G = cur;
+        }
+      }
+    } else {
+      G = cur;
+    }
+    cur = next;
+    const size_t gp = base + i * c.H + j;
+    bb.ground[gp] = (int8_t)G;
+    bb.label[gp] = (G == 1 || bb.range[gp] == FLT_MAX) ? -1 : 0;     // :295-301
+  }
+}
+
+__device__ __forceinline__ bool seg_edge(float ra, float rb, float sa, float ca, float theta) {
+  const float d1 = (ra < rb) ? rb : ra;  // std::max
+  const float d2 = (rb < ra) ? rb : ra;  // std::min
+  return lego_atan2f(d2 * sa, (d1 - d2 * ca)) > theta;                 // :421-423
+}
+
+__global__ void k_ccl_init(BatchBufs bb, DevCfg c) {
+  const int b = blockIdx.y;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= c.P) return;
+  const size_t base = (size_t)b * c.P;
+  const int L = bb.label[base + p];
+  bb.parent[base + p] = (L == 0) ? p : -1;
+  uint8_t e = 0;
+  if (L == 0) {
+    const int row = p / c.H, col = p - row * c.H;
+    const float r = bb.range[base + p];
+    const int qr = row * c.H + (col + 1 == c.H ? 0 : col + 1);        // column wrap :403-406
+    if (bb.label[base + qr] == 0 && seg_edge(r, bb.range[base + qr], c.sinAX, c.cosAX, c.theta)) e |= 1;
+    if (row + 1 < c.N) {
+      const int qd = p + c.H;
+      if (bb.label[base + qd] == 0 && seg_edge(r, bb.range[base + qd], c.sinAY, c.cosAY, c.theta)) e |= 2;
+    }
+  }
+  bb.edges[base + p] = e;
+}
+
+__device__ __forceinline__ int uf_load(int* a) {
+  return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int uf_find(int* par, int x) {
+  while (true) {
+    const int p = uf_load(&par[x]);
+    if (p == x) return x;
+    x = p;
+  }
+}
+__device__ __forceinline__ void uf_unite(int* par, int a, int b) {
+  while (true) {
+    a = uf_find(par, a);
+    b = uf_find(par, b);
+    if (a == b) return;
+    if (a < b) { const int t = a; a = b; b = t; }  // link the larger root under the smaller
+    const int old = atomicCAS(&par[a], a, b);
+    if (old == a) return;
+  }
+}
+
+__global__ void k_ccl_union(BatchBufs bb, DevCfg c) {
+  const int b = blockIdx.y;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= c.P) return;
+  const size_t base = (size_t)b * c.P;
+  const uint8_t e = bb.edges[base + p];
+  if (!e) return;
+  int* par = bb.parent + base;
+  const int row = p / c.H, col = p - row * c.H;
+  if (e & 1) uf_unite(par, p, row * c.H + (col + 1 == c.H ? 0 : col + 1));
+  if (e & 2) uf_unite(par, p, p + c.H);
+}
+
+__global__ void k_ccl_root(BatchBufs bb, DevCfg c) {
+  const int b = blockIdx.y;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= c.P) return;
+  const size_t base = (size_t)b * c.P;
+  if (bb.parent[base + p] < 0) return;
+  const int r = uf_find(bb.parent + base, p);
+  bb.root[base + p] = r;
+  atomicAdd(&bb.csize[base + r], 1);
+  if (r != p) {  // lineCountFlag is set only for pushed (non-seed) pixels (:431)
+    const int row = p / c.H;
+    atomicOr(&bb.rowmask[(base + r) * 2 + (row >> 6)], 1ull << (row & 63));
+  }
+}
+
+// Block-wide exclusive scan of up to 3 counters for 1024-thread blocks.
+struct Scan3 {
+  int v[3];
+};
+__device__ __forceinline__ Scan3 block_scan3(Scan3 in, Scan3* total, int* lds /*3*16+3*/) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  Scan3 out;
+  for (int k = 0; k < 3; ++k) {
+    // inclusive wave scan
+    int x = in.v[k];
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) lds[k * 16 + wave] = x;
+    out.v[k] = x - in.v[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    int s = 0;
+    for (int w = 0; w < nw; ++w) {
+      const int t = lds[threadIdx.x * 16 + w];
+      lds[threadIdx.x * 16 + w] = s;
+      s += t;
+    }
+    lds[48 + threadIdx.x] = s;
+  }
+  __syncthreads();
+  for (int k = 0; k < 3; ++k) {
+    out.v[k] += lds[k * 16 + wave];
+    total->v[k] = lds[48 + k];
+  }
+  __syncthreads();
+  return out;
+}
+
+__global__ void __launch_bounds__(1024) k_compact(BatchBufs bb, DevCfg c, int want_labels) {
+  __shared__ int lds[64];
+  const int b = blockIdx.x;
+  const size_t base = (size_t)b * c.P;
+  int segc = 0, outc = 0, labc = 0;
+  for (int t0 = 0; t0 < c.P; t0 += blockDim.x) {
+    const int p = t0 + threadIdx.x;
+    bool keep = false, outl = false, vroot = false, inseg = false, valid = false;
+    int r = -1;
+    int row = 0, col = 0;
+    if (p < c.P) {
+      row = p / c.H;
+      col = p - row * c.H;
+      const int L0 = bb.label[base + p];
+      const int8_t G = bb.ground[base + p];
+      if (L0 == 0) {
+        inseg = true;
+        r = bb.root[base + p];
+        const int sz = bb.csize[base + r];
+        const unsigned long long* rm = &bb.rowmask[(base + r) * 2];
+        const int lines = __popcll(rm[0]) + __popcll(rm[1]);
+        valid = sz >= 30 || (sz >= c.valid_pt && lines >= c.valid_line);  // :441-451
+        vroot = valid && r == p;
+        keep = valid;
+        outl = !valid && row > c.g && col % 5 == 0;                      // :328-334
+      } else if (G == 1) {
+        keep = !(col % 5 != 0 && col > 5 && col < c.H - 5);              // :337-340
+      }
+    }
+    Scan3 in{{keep ? 1 : 0, outl ? 1 : 0, vroot ? 1 : 0}}, tot;
+    Scan3 ex = block_scan3(in, &tot, lds);
+    if (p < c.P) {
+      if (col == 0) {  // ring boundaries (:323, :354)
+        bb.sri[b * c.N + row] = segc + ex.v[0] - 1 + 5;
+        if (row > 0) bb.eri[b * c.N + row - 1] = segc + ex.v[0] - 1 - 5;
+      }
+      if (vroot) bb.root[base + p] = -(labc + ex.v[2] + 1);  // label of a valid root, stored negated
+    }
+    __syncthreads();
+    if (p < c.P) {
+      if (want_labels && inseg) {
+        const int lr = valid ? -bb.root[base + r] : 999999;
+        bb.label[base + p] = lr;  // the final labelMat (root array holds -label at roots)
+      }
+      if (keep) {
+        const int pos = segc + ex.v[0];
+        bb.seg[base + pos] = bb.full[base + p];
+        bb.gflag[base + pos] = (bb.ground[base + p] == 1) ? 1 : 0;
+        bb.col[base + pos] = (uint32_t)col;
+        bb.srange[base + pos] = bb.range[base + p];
+      }
+      if (outl) bb.outl[base + outc + ex.v[1]] = bb.full[base + p];
+    }
+    segc += tot.v[0];
+    outc += tot.v[1];
+    labc += tot.v[2];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    bb.ns[b] = segc;
+    bb.nout[b] = outc;
+    bb.eri[b * c.N + c.N - 1] = segc - 1 - 5;
+    // findStartEndAngle :199-209
+    const float so = bb.rawang[2 * b];
+    float eo = (float)((double)bb.rawang[2 * b + 1] + 2 * M_PI);
+    if ((double)(eo - so) > 3 * M_PI) eo = (float)((double)eo - 2 * M_PI);
+    else if ((double)(eo - so) < M_PI) eo = (float)((double)eo + 2 * M_PI);
+    bb.orient[3 * b] = so;
+    bb.orient[3 * b + 1] = eo;
+    bb.orient[3 * b + 2] = eo - so;
+  }
+}
+
+void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hipStream_t s,
+               StageTimer* tm) {
+  const int P = c.P;
+  tm->mark("ip.memset", s);
+  hipMemsetAsync(bb.owner, 0xff, sizeof(int) * (size_t)B * P, s);
+  hipMemsetAsync(bb.csize, 0, sizeof(int) * (size_t)B * P, s);
+  hipMemsetAsync(bb.rowmask, 0, sizeof(unsigned long long) * 2 * (size_t)B * P, s);
+  tm->mark("ip.project", s);
+  dim3 gpts((bb.Nmax + 255) / 256, B), gpix((P + 255) / 256, B), gcol((c.H + 255) / 256, B);
+  k_project<<<gpts, 256, 0, s>>>(bb, c);
+  tm->mark("ip.pixels", s);
+  k_pixels<<<gpix, 256, 0, s>>>(bb, c);
+  tm->mark("ip.ground", s);
+  k_ground<<<gcol, 256, 0, s>>>(bb, c);
+  tm->mark("ip.ccl", s);
+  k_ccl_init<<<gpix, 256, 0, s>>>(bb, c);
+  k_ccl_union<<<gpix, 256, 0, s>>>(bb, c);
+  k_ccl_root<<<gpix, 256, 0, s>>>(bb, c);
+  tm->mark("ip.compact", s);
+  k_compact<<<B, 1024, 0, s>>>(bb, c, want_labels);
+}
+
+}  // namespace lego

@@ -1,0 +1,393 @@
+"""ctypes bindings for the lego C-ABI (include/lego_loam.h, include/lego_synth.h).
+
+This is the Python face of the drop-in boundary: the same struct layouts a
+ROS adapter would bind, used by tests/ and bench.py.
+
+Libraries (all built in-tree by __graft_entry__.build()):
+  lego-loam_amd/build/liblego_hip.so    product: HIP kernels + C-ABI
+  lego-loam_amd/build/liblego_synth.so  synthetic lidar source
+  oracle/build/liblego_oracle.so        CPU oracle (tests / cpu_baseline only)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+PKG_DIR = Path(__file__).resolve().parent
+REPO = PKG_DIR.parent
+BUILD = PKG_DIR / "build"
+HIP_LIB = BUILD / "liblego_hip.so"
+SYNTH_LIB = BUILD / "liblego_synth.so"
+ORACLE_LIB = REPO / "oracle" / "build" / "liblego_oracle.so"
+
+LEGO_OK, LEGO_E_NOT_DENSE, LEGO_E_CAPACITY, LEGO_E_DEVICE, LEGO_E_ARG, LEGO_E_STATE = range(6)
+LEGO_IP_IMAGES = 1
+
+f32p = C.POINTER(C.c_float)
+
+
+class PointXYZIR(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float), ("_pad0", C.c_float),
+                ("intensity", C.c_float), ("ring", C.c_uint16), ("_pad1", C.c_uint16),
+                ("_pad2", C.c_uint32 * 2)]
+
+
+class PointXYZI(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float), ("intensity", C.c_float)]
+
+
+XYZIR_DTYPE = np.dtype({"names": ["x", "y", "z", "_pad0", "intensity", "ring", "_pad1", "_pad2"],
+                        "formats": ["<f4", "<f4", "<f4", "<f4", "<f4", "<u2", "<u2", ("<u4", 2)],
+                        "offsets": [0, 4, 8, 12, 16, 20, 22, 24], "itemsize": 32})
+XYZI_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("intensity", "<f4")])
+assert C.sizeof(PointXYZIR) == 32 and C.sizeof(PointXYZI) == 16
+
+
+class SensorCfg(C.Structure):
+    _fields_ = [("n_scan", C.c_int32), ("horizon_scan", C.c_int32), ("ang_res_x", C.c_float),
+                ("ang_res_y", C.c_float), ("ang_bottom", C.c_float), ("ground_scan_ind", C.c_int32),
+                ("use_cloud_ring", C.c_int32), ("sensor_minimum_range", C.c_float),
+                ("sensor_mount_angle", C.c_float), ("segment_theta", C.c_float),
+                ("segment_valid_point_num", C.c_int32), ("segment_valid_line_num", C.c_int32),
+                ("segment_alpha_x", C.c_float), ("segment_alpha_y", C.c_float),
+                ("edge_threshold", C.c_float), ("surf_threshold", C.c_float),
+                ("nearest_feature_search_sq_dist", C.c_float), ("scan_period", C.c_float),
+                ("mapping_process_interval", C.c_double),
+                ("surrounding_keyframe_search_radius", C.c_float), ("skip_frame_num", C.c_int32)]
+
+
+class CloudInfo(C.Structure):
+    _fields_ = [("stamp", C.c_double), ("start_ring_index", C.POINTER(C.c_int32)),
+                ("end_ring_index", C.POINTER(C.c_int32)), ("start_orientation", C.c_float),
+                ("end_orientation", C.c_float), ("orientation_diff", C.c_float),
+                ("segmented_cloud_ground_flag", C.POINTER(C.c_uint8)),
+                ("segmented_cloud_col_ind", C.POINTER(C.c_uint32)),
+                ("segmented_cloud_range", f32p)]
+
+
+class IpOut(C.Structure):
+    _fields_ = [("info", CloudInfo), ("segmented_cloud", C.POINTER(PointXYZI)),
+                ("n_segmented", C.c_int32), ("outlier_cloud", C.POINTER(PointXYZI)),
+                ("n_outlier", C.c_int32), ("full_cloud", C.POINTER(PointXYZI)),
+                ("range_image", f32p), ("ground_image", C.POINTER(C.c_int8)),
+                ("label_image", C.POINTER(C.c_int32))]
+
+
+class FaOut(C.Structure):
+    _fields_ = [("stamp", C.c_double),
+                ("sharp", C.POINTER(PointXYZI)), ("n_sharp", C.c_int32),
+                ("less_sharp", C.POINTER(PointXYZI)), ("n_less_sharp", C.c_int32),
+                ("flat", C.POINTER(PointXYZI)), ("n_flat", C.c_int32),
+                ("less_flat", C.POINTER(PointXYZI)), ("n_less_flat", C.c_int32),
+                ("odom_valid", C.c_int32), ("transform_cur", C.c_float * 6),
+                ("transform_sum", C.c_float * 6), ("odom_quat", C.c_double * 4),
+                ("odom_pos", C.c_double * 3), ("publish_to_mapping", C.c_int32),
+                ("corner_last", C.POINTER(PointXYZI)), ("n_corner_last", C.c_int32),
+                ("surf_last", C.POINTER(PointXYZI)), ("n_surf_last", C.c_int32),
+                ("outlier_last", C.POINTER(PointXYZI)), ("n_outlier_last", C.c_int32)]
+
+
+class MoOut(C.Structure):
+    _fields_ = [("processed", C.c_int32), ("optimized", C.c_int32), ("iterations", C.c_int32),
+                ("transform_tobe_mapped", C.c_float * 6), ("transform_aft_mapped", C.c_float * 6),
+                ("transform_bef_mapped", C.c_float * 6), ("n_corner_map_ds", C.c_int32),
+                ("n_surf_map_ds", C.c_int32), ("n_corner_scan_ds", C.c_int32),
+                ("n_surf_scan_ds", C.c_int32), ("n_rows_last", C.c_int32)]
+
+
+class PoseRec(C.Structure):
+    _fields_ = [("stamp", C.c_double), ("transform_sum", C.c_float * 6),
+                ("n_segmented", C.c_int32), ("n_sharp", C.c_int32), ("n_less_sharp", C.c_int32),
+                ("n_flat", C.c_int32), ("n_less_flat", C.c_int32), ("odom_valid", C.c_int32),
+                ("flags", C.c_int32), ("_pad", C.c_int32)]
+
+
+assert C.sizeof(PoseRec) == 64
+
+
+class SynthCfg(C.Structure):
+    _fields_ = [("n_scan", C.c_int32), ("horizon_scan", C.c_int32), ("vert_min_deg", C.c_float),
+                ("vert_max_deg", C.c_float), ("mount_height", C.c_float),
+                ("ground_tilt_deg", C.c_float), ("noise_sigma", C.c_float),
+                ("dropout", C.c_float), ("max_range", C.c_float), ("dup_frac", C.c_float),
+                ("azimuth_jitter", C.c_float), ("speed_mps", C.c_float),
+                ("yaw_rate_dps", C.c_float), ("scan_period", C.c_float), ("n_boxes", C.c_int32),
+                ("n_cylinders", C.c_int32), ("n_walls", C.c_int32), ("seed", C.c_uint64)]
+
+
+# ------------------------------------------------------------------ loading
+_libs: dict[str, C.CDLL] = {}
+
+
+def _load(path: Path, key: str) -> C.CDLL:
+    if key not in _libs:
+        if not path.exists():
+            raise RuntimeError(f"{path} is not built; run __graft_entry__.build()")
+        _libs[key] = C.CDLL(str(path))
+    return _libs[key]
+
+
+def synth_lib() -> C.CDLL:
+    lib = _load(SYNTH_LIB, "synth")
+    lib.lego_synth_preset.argtypes = [C.c_char_p, C.c_uint64, C.POINTER(SynthCfg)]
+    lib.lego_synth_max_points.argtypes = [C.POINTER(SynthCfg)]
+    lib.lego_synth_max_points.restype = C.c_int32
+    lib.lego_synth_scan.argtypes = [C.POINTER(SynthCfg), C.c_int32, C.c_void_p, C.c_int32,
+                                    C.POINTER(C.c_int32), C.POINTER(C.c_double)]
+    lib.lego_synth_map.argtypes = [C.c_uint64, C.c_float, C.c_int32, C.c_int32, C.c_void_p,
+                                   C.c_void_p]
+    return lib
+
+
+def oracle_lib() -> C.CDLL:
+    """TEST INFRASTRUCTURE: the CPU oracle.  Only tests/, smoke() and bench's
+    cpu_baseline leg may call this."""
+    lib = _load(ORACLE_LIB, "oracle")
+    lib.lego_oracle_sensor_preset.argtypes = [C.c_char_p, C.POINTER(SensorCfg)]
+    lib.lego_oracle_create.argtypes = [C.POINTER(SensorCfg), C.POINTER(C.c_void_p)]
+    lib.lego_oracle_destroy.argtypes = [C.c_void_p]
+    lib.lego_oracle_set_options.argtypes = [C.c_void_p, C.c_uint32]
+    lib.lego_oracle_ip_process.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_double,
+                                           C.c_uint32, C.POINTER(IpOut)]
+    lib.lego_oracle_fa_process.argtypes = [C.c_void_p, C.POINTER(IpOut), C.POINTER(FaOut)]
+    lib.lego_oracle_mo_set_map.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32]
+    lib.lego_oracle_mo_process.argtypes = [C.c_void_p, C.POINTER(FaOut), C.POINTER(MoOut)]
+    lib.lego_oracle_voxel_grid.argtypes = [C.c_void_p, C.c_int32, C.c_float, C.c_int32,
+                                           C.c_void_p, C.POINTER(C.c_int32)]
+    for fn in ("atan2f",):
+        getattr(lib, "lego_oracle_" + fn).argtypes = [C.c_float, C.c_float]
+        getattr(lib, "lego_oracle_" + fn).restype = C.c_float
+    for fn in ("sinf", "cosf", "asinf"):
+        getattr(lib, "lego_oracle_" + fn).argtypes = [C.c_float]
+        getattr(lib, "lego_oracle_" + fn).restype = C.c_float
+    return lib
+
+
+HIP_EXPORTS = ["lego_sensor_preset", "lego_create", "lego_destroy", "lego_reset",
+               "lego_ip_process", "lego_fa_process", "lego_odom_batch", "lego_batch_fetch",
+               "lego_mo_set_map", "lego_mo_process", "lego_last_error", "lego_stage_times"]
+
+
+def hip_lib() -> C.CDLL:
+    """The product library.  Loading never falls back to anything else."""
+    lib = _load(HIP_LIB, "hip")
+    lib.lego_sensor_preset.argtypes = [C.c_char_p, C.POINTER(SensorCfg)]
+    lib.lego_create.argtypes = [C.POINTER(SensorCfg), C.c_int, C.c_int32, C.c_int32,
+                                C.POINTER(C.c_void_p)]
+    lib.lego_destroy.argtypes = [C.c_void_p]
+    lib.lego_reset.argtypes = [C.c_void_p]
+    lib.lego_ip_process.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_double, C.c_uint32,
+                                    C.POINTER(IpOut)]
+    lib.lego_fa_process.argtypes = [C.c_void_p, C.POINTER(IpOut), C.POINTER(FaOut)]
+    lib.lego_odom_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
+                                    C.c_int32, C.c_void_p]
+    lib.lego_batch_fetch.argtypes = [C.c_void_p, C.c_int32, C.POINTER(IpOut), C.POINTER(FaOut)]
+    lib.lego_mo_set_map.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32]
+    lib.lego_mo_process.argtypes = [C.c_void_p, C.POINTER(FaOut), C.POINTER(MoOut)]
+    lib.lego_last_error.restype = C.c_char_p
+    lib.lego_stage_times.argtypes = [C.c_void_p, C.POINTER(C.c_char_p), f32p, C.c_int32,
+                                     C.POINTER(C.c_int32)]
+    return lib
+
+
+def check(st: int, what: str, lib: C.CDLL | None = None) -> None:
+    if st != LEGO_OK:
+        msg = ""
+        if lib is not None and hasattr(lib, "lego_last_error"):
+            try:
+                msg = (lib.lego_last_error() or b"").decode()
+            except Exception:  # noqa: BLE001
+                msg = ""
+        raise RuntimeError(f"{what} failed with status {st} {msg}")
+
+
+# ------------------------------------------------------------------ helpers
+def synth_cfg(name: str = "VLP-16", seed: int = 0, **over) -> SynthCfg:
+    lib = synth_lib()
+    cfg = SynthCfg()
+    check(lib.lego_synth_preset(name.encode(), seed, C.byref(cfg)), "synth_preset")
+    for k, v in over.items():
+        setattr(cfg, k, v)
+    return cfg
+
+
+def synth_scan(cfg: SynthCfg, k: int) -> tuple[np.ndarray, float]:
+    lib = synth_lib()
+    cap = lib.lego_synth_max_points(C.byref(cfg))
+    buf = np.zeros(cap, dtype=XYZIR_DTYPE)
+    n = C.c_int32()
+    st = C.c_double()
+    check(lib.lego_synth_scan(C.byref(cfg), k, buf.ctypes.data, cap, C.byref(n), C.byref(st)),
+          "synth_scan")
+    return buf[: n.value].copy(), st.value
+
+
+def synth_map(seed: int, radius: float, n_surf: int, n_corner: int):
+    lib = synth_lib()
+    surf = np.zeros(n_surf, dtype=XYZI_DTYPE)
+    corner = np.zeros(n_corner, dtype=XYZI_DTYPE)
+    check(lib.lego_synth_map(seed, radius, n_surf, n_corner, surf.ctypes.data, corner.ctypes.data),
+          "synth_map")
+    return surf, corner
+
+
+def sensor_cfg(name: str = "VLP-16", lib: C.CDLL | None = None) -> SensorCfg:
+    lib = lib or oracle_lib()
+    cfg = SensorCfg()
+    fn = lib.lego_sensor_preset if hasattr(lib, "lego_sensor_preset") else lib.lego_oracle_sensor_preset
+    check(fn(name.encode(), C.byref(cfg)), "sensor_preset")
+    return cfg
+
+
+def _arr(ptr, n, dtype):
+    if n <= 0 or not ptr:
+        return np.zeros(0, dtype=dtype)
+    return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint8)), shape=(n * np.dtype(dtype).itemsize,)).view(dtype).copy()
+
+
+def ip_to_dict(o: IpOut, cfg: SensorCfg, images: bool = False) -> dict:
+    P = cfg.n_scan * cfg.horizon_scan
+    ns = o.n_segmented
+    d = {
+        "start_orientation": o.info.start_orientation,
+        "end_orientation": o.info.end_orientation,
+        "orientation_diff": o.info.orientation_diff,
+        "start_ring_index": _arr(o.info.start_ring_index, cfg.n_scan, np.int32),
+        "end_ring_index": _arr(o.info.end_ring_index, cfg.n_scan, np.int32),
+        "ground_flag": _arr(o.info.segmented_cloud_ground_flag, ns, np.uint8),
+        "col_ind": _arr(o.info.segmented_cloud_col_ind, ns, np.uint32),
+        "range": _arr(o.info.segmented_cloud_range, ns, np.float32),
+        "segmented": _arr(o.segmented_cloud, ns, XYZI_DTYPE),
+        "outlier": _arr(o.outlier_cloud, o.n_outlier, XYZI_DTYPE),
+    }
+    if images:
+        d["range_image"] = _arr(o.range_image, P, np.float32)
+        d["ground_image"] = _arr(o.ground_image, P, np.int8)
+        d["label_image"] = _arr(o.label_image, P, np.int32)
+        d["full_cloud"] = _arr(o.full_cloud, P, XYZI_DTYPE)
+    return d
+
+
+def fa_to_dict(o: FaOut) -> dict:
+    return {
+        "sharp": _arr(o.sharp, o.n_sharp, XYZI_DTYPE),
+        "less_sharp": _arr(o.less_sharp, o.n_less_sharp, XYZI_DTYPE),
+        "flat": _arr(o.flat, o.n_flat, XYZI_DTYPE),
+        "less_flat": _arr(o.less_flat, o.n_less_flat, XYZI_DTYPE),
+        "odom_valid": o.odom_valid,
+        "transform_cur": np.array(list(o.transform_cur), dtype=np.float32),
+        "transform_sum": np.array(list(o.transform_sum), dtype=np.float32),
+        "odom_quat": np.array(list(o.odom_quat)),
+        "odom_pos": np.array(list(o.odom_pos)),
+        "publish_to_mapping": o.publish_to_mapping,
+        "corner_last": _arr(o.corner_last, o.n_corner_last, XYZI_DTYPE),
+        "surf_last": _arr(o.surf_last, o.n_surf_last, XYZI_DTYPE),
+        "outlier_last": _arr(o.outlier_last, o.n_outlier_last, XYZI_DTYPE),
+    }
+
+
+class Oracle:
+    """TEST INFRASTRUCTURE: stateful oracle pipeline (one stream)."""
+
+    def __init__(self, cfg: SensorCfg, pcl_sort: bool = False):
+        self.lib = oracle_lib()
+        self.cfg = cfg
+        self.h = C.c_void_p()
+        check(self.lib.lego_oracle_create(C.byref(cfg), C.byref(self.h)), "oracle_create")
+        if pcl_sort:
+            self.lib.lego_oracle_set_options(self.h, 1)
+        self._ip = IpOut()
+        self._fa = FaOut()
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.lib.lego_oracle_destroy(self.h)
+            self.h = None
+
+    def ip(self, pts: np.ndarray, stamp: float, images: bool = False) -> dict:
+        pts = np.ascontiguousarray(pts, dtype=XYZIR_DTYPE)
+        check(self.lib.lego_oracle_ip_process(self.h, pts.ctypes.data, len(pts), stamp,
+                                              LEGO_IP_IMAGES if images else 0, C.byref(self._ip)),
+              "oracle_ip")
+        return ip_to_dict(self._ip, self.cfg, images)
+
+    def fa(self) -> dict:
+        check(self.lib.lego_oracle_fa_process(self.h, C.byref(self._ip), C.byref(self._fa)),
+              "oracle_fa")
+        return fa_to_dict(self._fa)
+
+    def mo_set_map(self, corner: np.ndarray, surf: np.ndarray) -> None:
+        check(self.lib.lego_oracle_mo_set_map(self.h, corner.ctypes.data, len(corner),
+                                              surf.ctypes.data, len(surf)), "oracle_mo_set_map")
+
+    def mo(self) -> dict:
+        out = MoOut()
+        check(self.lib.lego_oracle_mo_process(self.h, C.byref(self._fa), C.byref(out)), "oracle_mo")
+        return {k: (np.array(list(getattr(out, k)), dtype=np.float32)
+                    if k.startswith("transform") else getattr(out, k)) for k, _ in MoOut._fields_}
+
+
+class Lego:
+    """The product pipeline (HIP) behind the C-ABI, one stream per context."""
+
+    def __init__(self, cfg: SensorCfg, device: int = 0, max_points: int = 300000,
+                 max_batch: int = 1):
+        self.lib = hip_lib()
+        self.cfg = cfg
+        self.h = C.c_void_p()
+        check(self.lib.lego_create(C.byref(cfg), device, max_points, max_batch, C.byref(self.h)),
+              "lego_create", self.lib)
+        self._ip = IpOut()
+        self._fa = FaOut()
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.lego_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def reset(self):
+        check(self.lib.lego_reset(self.h), "lego_reset", self.lib)
+
+    def ip(self, pts: np.ndarray, stamp: float, images: bool = False) -> dict:
+        pts = np.ascontiguousarray(pts, dtype=XYZIR_DTYPE)
+        check(self.lib.lego_ip_process(self.h, pts.ctypes.data, len(pts), stamp,
+                                       LEGO_IP_IMAGES if images else 0, C.byref(self._ip)),
+              "lego_ip_process", self.lib)
+        return ip_to_dict(self._ip, self.cfg, images)
+
+    def fa(self) -> dict:
+        check(self.lib.lego_fa_process(self.h, C.byref(self._ip), C.byref(self._fa)),
+              "lego_fa_process", self.lib)
+        return fa_to_dict(self._fa)
+
+    def odom_batch(self, pts: np.ndarray, offsets: np.ndarray, stamps: np.ndarray) -> np.ndarray:
+        pts = np.ascontiguousarray(pts, dtype=XYZIR_DTYPE)
+        offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        stamps = np.ascontiguousarray(stamps, dtype=np.float64)
+        k = len(offsets) - 1
+        recs = (PoseRec * k)()
+        check(self.lib.lego_odom_batch(self.h, pts.ctypes.data, offsets.ctypes.data,
+                                       stamps.ctypes.data, k, 0, recs), "lego_odom_batch", self.lib)
+        return recs
+
+    def odom_batch_device(self, pts_ptr: int, offsets_ptr: int, stamps: np.ndarray, k: int, recs):
+        check(self.lib.lego_odom_batch(self.h, C.c_void_p(pts_ptr), C.c_void_p(offsets_ptr),
+                                       stamps.ctypes.data, k, 1, recs), "lego_odom_batch", self.lib)
+
+    def batch_fetch(self, k: int, images: bool = False) -> tuple[dict, dict]:
+        check(self.lib.lego_batch_fetch(self.h, k, C.byref(self._ip), C.byref(self._fa)),
+              "lego_batch_fetch", self.lib)
+        return ip_to_dict(self._ip, self.cfg, images), fa_to_dict(self._fa)
+
+    def stage_times(self) -> dict:
+        names = (C.c_char_p * 64)()
+        ms = (C.c_float * 64)()
+        n = C.c_int32()
+        check(self.lib.lego_stage_times(self.h, names, ms, 64, C.byref(n)), "stage_times", self.lib)
+        return {names[i].decode(): ms[i] for i in range(n.value)}

@@ -1,0 +1,43 @@
+// lego_oracle.h — TEST INFRASTRUCTURE ONLY.  CPU restatement of the reference
+// hot path, used as the parity checker by tests/, __graft_entry__.smoke() and
+// bench.py's cpu_baseline leg.  Never linked into the product.
+//
+// PARITY STATUS: "parity unpinned" against the reference binary — the
+// reference cannot be built here (needs ROS, PCL, OpenCV, GTSAM; SURVEY.md
+// §8c) and ships no tests or golden vectors.  What IS pinned:
+// the libm shim it uses (bit-exact vs this host's glibc, tests/test_numerics_shim.py),
+// libstdc++ std::sort (called directly, the same library the reference links),
+// and hand-derived known-answer tests (tests/test_oracle_kat.py).
+#pragma once
+#include "lego_loam.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct lego_oracle lego_oracle;
+
+int lego_oracle_sensor_preset(const char* name, lego_sensor_cfg* out);
+int lego_oracle_create(const lego_sensor_cfg* cfg, lego_oracle** out);
+int lego_oracle_destroy(lego_oracle* o);
+/* Options: bit 0 = PCL VoxelGrid in-voxel order via std::sort (unstable, the
+ * exact reference behaviour) instead of input order (the product's order). */
+int lego_oracle_set_options(lego_oracle* o, uint32_t opts);
+int lego_oracle_ip_process(lego_oracle* o, const lego_point_xyzir* pts, int32_t n,
+                           double stamp, uint32_t flags, lego_ip_out* out);
+int lego_oracle_fa_process(lego_oracle* o, const lego_ip_out* in, lego_fa_out* out);
+int lego_oracle_mo_set_map(lego_oracle* o, const lego_point_xyzi* corner, int32_t n_corner,
+                           const lego_point_xyzi* surf, int32_t n_surf);
+int lego_oracle_mo_process(lego_oracle* o, const lego_fa_out* in, lego_mo_out* out);
+
+/* Stand-alone pieces for known-answer tests. */
+int lego_oracle_voxel_grid(const lego_point_xyzi* in, int32_t n, float leaf,
+                           int32_t pcl_sort, lego_point_xyzi* out, int32_t* n_out);
+float lego_oracle_atan2f(float y, float x);
+float lego_oracle_sinf(float x);
+float lego_oracle_cosf(float x);
+float lego_oracle_asinf(float x);
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,126 @@
+"""GPU parity: the HIP path through the C-ABI vs the CPU oracle on the same
+seeded synthetic scans.  Bit-exact for images, labels, the segmented cloud,
+cloud_info and feature clouds; poses within the north-star tolerance 1e-4."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+POSE_TOL = 1e-4  # BASELINE.json north_star: "within 1e-4 on the 6-DoF pose"
+
+
+def bits(a):
+    return np.ascontiguousarray(a).view(np.uint8)
+
+
+def assert_ip_equal(g, o, images=True):
+    for k in ("start_orientation", "end_orientation", "orientation_diff"):
+        assert np.float32(g[k]).tobytes() == np.float32(o[k]).tobytes(), k
+    for k in ("start_ring_index", "end_ring_index", "ground_flag", "col_ind", "range",
+              "segmented", "outlier"):
+        assert g[k].shape == o[k].shape, (k, g[k].shape, o[k].shape)
+        assert np.array_equal(bits(g[k]), bits(o[k])), k
+    if images:
+        for k in ("range_image", "ground_image", "label_image", "full_cloud"):
+            assert np.array_equal(bits(g[k]), bits(o[k])), k
+
+
+def assert_feat_equal(g, o):
+    for k in ("sharp", "less_sharp", "flat", "less_flat"):
+        assert g[k].shape == o[k].shape, (k, g[k].shape, o[k].shape)
+        assert np.array_equal(bits(g[k]), bits(o[k])), k
+
+
+@pytest.mark.parametrize("sensor,seed,extra", [
+    ("VLP-16", 0, {}), ("VLP-16", 1, {}), ("VLP-16", 2, {"dup_frac": 0.05}),
+    ("HDL-64E", 2, {}), ("VLS-128", 3, {}),
+])
+def test_ip_parity(L, sensor, seed, extra):
+    cfg = L.sensor_cfg(sensor, L.hip_lib())
+    sc = L.synth_cfg(sensor, seed, **extra)
+    pts, stamp = L.synth_scan(sc, 0)
+    gpu = L.Lego(cfg, max_points=len(pts) + 16)
+    ora = L.Oracle(L.sensor_cfg(sensor))
+    assert_ip_equal(gpu.ip(pts, stamp, images=True), ora.ip(pts, stamp, images=True))
+    gpu.close()
+
+
+@pytest.mark.parametrize("sensor,seed,nscans", [("VLP-16", 1, 12), ("HDL-64E", 2, 3)])
+def test_stream_parity_node_api(L, sensor, seed, nscans):
+    """ip -> fa per scan through the node-shaped calls; features bit-exact,
+    poses within tolerance (and reported when bit-exact)."""
+    cfg = L.sensor_cfg(sensor, L.hip_lib())
+    sc = L.synth_cfg(sensor, seed)
+    gpu = L.Lego(cfg, max_points=L.synth_lib().lego_synth_max_points(L.C.byref(sc)))
+    ora = L.Oracle(L.sensor_cfg(sensor))
+    worst = 0.0
+    for k in range(nscans):
+        pts, stamp = L.synth_scan(sc, k)
+        assert_ip_equal(gpu.ip(pts, stamp), ora.ip(pts, stamp), images=False)
+        gf, of = gpu.fa(), ora.fa()
+        assert_feat_equal(gf, of)
+        assert gf["odom_valid"] == of["odom_valid"]
+        assert gf["publish_to_mapping"] == of["publish_to_mapping"]
+        d = float(np.max(np.abs(gf["transform_sum"].astype(np.float64) - of["transform_sum"])))
+        worst = max(worst, d)
+        assert d <= POSE_TOL, (k, gf["transform_sum"], of["transform_sum"])
+        if gf["publish_to_mapping"]:
+            for key in ("corner_last", "surf_last", "outlier_last"):
+                assert np.allclose(gf[key].view(np.float32), of[key].view(np.float32), atol=POSE_TOL)
+    print(f"{sensor}: worst |dpose| = {worst:.3g}")
+    gpu.close()
+
+
+def test_fa_on_oracle_input(L):
+    """GPU feature association fed the ORACLE's cloud_info (host upload path)."""
+    cfg = L.sensor_cfg("VLP-16", L.hip_lib())
+    sc = L.synth_cfg("VLP-16", 4)
+    gpu = L.Lego(cfg, max_points=40000)
+    ora = L.Oracle(L.sensor_cfg("VLP-16"))
+    for k in range(3):
+        pts, stamp = L.synth_scan(sc, k)
+        ora.ip(pts, stamp)
+        # feed the oracle's IpOut straight into the product's lego_fa_process
+        out = L.FaOut()
+        L.check(gpu.lib.lego_fa_process(gpu.h, L.C.byref(ora._ip), L.C.byref(out)), "fa", gpu.lib)
+        assert_feat_equal(L.fa_to_dict(out), ora.fa())
+    gpu.close()
+
+
+def test_batch_equals_node_path(L):
+    """lego_odom_batch over K scans == K node-shaped calls (same stream state)."""
+    cfg = L.sensor_cfg("VLP-16", L.hip_lib())
+    sc = L.synth_cfg("VLP-16", 5)
+    K = 8
+    scans = [L.synth_scan(sc, k) for k in range(K)]
+    pts = np.concatenate([s[0] for s in scans])
+    off = np.zeros(K + 1, np.int64)
+    off[1:] = np.cumsum([len(s[0]) for s in scans])
+    stamps = np.array([s[1] for s in scans])
+    gb = L.Lego(cfg, max_points=40000, max_batch=K)
+    recs = gb.odom_batch(pts, off, stamps)
+    ora = L.Oracle(L.sensor_cfg("VLP-16"))
+    for k in range(K):
+        ora.ip(*scans[k])
+        of = ora.fa()
+        gi, gf = gb.batch_fetch(k)
+        assert_feat_equal(gf, of)
+        r = recs[k]
+        assert r.n_sharp == len(of["sharp"]) and r.n_less_flat == len(of["less_flat"])
+        assert r.odom_valid == of["odom_valid"]
+        d = np.max(np.abs(np.array(list(r.transform_sum), np.float64) - of["transform_sum"]))
+        assert d <= POSE_TOL, (k, list(r.transform_sum), of["transform_sum"])
+    gb.close()
+
+
+def test_not_dense_rejected(L):
+    cfg = L.sensor_cfg("VLP-16", L.hip_lib())
+    sc = L.synth_cfg("VLP-16", 0)
+    pts, stamp = L.synth_scan(sc, 0)
+    pts = pts.copy()
+    pts["x"][10] = np.nan
+    gpu = L.Lego(cfg, max_points=len(pts) + 16)
+    out = L.IpOut()
+    st = gpu.lib.lego_ip_process(gpu.h, pts.ctypes.data, len(pts), stamp, 0, L.C.byref(out))
+    assert st == L.LEGO_E_NOT_DENSE
+    gpu.close()
