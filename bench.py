@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""bench.py — scans/sec of LeGO-LOAM's per-scan hot path on MI355X.
+
+Workload (BASELINE.json configs[1]): one synthetic VLP-16
+(16x1800) stream at 10 Hz — projection + ground + segmentation + features +
+two-step LM odometry for every scan, in stream order.  A "step" is one batch
+of `--batch` consecutive scans of the stream through lego_odom_batch with the
+points already resident in HBM.  With --gpus N each rank runs its own stream
+(seed 10 + rank, config C4) and the 64-B pose records of every step are
+gathered to rank 0 over RCCL (the hand-off to the serial pose graph).
+
+Prints ONE JSON line on rank 0 (contract in the task statement).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import importlib.util
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parent
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def load_ffi():
+    spec = importlib.util.spec_from_file_location("legoffi", REPO / "lego-loam_amd" / "legoffi.py")
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["legoffi"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def make_stream(L, sensor: str, seed: int, nscans: int):
+    sc = L.synth_cfg(sensor, seed)
+    scans = [L.synth_scan(sc, k) for k in range(nscans)]
+    pts = np.concatenate([s[0] for s in scans])
+    off = np.zeros(nscans + 1, np.int64)
+    off[1:] = np.cumsum([len(s[0]) for s in scans])
+    stamps = np.array([s[1] for s in scans], np.float64)
+    maxn = int(max(len(s[0]) for s in scans))
+    return pts, off, stamps, maxn
+
+
+def odom_alg_bytes(recs) -> float:
+    """Algorithmic HBM bytes of k_odom per launch: per scan it
+    reads the four feature clouds (16 B/pt), writes the TransformToEnd'ed
+    less-sharp/less-flat twice (last cloud + per-scan copy) and rebuilds the
+    two LBVHs (read 16 B, write 16 B point + 4 B index per point)."""
+    tot = 0.0
+    for r in recs:
+        f = r.n_sharp + r.n_less_sharp + r.n_flat + r.n_less_flat
+        last = r.n_less_sharp + r.n_less_flat
+        tot += 16 * f + 32 * last + 36 * last
+    return tot
+
+
+def cpu_baseline(L, sensor, seed, nscans, budget_s):
+    """The oracle (C++ restatement, 1 thread) over the same stream, repeated
+    until ~budget_s of CPU work."""
+    cfg = L.sensor_cfg(sensor)
+    sc = L.synth_cfg(sensor, seed)
+    scans = [L.synth_scan(sc, k) for k in range(nscans)]
+    done = 0
+    t0 = time.perf_counter()
+    passes = 0
+    while True:
+        ora = L.Oracle(cfg)
+        for pts, st in scans:
+            ora.ip(pts, st)
+            ora.fa()
+            done += 1
+        passes += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return done / dt, done, passes
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=100, help="scans per step")
+    ap.add_argument("--stream-len", type=int, default=600, help="synthetic stream length (C2: 600)")
+    ap.add_argument("--sensor", default="VLP-16")
+    ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of oracle work")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
+    ap.add_argument("--odom-profile", action="store_true", help="in-kernel phase stamps (diagnostic)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+
+    L = load_ffi()
+    lib = L.hip_lib()
+    cfg = L.sensor_cfg(args.sensor, lib)
+    seed = 1 if world == 1 else 10 + rank
+    pts, off, stamps, maxn = make_stream(L, args.sensor, seed, args.stream_len)
+    B = args.batch
+    nb = args.stream_len // B
+    # inputs resident in HBM before the timed region
+    d_pts = torch.from_numpy(pts.view(np.uint8)).to(dev)
+    d_off = [torch.from_numpy((off[i * B:(i + 1) * B + 1] - 0).astype(np.int64)).to(dev)
+             for i in range(nb)]
+    torch.cuda.synchronize()
+    gpu = L.Lego(cfg, device=local, max_points=maxn + 16, max_batch=B)
+    n_en = C.c_int32()
+    on = (C.c_float * 1)()
+    lib.lego_stage_times(gpu.h, None, on, 0, C.byref(n_en))  # enable the stage timer
+    if args.odom_profile:
+        lib.lego_odom_profile(gpu.h, 1, None)
+    recs = (L.PoseRec * B)()
+
+    def step(i):
+        j = i % nb
+        if j == 0:
+            gpu.reset()  # a new pass over the stream starts from a fresh odometry state
+        gpu.odom_batch_device(d_pts.data_ptr(), d_off[j].data_ptr(), stamps[j * B:(j + 1) * B], B, recs)
+        return gpu.stage_times()
+
+    for i in range(args.warmup):
+        step(i)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    stage_acc: dict[str, float] = {}
+    gathered = None
+    t0 = time.perf_counter()
+    alg_bytes = 0.0
+    for i in range(args.steps):
+        st = step(args.warmup + i)
+        for k, v in st.items():
+            stage_acc[k] = stage_acc.get(k, 0.0) + v
+        alg_bytes += odom_alg_bytes(recs)
+        if dist:
+            rec_t = torch.frombuffer(bytearray(bytes(recs)), dtype=torch.uint8).to(dev)
+            glist = [torch.empty_like(rec_t) for _ in range(world)] if rank == 0 else None
+            dist.gather(rec_t, glist, dst=0)
+            gathered = glist
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    total_scans = args.steps * B * world
+    value = total_scans / dt
+    ms_per_step = dt / args.steps * 1e3
+
+    if rank == 0:
+        odom_ms = stage_acc.get("odom.lm", 0.0) / args.steps
+        achieved = (alg_bytes / args.steps) / (odom_ms * 1e-3) / 1e9 if odom_ms > 0 else 0.0
+        traffic = None
+        pmc = REPO / "profiles" / "r01_pmc_summary.json"
+        if pmc.exists():
+            try:
+                traffic = json.loads(pmc.read_text()).get("k_odom_hbm_bytes_per_launch")
+            except Exception:  # noqa: BLE001
+                traffic = None
+        cpu = None
+        if not args.no_cpu:
+            v, n, passes = cpu_baseline(L, args.sensor, seed, args.stream_len, args.cpu_budget)
+            cpu = {"value": v, "unit": "scans/s", "cores": 1, "kind": "port",
+                   "sample": f"{n} scans ({passes} pass(es) over the {args.stream_len}-scan "
+                             f"{args.sensor} stream, seed {seed}) through oracle ip+fa incl. LM, 1 thread"}
+        if args.odom_profile:
+            prof = (C.c_uint64 * 16)()
+            lib.lego_odom_profile(gpu.h, -1, prof)
+            names = ["surf_nn", "surf", "corner_nn", "corner", "solve", "integrate", "to_end",
+                     "build", "resident", "", "", "", "nn_query", "scanline", "", ""]
+            nsc = (args.steps + args.warmup) * B
+            for i, nm in enumerate(names):
+                if not nm:
+                    continue
+                print(f"  odom.{nm:10s} {prof[i] / 100.0 / nsc:9.2f} us/scan", file=sys.stderr)
+            print(f"  iters/scan surf {prof[9] / nsc:.2f} corner {prof[10] / nsc:.2f} nn {prof[11] / nsc:.2f}"
+                  f"  nn queries/scan: shell1 {prof[14] / nsc:.1f} brute {prof[15] / nsc:.1f}",
+                  file=sys.stderr)
+        if args.stages:
+            tot = sum(stage_acc.values())
+            for k, v in sorted(stage_acc.items(), key=lambda kv: -kv[1]):
+                print(f"  {k:14s} {v / args.steps:9.3f} ms/step  {100 * v / max(tot, 1e-9):5.1f}%",
+                      file=sys.stderr)
+        line = {
+            "metric": "scans/sec (projection+seg+feat+LM) VLP-16 16x1800",
+            "value": value,
+            "unit": "scans/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded ray-cast VLP-16 stream, 1 m/s + 5 deg/s)",
+            "config": {"workload": f"C2: {args.sensor} stream @10Hz, full per-scan pipeline incl. "
+                                   f"2-step LM odometry, {B} scans/step",
+                       "scans_per_step": B, "stream_len": args.stream_len,
+                       "parallelism": f"stream-per-gpu x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_odom", "launch_ms": odom_ms},
+            "cpu_baseline": cpu,
+            "stages_ms_per_step": {k: v / args.steps for k, v in stage_acc.items()},
+        }
+        print(json.dumps(line))
+    gpu.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -206,6 +206,13 @@ const char* lego_last_error(void);
 int lego_stage_times(lego_ctx* ctx, const char** names, float* ms, int32_t cap,
                      int32_t* n);
 
+/* Diagnostic in-kernel phase counters of the odometry kernel (wall clock at
+ * 100 MHz): enable = 1/0 turns stamping on/off and zeroes the counters,
+ * enable = -1 leaves it unchanged; out16 (may be NULL) receives
+ * {surf NN iters, surf iters, corner NN iters, corner iters, solve, integrate,
+ *  to_end, lbvh build, LDS residency, #surf iters, #corner iters, #NN rounds}. */
+int lego_odom_profile(lego_ctx* ctx, int32_t enable, uint64_t* out16);
+
 #ifdef __cplusplus
 }
 #endif

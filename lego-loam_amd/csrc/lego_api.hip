@@ -70,6 +70,9 @@ struct lego_ctx {
   OdomBufs ob{};
   FaCarry* d_carry = nullptr;
   unsigned long long* d_gkeys = nullptr;
+  int* d_gqi = nullptr;
+  unsigned long long* d_prof = nullptr;  // in-kernel phase stamps (lego_odom_profile)
+  bool profOn = false;
   lego_point_xyzir* d_pts = nullptr;
   int64_t* d_off = nullptr;
   std::vector<void*> allocs;
@@ -272,12 +275,13 @@ int lego_create(const lego_sensor_cfg* cfg, int device, int32_t max_points, int3
   A(ob.st, 1);
   A(ob.cornerLast, (size_t)ob.capCorner);
   A(ob.surfLast, (size_t)ob.capSurf);
-  A(ob.nnCorner, (size_t)ob.capCorner);
-  A(ob.nnSurf, (size_t)ob.capSurf);
-  A(ob.nnCornerIdx, (size_t)ob.capCorner);
-  A(ob.nnSurfIdx, (size_t)ob.capSurf);
-  A(ob.nnCornerBox, odom_nn_box_count(ob.capCorner));
-  A(ob.nnSurfBox, odom_nn_box_count(ob.capSurf));
+  {
+    const size_t tc = odom_grid_table(ob.capCorner), ts = odom_grid_table(ob.capSurf);
+    A(ob.gC.keys, tc); A(ob.gC.cnt, tc); A(ob.gC.start, tc);
+    A(ob.gC.slot, (size_t)ob.capCorner); A(ob.gC.pts, (size_t)ob.capCorner); A(ob.gC.idx, (size_t)ob.capCorner);
+    A(ob.gS.keys, ts); A(ob.gS.cnt, ts); A(ob.gS.start, ts);
+    A(ob.gS.slot, (size_t)ob.capSurf); A(ob.gS.pts, (size_t)ob.capSurf); A(ob.gS.idx, (size_t)ob.capSurf);
+  }
   A(ob.sumOut, B * 6);
   A(ob.curOut, B * 6);
   A(ob.validOut, B);
@@ -290,6 +294,8 @@ int lego_create(const lego_sensor_cfg* cfg, int device, int32_t max_points, int3
     while (m < P) m <<= 1;
     A(x->d_gkeys, m);
   }
+  A(x->d_gqi, 3 * N * kFlatPerRing + 3 * N * kSharpPerRing);
+  A(x->d_prof, 16);
 #undef A
   bb.pts = x->d_pts;
   bb.off = x->d_off;
@@ -356,7 +362,7 @@ static int run_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* of
   launch_ip(bb, x->dc, B, want_labels, x->stream, &x->tm);
   if (with_fa) {
     launch_fa(bb, x->dc, B, x->d_carry, x->stream, &x->tm);
-    launch_odom(bb, x->ob, x->dc, B, x->stream, &x->tm, x->d_gkeys);
+    launch_odom(bb, x->ob, x->dc, B, x->stream, &x->tm, x->d_gkeys, x->d_gqi, x->profOn ? x->d_prof : nullptr);
   }
   x->tm.end(x->stream);
   HIPCHK(hipGetLastError());
@@ -515,7 +521,7 @@ int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
   x->stamps.assign(1, in->info.stamp);
   x->tm.begin();
   launch_fa(x->bb, x->dc, 1, x->d_carry, x->stream, &x->tm);
-  launch_odom(x->bb, x->ob, x->dc, 1, x->stream, &x->tm, x->d_gkeys);
+  launch_odom(x->bb, x->ob, x->dc, 1, x->stream, &x->tm, x->d_gkeys, x->d_gqi, x->profOn ? x->d_prof : nullptr);
   x->tm.end(x->stream);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(x->stream));
@@ -585,6 +591,19 @@ int lego_mo_process(lego_ctx* x, const lego_fa_out* in, lego_mo_out* out) {
   if (!x) return LEGO_E_ARG;
   set_err("scan-to-map is not in this build yet");
   return LEGO_E_STATE;
+}
+
+int lego_odom_profile(lego_ctx* x, int32_t enable, uint64_t* out16) {
+  if (!x) return LEGO_E_ARG;
+  HIPCHK(hipSetDevice(x->device));
+  if (out16) {
+    HIPCHK(hipMemcpy(out16, x->d_prof, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  }
+  if (enable >= 0) {
+    x->profOn = enable != 0;
+    HIPCHK(hipMemset(x->d_prof, 0, 16 * sizeof(uint64_t)));
+  }
+  return LEGO_OK;
 }
 
 int lego_stage_times(lego_ctx* x, const char** names, float* ms, int32_t cap, int32_t* n) {

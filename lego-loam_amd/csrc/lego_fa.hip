@@ -128,7 +128,7 @@ __host__ __device__ inline size_t extract_lds_bytes(int H) {
   return (s + 15) & ~(size_t)15;
 }
 
-__device__ ExtractLds carve(unsigned char* base, int H) {
+__device__ __forceinline__ ExtractLds carve(unsigned char* base, int H) {
   const size_t W = (size_t)H + 32;
   const size_t vox = (size_t)next_pow2((int)W);
   ExtractLds L;
@@ -151,7 +151,7 @@ enum { M_TIE = 0, M_LF = 1, M_OVF = 2, M_NSH = 3, M_NLS = 4, M_NFL = 5, M_D0 = 6
        M_MB0 = 8, M_MB1 = 9, M_MB2 = 10, M_WOFF = 16 };
 
 // Bitonic sort of m (power of two) entries in LDS by value, all threads.
-__device__ void bitonic_entries(SmoothEntry* a, int m) {
+__device__ __forceinline__ void bitonic_entries(SmoothEntry* a, int m) {
   for (int k = 2; k <= m; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
       for (int t = threadIdx.x; t < m / 2; t += blockDim.x) {
@@ -165,7 +165,7 @@ __device__ void bitonic_entries(SmoothEntry* a, int m) {
     }
   }
 }
-__device__ void bitonic_u64(unsigned long long* a, int m) {
+__device__ __forceinline__ void bitonic_u64(unsigned long long* a, int m) {
   for (int k = 2; k <= m; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
       for (int t = threadIdx.x; t < m / 2; t += blockDim.x) {
@@ -209,7 +209,7 @@ struct RingCtx {
 
 // neighbour suppression (:720-732, :751-767); negative indices break (the
 // reference reads colInd[-1] there — UB; SURVEY.md §9.7 policy).
-__device__ void suppress(const RingCtx& R, volatile uint8_t* picked, const uint16_t* col, int ind) {
+__device__ __forceinline__ void suppress(const RingCtx& R, volatile uint8_t* picked, const uint16_t* col, int ind) {
   const int w = ind - R.lo;
   picked[w] = 1;
   for (int l = 1; l <= 5; l++) {
@@ -234,7 +234,7 @@ __device__ __forceinline__ bool in_win(const RingCtx& R, int ind) {
   return ind >= R.lo && ind - R.lo < R.Wn;
 }
 
-__device__ void extract_ring(const BatchBufs& bb, const DevCfg& c, int b, int ring, FaCarry* carry,
+__device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& c, int b, int ring, FaCarry* carry,
                              const ExtractLds& L) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ns = bb.ns[b];

@@ -56,6 +56,16 @@ class StageTimer {
   size_t used_ = 0;
 };
 
+// Hash-grid nearest-neighbour index over a snapshot of a last cloud.
+struct NNGrid {
+  unsigned long long* keys;  // [T]
+  int* cnt;                  // [T]
+  int* start;                // [T]
+  int* slot;                 // [cap] per-point slot (build scratch)
+  float4* pts;               // [cap] cell-ordered snapshot
+  int* idx;                  // [cap] original index
+};
+
 // Odometry state kept on the device for one stream (featureAssociation.cpp
 // member variables that persist across scans).
 struct OdomState {
@@ -74,12 +84,7 @@ struct OdomBufs {
   OdomState* st;
   float4* cornerLast;   // [capCorner]
   float4* surfLast;     // [capSurf]
-  float4* nnCorner;     // NN structure point sets (copies at rebuild time)
-  float4* nnSurf;
-  int* nnCornerIdx;     // original index per sorted slot
-  int* nnSurfIdx;
-  float4* nnCornerBox;  // node boxes: [2*nodes] (lo, hi)
-  float4* nnSurfBox;
+  NNGrid gC, gS;        // hash grids over snapshots of the last clouds
   int capCorner, capSurf;
   // per-scan outputs of the batch
   float* sumOut;        // [B*6]
@@ -96,7 +101,7 @@ void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hip
 void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, FaCarry* d_carry, hipStream_t s,
                StageTimer* tm);
 void launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int B, hipStream_t s,
-                 StageTimer* tm, unsigned long long* gkeys);
-size_t odom_nn_box_count(int npts);
+                 StageTimer* tm, unsigned long long* gkeys, int* gqi, unsigned long long* prof);
+size_t odom_grid_table(int npts);
 
 }  // namespace lego

@@ -417,9 +417,11 @@ LEGO_HD bool cv_solve_qr(float (&A)[M][N], const float (&bin)[M], float (&x)[N])
   for (int i = 0; i < M; i++) b[i] = bin[i];
   float vl[M];
   float hF[N];
+#pragma unroll
   for (int l = 0; l < N; l++) {
     int vlSize = M - l;
     float vlNorm = 0.f;
+#pragma unroll
     for (int i = 0; i < vlSize; i++) {
       vl[i] = A[l + i][l];
       vlNorm += vl[i] * vl[i];
@@ -427,23 +429,34 @@ LEGO_HD bool cv_solve_qr(float (&A)[M][N], const float (&bin)[M], float (&x)[N])
     float tmpV = vl[0];
     vl[0] = vl[0] + (vl[0] >= 0 ? 1.f : -1.f) * lsqrtf(vlNorm);
     vlNorm = lsqrtf(vlNorm + vl[0] * vl[0] - tmpV * tmpV);
+#pragma unroll
     for (int i = 0; i < vlSize; i++) vl[i] /= vlNorm;
+#pragma unroll
     for (int j = l; j < N; j++) {
       float v_lA = 0.f;
+#pragma unroll
       for (int i = l; i < M; i++) v_lA += vl[i - l] * A[i][j];
+#pragma unroll
       for (int i = l; i < M; i++) A[i][j] -= 2 * vl[i - l] * v_lA;
     }
     hF[l] = vl[0] * vl[0];
+#pragma unroll
     for (int i = 1; i < vlSize; i++) A[l + i][l] = vl[i] / vl[0];
   }
+#pragma unroll
   for (int l = 0; l < N; l++) {
     vl[0] = 1.f;
+#pragma unroll
     for (int j = 1; j < M - l; j++) vl[j] = A[j + l][l];
     float v_lB = 0.f;
+#pragma unroll
     for (int i = l; i < M; i++) v_lB += vl[i - l] * b[i];
+#pragma unroll
     for (int i = l; i < M; i++) b[i] -= 2 * vl[i - l] * v_lB * hF[l];
   }
+#pragma unroll
   for (int i = N - 1; i >= 0; i--) {
+#pragma unroll
     for (int j = N - 1; j > i; j--) b[i] -= b[j] * A[i][j];
     if (lfabsf(A[i][i]) < eps) {
       for (int q = 0; q < N; q++) x[q] = 0.f;

@@ -4,18 +4,18 @@
 // (scan k's problem depends on scan k-1's result through transformCur and the
 // TransformToEnd'ed "last" clouds, featureAssociation.cpp:1759-1815), so the
 // per-scan chain never returns to the host.  Per LM iteration:
-//   A  1 lane / query : TransformToStart                         (:860-883)
-//   B  1 wave / query : nearest neighbour (every 5th iteration) in an LBVH
-//                       over the last cloud — exact, replaces KdTreeFLANN
-//                       (:1054,1165; ties -> lower index, FLANN's are
-//                       traversal-order dependent) — then the scan-line search
-//                       as ordered wave ballots (:1062-1099, :1173-1220),
-//                       keeping the reference's loop-bound quirk
-//   C  1 lane / query : line / plane residual, weight, row      (:1106-1151, 1228-1266)
-//   D  block reduce   : AtA, AtB with double accumulation (cv::gemm's float
-//                       path accumulates in double)
-//   E  lane 0         : QR solve, iteration-0 eigen degeneracy projection,
-//                       update, NaN reset, convergence (:1324-1376, :1425-1477)
+//   one lane per query, no barrier between the steps:
+//     TransformToStart (:860-883);
+//     every 5th iteration the nearest neighbour in an LBVH over the last
+//     cloud — exact, replaces KdTreeFLANN (:1054, :1165; ties -> lower index,
+//     FLANN's tie order is traversal dependent) — and the scan-line search
+//     loops exactly as written (:1062-1099, :1173-1220, incl. the loop-bound
+//     quirk, clamped to the cloud);
+//     line / plane residual, weight and Jacobian row (:1106-1151, :1228-1321)
+//   block reduce: AtA, AtB with double accumulation (cv::gemm's float path)
+//   lane 0: QR solve, iteration-0 eigen degeneracy projection, update, NaN
+//     reset, convergence test (:1324-1376, :1425-1477).
+// The last clouds and the LBVH node boxes live in LDS when they fit.
 // then integrateTransformation (:1697-1725) and publishCloudsLast.
 #include <climits>
 
@@ -24,10 +24,12 @@
 
 namespace lego {
 
-constexpr int kOdomThreads = 1024;
+constexpr int kOdomThreads = 512;
 constexpr int kOdomWaves = kOdomThreads / 64;
-constexpr int kLeaf = 64;
-constexpr int kLdsSortKeys = 16384;
+// LDS residency caps (VLP-16 fits entirely; larger sensors fall back to HBM)
+constexpr int kLdsSurf = 4096;      // last surf cloud points
+constexpr int kLdsCorner = 2048;    // last corner cloud points
+constexpr int kLdsQ = 512;          // queries with LDS-resident correspondence indices
 
 // ---------------------------------------------------------------- transforms
 struct Trig3 {
@@ -37,7 +39,7 @@ __device__ __forceinline__ Trig3 trig3(float rx, float ry, float rz) {
   return {lego_sinf(rx), lego_cosf(rx), lego_sinf(ry), lego_cosf(ry), lego_sinf(rz), lego_cosf(rz)};
 }
 
-__device__ float4 to_start(float4 pi, const float* tc) {  // :860-883
+__device__ __forceinline__ float4 to_start(float4 pi, const float* tc) {  // :860-883
   const float s = 10 * (pi.w - (float)(int)pi.w);
   const float rx = s * tc[0], ry = s * tc[1], rz = s * tc[2];
   const float tx = s * tc[3], ty = s * tc[4], tz = s * tc[5];
@@ -58,7 +60,7 @@ struct ImuEnd {
   float cRS, cPS, cYS, sRS, sPS, sYS;  // cosImu*Start / sinImu*Start
   float cYL, sYL, cPL, sPL, cRL, sRL;  // imu*Last
 };
-__device__ float4 to_end(float4 pi, const float* tc, const ImuEnd& im) {
+__device__ __forceinline__ float4 to_end(float4 pi, const float* tc, const ImuEnd& im) {
   const float s = 10 * (pi.w - (float)(int)pi.w);
   float rx = s * tc[0], ry = s * tc[1], rz = s * tc[2];
   float tx = s * tc[3], ty = s * tc[4], tz = s * tc[5];
@@ -105,7 +107,7 @@ __device__ float4 to_end(float4 pi, const float* tc, const ImuEnd& im) {
 }
 
 // AccumulateRotation :1015-1032
-__device__ void accumulate_rotation(float cx, float cy, float cz, float lx, float ly, float lz,
+__device__ __forceinline__ void accumulate_rotation(float cx, float cy, float cz, float lx, float ly, float lz,
                                     float& ox, float& oy, float& oz) {
   const float clx = lego_cosf(lx), slx = lego_sinf(lx), cly = lego_cosf(ly), sly = lego_sinf(ly);
   const float clz = lego_cosf(lz), slz = lego_sinf(lz);
@@ -126,7 +128,7 @@ __device__ void accumulate_rotation(float cx, float cy, float cz, float lx, floa
 }
 
 // PluginIMURotation :955-1013
-__device__ void plugin_imu_rotation(float bcx, float bcy, float bcz, float blx, float bly, float blz,
+__device__ __forceinline__ void plugin_imu_rotation(float bcx, float bcy, float bcz, float blx, float bly, float blz,
                                     float alx, float aly, float alz, float& acx, float& acy,
                                     float& acz) {
   const float sbcx = lego_sinf(bcx), cbcx = lego_cosf(bcx), sbcy = lego_sinf(bcy), cbcy = lego_cosf(bcy);
@@ -175,181 +177,142 @@ __device__ void plugin_imu_rotation(float bcx, float bcy, float bcz, float blx, 
   acz = lego_atan2f(srzcrx / lego_cosf(acx), crzcrx / lego_cosf(acx));
 }
 
+// In-kernel phase stamps (diagnostic; enabled per launch).  Thread 0 adds
+// wall_clock64 deltas (100 MHz) into prof[k].
+enum { P_SURF_NN = 0, P_SURF = 1, P_CORN_NN = 2, P_CORN = 3, P_SOLVE = 4, P_INTEG = 5,
+       P_TOEND = 6, P_BUILD = 7, P_RESID = 8, P_ITERS_S = 9, P_ITERS_C = 10, P_NNR = 11,
+       P_QUERY = 12, P_SCANLINE = 13, P_NN_SHELL1 = 14, P_NN_BRUTE = 15, P_NPROF = 16 };
+struct Stamp {
+  unsigned long long* prof;
+  unsigned long long t;
+  __device__ void start() { if (prof && threadIdx.x == 0) t = wall_clock64(); }
+  __device__ void add(int k) {
+    if (prof && threadIdx.x == 0) { const unsigned long long n = wall_clock64(); prof[k] += n - t; t = n; }
+  }
+  __device__ void count(int k) { if (prof && threadIdx.x == 0) prof[k] += 1; }
+};
+
 // ---------------------------------------------------------------- LDS layout
 struct OdomLds {
-  unsigned long long* keys;  // NN build (union with the query arrays)
-  float4* sel;               // [capQ] transformed queries
-  int* i1;                   // [capQ]
-  int* i2;
-  int* i3;
-  int* acc;                  // [capQ] row accepted
-  int* stack;                // [kOdomWaves * 64]
-  double* red;               // [kOdomWaves * 10]
-  float* f;                  // scalars: transformCur etc.
-  int* n;                    // int scalars
+  float4* lastS;     // [kLdsSurf]  (also the NN-build key scratch)
+  float4* lastC;     // [kLdsCorner]
+  int* qi;           // [3 * kLdsQ] correspondence indices
+  double* red;       // [kOdomWaves * 10]
+  float* f;          // 64 scalars
+  int* n;            // 64 scalars
+  OdomState* st;     // the stream state, resident for the kernel's lifetime
 };
 
 __host__ __device__ inline size_t odom_lds_bytes() {
-  size_t s = (size_t)kLdsSortKeys * 8;                   // keys / query union
-  s += (size_t)kOdomWaves * 64 * 4;                      // stacks
-  s += (size_t)kOdomWaves * 10 * 8;                      // reduce
-  s += 64 * 4 + 64 * 4;                                  // scalars
+  size_t s = 0;
+  s += (size_t)kLdsSurf * 16 + (size_t)kLdsCorner * 16;
+  s += (size_t)3 * kLdsQ * 4;
+  s += (size_t)kOdomWaves * 10 * 8;
+  s += 64 * 4 + 64 * 4;
+  s += 128;  // OdomState
   return s;
 }
-__host__ __device__ inline int odom_cap_q() {
-  // sel(16) + i1,i2,i3,acc(16) per query inside the 128 KiB union
-  return (kLdsSortKeys * 8) / 32;
-}
 
-__device__ OdomLds odom_carve(unsigned char* base) {
+__device__ __forceinline__ OdomLds odom_carve(unsigned char* base) {
   OdomLds L;
   size_t o = 0;
-  L.keys = (unsigned long long*)(base + o);
-  const int capQ = odom_cap_q();
-  L.sel = (float4*)(base + o);
-  L.i1 = (int*)(base + o + (size_t)capQ * 16);
-  L.i2 = L.i1 + capQ;
-  L.i3 = L.i2 + capQ;
-  L.acc = L.i3 + capQ;
-  o += (size_t)kLdsSortKeys * 8;
-  L.stack = (int*)(base + o); o += (size_t)kOdomWaves * 64 * 4;
+  L.lastS = (float4*)(base + o); o += (size_t)kLdsSurf * 16;
+  L.lastC = (float4*)(base + o); o += (size_t)kLdsCorner * 16;
   L.red = (double*)(base + o); o += (size_t)kOdomWaves * 10 * 8;
+  L.qi = (int*)(base + o); o += (size_t)3 * kLdsQ * 4;
   L.f = (float*)(base + o); o += 64 * 4;
   L.n = (int*)(base + o); o += 64 * 4;
+  L.st = (OdomState*)(base + o); o += 128;
   return L;
 }
 
-// scalar slots in L.f / L.n
-enum { F_CUR = 0, F_SUM = 6, F_MATP = 12, F_BB = 21 /* bbox 6 */ };
-enum { N_BREAK = 0, N_M = 1, N_DONE = 2, N_TMP = 3 };
+enum { F_BB = 0 /* bbox 6 */ };
+enum { N_BREAK = 0, N_M = 1 };
 
 // ---------------------------------------------------------------- NN index
-struct NNIndex {
-  float4* pts;   // sorted points (w = original intensity)
-  int* idx;      // original index of each sorted slot
-  float4* box;   // [2 * 2*L2]: lo at 2*node, hi at 2*node+1
-  int n, L2;
+// Hash grid over a snapshot of the last cloud (taken when the reference would
+// rebuild its kd-tree, featureAssociation.cpp:1785-1788): 0.5 m cells, open-
+// addressing table, points scattered into cell order by atomic cursors (no
+// sort).  A query is served by a 32-lane group: the 27 cells around it, then
+// the 98-cell shell, each accepted only when the best distance is provably
+// smaller than the covered radius; otherwise (or for small clouds) an exact
+// group-wide brute force.  Ties resolve to the lower original index.
+constexpr int kG = 32;              // lanes per query group
+constexpr float kCell = 0.5f;
+constexpr unsigned long long kEmpty = ~0ull;
+
+struct GridView {
+  const unsigned long long* keys;
+  const int* cnt;
+  const int* start;
+  const float4* pts;  // cell-ordered snapshot
+  const int* idx;     // original index of each slot
+  int T, n;
 };
 
-__device__ void bitonic_u64_any(unsigned long long* a, int m) {
-  for (int k = 2; k <= m; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int t = threadIdx.x; t < m / 2; t += blockDim.x) {
-        const int i = (t / j) * 2 * j + (t % j);
-        const int l = i + j;
-        const bool up = (i & k) == 0;
-        const unsigned long long x = a[i], y = a[l];
-        if ((x > y) == up) { a[i] = y; a[l] = x; }
-      }
-      __syncthreads();
-    }
-  }
+__device__ __forceinline__ unsigned long long cell_key(int ix, int iy, int iz) {
+  return ((unsigned long long)(unsigned)(ix + (1 << 20)) << 42) |
+         ((unsigned long long)(unsigned)(iy + (1 << 20)) << 21) | (unsigned long long)(unsigned)(iz + (1 << 20));
+}
+__device__ __forceinline__ unsigned hash_key(unsigned long long k) {
+  k ^= k >> 33; k *= 0xff51afd7ed558ccdULL; k ^= k >> 33;
+  return (unsigned)k;
+}
+__device__ __forceinline__ int cell_of(float v) { return (int)floorf(v * (1.0f / kCell)); }
+
+__host__ __device__ inline int grid_table_size(int n) {
+  int t = 64;
+  while (t < 2 * n) t <<= 1;
+  return t;
 }
 
-__device__ __forceinline__ unsigned spread10(unsigned v) {
-  v &= 1023u;
-  v = (v | (v << 16)) & 0x030000FFu;
-  v = (v | (v << 8)) & 0x0300F00Fu;
-  v = (v | (v << 4)) & 0x030C30C3u;
-  v = (v | (v << 2)) & 0x09249249u;
-  return v;
-}
-
-// Builds the LBVH over src[0..n): Morton-sorted 64-point leaves under an
-// implicit complete binary tree (node 1 = root, leaves at [L2, 2*L2)).
-__device__ void nn_build(const float4* src, int n, NNIndex& ix, const OdomLds& L,
-                         unsigned long long* gkeys) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  float mn[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
-  float mx[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
-  for (int t = tid; t < n; t += blockDim.x) {
-    const float4 p = src[t];
-    mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
-    mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
-  }
-  for (int q = 0; q < 3; ++q)
-    for (int o = 32; o > 0; o >>= 1) {
-      mn[q] = fminf(mn[q], __shfl_xor(mn[q], o, 64));
-      mx[q] = fmaxf(mx[q], __shfl_xor(mx[q], o, 64));
-    }
-  float* red = (float*)L.red;
-  if (lane == 0)
-    for (int q = 0; q < 3; ++q) { red[wave * 6 + q] = mn[q]; red[wave * 6 + 3 + q] = mx[q]; }
+// Builds the grid over src[0..n) (all threads; global buffers).
+__device__ __forceinline__ void grid_build(const float4* src, int n, unsigned long long* keys, int* cnt, int* start,
+                           int* slotOf, float4* pts, int* idx, const OdomLds& L) {
+  const int tid = threadIdx.x;
+  const int T = grid_table_size(n);
+  for (int t = tid; t < T; t += blockDim.x) { keys[t] = kEmpty; cnt[t] = 0; }
   __syncthreads();
-  if (tid < 6) {
-    float v = red[tid];
-    for (int w = 1; w < kOdomWaves; ++w) v = tid < 3 ? fminf(v, red[w * 6 + tid]) : fmaxf(v, red[w * 6 + tid]);
-    L.f[F_BB + tid] = v;
+  for (int i = tid; i < n; i += blockDim.x) {
+    const float4 p = src[i];
+    const unsigned long long k = cell_key(cell_of(p.x), cell_of(p.y), cell_of(p.z));
+    unsigned s = hash_key(k) & (T - 1);
+    while (true) {
+      const unsigned long long old = atomicCAS(&keys[s], kEmpty, k);
+      if (old == kEmpty || old == k) break;
+      s = (s + 1) & (T - 1);
+    }
+    slotOf[i] = (int)s;
+    atomicAdd(&cnt[s], 1);
   }
   __syncthreads();
-  const float lo0 = L.f[F_BB], lo1 = L.f[F_BB + 1], lo2 = L.f[F_BB + 2];
-  const float s0 = 1023.0f / fmaxf(L.f[F_BB + 3] - lo0, 1e-6f);
-  const float s1 = 1023.0f / fmaxf(L.f[F_BB + 4] - lo1, 1e-6f);
-  const float s2 = 1023.0f / fmaxf(L.f[F_BB + 5] - lo2, 1e-6f);
-  int m = 1;
-  while (m < n) m <<= 1;
-  unsigned long long* keys = (m <= kLdsSortKeys) ? L.keys : gkeys;
-  for (int t = tid; t < m; t += blockDim.x) {
-    unsigned long long k = ~0ull;
-    if (t < n) {
-      const float4 p = src[t];
-      const unsigned mc = (spread10((unsigned)((p.x - lo0) * s0)) << 2) |
-                          (spread10((unsigned)((p.y - lo1) * s1)) << 1) |
-                          spread10((unsigned)((p.z - lo2) * s2));
-      k = ((unsigned long long)mc << 32) | (unsigned)t;
+  // exclusive scan of cnt into start: each thread owns T/blockDim consecutive slots
+  {
+    const int per = (T + blockDim.x - 1) / blockDim.x;
+    const int b0 = tid * per, b1 = min(T, b0 + per);
+    int local = 0;
+    for (int t = b0; t < b1; ++t) local += cnt[t];
+    const int lane = tid & 63, wave = tid >> 6;
+    int x = local;
+    for (int o2 = 1; o2 < 64; o2 <<= 1) {
+      const int y = __shfl_up(x, o2, 64);
+      if (lane >= o2) x += y;
     }
-    keys[t] = k;
-  }
-  __syncthreads();
-  bitonic_u64_any(keys, m);
-  for (int t = tid; t < n; t += blockDim.x) {
-    const int o = (int)(keys[t] & 0xffffffffu);
-    ix.pts[t] = src[o];
-    ix.idx[t] = o;
-  }
-  __syncthreads();
-  const int nleaf = (n + kLeaf - 1) / kLeaf;
-  int L2 = 1;
-  while (L2 < nleaf) L2 <<= 1;
-  ix.n = n;
-  ix.L2 = L2;
-  // leaf boxes: one wave per leaf
-  for (int l = wave; l < L2; l += kOdomWaves) {
-    const int s = l * kLeaf + lane;
-    float a[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
-    float z[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
-    if (s < n) {
-      const float4 p = ix.pts[s];
-      a[0] = z[0] = p.x; a[1] = z[1] = p.y; a[2] = z[2] = p.z;
-    }
-    for (int q = 0; q < 3; ++q)
-      for (int o = 32; o > 0; o >>= 1) {
-        a[q] = fminf(a[q], __shfl_xor(a[q], o, 64));
-        z[q] = fmaxf(z[q], __shfl_xor(z[q], o, 64));
-      }
-    if (lane == 0) {
-      ix.box[2 * (L2 + l)] = make_float4(a[0], a[1], a[2], 0);
-      ix.box[2 * (L2 + l) + 1] = make_float4(z[0], z[1], z[2], 0);
-    }
-  }
-  __syncthreads();
-  for (int lvl = L2 >> 1; lvl >= 1; lvl >>= 1) {
-    for (int nd = lvl + tid; nd < 2 * lvl; nd += blockDim.x) {
-      const float4 al = ix.box[2 * (2 * nd)], ah = ix.box[2 * (2 * nd) + 1];
-      const float4 bl = ix.box[2 * (2 * nd + 1)], bh = ix.box[2 * (2 * nd + 1) + 1];
-      ix.box[2 * nd] = make_float4(fminf(al.x, bl.x), fminf(al.y, bl.y), fminf(al.z, bl.z), 0);
-      ix.box[2 * nd + 1] = make_float4(fmaxf(ah.x, bh.x), fmaxf(ah.y, bh.y), fmaxf(ah.z, bh.z), 0);
-    }
+    if (lane == 63) L.n[8 + wave] = x;
+    __syncthreads();
+    int woff = 0;
+    for (int w = 0; w < wave; ++w) woff += L.n[8 + w];
+    int run = woff + x - local;
+    for (int t = b0; t < b1; ++t) { start[t] = run; run += cnt[t]; cnt[t] = 0; }
     __syncthreads();
   }
-}
-
-__device__ __forceinline__ float box_d2(const NNIndex& ix, int nd, float4 q) {
-  const float4 lo = ix.box[2 * nd], hi = ix.box[2 * nd + 1];
-  const float gx = lo.x - q.x > 0 ? lo.x - q.x : (q.x - hi.x > 0 ? q.x - hi.x : 0.f);
-  const float gy = lo.y - q.y > 0 ? lo.y - q.y : (q.y - hi.y > 0 ? q.y - hi.y : 0.f);
-  const float gz = lo.z - q.z > 0 ? lo.z - q.z : (q.z - hi.z > 0 ? q.z - hi.z : 0.f);
-  return gx * gx + gy * gy + gz * gz;
+  for (int i = tid; i < n; i += blockDim.x) {
+    const int s = slotOf[i];
+    const int pos = start[s] + atomicAdd(&cnt[s], 1);
+    pts[pos] = src[i];
+    idx[pos] = i;
+  }
+  __syncthreads();
 }
 
 // L2_Simple distance order ((0 + d0^2) + d1^2) + d2^2 (FLANN)
@@ -361,149 +324,167 @@ __device__ __forceinline__ float flann_d2(float4 q, float4 p) {
   return r;
 }
 
-// One wave: exact nearest neighbour with d2 < bound (ties -> lower original
-// index).  Returns the original index or -1.
-__device__ int nn_query_wave(const NNIndex& ix, float4 q, float bound, int* stack) {
-  const int lane = threadIdx.x & 63;
-  if (ix.n <= 0) return -1;
-  float best = bound;
-  int bestIdx = INT_MAX;
-  int sp = 0;
-  if (lane == 0) stack[0] = 1;
-  sp = 1;
-  __builtin_amdgcn_wave_barrier();
-  while (sp > 0) {
-    const int nd = ((volatile int*)stack)[sp - 1];
-    --sp;
-    const float bd = box_d2(ix, nd, q);
-    if (bd > best * 1.0001f + 1e-6f) continue;
-    if (nd >= ix.L2) {
-      const int s = (nd - ix.L2) * kLeaf + lane;
-      float d = __builtin_inff();
-      int id = INT_MAX;
-      if (s < ix.n) {
-        d = flann_d2(q, ix.pts[s]);
-        id = ix.idx[s];
-      }
-      // wave lexicographic min of (d, id)
-      for (int o = 32; o > 0; o >>= 1) {
-        const float d2 = __shfl_xor(d, o, 64);
-        const int i2 = __shfl_xor(id, o, 64);
-        if (d2 < d || (d2 == d && i2 < id)) { d = d2; id = i2; }
-      }
-      if (d < best || (d == best && id < bestIdx)) { best = d; bestIdx = id; }
-    } else {
-      const int a = 2 * nd, b = 2 * nd + 1;
-      const float da = box_d2(ix, a, q), db = box_d2(ix, b, q);
-      const int nearC = da <= db ? a : b, farC = da <= db ? b : a;
-      if (lane == 0) {
-        ((volatile int*)stack)[sp] = farC;
-        ((volatile int*)stack)[sp + 1] = nearC;
-      }
-      sp += 2;
-      __builtin_amdgcn_wave_barrier();
-    }
+__device__ __forceinline__ void lex_min(float& d, int& i, float d2, int i2) {
+  if (d2 < d || (d2 == d && i2 < i)) { d = d2; i = i2; }
+}
+__device__ __forceinline__ void group_lex_min(float& d, int& i) {
+  for (int o = kG / 2; o > 0; o >>= 1) {
+    const float d2 = __shfl_xor(d, o, 64);
+    const int i2 = __shfl_xor(i, o, 64);
+    lex_min(d, i, d2, i2);
   }
-  return (bestIdx != INT_MAX && best < bound) ? bestIdx : -1;
 }
 
-// lexicographic (d, order) min across the wave among `cand` lanes
-__device__ __forceinline__ void wave_argmin(bool cand, float d, int order, int j, float* bd, int* bo,
-                                            int* bj) {
-  float v = cand ? d : __builtin_inff();
-  int o = cand ? order : INT_MAX;
-  int jj = cand ? j : -1;
-  for (int s = 32; s > 0; s >>= 1) {
-    const float v2 = __shfl_xor(v, s, 64);
-    const int o2 = __shfl_xor(o, s, 64);
-    const int j2 = __shfl_xor(jj, s, 64);
-    if (v2 < v || (v2 == v && o2 < o)) { v = v2; o = o2; jj = j2; }
+__device__ __forceinline__ void scan_cell(const GridView& v, float4 q, int ix, int iy, int iz, float& bd,
+                                          int& bi) {
+  const unsigned long long k = cell_key(ix, iy, iz);
+  unsigned s = hash_key(k) & (v.T - 1);
+  while (true) {
+    const unsigned long long kk = v.keys[s];
+    if (kk == kEmpty) return;
+    if (kk == k) break;
+    s = (s + 1) & (v.T - 1);
   }
-  *bd = v;
-  *bo = o;
-  *bj = jj;
+  const int b = v.start[s], e = b + v.cnt[s];
+  for (int t = b; t < e; ++t) lex_min(bd, bi, flann_d2(q, v.pts[t]), v.idx[t]);
+}
+
+// Exact nearest neighbour with d2 < bound, by the calling 32-lane group.
+__device__ __forceinline__ int grid_nn(const GridView& v, float4 q, float bound, int g,
+                                       unsigned long long* prof) {
+  if (v.n <= 0) return -1;
+  float bd = bound;
+  int bi = INT_MAX;
+  if (v.n > 4 * kG) {
+    const int cx = cell_of(q.x), cy = cell_of(q.y), cz = cell_of(q.z);
+    // shell 1: the 27 cells (covered radius >= 1 cell)
+    if (g < 27) scan_cell(v, q, cx + g % 3 - 1, cy + (g / 3) % 3 - 1, cz + g / 9 - 1, bd, bi);
+    group_lex_min(bd, bi);
+    if (bd < kCell * kCell * 0.99999f) {
+      if (prof && g == 0) atomicAdd(&prof[P_NN_SHELL1], 1ull);
+      return (bi != INT_MAX && bd < bound) ? bi : -1;
+    }
+    // shell 2: the 98 cells at Chebyshev distance 2 (covered radius >= 2 cells)
+    for (int c = g; c < 125; c += kG) {
+      const int dx = c % 5 - 2, dy = (c / 5) % 5 - 2, dz = c / 25 - 2;
+      if (abs(dx) == 2 || abs(dy) == 2 || abs(dz) == 2) scan_cell(v, q, cx + dx, cy + dy, cz + dz, bd, bi);
+    }
+    group_lex_min(bd, bi);
+    if (bd < 4 * kCell * kCell * 0.99999f) return (bi != INT_MAX && bd < bound) ? bi : -1;
+  }
+  // exact fallback: every point
+  if (prof && g == 0) atomicAdd(&prof[P_NN_BRUTE], 1ull);
+  for (int t = g; t < v.n; t += kG) lex_min(bd, bi, flann_d2(q, v.pts[t]), v.idx[t]);
+  group_lex_min(bd, bi);
+  return (bi != INT_MAX && bd < bound) ? bi : -1;
 }
 
 __device__ __forceinline__ float line_d2(float4 a, float4 s) {  // the scan-line distance
   return (a.x - s.x) * (a.x - s.x) + (a.y - s.y) * (a.y - s.y) + (a.z - s.z) * (a.z - s.z);
 }
 
-// Scan-line search around `ci` (featureAssociation.cpp:1062-1099 corner,
-// :1173-1220 surf).  Sequential semantics: the running minimum with strict <
-// keeps the first point in visiting order.
-__device__ void scanline_wave(const float4* last, int lastN, int jend, int ci, float4 sel,
-                              bool surf, float nn_sq, int* o2, int* o3) {
-  const int lane = threadIdx.x & 63;
+// ordered (d, visit order) argmin over the group's candidate lanes
+__device__ __forceinline__ void group_argmin(bool cand, float d, int ord, int j, float* bd, int* bj) {
+  float v = cand ? d : __builtin_inff();
+  int o = cand ? ord : INT_MAX;
+  int jj = cand ? j : -1;
+  for (int s = kG / 2; s > 0; s >>= 1) {
+    const float v2 = __shfl_xor(v, s, 64);
+    const int o2 = __shfl_xor(o, s, 64);
+    const int j2 = __shfl_xor(jj, s, 64);
+    if (v2 < v || (v2 == v && o2 < o)) { v = v2; o = o2; jj = j2; }
+  }
+  *bd = v;
+  *bj = jj;
+}
+
+__device__ __forceinline__ unsigned group_ballot(bool p, int gbase) {
+  return (unsigned)(__ballot(p) >> gbase);
+}
+
+// Scan-line search around `ci` (corner :1062-1099, surf :1173-1220): the
+// reference's sequential loops, kG indices per step.  The sequential running
+// minimum with a strict < keeps the FIRST point in visiting order among equal
+// distances, so every lane keeps a lexicographic (distance, visit rank) minimum
+// over the indices it visits and one group reduction combines them.
+// int(I) > cScan + 2.5 <=> int(I) > cScan + 2 (and < cScan - 2.5 <=> < cScan - 2).
+__device__ __forceinline__ void group_lex_min3(float& d, int& r, int& j) {
+  for (int s = kG / 2; s > 0; s >>= 1) {
+    const float d2 = __shfl_xor(d, s, 64);
+    const int r2 = __shfl_xor(r, s, 64);
+    const int j2 = __shfl_xor(j, s, 64);
+    if (d2 < d || (d2 == d && r2 < r)) { d = d2; r = r2; j = j2; }
+  }
+}
+
+__device__ __forceinline__ void scanline_group(const float4* last, int jend, int ci, float4 sel, bool surf,
+                                               float nn_sq, int g, int gbase, int* o2, int* o3) {
   const int cScan = (int)last[ci].w;
   float m2 = nn_sq, m3 = nn_sq;
-  int i2 = -1, i3 = -1;
-  // forward
-  for (int j0 = ci + 1; j0 < jend; j0 += 64) {
-    const int j = j0 + lane;
+  int r2 = INT_MAX, r3 = INT_MAX, i2 = -1, i3 = -1;
+  for (int j0 = ci + 1; j0 < jend; j0 += kG) {
+    const int j = j0 + g;
     const bool inr = j < jend;
     float4 p = make_float4(0, 0, 0, 0);
     int rj = 0;
     if (inr) { p = last[j]; rj = (int)p.w; }
-    const bool brk = inr && (double)rj > cScan + 2.5;
-    const unsigned long long bm = __ballot(brk);
-    const int lim = bm ? (__ffsll((long long)bm) - 1) : 64;
-    const bool v = inr && lane < lim;
-    const float d = v ? line_d2(p, sel) : 0.f;
-    float bd; int bo, bj;
-    if (surf) {
-      wave_argmin(v && rj <= cScan, d, lane, j, &bd, &bo, &bj);
-      if (bj >= 0 && bd < m2) { m2 = bd; i2 = bj; }
-      wave_argmin(v && rj > cScan, d, lane, j, &bd, &bo, &bj);
-      if (bj >= 0 && bd < m3) { m3 = bd; i3 = bj; }
-    } else {
-      wave_argmin(v && rj > cScan, d, lane, j, &bd, &bo, &bj);
-      if (bj >= 0 && bd < m2) { m2 = bd; i2 = bj; }
+    const unsigned bm = group_ballot(inr && rj > cScan + 2, gbase);
+    const int lim = bm ? (__ffs(bm) - 1) : kG;
+    if (inr && g < lim) {
+      const float d = line_d2(p, sel);
+      const int rank = j - ci;
+      if (surf) {
+        if (rj <= cScan) { if (d < m2) { m2 = d; r2 = rank; i2 = j; } }
+        else if (d < m3) { m3 = d; r3 = rank; i3 = j; }
+      } else if (rj > cScan && d < m2) { m2 = d; r2 = rank; i2 = j; }
     }
     if (bm) break;
   }
-  // backward
-  for (int j0 = ci - 1; j0 >= 0; j0 -= 64) {
-    const int j = j0 - lane;
+  const int fwdSpan = jend - ci;
+  for (int j0 = ci - 1; j0 >= 0; j0 -= kG) {
+    const int j = j0 - g;
     const bool inr = j >= 0;
     float4 p = make_float4(0, 0, 0, 0);
     int rj = 0;
     if (inr) { p = last[j]; rj = (int)p.w; }
-    const bool brk = inr && (double)rj < cScan - 2.5;
-    const unsigned long long bm = __ballot(brk);
-    const int lim = bm ? (__ffsll((long long)bm) - 1) : 64;
-    const bool v = inr && lane < lim;
-    const float d = v ? line_d2(p, sel) : 0.f;
-    float bd; int bo, bj;
-    if (surf) {
-      wave_argmin(v && rj >= cScan, d, lane, j, &bd, &bo, &bj);
-      if (bj >= 0 && bd < m2) { m2 = bd; i2 = bj; }
-      wave_argmin(v && rj < cScan, d, lane, j, &bd, &bo, &bj);
-      if (bj >= 0 && bd < m3) { m3 = bd; i3 = bj; }
-    } else {
-      wave_argmin(v && rj < cScan, d, lane, j, &bd, &bo, &bj);
-      if (bj >= 0 && bd < m2) { m2 = bd; i2 = bj; }
+    const unsigned bm = group_ballot(inr && rj < cScan - 2, gbase);
+    const int lim = bm ? (__ffs(bm) - 1) : kG;
+    if (inr && g < lim) {
+      const float d = line_d2(p, sel);
+      const int rank = fwdSpan + (ci - j);
+      if (surf) {
+        if (rj >= cScan) { if (d < m2) { m2 = d; r2 = rank; i2 = j; } }
+        else if (d < m3) { m3 = d; r3 = rank; i3 = j; }
+      } else if (rj < cScan && d < m2) { m2 = d; r2 = rank; i2 = j; }
     }
     if (bm) break;
   }
+  group_lex_min3(m2, r2, i2);
+  if (surf) group_lex_min3(m3, r3, i3);
   *o2 = i2;
-  *o3 = i3;
+  *o3 = surf ? i3 : -1;
 }
 
 // ---------------------------------------------------------------- reduction
-// 9 doubles (AtA upper triangle 6 + AtB 3) summed over the block.
-__device__ void block_sum9(double v[9], const OdomLds& L, double out[9]) {
+// 9 doubles (AtA upper triangle 6 + AtB 3) + the row count over the block.
+__device__ __forceinline__ void block_sum9(double v[9], int m, const OdomLds& L, double out[9], int* mt) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int k = 0; k < 9; ++k)
     for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
-  if (lane == 0)
+  for (int o = 32; o > 0; o >>= 1) m += __shfl_xor(m, o, 64);
+  if (lane == 0) {
     for (int k = 0; k < 9; ++k) L.red[wave * 10 + k] = v[k];
+    L.red[wave * 10 + 9] = (double)m;
+  }
   __syncthreads();
   for (int k = 0; k < 9; ++k) {
     double s = 0;
     for (int w = 0; w < kOdomWaves; ++w) s += L.red[w * 10 + k];
     out[k] = s;
   }
-  __syncthreads();
+  double ms = 0;
+  for (int w = 0; w < kOdomWaves; ++w) ms += L.red[w * 10 + 9];
+  *mt = (int)ms;
 }
 
 struct ScanFeat {
@@ -514,12 +495,11 @@ struct ScanFeat {
 };
 
 // Shared tail of calculateTransformationSurf / Corner.  Thread 0 only.
-__device__ bool solve_step(float (&AtA)[3][3], float (&AtB)[3], int iter, OdomState* st,
+__device__ __forceinline__ void solve_step(float (&AtA)[3][3], float (&AtB)[3], int iter, OdomState* st,
                            float (&X)[3]) {
   float Aq[3][3];
   for (int a = 0; a < 3; ++a) for (int b = 0; b < 3; ++b) Aq[a][b] = AtA[a][b];
-  float bq[3] = {AtB[0], AtB[1], AtB[2]};
-  cv_solve_qr<3, 3>(Aq, bq, X);
+  cv_solve_qr<3, 3>(Aq, AtB, X);
   float (&P)[3][3] = *reinterpret_cast<float(*)[3][3]>(st->matP);
   if (iter == 0) {
     float E[3], V[3][3], V2[3][3], Ae[3][3];
@@ -543,49 +523,57 @@ __device__ bool solve_step(float (&AtA)[3][3], float (&AtB)[3], int iter, OdomSt
     float X2[3] = {X[0], X[1], X[2]};
     cv_matvec<3>(P, X2, X);
   }
-  return true;
 }
 
 __device__ __forceinline__ double r2d(double r) { return r * 180.0 / M_PI; }
 
-// One LM loop (surf: 25 iterations of findCorrespondingSurfFeatures +
-// calculateTransformationSurf; corner likewise).  updateTransformation :1666-1695.
-__device__ void lm_loop(bool surf, const ScanFeat& F, const float4* last, int lastN,
-                        const NNIndex& nn, OdomState* st, const OdomLds& L, const DevCfg& c) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+// One LM loop (surf: <= 25 x {findCorrespondingSurfFeatures;
+// calculateTransformationSurf}; corner likewise) — updateTransformation :1666-1695.
+__device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const float4* last, int lastN,
+                        const GridView& nn, OdomState* st, const OdomLds& L, int* gqi,
+                        const DevCfg& c, Stamp& S) {
+  const int tid = threadIdx.x;
   const float4* qp = surf ? F.flat : F.sharp;
   const int nQ = surf ? F.nFlat : F.nSharp;
   const int jend = min(nQ, lastN);  // the reference bounds by the query count (:1062, :1173)
+  int* qi = (nQ <= kLdsQ) ? L.qi : gqi;
+  const int qs = (nQ <= kLdsQ) ? kLdsQ : nQ;  // stride between the three index arrays
+  const int g = tid & (kG - 1), gbase = tid & 63 & ~(kG - 1), grp = tid / kG;
+  const int ngrp = blockDim.x / kG;
   for (int it = 0; it < 25; it++) {
-    // A: TransformToStart
-    for (int q = tid; q < nQ; q += blockDim.x) L.sel[q] = to_start(qp[q], st->transformCur);
-    __syncthreads();
-    // B: correspondences
-    if (it % 5 == 0) {
-      for (int q = wave; q < nQ; q += kOdomWaves) {
-        const float4 sel = L.sel[q];
-        int ci = nn_query_wave(nn, sel, c.nn_sq, L.stack + wave * 64);
-        if (ci >= lastN) ci = -1;  // stale tree over a smaller cloud
-        int i2 = -1, i3 = -1;
-        if (ci >= 0) scanline_wave(last, lastN, jend, ci, sel, surf, c.nn_sq, &i2, &i3);
-        if (lane == 0) { L.i1[q] = ci; L.i2[q] = i2; L.i3[q] = i3; }
-      }
-      __syncthreads();
-    }
-    // C + D: rows and normal equations
-    const float* tc = st->transformCur;
-    const Trig3 T = trig3(tc[0], tc[1], tc[2]);
-    const float srx = T.srx, crx = T.crx, sry = T.sry, cry = T.cry, srz = T.srz, crz = T.crz;
+    S.start();
+    S.count(surf ? P_ITERS_S : P_ITERS_C);
+    if (it % 5 == 0) S.count(P_NNR);
+    float tc[6];
+    for (int i = 0; i < 6; ++i) tc[i] = st->transformCur[i];
+    const float srx = lego_sinf(tc[0]), crx = lego_cosf(tc[0]);
+    const float sry = lego_sinf(tc[1]), cry = lego_cosf(tc[1]);
+    const float srz = lego_sinf(tc[2]), crz = lego_cosf(tc[2]);
     const float tx = tc[3], ty = tc[4], tz = tc[5];
     double acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     int mloc = 0;
+    if (it % 5 == 0) {
+      // nearest neighbour + scan-line search, one 32-lane group per query
+      for (int q = grp; q < nQ; q += ngrp) {
+        const float4 sel = to_start(qp[q], tc);
+        int i1 = grid_nn(nn, sel, c.nn_sq, g, S.prof);
+        if (i1 >= lastN) i1 = -1;  // stale snapshot of a larger cloud
+        int i2 = -1, i3 = -1;
+        if (i1 >= 0) scanline_group(last, jend, i1, sel, surf, c.nn_sq, g, gbase, &i2, &i3);
+        if (g == 0) { qi[q] = i1; qi[qs + q] = i2; qi[2 * qs + q] = i3; }
+      }
+      __syncthreads();
+      S.add(P_QUERY);
+    }
     for (int q = tid; q < nQ; q += blockDim.x) {
-      const float4 sel = L.sel[q];
+      const float4 po = qp[q];
+      const float4 sel = to_start(po, tc);
+      const int i1 = qi[q], i2 = qi[qs + q], i3 = qi[2 * qs + q];
       float4 cf;
       bool ok = false;
       if (surf) {
-        if (L.i2[q] >= 0 && L.i3[q] >= 0) {
-          const float4 t1 = last[L.i1[q]], t2 = last[L.i2[q]], t3 = last[L.i3[q]];
+        if (i2 >= 0 && i3 >= 0) {
+          const float4 t1 = last[i1], t2 = last[i2], t3 = last[i3];
           float pa = (t2.y - t1.y) * (t3.z - t1.z) - (t3.y - t1.y) * (t2.z - t1.z);
           float pb = (t2.z - t1.z) * (t3.x - t1.x) - (t3.z - t1.z) * (t2.x - t1.x);
           float pc = (t2.x - t1.x) * (t3.y - t1.y) - (t3.x - t1.x) * (t2.y - t1.y);
@@ -603,8 +591,8 @@ __device__ void lm_loop(bool surf, const ScanFeat& F, const float4* last, int la
           }
         }
       } else {
-        if (L.i2[q] >= 0) {
-          const float4 t1 = last[L.i1[q]], t2 = last[L.i2[q]];
+        if (i2 >= 0) {
+          const float4 t1 = last[i1], t2 = last[i2];
           const float x0 = sel.x, y0 = sel.y, z0 = sel.z;
           const float x1 = t1.x, y1 = t1.y, z1 = t1.z, x2 = t2.x, y2 = t2.y, z2 = t2.z;
           const float m11 = ((x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1));
@@ -625,7 +613,6 @@ __device__ void lm_loop(bool surf, const ScanFeat& F, const float4* last, int la
         }
       }
       if (ok) {
-        const float4 po = qp[q];
         float a0, a1, a2;
         if (surf) {  // :1291-1321
           const float a1_ = crx * sry * srz, a2_ = crx * crz * sry, a3 = srx * sry, a4 = tx * a1_ - ty * a2_ - tz * a3;
@@ -660,16 +647,11 @@ __device__ void lm_loop(bool surf, const ScanFeat& F, const float4* last, int la
         mloc++;
       }
     }
-    // row count
-    int mw = mloc;
-    for (int o = 32; o > 0; o >>= 1) mw += __shfl_xor(mw, o, 64);
-    if (lane == 0) L.stack[wave * 64] = mw;
     double tot[9];
-    block_sum9(acc, L, tot);
+    int M;
+    block_sum9(acc, mloc, L, tot, &M);
+    S.add(surf ? (it % 5 == 0 ? P_SURF_NN : P_SURF) : (it % 5 == 0 ? P_CORN_NN : P_CORN));
     if (tid == 0) {
-      int M = 0;
-      for (int w = 0; w < kOdomWaves; ++w) M += L.stack[w * 64];
-      L.n[N_M] = M;
       L.n[N_BREAK] = 0;
       if (M >= 10) {
         float AtA[3][3] = {{(float)tot[0], (float)tot[1], (float)tot[2]},
@@ -700,25 +682,49 @@ __device__ void lm_loop(bool surf, const ScanFeat& F, const float4* last, int la
       __threadfence_block();
     }
     __syncthreads();
+    S.add(P_SOLVE);
     const int brk = L.n[N_BREAK];
     __syncthreads();
     if (brk) break;
   }
 }
 
+// Copies the last clouds into LDS when they fit.
+struct Resident {
+  const float4* lastS;
+  const float4* lastC;
+  GridView nnS, nnC;
+};
+
+__device__ __forceinline__ void make_resident(const OdomBufs& ob, const OdomState* st, const OdomLds& L, Resident& R) {
+  const int tid = threadIdx.x;
+  const int ns = st->surfLastNum, nc = st->cornerLastNum;
+  R.lastS = ns <= kLdsSurf ? L.lastS : ob.surfLast;
+  R.lastC = nc <= kLdsCorner ? L.lastC : ob.cornerLast;
+  R.nnS = GridView{ob.gS.keys, ob.gS.cnt, ob.gS.start, ob.gS.pts, ob.gS.idx,
+                   grid_table_size(st->nnSurfNum), st->nnSurfNum};
+  R.nnC = GridView{ob.gC.keys, ob.gC.cnt, ob.gC.start, ob.gC.pts, ob.gC.idx,
+                   grid_table_size(st->nnCornerNum), st->nnCornerNum};
+  if (ns <= kLdsSurf) for (int t = tid; t < ns; t += blockDim.x) L.lastS[t] = ob.surfLast[t];
+  if (nc <= kLdsCorner) for (int t = tid; t < nc; t += blockDim.x) L.lastC[t] = ob.cornerLast[t];
+  __syncthreads();
+}
+
 __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob, DevCfg c, int B,
-                                                      unsigned long long* gkeys) {
+                                                      unsigned long long* gkeys, int* gqi,
+                                                      unsigned long long* prof) {
+  Stamp S{prof, 0};
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   const OdomLds L = odom_carve(lds_raw);
   const int tid = threadIdx.x;
-  OdomState* st = ob.st;
-  NNIndex nnC{ob.nnCorner, ob.nnCornerIdx, ob.nnCornerBox, st->nnCornerNum, 0};
-  NNIndex nnS{ob.nnSurf, ob.nnSurfIdx, ob.nnSurfBox, st->nnSurfNum, 0};
-  // L2 of the stored trees follows from n
-  {
-    int l2 = 1; while (l2 < (nnC.n + kLeaf - 1) / kLeaf) l2 <<= 1; nnC.L2 = l2;
-    l2 = 1; while (l2 < (nnS.n + kLeaf - 1) / kLeaf) l2 <<= 1; nnS.L2 = l2;
-  }
+  static_assert(sizeof(OdomState) <= 128, "OdomState LDS slot");
+  OdomState* st = L.st;
+  if (tid < (int)(sizeof(OdomState) / 4)) ((int*)st)[tid] = ((const int*)ob.st)[tid];
+  __syncthreads();
+  Resident R;
+  S.start();
+  make_resident(ob, st, L, R);
+  S.add(P_RESID);
   const ImuEnd im{1.f, 1.f, 1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 1.f, 0.f, 1.f, 0.f};
   for (int b = 0; b < B; ++b) {
     ScanFeat F;
@@ -729,97 +735,94 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     F.lflat = bb.f_lflat + (size_t)b * c.P; F.nLF = fc[3];
     float4* cEnd = ob.cornerEnd + (size_t)b * ob.capLS;
     float4* sEnd = ob.surfEnd + (size_t)b * c.P;
-    if (!st->inited) {
-      // checkSystemInitialization :1605-1637 (no TransformToEnd)
-      for (int t = tid; t < F.nLS; t += blockDim.x) { ob.cornerLast[t] = F.lsharp[t]; cEnd[t] = F.lsharp[t]; }
-      for (int t = tid; t < F.nLF; t += blockDim.x) { ob.surfLast[t] = F.lflat[t]; sEnd[t] = F.lflat[t]; }
-      __syncthreads();
-      nn_build(ob.cornerLast, F.nLS, nnC, L, gkeys);
-      nn_build(ob.surfLast, F.nLF, nnS, L, gkeys);
+    const bool init = !st->inited;
+    if (!init) {
+      // updateInitialGuess is a no-op without IMU
+      if (st->cornerLastNum >= 10 && st->surfLastNum >= 100) {
+        lm_loop(true, F, R.lastS, st->surfLastNum, R.nnS, st, L, gqi, c, S);
+        lm_loop(false, F, R.lastC, st->cornerLastNum, R.nnC, st, L, gqi, c, S);
+      }
+      // integrateTransformation :1697-1725
+      S.start();
       if (tid == 0) {
-        st->cornerLastNum = F.nLS;
-        st->surfLastNum = F.nLF;
-        st->nnCornerNum = F.nLS;
-        st->nnSurfNum = F.nLF;
-        st->transformSum[0] += 0.0f;  // += imuPitchStart
-        st->transformSum[2] += 0.0f;  // += imuRollStart
-        st->inited = 1;
-        ob.validOut[b] = 0;
-        ob.pubOut[b] = 0;
-        for (int i = 0; i < 6; ++i) { ob.sumOut[b * 6 + i] = st->transformSum[i]; ob.curOut[b * 6 + i] = st->transformCur[i]; }
+        float* ts = st->transformSum;
+        const float* tc = st->transformCur;
+        float rx, ry, rz;
+        accumulate_rotation(ts[0], ts[1], ts[2], -tc[0], -tc[1], -tc[2], rx, ry, rz);
+        const float x1 = lego_cosf(rz) * (tc[3] - 0.0f) - lego_sinf(rz) * (tc[4] - 0.0f);
+        const float y1 = lego_sinf(rz) * (tc[3] - 0.0f) + lego_cosf(rz) * (tc[4] - 0.0f);
+        const float z1 = tc[5] - 0.0f;
+        const float x2 = x1;
+        const float y2 = lego_cosf(rx) * y1 - lego_sinf(rx) * z1;
+        const float z2 = lego_sinf(rx) * y1 + lego_cosf(rx) * z1;
+        const float tx = ts[3] - (lego_cosf(ry) * x2 + lego_sinf(ry) * z2);
+        const float ty = ts[4] - y2;
+        const float tz = ts[5] - (-lego_sinf(ry) * x2 + lego_cosf(ry) * z2);
+        plugin_imu_rotation(rx, ry, rz, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, rx, ry, rz);
+        ts[0] = rx; ts[1] = ry; ts[2] = rz; ts[3] = tx; ts[4] = ty; ts[5] = tz;
         __threadfence_block();
       }
       __syncthreads();
-      continue;
+      S.add(P_INTEG);
     }
-    // updateInitialGuess: a no-op without IMU
-    if (st->cornerLastNum >= 10 && st->surfLastNum >= 100) {
-      lm_loop(true, F, ob.surfLast, st->surfLastNum, nnS, st, L, c);
-      lm_loop(false, F, ob.cornerLast, st->cornerLastNum, nnC, st, L, c);
-    }
-    // integrateTransformation :1697-1725
-    if (tid == 0) {
-      float* ts = st->transformSum;
-      const float* tc = st->transformCur;
-      float rx, ry, rz;
-      accumulate_rotation(ts[0], ts[1], ts[2], -tc[0], -tc[1], -tc[2], rx, ry, rz);
-      const float x1 = lego_cosf(rz) * (tc[3] - 0.0f) - lego_sinf(rz) * (tc[4] - 0.0f);
-      const float y1 = lego_sinf(rz) * (tc[3] - 0.0f) + lego_cosf(rz) * (tc[4] - 0.0f);
-      const float z1 = tc[5] - 0.0f;
-      const float x2 = x1;
-      const float y2 = lego_cosf(rx) * y1 - lego_sinf(rx) * z1;
-      const float z2 = lego_sinf(rx) * y1 + lego_cosf(rx) * z1;
-      const float tx = ts[3] - (lego_cosf(ry) * x2 + lego_sinf(ry) * z2);
-      const float ty = ts[4] - y2;
-      const float tz = ts[5] - (-lego_sinf(ry) * x2 + lego_cosf(ry) * z2);
-      plugin_imu_rotation(rx, ry, rz, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, rx, ry, rz);
-      ts[0] = rx; ts[1] = ry; ts[2] = rz; ts[3] = tx; ts[4] = ty; ts[5] = tz;
-      ob.validOut[b] = 1;
-      for (int i = 0; i < 6; ++i) { ob.sumOut[b * 6 + i] = ts[i]; ob.curOut[b * 6 + i] = tc[i]; }
-      __threadfence_block();
-    }
-    __syncthreads();
-    // publishCloudsLast :1759-1815
+    S.start();
+    // hand-off: checkSystemInitialization (:1605-1637, no TransformToEnd) or
+    // publishCloudsLast (:1759-1815)
+    float tcur[6];
+    for (int i = 0; i < 6; ++i) tcur[i] = st->transformCur[i];
     for (int t = tid; t < F.nLS; t += blockDim.x) {
-      const float4 p = to_end(F.lsharp[t], st->transformCur, im);
+      const float4 p = init ? F.lsharp[t] : to_end(F.lsharp[t], tcur, im);
       ob.cornerLast[t] = p;
       cEnd[t] = p;
     }
     for (int t = tid; t < F.nLF; t += blockDim.x) {
-      const float4 p = to_end(F.lflat[t], st->transformCur, im);
+      const float4 p = init ? F.lflat[t] : to_end(F.lflat[t], tcur, im);
       ob.surfLast[t] = p;
       sEnd[t] = p;
     }
     __syncthreads();
-    const bool rebuild = F.nLS > 10 && F.nLF > 100;
+    S.add(P_TOEND);
+    const bool rebuild = init || (F.nLS > 10 && F.nLF > 100);
+    unsigned long long tb = 0;
+    if (prof && tid == 0) tb = wall_clock64();
     if (rebuild) {
-      nn_build(ob.cornerLast, F.nLS, nnC, L, gkeys);
-      nn_build(ob.surfLast, F.nLF, nnS, L, gkeys);
+      grid_build(ob.cornerLast, F.nLS, ob.gC.keys, ob.gC.cnt, ob.gC.start, ob.gC.slot, ob.gC.pts, ob.gC.idx, L);
+      grid_build(ob.surfLast, F.nLF, ob.gS.keys, ob.gS.cnt, ob.gS.start, ob.gS.slot, ob.gS.pts, ob.gS.idx, L);
     }
+    if (prof && tid == 0) prof[P_BUILD] += wall_clock64() - tb;
     if (tid == 0) {
       st->cornerLastNum = F.nLS;
       st->surfLastNum = F.nLF;
       if (rebuild) { st->nnCornerNum = F.nLS; st->nnSurfNum = F.nLF; }
-      st->frameCount++;
       int pub = 0;
-      if (st->frameCount >= c.skip + 1) { st->frameCount = 0; pub = 1; }
+      if (init) {
+        st->transformSum[0] += 0.0f;  // += imuPitchStart
+        st->transformSum[2] += 0.0f;  // += imuRollStart
+        st->inited = 1;
+      } else {
+        st->frameCount++;
+        if (st->frameCount >= c.skip + 1) { st->frameCount = 0; pub = 1; }
+      }
+      ob.validOut[b] = init ? 0 : 1;
       ob.pubOut[b] = pub;
+      for (int i = 0; i < 6; ++i) { ob.sumOut[b * 6 + i] = st->transformSum[i]; ob.curOut[b * 6 + i] = st->transformCur[i]; }
       __threadfence_block();
     }
     __syncthreads();
+    S.start();
+    make_resident(ob, st, L, R);
+    S.add(P_RESID);
   }
+  __syncthreads();
+  if (tid < (int)(sizeof(OdomState) / 4)) ((int*)ob.st)[tid] = ((const int*)st)[tid];
 }
 
-size_t odom_nn_box_count(int npts) {
-  int l2 = 1;
-  while (l2 < (npts + kLeaf - 1) / kLeaf) l2 <<= 1;
-  return (size_t)4 * l2;  // 2 float4 per node, 2*L2 nodes
-}
+size_t odom_grid_table(int npts) { return (size_t)grid_table_size(npts); }
 
 void launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int B, hipStream_t s,
-                 StageTimer* tm, unsigned long long* gkeys) {
+                 StageTimer* tm, unsigned long long* gkeys, int* gqi, unsigned long long* prof) {
   tm->mark("odom.lm", s);
-  k_odom<<<1, kOdomThreads, odom_lds_bytes(), s>>>(bb, ob, c, B, gkeys);
+  k_odom<<<1, kOdomThreads, odom_lds_bytes(), s>>>(bb, ob, c, B, gkeys, gqi, prof);
 }
 
 }  // namespace lego

@@ -168,7 +168,8 @@ def oracle_lib() -> C.CDLL:
 
 HIP_EXPORTS = ["lego_sensor_preset", "lego_create", "lego_destroy", "lego_reset",
                "lego_ip_process", "lego_fa_process", "lego_odom_batch", "lego_batch_fetch",
-               "lego_mo_set_map", "lego_mo_process", "lego_last_error", "lego_stage_times"]
+               "lego_mo_set_map", "lego_mo_process", "lego_last_error", "lego_stage_times",
+               "lego_odom_profile"]
 
 
 def hip_lib() -> C.CDLL:
@@ -188,6 +189,7 @@ def hip_lib() -> C.CDLL:
     lib.lego_mo_set_map.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32]
     lib.lego_mo_process.argtypes = [C.c_void_p, C.POINTER(FaOut), C.POINTER(MoOut)]
     lib.lego_last_error.restype = C.c_char_p
+    lib.lego_odom_profile.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
     lib.lego_stage_times.argtypes = [C.c_void_p, C.POINTER(C.c_char_p), f32p, C.c_int32,
                                      C.POINTER(C.c_int32)]
     return lib

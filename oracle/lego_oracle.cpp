@@ -983,15 +983,22 @@ struct FeatureAssociation {
   // updateTransformation :1666-1695
   void updateTransformation() {
     if (cornerLastNum < 10 || surfLastNum < 100) return;
+    statScans++;
     for (int it = 0; it < 25; it++) {
       laserCloudOri.clear(); coeffSel.clear();
+      statSurfIters++;
+      if (it % 5 == 0) statNNRounds++;
       findCorrespondingSurf(it);
+      statRows += (long)laserCloudOri.size();
       if (laserCloudOri.size() < 10) continue;
       if (!calcSurf(it)) break;
     }
     for (int it = 0; it < 25; it++) {
       laserCloudOri.clear(); coeffSel.clear();
+      statCornerIters++;
+      if (it % 5 == 0) statNNRounds++;
       findCorrespondingCorner(it);
+      statRows += (long)laserCloudOri.size();
       if (laserCloudOri.size() < 10) continue;
       if (!calcCorner(it)) break;
     }
@@ -1093,6 +1100,7 @@ struct FeatureAssociation {
     return LEGO_OK;
   }
   std::vector<Pt> pubSharp, pubLessSharp, pubFlat, pubLessFlat;
+  long statSurfIters = 0, statCornerIters = 0, statNNRounds = 0, statScans = 0, statRows = 0;
 };
 
 #include "oracle_mo.inc"
@@ -1242,5 +1250,12 @@ extern "C" int lego_oracle_mo_process(lego_oracle* o, const lego_fa_out* in, leg
   out->n_corner_scan_ds = (int32_t)mo.cornerLastDS.size();
   out->n_surf_scan_ds = (int32_t)mo.surfTotalLastDS.size();
   out->n_rows_last = mo.rowsLast;
+  return LEGO_OK;
+}
+
+extern "C" int lego_oracle_stats(lego_oracle* o, long* out5) {
+  if (!o || !out5) return LEGO_E_ARG;
+  out5[0] = o->fa->statScans; out5[1] = o->fa->statSurfIters; out5[2] = o->fa->statCornerIters;
+  out5[3] = o->fa->statNNRounds; out5[4] = o->fa->statRows;
   return LEGO_OK;
 }

@@ -30,6 +30,9 @@ int lego_oracle_mo_set_map(lego_oracle* o, const lego_point_xyzi* corner, int32_
                            const lego_point_xyzi* surf, int32_t n_surf);
 int lego_oracle_mo_process(lego_oracle* o, const lego_fa_out* in, lego_mo_out* out);
 
+/* LM statistics: scans, surf iterations, corner iterations, NN rounds, rows. */
+int lego_oracle_stats(lego_oracle* o, long* out5);
+
 /* Stand-alone pieces for known-answer tests. */
 int lego_oracle_voxel_grid(const lego_point_xyzi* in, int32_t n, float leaf,
                            int32_t pcl_sort, lego_point_xyzi* out, int32_t* n_out);
