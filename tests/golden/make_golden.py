@@ -1,0 +1,87 @@
+#!/usr/bin/env python3
+"""Regenerates tests/golden/*.npz from the CPU oracle (test infrastructure).
+
+The reference ships no golden data and cannot be built here (SURVEY.md §4,
+§8c), so these fixtures are the oracle's own outputs on seeded synthetic
+inputs.  They pin the oracle against regressions and carry the inputs to the
+GPU box, where tests/test_golden.py checks the HIP product against them.
+
+  python tests/golden/make_golden.py
+"""
+import hashlib
+import importlib.util
+import sys
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parents[2]
+OUT = Path(__file__).resolve().parent
+
+
+def ffi():
+    spec = importlib.util.spec_from_file_location("legoffi", REPO / "lego-loam_amd" / "legoffi.py")
+    m = importlib.util.module_from_spec(spec)
+    sys.modules["legoffi"] = m
+    spec.loader.exec_module(m)
+    return m
+
+
+def sha(a) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def scan_fixture(L, sensor, seed, k, name, full=True):
+    sc = L.synth_cfg(sensor, seed)
+    pts, stamp = L.synth_scan(sc, k)
+    ora = L.Oracle(L.sensor_cfg(sensor))
+    ip = ora.ip(pts, stamp, images=True)
+    fa = ora.fa()
+    d = {"input": pts.view(np.uint8), "stamp": np.float64(stamp), "input_sha": np.bytes_(sha(pts))}
+    keys_ip = ["start_ring_index", "end_ring_index", "ground_flag", "col_ind", "range", "segmented", "outlier",
+               "label_image", "ground_image", "range_image"]
+    for key in keys_ip:
+        if full or key in ("start_ring_index", "end_ring_index"):
+            d["ip_" + key] = ip[key].view(np.uint8) if ip[key].dtype.names else ip[key]
+        d["sha_ip_" + key] = np.bytes_(sha(ip[key]))
+    d["orient"] = np.array([ip["start_orientation"], ip["end_orientation"], ip["orientation_diff"]], np.float32)
+    for key in ("sharp", "less_sharp", "flat", "less_flat"):
+        if full:
+            d["fa_" + key] = fa[key].view(np.uint8)
+        d["sha_fa_" + key] = np.bytes_(sha(fa[key]))
+    if not full:
+        del d["input"]
+    np.savez_compressed(OUT / f"{name}.npz", **d)
+
+
+def stream_fixture(L, sensor, seed, n, name):
+    sc = L.synth_cfg(sensor, seed)
+    ora = L.Oracle(L.sensor_cfg(sensor))
+    sums, counts, shas, in_shas = [], [], [], []
+    for k in range(n):
+        pts, stamp = L.synth_scan(sc, k)
+        in_shas.append(sha(pts))
+        ip = ora.ip(pts, stamp)
+        fa = ora.fa()
+        sums.append(fa["transform_sum"])
+        counts.append([len(ip["segmented"]), len(fa["sharp"]), len(fa["less_sharp"]), len(fa["flat"]),
+                       len(fa["less_flat"]), fa["odom_valid"], fa["publish_to_mapping"]])
+        shas.append(sha(np.concatenate([fa[k2].view(np.uint8) for k2 in
+                                        ("sharp", "less_sharp", "flat", "less_flat")])))
+    np.savez_compressed(OUT / f"{name}.npz", transform_sum=np.array(sums, np.float32),
+                        counts=np.array(counts, np.int32), feat_sha=np.array(shas, dtype="S64"),
+                        input_sha=np.array(in_shas, dtype="S64"), sensor=np.bytes_(sensor),
+                        seed=np.int64(seed))
+
+
+def main():
+    L = ffi()
+    scan_fixture(L, "VLP-16", 0, 0, "vlp16_seed0_scan0", full=True)
+    scan_fixture(L, "HDL-64E", 2, 0, "hdl64_seed2_scan0", full=False)
+    stream_fixture(L, "VLP-16", 1, 20, "vlp16_seed1_stream20")
+    for p in sorted(OUT.glob("*.npz")):
+        print(p.name, p.stat().st_size)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,21 @@
+/* Prints sizeof/offsetof of the C-ABI structs (include/lego_loam.h,
+ * include/lego_synth.h) so tests/test_abi.py can check the ctypes mirror. */
+#include <stddef.h>
+#include <stdio.h>
+#include "lego_loam.h"
+#include "lego_synth.h"
+#define S(t) printf(#t " %zu\n", sizeof(t))
+#define O(t, f) printf(#t "." #f " %zu\n", offsetof(t, f))
+int main(void) {
+  S(lego_point_xyzir); O(lego_point_xyzir, intensity); O(lego_point_xyzir, ring);
+  S(lego_point_xyzi);
+  S(lego_sensor_cfg); O(lego_sensor_cfg, mapping_process_interval); O(lego_sensor_cfg, skip_frame_num);
+  S(lego_cloud_info); O(lego_cloud_info, segmented_cloud_range);
+  S(lego_ip_out); O(lego_ip_out, n_segmented); O(lego_ip_out, label_image);
+  S(lego_fa_out); O(lego_fa_out, odom_valid); O(lego_fa_out, odom_quat); O(lego_fa_out, publish_to_mapping);
+  O(lego_fa_out, n_outlier_last);
+  S(lego_mo_out); O(lego_mo_out, transform_bef_mapped); O(lego_mo_out, n_rows_last);
+  S(lego_pose_rec); O(lego_pose_rec, n_segmented); O(lego_pose_rec, flags);
+  S(lego_synth_cfg); O(lego_synth_cfg, seed);
+  return 0;
+}

@@ -1,0 +1,105 @@
+"""Golden fixtures (tests/golden/*.npz, made by tests/golden/make_golden.py).
+
+CPU: the synthetic source and the oracle still reproduce them exactly.
+GPU: the HIP product reproduces them exactly (inputs travel in the fixture,
+so this holds even if the synthetic generator changes)."""
+import hashlib
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+GOLD = Path(__file__).resolve().parent / "golden"
+
+
+def sha(a) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def load(name):
+    return np.load(GOLD / f"{name}.npz", allow_pickle=False)
+
+
+def check_scan(L, g, ip, fa, full):
+    for key in ("start_ring_index", "end_ring_index", "ground_flag", "col_ind", "range", "segmented",
+                "outlier", "label_image", "ground_image", "range_image"):
+        assert sha(ip[key]) == g["sha_ip_" + key].item().decode(), key
+    np.testing.assert_array_equal(
+        np.array([ip["start_orientation"], ip["end_orientation"], ip["orientation_diff"]], np.float32).view(np.uint32),
+        g["orient"].view(np.uint32))
+    for key in ("sharp", "less_sharp", "flat", "less_flat"):
+        assert sha(fa[key]) == g["sha_fa_" + key].item().decode(), key
+    if full:
+        np.testing.assert_array_equal(ip["label_image"], g["ip_label_image"])
+        np.testing.assert_array_equal(ip["segmented"].view(np.uint8), g["ip_segmented"])
+
+
+def test_synth_reproduces_inputs(L):
+    g = load("vlp16_seed0_scan0")
+    pts, stamp = L.synth_scan(L.synth_cfg("VLP-16", 0), 0)
+    assert sha(pts) == g["input_sha"].item().decode()
+    s = load("vlp16_seed1_stream20")
+    sc = L.synth_cfg("VLP-16", 1)
+    for k in (0, 7, 19):
+        assert sha(L.synth_scan(sc, k)[0]) == s["input_sha"][k].decode()
+
+
+def test_oracle_reproduces_scan_fixture(L):
+    g = load("vlp16_seed0_scan0")
+    pts = g["input"].view(L.XYZIR_DTYPE)
+    ora = L.Oracle(L.sensor_cfg("VLP-16"))
+    ip = ora.ip(pts, float(g["stamp"]), images=True)
+    check_scan(L, g, ip, ora.fa(), True)
+
+
+def test_oracle_reproduces_hdl64_fixture(L):
+    g = load("hdl64_seed2_scan0")
+    pts, stamp = L.synth_scan(L.synth_cfg("HDL-64E", 2), 0)
+    assert sha(pts) == g["input_sha"].item().decode()
+    ora = L.Oracle(L.sensor_cfg("HDL-64E"))
+    ip = ora.ip(pts, stamp, images=True)
+    check_scan(L, g, ip, ora.fa(), False)
+
+
+def test_oracle_reproduces_stream_fixture(L):
+    s = load("vlp16_seed1_stream20")
+    sc = L.synth_cfg("VLP-16", 1)
+    ora = L.Oracle(L.sensor_cfg("VLP-16"))
+    for k in range(len(s["counts"])):
+        pts, stamp = L.synth_scan(sc, k)
+        ip = ora.ip(pts, stamp)
+        fa = ora.fa()
+        np.testing.assert_array_equal(fa["transform_sum"].view(np.uint32), s["transform_sum"][k].view(np.uint32))
+        feats = np.concatenate([fa[key].view(np.uint8) for key in ("sharp", "less_sharp", "flat", "less_flat")])
+        assert sha(feats) == s["feat_sha"][k].decode()
+
+
+@pytest.mark.gpu
+def test_product_reproduces_scan_fixture(L):
+    g = load("vlp16_seed0_scan0")
+    pts = g["input"].view(L.XYZIR_DTYPE)
+    gpu = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=len(pts) + 16)
+    ip = gpu.ip(pts, float(g["stamp"]), images=True)
+    check_scan(L, g, ip, gpu.fa(), True)
+    gpu.close()
+
+
+@pytest.mark.gpu
+def test_product_reproduces_stream_fixture(L):
+    """Features bit-exact per scan; pose within 1e-4 (north star), and the
+    number of scans whose pose is bit-exact is reported."""
+    s = load("vlp16_seed1_stream20")
+    sc = L.synth_cfg("VLP-16", 1)
+    gpu = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=40000)
+    exact = 0
+    for k in range(len(s["counts"])):
+        pts, stamp = L.synth_scan(sc, k)
+        gpu.ip(pts, stamp)
+        fa = gpu.fa()
+        feats = np.concatenate([fa[key].view(np.uint8) for key in ("sharp", "less_sharp", "flat", "less_flat")])
+        assert sha(feats) == s["feat_sha"][k].decode(), k
+        d = np.abs(fa["transform_sum"].astype(np.float64) - s["transform_sum"][k])
+        assert d.max() <= 1e-4, (k, d)
+        exact += int(np.array_equal(fa["transform_sum"].view(np.uint32), s["transform_sum"][k].view(np.uint32)))
+    print(f"bit-exact poses: {exact}/{len(s['counts'])}")
+    gpu.close()

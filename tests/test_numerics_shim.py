@@ -1,0 +1,49 @@
+"""The float libm restatement (lego_numerics.h) that both the oracle and the
+gfx950 kernels use must equal this host's glibc bit for bit — the reference
+calls glibc's atan2f/sinf/cosf/asinf on its hot path.
+LEGO_EXHAUSTIVE=1 checks every float (≈1 min on 8 cores)."""
+import os
+import subprocess
+from pathlib import Path
+
+import pytest
+
+REPO = Path(__file__).resolve().parent.parent
+
+
+def _build(tmp_path, name, src):
+    exe = tmp_path / name
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-pthread", str(src), "-o", str(exe)],
+                   check=True)
+    return exe
+
+
+def test_libm_shim_matches_glibc(tmp_path):
+    exe = _build(tmp_path, "shim_check", REPO / "tests/native/shim_check.cpp")
+    stride = "1" if os.environ.get("LEGO_EXHAUSTIVE") else "97"
+    r = subprocess.run([str(exe), stride, "2000000"], capture_output=True, text=True, timeout=900)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout
+
+
+def test_introsort_port_matches_std_sort(tmp_path):
+    exe = _build(tmp_path, "introsort_check", REPO / "tests/native/introsort_check.cpp")
+    r = subprocess.run([str(exe), "20000"], capture_output=True, text=True, timeout=600)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout
+
+
+def test_segmentation_alpha_constants(L):
+    """sin/cos of segmentAlphaX/Y (imageProjection.cpp:421) — bit patterns
+    recorded in SURVEY.md §9.3 for VLP-16."""
+    import numpy as np
+
+    cfg = L.sensor_cfg("VLP-16")
+    lib = L.oracle_lib()
+    sx, cx = lib.lego_oracle_sinf(cfg.segment_alpha_x), lib.lego_oracle_cosf(cfg.segment_alpha_x)
+    sy, cy = lib.lego_oracle_sinf(cfg.segment_alpha_y), lib.lego_oracle_cosf(cfg.segment_alpha_y)
+    assert float(np.float32(sx)).hex() == "0x1.c986d40000000p-9"
+    assert float(np.float32(cx)).hex() == "0x1.ffff340000000p-1"
+    assert float(np.float32(sy)).hex() == "0x1.1de58c0000000p-5"
+    assert float(np.float32(cy)).hex() == "0x1.ffb0280000000p-1"
+    assert float(np.float32(cfg.segment_theta)).hex() == "0x1.0c15240000000p+0"  # 0x3f860a92

@@ -1,0 +1,138 @@
+"""Known-answer tests for the CPU oracle, derived by hand from the reference
+source (the reference ships no tests or golden data — SURVEY.md §4).  Each
+case names the lines whose behaviour it pins."""
+import math
+
+import numpy as np
+import pytest
+
+H, N, G = 1800, 16, 7  # VLP-16 (utility.h:63-68)
+
+
+def pt(L, ring, col, rng, elev_deg=None, inten=0.0):
+    """A point that projects to (ring, col) at range rng: column centre azimuth
+    theta = 0.2*col - 180 deg (imageProjection.cpp:235-237 inverted)."""
+    th = math.radians(0.2 * col - 180.0)
+    el = math.radians(-15.0 + 2.0 * ring if elev_deg is None else elev_deg)
+    p = np.zeros(1, dtype=L.XYZIR_DTYPE)
+    p["x"] = rng * math.cos(el) * math.cos(th)
+    p["y"] = rng * math.cos(el) * math.sin(th)
+    p["z"] = rng * math.sin(el)
+    p["intensity"] = inten
+    p["ring"] = ring
+    return p
+
+
+def run_ip(L, pts):
+    ora = L.Oracle(L.sensor_cfg("VLP-16"))
+    return ora.ip(np.concatenate(pts), 0.0, images=True)
+
+
+def idx(r, c):
+    return r * H + c
+
+
+def test_projection_last_writer_wins(L):
+    """:219-256 — ring -> row, atan2f -> column, range < 1 m dropped, ring >=
+    N_SCAN dropped, later points overwrite earlier ones, intensity = row + col/1e4."""
+    pts = [pt(L, 3, 900, 10.0), pt(L, 3, 900, 20.0),  # same pixel: the second wins
+           pt(L, 5, 1000, 0.5),                         # below sensorMinimumRange
+           pt(L, 4, 450, 7.0)]
+    bad = pt(L, 3, 100, 5.0)
+    bad["ring"] = 16                                    # rowIdn >= N_SCAN
+    out = run_ip(L, pts + [bad])
+    r = out["range_image"]
+    assert r[idx(3, 900)] == pytest.approx(20.0, abs=1e-5)
+    assert r[idx(4, 450)] == pytest.approx(7.0, abs=1e-5)
+    assert r[idx(5, 1000)] == np.finfo(np.float32).max
+    assert r[idx(3, 100)] == np.finfo(np.float32).max
+    fc = out["full_cloud"]
+    assert fc["intensity"][idx(3, 900)] == np.float32(3 + 900 / 10000.0)
+    assert fc["intensity"][idx(4, 450)] == np.float32(4 + 450 / 10000.0)
+    assert fc["intensity"][idx(5, 1000)] == -1.0 and np.isnan(fc["x"][idx(5, 1000)])
+    assert (r < np.finfo(np.float32).max).sum() == 2
+
+
+def test_ground_overwrite_semantics(L):
+    """:267-291 — column walk i = 0..g-1: an invalid pair writes -1 at row i,
+    overwriting the 1 the previous (valid, flat) pair wrote there."""
+    col = 900
+    pts = []
+    for ring in range(4):  # rows 0..3 on the plane z = -0.6
+        el = math.radians(-15.0 + 2.0 * ring)
+        pts.append(pt(L, ring, col, 0.6 / math.sin(-el)))
+    for ring in (5, 6, 7):  # a wall at 5 m: steep pairs
+        el = math.radians(-15.0 + 2.0 * ring)
+        pts.append(pt(L, ring, col, 5.0 / math.cos(el)))
+    out = run_ip(L, pts)
+    g = out["ground_image"].reshape(N, H)[:, col]
+    np.testing.assert_array_equal(g[:8], [1, 1, 1, -1, -1, 0, 0, 0])
+    assert (g[8:] == 0).all()
+    lab = out["label_image"].reshape(N, H)[:, col]
+    assert (lab[:3] == -1).all()          # ground
+    assert lab[4] == -1                   # empty pixel (range FLT_MAX)
+
+
+def test_segmentation_validity_rules(L):
+    """:370-460 — components of the 4-neighbourhood with column wrap; valid if
+    size >= 30 or (size >= 5 and >= 3 distinct rows among the PUSHED pixels:
+    lineCountFlag is never set for the seed, :431); labels count valid
+    components in raster order of their seeds; invalid ones become 999999."""
+    pts = []
+    # A: 30 pixels in row 10, cols 100..129, range 10 -> valid
+    pts += [pt(L, 10, c, 10.0) for c in range(100, 130)]
+    # B: seed (9,300) alone on its row, pushed rows {10, 11}: 5 px, 2 lines -> INVALID
+    pts += [pt(L, r, c, 10.0) for r, c in [(9, 300), (10, 300), (11, 300), (11, 301), (11, 302)]]
+    # C: seed (9,500); pushed rows {9, 10, 11, 12}: 5 px, 4 lines -> valid
+    pts += [pt(L, r, c, 10.0) for r, c in [(9, 500), (9, 501), (10, 500), (11, 500), (12, 500)]]
+    # D: 4 pixels -> invalid
+    pts += [pt(L, 13, c, 10.0) for c in range(700, 704)]
+    # E: 30 pixels across the column wrap (row 14, cols 1790..1799 and 0..19) -> valid
+    pts += [pt(L, 14, c, 10.0) for c in list(range(1790, 1800)) + list(range(0, 20))]
+    # F: range jump breaks the edge test: two singletons
+    pts += [pt(L, 15, 900, 10.0), pt(L, 15, 901, 20.0)]
+    out = run_ip(L, pts)
+    lab = out["label_image"].reshape(N, H)
+    # raster order of seeds: C (9,500) < A (10,100) < E (14,0)
+    assert (lab[10, 100:130] == 2).all()
+    for r, c in [(9, 300), (10, 300), (11, 300), (11, 301), (11, 302)]:
+        assert lab[r, c] == 999999
+    for r, c in [(9, 500), (9, 501), (10, 500), (11, 500), (12, 500)]:
+        assert lab[r, c] == 1
+    assert (lab[13, 700:704] == 999999).all()
+    assert (lab[14, 1790:1800] == 3).all() and (lab[14, 0:20] == 3).all()
+    assert lab[15, 900] == 999999 and lab[15, 901] == 999999
+    # segmented cloud = valid labels (no ground here), row-major; outliers: invalid,
+    # row > g and col % 5 == 0 (:328-334)
+    assert len(out["segmented"]) == 30 + 5 + 30
+    outl_cols = sorted(int(round(float(i) % 1 * 1e4)) for i in out["outlier"]["intensity"])
+    # B's (9|10|11, 300), D's (13, 700), F's (15, 900)
+    assert outl_cols == [300, 300, 300, 700, 900]
+    # cloud_info ring indices (:323, :354): start = count_before - 1 + 5, end = count_after - 1 - 5
+    sri, eri = out["start_ring_index"], out["end_ring_index"]
+    counts = np.bincount(np.floor(out["segmented"]["intensity"]).astype(int), minlength=N)
+    before = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    np.testing.assert_array_equal(sri, before - 1 + 5)
+    np.testing.assert_array_equal(eri, np.cumsum(counts) - 1 - 5)
+
+
+def test_voxel_grid_centroids(L):
+    """pcl::VoxelGrid: ijk = floor(p/leaf) - floor(min/leaf), idx = i + j*dx + k*dx*dy,
+    output ordered by idx, centroid = float sum / count (PCL 1.8 voxel_grid.hpp)."""
+    import ctypes as C
+
+    pts = np.array([(0.05, 0.05, 0.05, 1.0), (0.15, 0.1, 0.1, 3.0), (0.25, 0.0, 0.0, 5.0),
+                    (0.05, 0.45, 0.0, 7.0)], dtype=L.XYZI_DTYPE)
+    out = np.zeros(8, dtype=L.XYZI_DTYPE)
+    n = C.c_int32()
+    lib = L.oracle_lib()
+    assert lib.lego_oracle_voxel_grid(pts.ctypes.data, len(pts), 0.2, 0, out.ctypes.data, C.byref(n)) == 0
+    f = np.float32
+    # voxels (i,j,k): p0,p1 -> (0,0,0); p2 -> (1,0,0); p3 -> (0,2,0); idx = i + j*dx, dx = 2
+    exp = [((f(0.05) + f(0.15)) / f(2), (f(0.05) + f(0.1)) / f(2), (f(0.05) + f(0.1)) / f(2), f(2.0)),
+           (f(0.25), f(0.0), f(0.0), f(5.0)),
+           (f(0.05), f(0.45), f(0.0), f(7.0))]
+    got = out[: n.value]
+    assert n.value == 3
+    for g_, e in zip(got, exp):
+        assert tuple(np.float32(v) for v in g_) == tuple(np.float32(v) for v in e)
