@@ -184,7 +184,12 @@ int lego_fa_process(lego_ctx* ctx, const lego_ip_out* in, lego_fa_out* out);
 /* Device-resident batch: scans k=0..nscans-1 are the points
  * pts[offsets[k] .. offsets[k+1]).  pts/offsets are device pointers when
  * on_device != 0, host pointers otherwise.  Runs ip + fa + odometry for every
- * scan in stream order and writes one record per scan to recs (host). */
+ * scan in stream order and writes one record per scan to recs (host).
+ * offsets[k+1] > offsets[k] (an empty scan is LEGO_E_ARG, nothing runs) and
+ * every scan <= max_points (LEGO_E_CAPACITY).  A non-finite point anywhere in
+ * the batch is LEGO_E_NOT_DENSE, detected on the device after the batch ran:
+ * the stream state is then undefined and the caller must lego_reset (the
+ * reference shuts the node down, imageProjection.cpp:174-177). */
 int lego_odom_batch(lego_ctx* ctx, const lego_point_xyzir* pts,
                     const int64_t* offsets, const double* stamps,
                     int32_t nscans, int32_t on_device, lego_pose_rec* recs);

@@ -83,7 +83,7 @@ struct lego_ctx {
   // host staging (library-owned outputs)
   std::vector<lego_point_xyzi> h_seg, h_outl, h_full, h_sharp, h_lsharp, h_flat, h_lflat;
   std::vector<lego_point_xyzi> h_cornerLast, h_surfLast, h_outlLast;
-  std::vector<int32_t> h_sri, h_eri, h_label;
+  std::vector<int32_t> h_sri, h_eri, h_label, h_bad;
   std::vector<uint8_t> h_gflag;
   std::vector<uint32_t> h_col;
   std::vector<float> h_range, h_rimg;
@@ -100,9 +100,9 @@ struct lego_ctx {
     return e;
   }
   ~lego_ctx() {
-    if (device >= 0) hipSetDevice(device);
-    for (void* p : allocs) hipFree(p);
-    if (stream) hipStreamDestroy(stream);
+    if (device >= 0) (void)hipSetDevice(device);
+    for (void* p : allocs) (void)hipFree(p);
+    if (stream) (void)hipStreamDestroy(stream);
   }
 };
 
@@ -242,6 +242,7 @@ int lego_create(const lego_sensor_cfg* cfg, int device, int32_t max_points, int3
   A(bb.csize, B * P);
   A(bb.rowmask, B * P * 2);
   A(bb.rawang, B * 2);
+  A(bb.bad, B);
   A(bb.seg, B * P);
   A(bb.gflag, B * P);
   A(bb.col, B * P);
@@ -327,37 +328,48 @@ static int run_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* of
                      int on_device, int want_labels, bool with_fa) {
   HIPCHK(hipSetDevice(x->device));
   BatchBufs bb = x->bb;
+  // Per-scan sizes are validated on the host in both modes: an empty scan is
+  // undefined upstream (findStartEndAngle reads points[0] and points[size-1],
+  // imageProjection.cpp:201-203) and a scan above capacity would overrun the
+  // per-point work buffers.
+  std::vector<int64_t> off(B + 1);
+  if (on_device) {
+    HIPCHK(hipMemcpyAsync(off.data(), offsets, sizeof(int64_t) * (B + 1), hipMemcpyDeviceToHost,
+                          x->stream));
+    HIPCHK(hipStreamSynchronize(x->stream));
+  } else {
+    for (int k = 0; k <= B; ++k) off[k] = offsets[k];
+  }
+  int mx = 0;
+  for (int k = 0; k < B; ++k) {
+    const int64_t n = off[k + 1] - off[k];
+    if (n <= 0) {
+      set_err("scan %d of the batch is empty (offsets must be strictly increasing)", k);
+      return LEGO_E_ARG;
+    }
+    if (n > x->maxPoints) {
+      set_err("scan %d has %lld points > capacity %d", k, (long long)n, x->maxPoints);
+      return LEGO_E_CAPACITY;
+    }
+    mx = std::max<int>(mx, (int)n);
+  }
   if (on_device) {
     bb.pts = pts;
     bb.off = offsets;
-    int64_t last = 0, first = 0;
-    HIPCHK(hipMemcpyAsync(&first, offsets, sizeof(int64_t), hipMemcpyDeviceToHost, x->stream));
-    HIPCHK(hipMemcpyAsync(&last, offsets + B, sizeof(int64_t), hipMemcpyDeviceToHost, x->stream));
-    HIPCHK(hipStreamSynchronize(x->stream));
-    (void)first;
-    (void)last;
-    bb.Nmax = x->maxPoints;
   } else {
-    int64_t total = offsets[B] - offsets[0];
-    for (int k = 0; k < B; ++k)
-      if (offsets[k + 1] - offsets[k] > x->maxPoints || offsets[k + 1] < offsets[k]) {
-        set_err("scan %d has %lld points > capacity %d", k, (long long)(offsets[k + 1] - offsets[k]),
-                x->maxPoints);
-        return LEGO_E_CAPACITY;
-      }
+    const int64_t total = off[B] - off[0];
     if (total > (int64_t)x->maxPoints * x->maxBatch) return LEGO_E_CAPACITY;
-    std::vector<int64_t> off(B + 1);
-    for (int k = 0; k <= B; ++k) off[k] = offsets[k] - offsets[0];
-    HIPCHK(hipMemcpyAsync(x->d_pts, pts + offsets[0], sizeof(lego_point_xyzir) * total,
+    const int64_t base = off[0];
+    for (int k = 0; k <= B; ++k) off[k] -= base;
+    HIPCHK(hipMemcpyAsync(x->d_pts, pts + base, sizeof(lego_point_xyzir) * total,
                           hipMemcpyHostToDevice, x->stream));
     HIPCHK(hipMemcpyAsync(x->d_off, off.data(), sizeof(int64_t) * (B + 1), hipMemcpyHostToDevice,
                           x->stream));
     bb.pts = x->d_pts;
     bb.off = x->d_off;
-    int mx = 0;
-    for (int k = 0; k < B; ++k) mx = std::max<int>(mx, (int)(off[k + 1] - off[k]));
-    bb.Nmax = std::max(mx, 1);
   }
+  bb.Nmax = mx;
+  HIPCHK(hipMemsetAsync(bb.bad, 0, sizeof(int) * B, x->stream));
   x->tm.begin();
   launch_ip(bb, x->dc, B, want_labels, x->stream, &x->tm);
   if (with_fa) {
@@ -366,9 +378,17 @@ static int run_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* of
   }
   x->tm.end(x->stream);
   HIPCHK(hipGetLastError());
+  x->h_bad.resize(B);
+  HIPCHK(hipMemcpyAsync(x->h_bad.data(), bb.bad, sizeof(int) * B, hipMemcpyDeviceToHost, x->stream));
   HIPCHK(hipStreamSynchronize(x->stream));
   x->tm.collect(x->tnames, x->tms);
   x->lastB = B;
+  for (int k = 0; k < B; ++k)
+    if (x->h_bad[k]) {
+      x->lastB = 0;
+      set_err("scan %d of the batch has non-finite xyz (the cloud must be dense)", k);
+      return LEGO_E_NOT_DENSE;
+    }
   return LEGO_OK;
 }
 

@@ -62,6 +62,7 @@ struct BatchBufs {
   int* csize;                // [B*P]
   unsigned long long* rowmask;  // [B*P*2]
   float* rawang;             // [B*2]
+  int* bad;                  // [B]  non-finite xyz seen (imageProjection.cpp:174-176)
   // ---- segmented cloud + cloud_info
   float4* seg;               // [B*P]
   uint8_t* gflag;            // [B*P]

@@ -561,8 +561,8 @@ __global__ void k_fa_compact(BatchBufs bb, DevCfg c) {
 void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, FaCarry* d_carry, hipStream_t s,
                StageTimer* tm) {
   tm->mark("fa.deskew", s);
-  hipMemsetAsync(bb.firsthalf, 0x7f, sizeof(int) * B, s);
-  hipMemsetAsync(bb.fa_flags, 0, sizeof(int) * B, s);
+  (void)hipMemsetAsync(bb.firsthalf, 0x7f, sizeof(int) * B, s);
+  (void)hipMemsetAsync(bb.fa_flags, 0, sizeof(int) * B, s);
   dim3 gpts((c.P + 255) / 256, B);
   k_fa_half<<<gpts, 256, 0, s>>>(bb, c);
   k_fa_point<<<gpts, 256, 0, s>>>(bb, c);

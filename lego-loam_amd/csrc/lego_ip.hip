@@ -31,6 +31,10 @@ __global__ void k_project(BatchBufs bb, DevCfg c) {
   const float4 xyz = *(const float4*)pp;
   const uint16_t ring = pp->ring;
   const float x = xyz.x, y = xyz.y, z = xyz.z;
+  if (!__builtin_isfinite(x) || !__builtin_isfinite(y) || !__builtin_isfinite(z)) {
+    bb.bad[b] = 1;  // the host rejects the batch with LEGO_E_NOT_DENSE
+    return;
+  }
   if (i == 0) bb.rawang[2 * b] = -lego_atan2f(y, x);                   // :201
   if (i == n - 1) bb.rawang[2 * b + 1] = -lego_atan2f(y, x);           // :202
   const int row = ring;
@@ -292,9 +296,10 @@ void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hip
                StageTimer* tm) {
   const int P = c.P;
   tm->mark("ip.memset", s);
-  hipMemsetAsync(bb.owner, 0xff, sizeof(int) * (size_t)B * P, s);
-  hipMemsetAsync(bb.csize, 0, sizeof(int) * (size_t)B * P, s);
-  hipMemsetAsync(bb.rowmask, 0, sizeof(unsigned long long) * 2 * (size_t)B * P, s);
+  // launch-path errors are sticky: the caller checks hipGetLastError() after the batch
+  (void)hipMemsetAsync(bb.owner, 0xff, sizeof(int) * (size_t)B * P, s);
+  (void)hipMemsetAsync(bb.csize, 0, sizeof(int) * (size_t)B * P, s);
+  (void)hipMemsetAsync(bb.rowmask, 0, sizeof(unsigned long long) * 2 * (size_t)B * P, s);
   tm->mark("ip.project", s);
   dim3 gpts((bb.Nmax + 255) / 256, B), gpix((P + 255) / 256, B), gcol((c.H + 255) / 256, B);
   k_project<<<gpts, 256, 0, s>>>(bb, c);

@@ -22,10 +22,14 @@ class StageTimer {
     if (!enabled) return;
     if (used_ >= events_.size()) {
       hipEvent_t e;
-      hipEventCreate(&e);
+      if (hipEventCreate(&e) != hipSuccess) {  // timing is diagnostic: drop it, never fail the call
+        enabled = false;
+        return;
+      }
       events_.push_back(e);
     }
-    hipEventRecord(events_[used_++], s);
+    if (hipEventRecord(events_[used_], s) != hipSuccess) return;
+    ++used_;
     names_.push_back(name);
   }
   void end(hipStream_t s) { mark("__end__", s); }
@@ -35,7 +39,7 @@ class StageTimer {
     ms.clear();
     for (size_t i = 0; i + 1 < used_; ++i) {
       float t = 0;
-      hipEventElapsedTime(&t, events_[i], events_[i + 1]);
+      if (hipEventElapsedTime(&t, events_[i], events_[i + 1]) != hipSuccess) t = 0;
       size_t k = 0;
       for (; k < names.size(); ++k)
         if (names[k] == names_[i]) break;
@@ -47,7 +51,7 @@ class StageTimer {
     }
   }
   ~StageTimer() {
-    for (auto e : events_) hipEventDestroy(e);
+    for (auto e : events_) (void)hipEventDestroy(e);
   }
 
  private:

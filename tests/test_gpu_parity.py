@@ -124,3 +124,46 @@ def test_not_dense_rejected(L):
     st = gpu.lib.lego_ip_process(gpu.h, pts.ctypes.data, len(pts), stamp, 0, L.C.byref(out))
     assert st == L.LEGO_E_NOT_DENSE
     gpu.close()
+
+
+def test_batch_argument_checks(L):
+    """Empty scans and over-capacity scans are refused before any launch; a
+    non-finite point is caught on the device (LEGO_E_NOT_DENSE), on both the
+    host-buffer and the device-buffer paths."""
+    import torch
+
+    cfg = L.sensor_cfg("VLP-16", L.hip_lib())
+    sc = L.synth_cfg("VLP-16", 0)
+    a, sa = L.synth_scan(sc, 0)
+    b, sb = L.synth_scan(sc, 1)
+    pts = np.concatenate([a, b])
+    gpu = L.Lego(cfg, max_points=max(len(a), len(b)) + 16, max_batch=4)
+    recs = (L.PoseRec * 3)()
+    lib = gpu.lib
+    stamps = np.array([sa, sa, sb])
+
+    def call(p, off, on_device=0):
+        if on_device:
+            dp = torch.from_numpy(p.view(np.uint8)).cuda()
+            do = torch.from_numpy(off).cuda()
+            return lib.lego_odom_batch(gpu.h, dp.data_ptr(), do.data_ptr(), stamps.ctypes.data, len(off) - 1,
+                                       1, recs)
+        return lib.lego_odom_batch(gpu.h, p.ctypes.data, off.ctypes.data, stamps.ctypes.data, len(off) - 1, 0,
+                                   recs)
+
+    empty = np.array([0, len(a), len(a), len(pts)], np.int64)
+    assert call(pts, empty) == L.LEGO_E_ARG
+    assert call(pts, empty, 1) == L.LEGO_E_ARG
+    small = L.Lego(cfg, max_points=1000, max_batch=4)
+    assert small.lib.lego_odom_batch(small.h, pts.ctypes.data, np.array([0, len(a)], np.int64).ctypes.data,
+                                     stamps.ctypes.data, 1, 0, recs) == L.LEGO_E_CAPACITY
+    small.close()
+    bad = pts.copy()
+    bad["z"][len(a) + 7] = np.inf
+    two = np.array([0, len(a), len(pts)], np.int64)
+    assert call(bad, two) == L.LEGO_E_NOT_DENSE
+    gpu.reset()
+    assert call(bad, two, 1) == L.LEGO_E_NOT_DENSE
+    gpu.reset()
+    assert call(pts, two, 1) == L.LEGO_OK
+    gpu.close()

@@ -32,15 +32,19 @@ def idx(r, c):
     return r * H + c
 
 
-def test_projection_last_writer_wins(L):
-    """:219-256 — ring -> row, atan2f -> column, range < 1 m dropped, ring >=
-    N_SCAN dropped, later points overwrite earlier ones, intensity = row + col/1e4."""
+def cloud_projection(L):
     pts = [pt(L, 3, 900, 10.0), pt(L, 3, 900, 20.0),  # same pixel: the second wins
            pt(L, 5, 1000, 0.5),                         # below sensorMinimumRange
            pt(L, 4, 450, 7.0)]
     bad = pt(L, 3, 100, 5.0)
     bad["ring"] = 16                                    # rowIdn >= N_SCAN
-    out = run_ip(L, pts + [bad])
+    return pts + [bad]
+
+
+def test_projection_last_writer_wins(L):
+    """:219-256 — ring -> row, atan2f -> column, range < 1 m dropped, ring >=
+    N_SCAN dropped, later points overwrite earlier ones, intensity = row + col/1e4."""
+    out = run_ip(L, cloud_projection(L))
     r = out["range_image"]
     assert r[idx(3, 900)] == pytest.approx(20.0, abs=1e-5)
     assert r[idx(4, 450)] == pytest.approx(7.0, abs=1e-5)
@@ -53,10 +57,7 @@ def test_projection_last_writer_wins(L):
     assert (r < np.finfo(np.float32).max).sum() == 2
 
 
-def test_ground_overwrite_semantics(L):
-    """:267-291 — column walk i = 0..g-1: an invalid pair writes -1 at row i,
-    overwriting the 1 the previous (valid, flat) pair wrote there."""
-    col = 900
+def cloud_ground(L, col=900):
     pts = []
     for ring in range(4):  # rows 0..3 on the plane z = -0.6
         el = math.radians(-15.0 + 2.0 * ring)
@@ -64,7 +65,14 @@ def test_ground_overwrite_semantics(L):
     for ring in (5, 6, 7):  # a wall at 5 m: steep pairs
         el = math.radians(-15.0 + 2.0 * ring)
         pts.append(pt(L, ring, col, 5.0 / math.cos(el)))
-    out = run_ip(L, pts)
+    return pts
+
+
+def test_ground_overwrite_semantics(L):
+    """:267-291 — column walk i = 0..g-1: an invalid pair writes -1 at row i,
+    overwriting the 1 the previous (valid, flat) pair wrote there."""
+    col = 900
+    out = run_ip(L, cloud_ground(L, col))
     g = out["ground_image"].reshape(N, H)[:, col]
     np.testing.assert_array_equal(g[:8], [1, 1, 1, -1, -1, 0, 0, 0])
     assert (g[8:] == 0).all()
@@ -73,11 +81,7 @@ def test_ground_overwrite_semantics(L):
     assert lab[4] == -1                   # empty pixel (range FLT_MAX)
 
 
-def test_segmentation_validity_rules(L):
-    """:370-460 — components of the 4-neighbourhood with column wrap; valid if
-    size >= 30 or (size >= 5 and >= 3 distinct rows among the PUSHED pixels:
-    lineCountFlag is never set for the seed, :431); labels count valid
-    components in raster order of their seeds; invalid ones become 999999."""
+def cloud_segmentation(L):
     pts = []
     # A: 30 pixels in row 10, cols 100..129, range 10 -> valid
     pts += [pt(L, 10, c, 10.0) for c in range(100, 130)]
@@ -91,7 +95,15 @@ def test_segmentation_validity_rules(L):
     pts += [pt(L, 14, c, 10.0) for c in list(range(1790, 1800)) + list(range(0, 20))]
     # F: range jump breaks the edge test: two singletons
     pts += [pt(L, 15, 900, 10.0), pt(L, 15, 901, 20.0)]
-    out = run_ip(L, pts)
+    return pts
+
+
+def test_segmentation_validity_rules(L):
+    """:370-460 — components of the 4-neighbourhood with column wrap; valid if
+    size >= 30 or (size >= 5 and >= 3 distinct rows among the PUSHED pixels:
+    lineCountFlag is never set for the seed, :431); labels count valid
+    components in raster order of their seeds; invalid ones become 999999."""
+    out = run_ip(L, cloud_segmentation(L))
     lab = out["label_image"].reshape(N, H)
     # raster order of seeds: C (9,500) < A (10,100) < E (14,0)
     assert (lab[10, 100:130] == 2).all()
@@ -136,3 +148,58 @@ def test_voxel_grid_centroids(L):
     assert n.value == 3
     for g_, e in zip(got, exp):
         assert tuple(np.float32(v) for v in g_) == tuple(np.float32(v) for v in e)
+
+
+def cloud_single(L):
+    return [pt(L, 8, 1234, 12.0)]
+
+
+def test_empty_scan_rejected(L):
+    """findStartEndAngle reads points[0] and points[size-1]
+    (imageProjection.cpp:201-203), so an empty scan is undefined upstream; the
+    boundary rejects it with LEGO_E_ARG instead."""
+    ora = L.Oracle(L.sensor_cfg("VLP-16"))
+    with pytest.raises(RuntimeError, match="status 4"):
+        ora.ip(np.zeros(0, dtype=L.XYZIR_DTYPE), 0.0)
+
+
+def test_single_point_scan(L):
+    """One point: projected, too small to segment, an outlier only if its column
+    is a multiple of 5 (1234 is not), no features."""
+    ora = L.Oracle(L.sensor_cfg("VLP-16"))
+    out = ora.ip(np.concatenate(cloud_single(L)), 0.0, images=True)
+    assert (out["range_image"] < np.finfo(np.float32).max).sum() == 1
+    assert out["label_image"].reshape(N, H)[8, 1234] == 999999
+    assert len(out["segmented"]) == 0 and len(out["outlier"]) == 0
+    fa = ora.fa()
+    assert all(len(fa[k]) == 0 for k in ("sharp", "less_sharp", "flat", "less_flat"))
+
+
+@pytest.mark.gpu
+def test_product_rejects_empty_scan(L):
+    gpu = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=64)
+    with pytest.raises(RuntimeError, match="status 4"):
+        gpu.ip(np.zeros(0, dtype=L.XYZIR_DTYPE), 0.0)
+    gpu.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("make", [cloud_single, cloud_projection, cloud_ground, cloud_segmentation])
+def test_product_on_kat_clouds(L, make):
+    """The HIP product on the hand-built clouds: every image and cloud equal to
+    the oracle's, bit for bit (empty and near-empty scans included)."""
+    pts = np.concatenate(make(L))
+    ora = L.Oracle(L.sensor_cfg("VLP-16"))
+    o = ora.ip(pts, 0.0, images=True)
+    gpu = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=len(pts) + 16)
+    g = gpu.ip(pts, 0.0, images=True)
+    for k, v in o.items():
+        a, b = np.asarray(v), np.asarray(g[k])
+        if a.ndim == 0:
+            a, b = np.array([v], np.float32), np.array([g[k]], np.float32)
+        if a.dtype.names:
+            a, b = a.view(np.uint8), b.view(np.uint8)
+        elif a.dtype.kind == "f":
+            a, b = a.view(np.uint32), b.view(np.uint32)
+        np.testing.assert_array_equal(a, b, err_msg=k)
+    gpu.close()
