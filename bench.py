@@ -36,6 +36,13 @@ def load_ffi():
     return mod
 
 
+def load_multistream():
+    sys.path.insert(0, str(REPO / "lego-loam_amd"))
+    import multistream
+
+    return multistream
+
+
 def make_stream(L, sensor: str, seed: int, nscans: int):
     sc = L.synth_cfg(sensor, seed)
     scans = [L.synth_scan(sc, k) for k in range(nscans)]
@@ -110,9 +117,11 @@ def main():
     dev = torch.device("cuda", local)
 
     L = load_ffi()
+    ms = load_multistream()
     lib = L.hip_lib()
     cfg = L.sensor_cfg(args.sensor, lib)
-    seed = 1 if world == 1 else 10 + rank
+    # N=1: the C2 stream (seed 1).  N>1: C4, stream `rank` (seed 10 + rank).
+    seed = 1 if world == 1 else ms.stream_seed(ms.streams_of_rank(world, world, rank)[0])
     pts, off, stamps, maxn = make_stream(L, args.sensor, seed, args.stream_len)
     B = args.batch
     nb = args.stream_len // B
@@ -150,11 +159,8 @@ def main():
         for k, v in st.items():
             stage_acc[k] = stage_acc.get(k, 0.0) + v
         alg_bytes += odom_alg_bytes(recs)
-        if dist:
-            rec_t = torch.frombuffer(bytearray(bytes(recs)), dtype=torch.uint8).to(dev)
-            glist = [torch.empty_like(rec_t) for _ in range(world)] if rank == 0 else None
-            dist.gather(rec_t, glist, dst=0)
-            gathered = glist
+        if dist:  # hand-off of the step's pose records to the serial consumer on rank 0
+            gathered = ms.gather_pose_records(ms.recs_to_bytes(recs), dist, dev)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()

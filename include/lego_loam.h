@@ -215,7 +215,8 @@ int lego_stage_times(lego_ctx* ctx, const char** names, float* ms, int32_t cap,
  * 100 MHz): enable = 1/0 turns stamping on/off and zeroes the counters,
  * enable = -1 leaves it unchanged; out16 (may be NULL) receives
  * {surf NN iters, surf iters, corner NN iters, corner iters, solve, integrate,
- *  to_end, lbvh build, LDS residency, #surf iters, #corner iters, #NN rounds}. */
+ *  to_end, NN grid build, LDS residency, #surf iters, #corner iters, #NN rounds,
+ *  nn query, scan-line, #shell-1 queries, #brute-force queries}. */
 int lego_odom_profile(lego_ctx* ctx, int32_t enable, uint64_t* out16);
 
 #ifdef __cplusplus

@@ -1,22 +1,22 @@
 // lego_odom.hip — the two-step LM odometry of featureAssociation on gfx950.
 //
-// One persistent 1024-thread workgroup walks the batch's scans in stream order
+// One persistent 512-thread workgroup walks the batch's scans in stream order
 // (scan k's problem depends on scan k-1's result through transformCur and the
 // TransformToEnd'ed "last" clouds, featureAssociation.cpp:1759-1815), so the
 // per-scan chain never returns to the host.  Per LM iteration:
-//   one lane per query, no barrier between the steps:
-//     TransformToStart (:860-883);
-//     every 5th iteration the nearest neighbour in an LBVH over the last
-//     cloud — exact, replaces KdTreeFLANN (:1054, :1165; ties -> lower index,
-//     FLANN's tie order is traversal dependent) — and the scan-line search
-//     loops exactly as written (:1062-1099, :1173-1220, incl. the loop-bound
-//     quirk, clamped to the cloud);
-//     line / plane residual, weight and Jacobian row (:1106-1151, :1228-1321)
-//   block reduce: AtA, AtB with double accumulation (cv::gemm's float path)
+//   every 5th iteration, one 32-lane group per query: TransformToStart
+//     (:860-883), the exact nearest neighbour in a hash grid over the last
+//     cloud (replaces KdTreeFLANN, :1054, :1165; ties -> lower index, FLANN's
+//     tie order is traversal dependent) and the scan-line search loops as
+//     written (:1062-1099, :1173-1220, incl. the loop-bound quirk);
+//   one lane per query: line / plane residual, weight and Jacobian row
+//     (:1106-1151, :1228-1321);
+//   block reduce: AtA, AtB with double accumulation (cv::gemm's float path);
 //   lane 0: QR solve, iteration-0 eigen degeneracy projection, update, NaN
 //     reset, convergence test (:1324-1376, :1425-1477).
-// The last clouds and the LBVH node boxes live in LDS when they fit.
-// then integrateTransformation (:1697-1725) and publishCloudsLast.
+// Then integrateTransformation (:1697-1725) and publishCloudsLast (ToEnd,
+// swap, grid rebuild).  The last clouds, the odometry state and the
+// correspondence indices live in LDS when they fit (VLP-16 always does).
 #include <climits>
 
 #include "lego_device.h"

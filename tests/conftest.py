@@ -48,6 +48,14 @@ def ensure_built():
 @pytest.fixture(scope="session")
 def L():
     ensure_built()
+    # PyTorch ships its own HIP runtime next to /opt/rocm's, which our library
+    # links.  Both work in one process only when torch's initialises first (a
+    # later torch init reports "No HIP GPUs are available"), so GPU sessions
+    # bring torch up before the first context is created, as bench.py does.
+    if gpu_available():
+        import torch
+
+        torch.cuda.init()
     return _load_ffi()
 
 
