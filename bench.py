@@ -191,17 +191,19 @@ def main():
                    "sample": f"{n} scans ({passes} pass(es) over the {args.stream_len}-scan "
                              f"{args.sensor} stream, seed {seed}) through oracle ip+fa incl. LM, 1 thread"}
         if args.odom_profile:
-            prof = (C.c_uint64 * 16)()
+            prof = (C.c_uint64 * 32)()
             lib.lego_odom_profile(gpu.h, -1, prof)
             names = ["surf_nn", "surf", "corner_nn", "corner", "solve", "integrate", "to_end",
-                     "build", "resident", "", "", "", "nn_query", "scanline", "", ""]
+                     "build", "resident", "", "", "", "nn_shells"]
             nsc = (args.steps + args.warmup) * B
             for i, nm in enumerate(names):
-                if not nm:
-                    continue
-                print(f"  odom.{nm:10s} {prof[i] / 100.0 / nsc:9.2f} us/scan", file=sys.stderr)
+                if nm:
+                    print(f"  odom.{nm:10s} {prof[i] / 100.0 / nsc:9.2f} us/scan", file=sys.stderr)
             print(f"  iters/scan surf {prof[9] / nsc:.2f} corner {prof[10] / nsc:.2f} nn {prof[11] / nsc:.2f}"
-                  f"  nn queries/scan: shell1 {prof[14] / nsc:.1f} brute {prof[15] / nsc:.1f}",
+                  f"  per scan: nn shell-1 {prof[14] / nsc:.1f}, nn exhaustive {prof[15] / nsc:.1f},"
+                  f" scan-line indexed {prof[20] / nsc:.1f}, scan-line literal {prof[13] / nsc:.1f}",
+                  file=sys.stderr)
+            print(f"  odom.nn_exhaust {prof[17] / 100.0 / nsc:9.2f} us/scan\n  odom.scan_line  {prof[18] / 100.0 / nsc:9.2f} us/scan",
                   file=sys.stderr)
         if args.stages:
             tot = sum(stage_acc.values())

@@ -213,11 +213,12 @@ int lego_stage_times(lego_ctx* ctx, const char** names, float* ms, int32_t cap,
 
 /* Diagnostic in-kernel phase counters of the odometry kernel (wall clock at
  * 100 MHz): enable = 1/0 turns stamping on/off and zeroes the counters,
- * enable = -1 leaves it unchanged; out16 (may be NULL) receives
+ * enable = -1 leaves it unchanged; out32 (may be NULL) receives
  * {surf NN iters, surf iters, corner NN iters, corner iters, solve, integrate,
  *  to_end, NN grid build, LDS residency, #surf iters, #corner iters, #NN rounds,
- *  nn query, scan-line, #shell-1 queries, #brute-force queries}. */
-int lego_odom_profile(lego_ctx* ctx, int32_t enable, uint64_t* out16);
+ *  nn query, -, #shell-1 queries, #brute-force queries, then group-0 splits of
+ *  the NN loop: to_start, grid NN, scan-line, #queries; 12 spare}. */
+int lego_odom_profile(lego_ctx* ctx, int32_t enable, uint64_t* out32);
 
 #ifdef __cplusplus
 }

@@ -69,8 +69,6 @@ struct lego_ctx {
   BatchBufs bb{};
   OdomBufs ob{};
   FaCarry* d_carry = nullptr;
-  unsigned long long* d_gkeys = nullptr;
-  int* d_gqi = nullptr;
   unsigned long long* d_prof = nullptr;  // in-kernel phase stamps (lego_odom_profile)
   bool profOn = false;
   lego_point_xyzir* d_pts = nullptr;
@@ -274,14 +272,37 @@ int lego_create(const lego_sensor_cfg* cfg, int device, int32_t max_points, int3
   ob.capCorner = ob.capLS;
   ob.capSurf = (int)P;
   A(ob.st, 1);
-  A(ob.cornerLast, (size_t)ob.capCorner);
-  A(ob.surfLast, (size_t)ob.capSurf);
   {
-    const size_t tc = odom_grid_table(ob.capCorner), ts = odom_grid_table(ob.capSurf);
-    A(ob.gC.keys, tc); A(ob.gC.cnt, tc); A(ob.gC.start, tc);
-    A(ob.gC.slot, (size_t)ob.capCorner); A(ob.gC.pts, (size_t)ob.capCorner); A(ob.gC.idx, (size_t)ob.capCorner);
-    A(ob.gS.keys, ts); A(ob.gS.cnt, ts); A(ob.gS.start, ts);
-    A(ob.gS.slot, (size_t)ob.capSurf); A(ob.gS.pts, (size_t)ob.capSurf); A(ob.gS.idx, (size_t)ob.capSurf);
+    // workgroups of the odometry launch (cooperative: all resident at once)
+    int cus = 0, coop = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 1;
+    if (hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device) != hipSuccess) coop = 0;
+    ob.G = coop ? odom_workgroups((int)N, cus) : 1;
+    const size_t G = ob.G;
+    for (int k = 0; k < 2; ++k) {
+      A(ob.cornerLast[k], G * ob.capCorner);
+      A(ob.surfLast[k], G * ob.capSurf);
+    }
+    int gTC = 0, gTS = 0, az = 0;
+    odom_index_caps(ob.capCorner, ob.capSurf, (int)N, &gTC, &gTS, &az);
+    ob.gTC = gTC;
+    ob.gTS = gTS;
+    ob.azB = az;
+    ob.cntCap = std::max(std::max(gTC, gTS), az);
+    A(ob.nC.gEnd, G * gTC); A(ob.nC.gOrd, G * ob.capCorner);
+    A(ob.nC.aEnd, G * az); A(ob.nC.aOrd, G * ob.capCorner);
+    A(ob.nS.gEnd, G * gTS); A(ob.nS.gOrd, G * ob.capSurf);
+    A(ob.nS.aEnd, G * az); A(ob.nS.aOrd, G * ob.capSurf);
+    A(ob.cnt, G * ob.cntCap);
+    ob.capQ = (int)(N * kFlatPerRing);
+    A(ob.qi, G * 3 * ob.capQ);
+    // exchange block: 16-byte timeout word, then 2 x 3 x capQ granules
+    ob.xbytes = 16 + sizeof(unsigned long long) * 2 * 3 * (size_t)ob.capQ;
+    unsigned char* xb = nullptr;
+    A(xb, ob.xbytes);
+    ob.xblock = xb;
+    ob.xerr = (unsigned*)xb;
+    ob.xg = (unsigned long long*)(xb + 16);
   }
   A(ob.sumOut, B * 6);
   A(ob.curOut, B * 6);
@@ -290,13 +311,7 @@ int lego_create(const lego_sensor_cfg* cfg, int device, int32_t max_points, int3
   A(ob.cornerEnd, B * ob.capLS);
   A(ob.surfEnd, B * P);
   A(x->d_carry, 1);
-  {
-    size_t m = 1;
-    while (m < P) m <<= 1;
-    A(x->d_gkeys, m);
-  }
-  A(x->d_gqi, 3 * N * kFlatPerRing + 3 * N * kSharpPerRing);
-  A(x->d_prof, 16);
+  A(x->d_prof, 32);
 #undef A
   bb.pts = x->d_pts;
   bb.off = x->d_off;
@@ -374,13 +389,22 @@ static int run_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* of
   launch_ip(bb, x->dc, B, want_labels, x->stream, &x->tm);
   if (with_fa) {
     launch_fa(bb, x->dc, B, x->d_carry, x->stream, &x->tm);
-    launch_odom(bb, x->ob, x->dc, B, x->stream, &x->tm, x->d_gkeys, x->d_gqi, x->profOn ? x->d_prof : nullptr);
+    if (launch_odom(bb, x->ob, x->dc, B, x->stream, &x->tm, x->profOn ? x->d_prof : nullptr) != 0) {
+      set_err("odometry launch failed (%d workgroups)", x->ob.G);
+      return LEGO_E_DEVICE;
+    }
   }
   x->tm.end(x->stream);
   HIPCHK(hipGetLastError());
   x->h_bad.resize(B);
   HIPCHK(hipMemcpyAsync(x->h_bad.data(), bb.bad, sizeof(int) * B, hipMemcpyDeviceToHost, x->stream));
+  unsigned xerr = 0;
+  if (with_fa) HIPCHK(hipMemcpyAsync(&xerr, x->ob.xerr, sizeof(xerr), hipMemcpyDeviceToHost, x->stream));
   HIPCHK(hipStreamSynchronize(x->stream));
+  if (xerr) {
+    set_err("odometry workgroup exchange timed out");
+    return LEGO_E_DEVICE;
+  }
   x->tm.collect(x->tnames, x->tms);
   x->lastB = B;
   for (int k = 0; k < B; ++k)
@@ -541,10 +565,19 @@ int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
   x->stamps.assign(1, in->info.stamp);
   x->tm.begin();
   launch_fa(x->bb, x->dc, 1, x->d_carry, x->stream, &x->tm);
-  launch_odom(x->bb, x->ob, x->dc, 1, x->stream, &x->tm, x->d_gkeys, x->d_gqi, x->profOn ? x->d_prof : nullptr);
+  if (launch_odom(x->bb, x->ob, x->dc, 1, x->stream, &x->tm, x->profOn ? x->d_prof : nullptr) != 0) {
+    set_err("odometry launch failed (%d workgroups)", x->ob.G);
+    return LEGO_E_DEVICE;
+  }
   x->tm.end(x->stream);
   HIPCHK(hipGetLastError());
+  unsigned xerr = 0;
+  HIPCHK(hipMemcpyAsync(&xerr, x->ob.xerr, sizeof(xerr), hipMemcpyDeviceToHost, x->stream));
   HIPCHK(hipStreamSynchronize(x->stream));
+  if (xerr) {
+    set_err("odometry workgroup exchange timed out");
+    return LEGO_E_DEVICE;
+  }
   x->lastB = 1;
   x->lastIpDevice = false;
   return fetch_fa(x, 0, out);
@@ -613,15 +646,15 @@ int lego_mo_process(lego_ctx* x, const lego_fa_out* in, lego_mo_out* out) {
   return LEGO_E_STATE;
 }
 
-int lego_odom_profile(lego_ctx* x, int32_t enable, uint64_t* out16) {
+int lego_odom_profile(lego_ctx* x, int32_t enable, uint64_t* out32) {
   if (!x) return LEGO_E_ARG;
   HIPCHK(hipSetDevice(x->device));
-  if (out16) {
-    HIPCHK(hipMemcpy(out16, x->d_prof, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  if (out32) {
+    HIPCHK(hipMemcpy(out32, x->d_prof, 32 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   }
   if (enable >= 0) {
     x->profOn = enable != 0;
-    HIPCHK(hipMemset(x->d_prof, 0, 16 * sizeof(uint64_t)));
+    HIPCHK(hipMemset(x->d_prof, 0, 32 * sizeof(uint64_t)));
   }
   return LEGO_OK;
 }

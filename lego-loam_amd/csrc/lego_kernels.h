@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
+
 #include <string>
 #include <vector>
 
@@ -60,14 +62,13 @@ class StageTimer {
   size_t used_ = 0;
 };
 
-// Hash-grid nearest-neighbour index over a snapshot of a last cloud.
-struct NNGrid {
-  unsigned long long* keys;  // [T]
-  int* cnt;                  // [T]
-  int* start;                // [T]
-  int* slot;                 // [cap] per-point slot (build scratch)
-  float4* pts;               // [cap] cell-ordered snapshot
-  int* idx;                  // [cap] original index
+// HBM form of the two NN indexes over one last cloud (sensors whose working
+// set does not fit LDS); see lego_odom.hip.
+struct NNIndexBufs {
+  uint32_t* gEnd;  // [gT]        fine-grid bucket ends
+  uint32_t* gOrd;  // [cap]       point order
+  uint32_t* aEnd;  // [N * NB]    ring x azimuth bucket ends
+  uint32_t* aOrd;  // [cap]
 };
 
 // Odometry state kept on the device for one stream (featureAssociation.cpp
@@ -79,18 +80,32 @@ struct OdomState {
   int isDegenerate;
   int inited;            // systemInitedLM
   int cornerLastNum, surfLastNum;
-  int nnCornerNum, nnSurfNum;  // point sets the NN structures were built on
+  int nnCornerNum, nnSurfNum;  // sizes of the clouds the NN indexes were built on
   int frameCount;
-  int _pad[3];
+  int curBuf;    // HBM buffer holding the current last clouds
+  int snapBuf;   // HBM buffer holding the indexes' snapshot (== curBuf unless stale)
+  int resident;  // current last clouds (and indexes) are LDS-resident
 };
 
+// Device buffers of the odometry kernel.  Arrays marked [G x] hold one private
+// copy per workgroup of the launch (the workgroups redundantly run the same
+// serial chain and split only the NN searches); the kernel offsets them.
 struct OdomBufs {
   OdomState* st;
-  float4* cornerLast;   // [capCorner]
-  float4* surfLast;     // [capSurf]
-  NNGrid gC, gS;        // hash grids over snapshots of the last clouds
-  int capCorner, capSurf;
-  // per-scan outputs of the batch
+  float4* cornerLast[2];  // [G x capCorner] double-buffered: current / stale snapshot
+  float4* surfLast[2];    // [G x capSurf]
+  NNIndexBufs nC, nS;     // [G x] HBM indexes (sensors too large for LDS)
+  uint32_t* cnt;          // [G x cntCap] index-build counters
+  int* qi;                // [G x 3 * capQ] HBM correspondences
+  int gTC, gTS, azB, cntCap;
+  int capCorner, capSurf, capQ;
+  int G;                  // workgroups per launch
+  // exchange (zeroed before each launch): timeout word, then 2 x 3 x capQ granules
+  void* xblock;
+  size_t xbytes;
+  unsigned* xerr;
+  unsigned long long* xg;
+  // per-scan outputs of the batch (workgroup 0)
   float* sumOut;        // [B*6]
   float* curOut;        // [B*6]
   int* validOut;        // [B]
@@ -104,8 +119,11 @@ void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hip
                StageTimer* tm);
 void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, FaCarry* d_carry, hipStream_t s,
                StageTimer* tm);
-void launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int B, hipStream_t s,
-                 StageTimer* tm, unsigned long long* gkeys, int* gqi, unsigned long long* prof);
-size_t odom_grid_table(int npts);
+// Returns 0 on a successful launch.
+int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int B, hipStream_t s,
+                StageTimer* tm, unsigned long long* prof);
+int odom_workgroups(int N, int cusAvailable);
+// HBM index sizes for clouds of up to capCorner / capSurf points.
+void odom_index_caps(int capCorner, int capSurf, int N, int* gTC, int* gTS, int* azBuckets);
 
 }  // namespace lego

@@ -319,15 +319,18 @@ LEGO_HD float cv_hypot(float a, float b) {
 
 // cv::eigen for a symmetric float matrix: eigenvalues W in descending order,
 // eigenvectors as the ROWS of V.  A is destroyed.
+// The pivot bookkeeping indR/indC is caller-provided so device code can keep
+// it (and A, W, V) in LDS: the Jacobi sweep indexes them dynamically, which in
+// registers would become scratch memory.
 template <int N>
-LEGO_HD void cv_eigen_sym(float (&A)[N][N], float (&W)[N], float (&V)[N][N]) {
+LEGO_HD void cv_eigen_sym_ws(float (&A)[N][N], float (&W)[N], float (&V)[N][N], int (&indR)[N],
+                             int (&indC)[N]) {
   const float eps = 1.1920928955078125e-07f;  // FLT_EPSILON
   int i, j, k, m;
   for (i = 0; i < N; i++) {
     for (j = 0; j < N; j++) V[i][j] = 0.f;
     V[i][i] = 1.f;
   }
-  int indR[N], indC[N];
   float mv = 0.f;
   for (k = 0; k < N; k++) {
     W[k] = A[k][k];
@@ -405,6 +408,12 @@ LEGO_HD void cv_eigen_sym(float (&A)[N][N], float (&W)[N], float (&V)[N][N]) {
       for (i = 0; i < N; i++) { float tv = V[m][i]; V[m][i] = V[k][i]; V[k][i] = tv; }
     }
   }
+}
+
+template <int N>
+LEGO_HD void cv_eigen_sym(float (&A)[N][N], float (&W)[N], float (&V)[N][N]) {
+  int indR[N], indC[N];
+  cv_eigen_sym_ws<N>(A, W, V, indR, indC);
 }
 
 // cv::solve(A, b, x, DECOMP_QR) for a square float system with one rhs

@@ -4,20 +4,30 @@
 // (scan k's problem depends on scan k-1's result through transformCur and the
 // TransformToEnd'ed "last" clouds, featureAssociation.cpp:1759-1815), so the
 // per-scan chain never returns to the host.  Per LM iteration:
-//   every 5th iteration, one 32-lane group per query: TransformToStart
-//     (:860-883), the exact nearest neighbour in a hash grid over the last
-//     cloud (replaces KdTreeFLANN, :1054, :1165; ties -> lower index, FLANN's
-//     tie order is traversal dependent) and the scan-line search loops as
-//     written (:1062-1099, :1173-1220, incl. the loop-bound quirk);
+//   every 5th iteration: TransformToStart of every query (:860-883, one lane
+//     each), then one 16-lane group per query finds
+//       - the exact nearest neighbour in the last cloud (replaces KdTreeFLANN,
+//         :1054, :1165; ties -> lower index, FLANN's tie order is traversal
+//         dependent): a 0.5 m hash grid, two shells with provable coverage,
+//         then an exact ring x azimuth bucket search;
+//       - the scan-line neighbours (:1062-1099, :1173-1220, incl. the
+//         loop-bound quirk): the reference's sequential loops visit an index
+//         window bounded by ring breaks; the window is read off per-ring
+//         first/last indices, and the minimum over it is searched in the
+//         ring x azimuth buckets with an angular lower bound, keeping the
+//         (distance, visit order) tie rule of the loops;
 //   one lane per query: line / plane residual, weight and Jacobian row
 //     (:1106-1151, :1228-1321);
 //   block reduce: AtA, AtB with double accumulation (cv::gemm's float path);
-//   lane 0: QR solve, iteration-0 eigen degeneracy projection, update, NaN
-//     reset, convergence test (:1324-1376, :1425-1477).
-// Then integrateTransformation (:1697-1725) and publishCloudsLast (ToEnd,
-// swap, grid rebuild).  The last clouds, the odometry state and the
-// correspondence indices live in LDS when they fit (VLP-16 always does).
+//   lane 0: QR solve, iteration-0 eigen degeneracy projection (workspace in
+//     LDS), update, NaN reset, convergence test (:1324-1376, :1425-1477).
+// Then integrateTransformation (:1697-1725) and publishCloudsLast (ToEnd, swap,
+// index rebuild).  For VLP-16-class sensors the last clouds, both NN indexes,
+// the query transforms and correspondences and the state all live in LDS; the
+// same code runs from HBM buffers for larger sensors.
 #include <climits>
+#include <cstdint>
+#include <type_traits>
 
 #include "lego_device.h"
 #include "lego_kernels.h"
@@ -26,10 +36,17 @@ namespace lego {
 
 constexpr int kOdomThreads = 512;
 constexpr int kOdomWaves = kOdomThreads / 64;
-// LDS residency caps (VLP-16 fits entirely; larger sensors fall back to HBM)
-constexpr int kLdsSurf = 4096;      // last surf cloud points
-constexpr int kLdsCorner = 2048;    // last corner cloud points
-constexpr int kLdsQ = 512;          // queries with LDS-resident correspondence indices
+constexpr int kGL = 64;                       // lanes per query group (one wave)
+constexpr int kNGrp = kOdomThreads / kGL;
+// LDS residency caps (VLP-16 / OS1-16 fit; larger sensors use the HBM path)
+constexpr int kLdsSurf = 4096;                // last surf cloud points
+constexpr int kLdsCorner = 2048;              // last corner cloud points
+constexpr int kLdsQ = 384;                    // queries (flat <= 24 N, sharp <= 12 N)
+constexpr int kLdsGridS = 2048, kLdsGridC = 1024;  // fine-grid buckets
+constexpr int kLdsAz = 2048;                  // ring x azimuth buckets per cloud
+constexpr int kKeyTab = kMaxRings + 4;
+constexpr int kLdsCnt = kLdsGridS > kLdsAz ? kLdsGridS : kLdsAz;
+constexpr float kCell = 0.5f;
 
 // ---------------------------------------------------------------- transforms
 struct Trig3 {
@@ -181,73 +198,48 @@ __device__ __forceinline__ void plugin_imu_rotation(float bcx, float bcy, float 
 // wall_clock64 deltas (100 MHz) into prof[k].
 enum { P_SURF_NN = 0, P_SURF = 1, P_CORN_NN = 2, P_CORN = 3, P_SOLVE = 4, P_INTEG = 5,
        P_TOEND = 6, P_BUILD = 7, P_RESID = 8, P_ITERS_S = 9, P_ITERS_C = 10, P_NNR = 11,
-       P_QUERY = 12, P_SCANLINE = 13, P_NN_SHELL1 = 14, P_NN_BRUTE = 15, P_NPROF = 16 };
+       P_QUERY = 12, P_SCANLINE = 13, P_NN_SHELL1 = 14, P_NN_BRUTE = 15,
+       P_G0_TOSTART = 16, P_G0_NN = 17, P_G0_SCAN = 18, P_G0_Q = 19, P_AZLINE = 20, P_NPROF = 32 };
 struct Stamp {
   unsigned long long* prof;
   unsigned long long t;
-  __device__ void start() { if (prof && threadIdx.x == 0) t = wall_clock64(); }
-  __device__ void add(int k) {
+  __device__ __forceinline__ void start() { if (prof && threadIdx.x == 0) t = wall_clock64(); }
+  __device__ __forceinline__ void add(int k) {
     if (prof && threadIdx.x == 0) { const unsigned long long n = wall_clock64(); prof[k] += n - t; t = n; }
   }
-  __device__ void count(int k) { if (prof && threadIdx.x == 0) prof[k] += 1; }
+  __device__ __forceinline__ void count(int k) { if (prof && threadIdx.x == 0) prof[k] += 1; }
 };
 
-// ---------------------------------------------------------------- LDS layout
-struct OdomLds {
-  float4* lastS;     // [kLdsSurf]  (also the NN-build key scratch)
-  float4* lastC;     // [kLdsCorner]
-  int* qi;           // [3 * kLdsQ] correspondence indices
-  double* red;       // [kOdomWaves * 10]
-  float* f;          // 64 scalars
-  int* n;            // 64 scalars
-  OdomState* st;     // the stream state, resident for the kernel's lifetime
+// ---------------------------------------------------------------- NN indexes
+// Two bucket indexes over one last cloud, both built by counting sort:
+//   fine grid  0.5 m cells hashed into T buckets;
+//   az lists   bucket = key * NB + azimuth bin, key = int(intensity) (the ring
+//              the scan-line loops test), azimuth about the camera y (up) axis.
+// A bucket array holds END offsets into a point-order array (begin = the
+// previous bucket's end).  Order inside a bucket is arbitrary: every search
+// keeps a lexicographic minimum, so the result does not depend on it.
+template <class Idx>
+struct NNView {
+  const float4* pts;
+  int n;
+  const Idx* gEnd;
+  const Idx* gOrd;
+  int T;
+  const Idx* aEnd;
+  const Idx* aOrd;
+  int NB, NK;
+  const int* sufFirst;  // [NK + 1] first index whose key >= k
+  const int* preLast;   // [NK]     last index whose key <= k
+  const int* kFirst;    // [NK]     first / last index of key k (INT_MAX / -1 if none)
+  const int* kLast;
+  int irregular;        // a key outside [0, NK): the az lists are not built
 };
 
-__host__ __device__ inline size_t odom_lds_bytes() {
-  size_t s = 0;
-  s += (size_t)kLdsSurf * 16 + (size_t)kLdsCorner * 16;
-  s += (size_t)3 * kLdsQ * 4;
-  s += (size_t)kOdomWaves * 10 * 8;
-  s += 64 * 4 + 64 * 4;
-  s += 128;  // OdomState
-  return s;
-}
-
-__device__ __forceinline__ OdomLds odom_carve(unsigned char* base) {
-  OdomLds L;
-  size_t o = 0;
-  L.lastS = (float4*)(base + o); o += (size_t)kLdsSurf * 16;
-  L.lastC = (float4*)(base + o); o += (size_t)kLdsCorner * 16;
-  L.red = (double*)(base + o); o += (size_t)kOdomWaves * 10 * 8;
-  L.qi = (int*)(base + o); o += (size_t)3 * kLdsQ * 4;
-  L.f = (float*)(base + o); o += 64 * 4;
-  L.n = (int*)(base + o); o += 64 * 4;
-  L.st = (OdomState*)(base + o); o += 128;
-  return L;
-}
-
-enum { F_BB = 0 /* bbox 6 */ };
-enum { N_BREAK = 0, N_M = 1 };
-
-// ---------------------------------------------------------------- NN index
-// Hash grid over a snapshot of the last cloud (taken when the reference would
-// rebuild its kd-tree, featureAssociation.cpp:1785-1788): 0.5 m cells, open-
-// addressing table, points scattered into cell order by atomic cursors (no
-// sort).  A query is served by a 32-lane group: the 27 cells around it, then
-// the 98-cell shell, each accepted only when the best distance is provably
-// smaller than the covered radius; otherwise (or for small clouds) an exact
-// group-wide brute force.  Ties resolve to the lower original index.
-constexpr int kG = 32;              // lanes per query group
-constexpr float kCell = 0.5f;
-constexpr unsigned long long kEmpty = ~0ull;
-
-struct GridView {
-  const unsigned long long* keys;
-  const int* cnt;
-  const int* start;
-  const float4* pts;  // cell-ordered snapshot
-  const int* idx;     // original index of each slot
-  int T, n;
+template <class Idx>
+struct NNStore {
+  Idx *gEnd, *gOrd, *aEnd, *aOrd;
+  int *sufFirst, *preLast, *kFirst, *kLast, *irregular;
+  int Tcap;
 };
 
 __device__ __forceinline__ unsigned long long cell_key(int ix, int iy, int iz) {
@@ -259,60 +251,115 @@ __device__ __forceinline__ unsigned hash_key(unsigned long long k) {
   return (unsigned)k;
 }
 __device__ __forceinline__ int cell_of(float v) { return (int)floorf(v * (1.0f / kCell)); }
+__device__ __forceinline__ int fine_bucket(int ix, int iy, int iz, int T) {
+  return (int)(hash_key(cell_key(ix, iy, iz)) & (unsigned)(T - 1));
+}
 
-__host__ __device__ inline int grid_table_size(int n) {
+constexpr float kTwoPi = 6.28318530717958647692f;
+// azimuth in [0, 2 pi] about the camera y axis (x = lidar y, z = lidar x)
+__device__ __forceinline__ float az_of(float x, float z) { return atan2f(x, z) + 3.14159265358979323846f; }
+__device__ __forceinline__ int az_bin(float a, int NB) {
+  const int b = (int)(a * ((float)NB / kTwoPi));
+  return b < 0 ? 0 : (b >= NB ? NB - 1 : b);
+}
+__host__ __device__ inline int az_nb(int N) {
+  int nb = 128;
+  while (nb > 32 && N * nb > kLdsAz) nb >>= 1;
+  return nb;
+}
+__host__ __device__ inline int fine_T(int n, int cap) {
   int t = 64;
-  while (t < 2 * n) t <<= 1;
+  while (t < n / 2 && t < cap) t <<= 1;
   return t;
 }
 
-// Builds the grid over src[0..n) (all threads; global buffers).
-__device__ __forceinline__ void grid_build(const float4* src, int n, unsigned long long* keys, int* cnt, int* start,
-                           int* slotOf, float4* pts, int* idx, const OdomLds& L) {
+// exclusive scan of a[0..n) in place, all threads of the block
+__device__ __forceinline__ void block_exscan(unsigned* a, int n, int* wtot) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int per = (n + kOdomThreads - 1) / kOdomThreads;
+  const int b0 = min(n, tid * per), b1 = min(n, b0 + per);
+  unsigned local = 0;
+  for (int t = b0; t < b1; ++t) local += a[t];
+  unsigned x = local;
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wtot[wave] = (int)x;
+  __syncthreads();
+  unsigned run = x - local;
+  for (int w = 0; w < wave; ++w) run += (unsigned)wtot[w];
+  for (int t = b0; t < b1; ++t) {
+    const unsigned cnt = a[t];
+    a[t] = run;
+    run += cnt;
+  }
+  __syncthreads();
+}
+
+// counting sort of point indices 0..n-1 into nb buckets
+template <class Idx, class Bid>
+__device__ __forceinline__ void bucket_build(int n, int nb, const Bid& bid, unsigned* cnt, Idx* E, Idx* Ord,
+                                             int* wtot) {
   const int tid = threadIdx.x;
-  const int T = grid_table_size(n);
-  for (int t = tid; t < T; t += blockDim.x) { keys[t] = kEmpty; cnt[t] = 0; }
+  for (int b = tid; b < nb; b += kOdomThreads) cnt[b] = 0;
   __syncthreads();
-  for (int i = tid; i < n; i += blockDim.x) {
-    const float4 p = src[i];
-    const unsigned long long k = cell_key(cell_of(p.x), cell_of(p.y), cell_of(p.z));
-    unsigned s = hash_key(k) & (T - 1);
-    while (true) {
-      const unsigned long long old = atomicCAS(&keys[s], kEmpty, k);
-      if (old == kEmpty || old == k) break;
-      s = (s + 1) & (T - 1);
-    }
-    slotOf[i] = (int)s;
-    atomicAdd(&cnt[s], 1);
+  for (int i = tid; i < n; i += kOdomThreads) atomicAdd(&cnt[bid(i)], 1u);
+  __syncthreads();
+  block_exscan(cnt, nb, wtot);
+  for (int i = tid; i < n; i += kOdomThreads) Ord[atomicAdd(&cnt[bid(i)], 1u)] = (Idx)i;
+  __syncthreads();
+  for (int b = tid; b < nb; b += kOdomThreads) E[b] = (Idx)cnt[b];
+  __syncthreads();
+}
+
+// Builds both indexes and the per-key first/last tables over pts[0..n).
+template <class Idx>
+__device__ __forceinline__ void nn_build(const float4* pts, int n, int NK, const NNStore<Idx>& S, unsigned* cnt,
+                                         int* wtot) {
+  int* kfirst = S.kFirst;
+  int* klast = S.kLast;
+  const int tid = threadIdx.x;
+  const int T = fine_T(n, S.Tcap), NB = az_nb(NK);
+  for (int k = tid; k < NK; k += kOdomThreads) { kfirst[k] = INT_MAX; klast[k] = -1; }
+  if (tid == 0) *S.irregular = 0;
+  __syncthreads();
+  for (int i = tid; i < n; i += kOdomThreads) {
+    const int k = (int)pts[i].w;
+    if (k < 0 || k >= NK) { *S.irregular = 1; continue; }
+    atomicMin(&kfirst[k], i);
+    atomicMax(&klast[k], i);
   }
   __syncthreads();
-  // exclusive scan of cnt into start: each thread owns T/blockDim consecutive slots
-  {
-    const int per = (T + blockDim.x - 1) / blockDim.x;
-    const int b0 = tid * per, b1 = min(T, b0 + per);
-    int local = 0;
-    for (int t = b0; t < b1; ++t) local += cnt[t];
-    const int lane = tid & 63, wave = tid >> 6;
-    int x = local;
-    for (int o2 = 1; o2 < 64; o2 <<= 1) {
-      const int y = __shfl_up(x, o2, 64);
-      if (lane >= o2) x += y;
-    }
-    if (lane == 63) L.n[8 + wave] = x;
-    __syncthreads();
-    int woff = 0;
-    for (int w = 0; w < wave; ++w) woff += L.n[8 + w];
-    int run = woff + x - local;
-    for (int t = b0; t < b1; ++t) { start[t] = run; run += cnt[t]; cnt[t] = 0; }
-    __syncthreads();
+  const int irregular = *S.irregular;
+  if (tid == 0) {
+    int m = INT_MAX;
+    S.sufFirst[NK] = INT_MAX;
+    for (int k = NK - 1; k >= 0; --k) { m = min(m, kfirst[k]); S.sufFirst[k] = m; }
+    int M = -1;
+    for (int k = 0; k < NK; ++k) { M = max(M, klast[k]); S.preLast[k] = M; }
   }
-  for (int i = tid; i < n; i += blockDim.x) {
-    const int s = slotOf[i];
-    const int pos = start[s] + atomicAdd(&cnt[s], 1);
-    pts[pos] = src[i];
-    idx[pos] = i;
-  }
-  __syncthreads();
+  bucket_build<Idx>(
+      n, T,
+      [&](int i) {
+        const float4 p = pts[i];
+        return fine_bucket(cell_of(p.x), cell_of(p.y), cell_of(p.z), T);
+      },
+      cnt, S.gEnd, S.gOrd, wtot);
+  if (!irregular)
+    bucket_build<Idx>(
+        n, NK * NB,
+        [&](int i) {
+          const float4 p = pts[i];
+          return (int)p.w * NB + az_bin(az_of(p.x, p.z), NB);
+        },
+        cnt, S.aEnd, S.aOrd, wtot);
+}
+
+template <class Idx>
+__device__ __forceinline__ void bucket_range(const Idx* E, int b, int& lo, int& hi) {
+  lo = b ? (int)E[b - 1] : 0;
+  hi = (int)E[b];
 }
 
 // L2_Simple distance order ((0 + d0^2) + d1^2) + d2^2 (FLANN)
@@ -323,93 +370,23 @@ __device__ __forceinline__ float flann_d2(float4 q, float4 p) {
   d = q.z - p.z; r += d * d;
   return r;
 }
+__device__ __forceinline__ float line_d2(float4 a, float4 s) {  // the scan-line distance
+  return (a.x - s.x) * (a.x - s.x) + (a.y - s.y) * (a.y - s.y) + (a.z - s.z) * (a.z - s.z);
+}
 
 __device__ __forceinline__ void lex_min(float& d, int& i, float d2, int i2) {
   if (d2 < d || (d2 == d && i2 < i)) { d = d2; i = i2; }
 }
 __device__ __forceinline__ void group_lex_min(float& d, int& i) {
-  for (int o = kG / 2; o > 0; o >>= 1) {
+  for (int o = kGL / 2; o > 0; o >>= 1) {
     const float d2 = __shfl_xor(d, o, 64);
     const int i2 = __shfl_xor(i, o, 64);
     lex_min(d, i, d2, i2);
   }
 }
-
-__device__ __forceinline__ void scan_cell(const GridView& v, float4 q, int ix, int iy, int iz, float& bd,
-                                          int& bi) {
-  const unsigned long long k = cell_key(ix, iy, iz);
-  unsigned s = hash_key(k) & (v.T - 1);
-  while (true) {
-    const unsigned long long kk = v.keys[s];
-    if (kk == kEmpty) return;
-    if (kk == k) break;
-    s = (s + 1) & (v.T - 1);
-  }
-  const int b = v.start[s], e = b + v.cnt[s];
-  for (int t = b; t < e; ++t) lex_min(bd, bi, flann_d2(q, v.pts[t]), v.idx[t]);
-}
-
-// Exact nearest neighbour with d2 < bound, by the calling 32-lane group.
-__device__ __forceinline__ int grid_nn(const GridView& v, float4 q, float bound, int g,
-                                       unsigned long long* prof) {
-  if (v.n <= 0) return -1;
-  float bd = bound;
-  int bi = INT_MAX;
-  if (v.n > 4 * kG) {
-    const int cx = cell_of(q.x), cy = cell_of(q.y), cz = cell_of(q.z);
-    // shell 1: the 27 cells (covered radius >= 1 cell)
-    if (g < 27) scan_cell(v, q, cx + g % 3 - 1, cy + (g / 3) % 3 - 1, cz + g / 9 - 1, bd, bi);
-    group_lex_min(bd, bi);
-    if (bd < kCell * kCell * 0.99999f) {
-      if (prof && g == 0) atomicAdd(&prof[P_NN_SHELL1], 1ull);
-      return (bi != INT_MAX && bd < bound) ? bi : -1;
-    }
-    // shell 2: the 98 cells at Chebyshev distance 2 (covered radius >= 2 cells)
-    for (int c = g; c < 125; c += kG) {
-      const int dx = c % 5 - 2, dy = (c / 5) % 5 - 2, dz = c / 25 - 2;
-      if (abs(dx) == 2 || abs(dy) == 2 || abs(dz) == 2) scan_cell(v, q, cx + dx, cy + dy, cz + dz, bd, bi);
-    }
-    group_lex_min(bd, bi);
-    if (bd < 4 * kCell * kCell * 0.99999f) return (bi != INT_MAX && bd < bound) ? bi : -1;
-  }
-  // exact fallback: every point
-  if (prof && g == 0) atomicAdd(&prof[P_NN_BRUTE], 1ull);
-  for (int t = g; t < v.n; t += kG) lex_min(bd, bi, flann_d2(q, v.pts[t]), v.idx[t]);
-  group_lex_min(bd, bi);
-  return (bi != INT_MAX && bd < bound) ? bi : -1;
-}
-
-__device__ __forceinline__ float line_d2(float4 a, float4 s) {  // the scan-line distance
-  return (a.x - s.x) * (a.x - s.x) + (a.y - s.y) * (a.y - s.y) + (a.z - s.z) * (a.z - s.z);
-}
-
-// ordered (d, visit order) argmin over the group's candidate lanes
-__device__ __forceinline__ void group_argmin(bool cand, float d, int ord, int j, float* bd, int* bj) {
-  float v = cand ? d : __builtin_inff();
-  int o = cand ? ord : INT_MAX;
-  int jj = cand ? j : -1;
-  for (int s = kG / 2; s > 0; s >>= 1) {
-    const float v2 = __shfl_xor(v, s, 64);
-    const int o2 = __shfl_xor(o, s, 64);
-    const int j2 = __shfl_xor(jj, s, 64);
-    if (v2 < v || (v2 == v && o2 < o)) { v = v2; o = o2; jj = j2; }
-  }
-  *bd = v;
-  *bj = jj;
-}
-
-__device__ __forceinline__ unsigned group_ballot(bool p, int gbase) {
-  return (unsigned)(__ballot(p) >> gbase);
-}
-
-// Scan-line search around `ci` (corner :1062-1099, surf :1173-1220): the
-// reference's sequential loops, kG indices per step.  The sequential running
-// minimum with a strict < keeps the FIRST point in visiting order among equal
-// distances, so every lane keeps a lexicographic (distance, visit rank) minimum
-// over the indices it visits and one group reduction combines them.
-// int(I) > cScan + 2.5 <=> int(I) > cScan + 2 (and < cScan - 2.5 <=> < cScan - 2).
+// (distance, visit rank) minimum carrying the index
 __device__ __forceinline__ void group_lex_min3(float& d, int& r, int& j) {
-  for (int s = kG / 2; s > 0; s >>= 1) {
+  for (int s = kGL / 2; s > 0; s >>= 1) {
     const float d2 = __shfl_xor(d, s, 64);
     const int r2 = __shfl_xor(r, s, 64);
     const int j2 = __shfl_xor(j, s, 64);
@@ -417,19 +394,189 @@ __device__ __forceinline__ void group_lex_min3(float& d, int& r, int& j) {
   }
 }
 
+// Walks list k's azimuth buckets outward from the query's bin in one
+// direction (dir 0: bq .. bq + NB/2, dir 1: bq - 1 .. bq - NB/2 + 1, together
+// every bin once), visiting the offsets m = m0 + off, m0 + off + stride, ...
+// (several lanes share one walk), and stops once the angular lower bound on
+// the distance, rq * sin(min(dphi, pi/2)) with rq the query's distance from
+// the y axis, exceeds sqrt(bound()).  Margins absorb the float azimuths.
+template <class Idx, class Visit, class Bound>
+__device__ __forceinline__ void az_walk(const NNView<Idx>& v, int k, float aq, float rq, int dir, int stride, int off,
+                                        const Visit& visit, const Bound& bound) {
+  const int NB = v.NB;
+  const float w = kTwoPi / (float)NB;
+  const int bq = az_bin(aq, NB);
+  const int m0 = dir ? 1 : 0, m1 = dir ? NB / 2 - 1 : NB / 2;
+  for (int m = m0 + off; m <= m1; m += stride) {
+    int b;
+    float lbphi;
+    if (dir == 0) {
+      b = bq + m;
+      lbphi = m == 0 ? 0.f : (float)b * w - aq;
+      if (b >= NB) b -= NB;
+    } else {
+      b = bq - m;
+      lbphi = aq - (float)(b + 1) * w;
+      if (b < 0) b += NB;
+    }
+    const float a = lbphi - 1e-4f;
+    if (a > 0.f) {
+      const float lb = rq * (a >= 1.5707963f ? 1.f : __sinf(a) - 1e-5f) - 1e-4f;
+      if (lb > 0.f && lb * lb > bound()) break;
+    }
+    int lo, hi;
+    bucket_range(v.aEnd, k * NB + b, lo, hi);
+    for (int t = lo; t < hi; ++t) visit((int)v.aOrd[t]);
+  }
+}
+
+// Exact nearest neighbour with d2 < bound, by the calling kGL-lane group: the
+// fine grid's 27-cell and 98-cell shells, each accepted only when the best
+// distance is provably below the radius the shell covers, then every key's
+// azimuth list pruned by the best so far (or every point when the lists are
+// not built).
+template <class Idx>
+__device__ __forceinline__ int nn_i1(const NNView<Idx>& v, float4 q, float bound, int g, unsigned long long* prof) {
+  if (v.n <= 0) return -1;
+  float bd = bound;
+  int bi = INT_MAX;
+  const int cx = cell_of(q.x), cy = cell_of(q.y), cz = cell_of(q.z);
+  auto scan = [&](int ix, int iy, int iz) {
+    int lo, hi;
+    bucket_range(v.gEnd, fine_bucket(ix, iy, iz, v.T), lo, hi);
+    for (int t = lo; t < hi; ++t) {
+      const int j = (int)v.gOrd[t];
+      lex_min(bd, bi, flann_d2(q, v.pts[j]), j);
+    }
+  };
+  for (int c = g; c < 27; c += kGL) scan(cx + c % 3 - 1, cy + (c / 3) % 3 - 1, cz + c / 9 - 1);
+  group_lex_min(bd, bi);
+  if (bd < kCell * kCell * 0.99999f) {
+    if (prof && g == 0) atomicAdd(&prof[P_NN_SHELL1], 1ull);
+    return (bi != INT_MAX && bd < bound) ? bi : -1;
+  }
+  for (int c = g; c < 125; c += kGL) {
+    const int dx = c % 5 - 2, dy = (c / 5) % 5 - 2, dz = c / 25 - 2;
+    if (abs(dx) == 2 || abs(dy) == 2 || abs(dz) == 2) scan(cx + dx, cy + dy, cz + dz);
+  }
+  group_lex_min(bd, bi);
+  if (bd < 4 * kCell * kCell * 0.99999f) return (bi != INT_MAX && bd < bound) ? bi : -1;
+  if (prof && g == 0) atomicAdd(&prof[P_NN_BRUTE], 1ull);
+  if (v.irregular) {
+    for (int j = g; j < v.n; j += kGL) lex_min(bd, bi, flann_d2(q, v.pts[j]), j);
+  } else {
+    const float aq = az_of(q.x, q.z), rq = __builtin_sqrtf(q.x * q.x + q.z * q.z);
+    const int ntask = 2 * v.NK, lpt = ntask >= kGL ? 1 : kGL / ntask;
+    for (int task = g / lpt; task < ntask; task += kGL / lpt)
+      az_walk(
+          v, task >> 1, aq, rq, task & 1, lpt, g % lpt, [&](int j) { lex_min(bd, bi, flann_d2(q, v.pts[j]), j); },
+          [&] { return bd; });
+  }
+  group_lex_min(bd, bi);
+  return (bi != INT_MAX && bd < bound) ? bi : -1;
+}
+
+// Exact nearest neighbour by brute force (stale snapshot, rare).
+__device__ __forceinline__ int nn_brute(const float4* pts, int n, float4 q, float bound, int g) {
+  float bd = bound;
+  int bi = INT_MAX;
+  for (int j = g; j < n; j += kGL) lex_min(bd, bi, flann_d2(q, pts[j]), j);
+  group_lex_min(bd, bi);
+  return (bi != INT_MAX && bd < bound) ? bi : -1;
+}
+
+// Scan-line neighbours of closest point ci (corner :1062-1099, surf
+// :1173-1220), by the calling kGL-lane group.  The forward loop visits
+// (ci, min(F, jend)) where F is the first index after ci whose key exceeds
+// cScan + 2 (int(I) > cScan + 2.5); the backward loop visits (B, ci) where B
+// is the last index before ci whose key is below cScan - 2.  F and B come from
+// the per-key tables when the keys are ordered enough for that to be exact
+// (otherwise false: the caller runs the loops literally).  Every point of that
+// window is a candidate, classed by its key and side exactly as the loops do;
+// the loops' strict < keeps the first visited among equal distances, i.e. the
+// smallest visit rank.  Only the lists of keys cScan-2 .. cScan+2 can hold
+// candidates: a list partly inside the window is scanned over its index span,
+// a list wholly inside is searched through its azimuth buckets, pruned by the
+// best found so far.
+template <class Idx>
+__device__ __forceinline__ bool nn_lines(const NNView<Idx>& v, int ci, int jend, float4 sel, bool surf, float nn_sq,
+                                         int g, int* o2, int* o3) {
+  if (v.irregular) return false;
+  const int cScan = (int)v.pts[ci].w;
+  const int F = (cScan + 3 <= v.NK) ? v.sufFirst[cScan + 3] : INT_MAX;
+  const int B = (cScan - 3 >= 0) ? v.preLast[cScan - 3] : -1;
+  if (F <= ci || B >= ci) return false;
+  const int fwdEnd = min(F, jend);
+  const int hi = fwdEnd > ci ? fwdEnd : ci;  // window = (B, hi) \ {ci}
+  float m2 = nn_sq, m3 = nn_sq;
+  int r2 = INT_MAX, r3 = INT_MAX, i2 = -1, i3 = -1;
+  auto visit = [&](int j, int kj) {
+    if (j == ci || j <= B || j >= hi) return;
+    const bool fwd = j > ci;
+    bool cls2 = true;
+    if (surf) cls2 = fwd ? (kj <= cScan) : (kj >= cScan);
+    else if (fwd ? kj <= cScan : kj >= cScan) return;
+    const float d = line_d2(v.pts[j], sel);
+    if (!(d < nn_sq)) return;
+    const int rank = fwd ? j - ci : (jend - ci) + (ci - j);
+    // selects, not a branch between the two minima (keeps them in registers)
+    const bool u2 = cls2 && (d < m2 || (d == m2 && rank < r2));
+    const bool u3 = !cls2 && (d < m3 || (d == m3 && rank < r3));
+    m2 = u2 ? d : m2; r2 = u2 ? rank : r2; i2 = u2 ? j : i2;
+    m3 = u3 ? d : m3; r3 = u3 ? rank : r3; i3 = u3 ? j : i3;
+  };
+  int azK[4];
+  int nAz = 0;
+  for (int dk = -2; dk <= 2; ++dk) {
+    const int k = cScan + dk;
+    if (k < 0 || k >= v.NK) continue;
+    if (!surf && dk == 0) continue;  // a corner candidate's key differs from cScan
+    const int kf = v.kFirst[k], kl = v.kLast[k];
+    if (kl <= B || kf >= hi) continue;  // no member inside the window
+    if (dk != 0 && kf > B && kl < hi) { azK[nAz++] = k; continue; }
+    const int lo = max(kf, B + 1), up = min(kl, hi - 1);  // partly inside
+    for (int j = lo + g; j <= up; j += kGL) visit(j, (int)v.pts[j].w);
+  }
+  if (nAz) {
+    // share the scans' minima so the walks prune against them
+    group_lex_min3(m2, r2, i2);
+    if (surf) group_lex_min3(m3, r3, i3);
+    const float aq = az_of(sel.x, sel.z), rq = __builtin_sqrtf(sel.x * sel.x + sel.z * sel.z);
+    const int ntask = 2 * nAz, lpt = kGL / 8;  // <= 8 walks, kGL / 8 lanes each
+    const int task = g / lpt;
+    if (task < ntask) {
+      const int k = azK[task >> 1];
+      const bool fwdP = v.kLast[k] > ci, bwdP = v.kFirst[k] < ci;
+      const bool c2 = surf ? ((fwdP && k <= cScan) || (bwdP && k >= cScan)) : true;
+      const bool c3 = surf && ((fwdP && k > cScan) || (bwdP && k < cScan));
+      az_walk(v, k, aq, rq, task & 1, lpt, g % lpt, [&](int j) { visit(j, k); },
+              [&] { return (c2 && c3) ? fmaxf(m2, m3) : (c2 ? m2 : m3); });
+    }
+  }
+  group_lex_min3(m2, r2, i2);
+  if (surf) group_lex_min3(m3, r3, i3);
+  *o2 = i2;
+  *o3 = surf ? i3 : -1;
+  return true;
+}
+
+// The reference's sequential loops, kGL indices per step (fallback).  Every
+// lane keeps a lexicographic (distance, visit rank) minimum over the indices
+// it visits and one group reduction combines them.
+// int(I) > cScan + 2.5 <=> int(I) > cScan + 2 (and < cScan - 2.5 <=> < cScan - 2).
 __device__ __forceinline__ void scanline_group(const float4* last, int jend, int ci, float4 sel, bool surf,
-                                               float nn_sq, int g, int gbase, int* o2, int* o3) {
+                                               float nn_sq, int g, int* o2, int* o3) {
   const int cScan = (int)last[ci].w;
   float m2 = nn_sq, m3 = nn_sq;
   int r2 = INT_MAX, r3 = INT_MAX, i2 = -1, i3 = -1;
-  for (int j0 = ci + 1; j0 < jend; j0 += kG) {
+  for (int j0 = ci + 1; j0 < jend; j0 += kGL) {
     const int j = j0 + g;
     const bool inr = j < jend;
     float4 p = make_float4(0, 0, 0, 0);
     int rj = 0;
     if (inr) { p = last[j]; rj = (int)p.w; }
-    const unsigned bm = group_ballot(inr && rj > cScan + 2, gbase);
-    const int lim = bm ? (__ffs(bm) - 1) : kG;
+    const unsigned long long bm = __ballot(inr && rj > cScan + 2);
+    const int lim = bm ? (__ffsll((long long)bm) - 1) : kGL;
     if (inr && g < lim) {
       const float d = line_d2(p, sel);
       const int rank = j - ci;
@@ -441,14 +588,14 @@ __device__ __forceinline__ void scanline_group(const float4* last, int jend, int
     if (bm) break;
   }
   const int fwdSpan = jend - ci;
-  for (int j0 = ci - 1; j0 >= 0; j0 -= kG) {
+  for (int j0 = ci - 1; j0 >= 0; j0 -= kGL) {
     const int j = j0 - g;
     const bool inr = j >= 0;
     float4 p = make_float4(0, 0, 0, 0);
     int rj = 0;
     if (inr) { p = last[j]; rj = (int)p.w; }
-    const unsigned bm = group_ballot(inr && rj < cScan - 2, gbase);
-    const int lim = bm ? (__ffs(bm) - 1) : kG;
+    const unsigned long long bm = __ballot(inr && rj < cScan - 2);
+    const int lim = bm ? (__ffsll((long long)bm) - 1) : kGL;
     if (inr && g < lim) {
       const float d = line_d2(p, sel);
       const int rank = fwdSpan + (ci - j);
@@ -465,8 +612,117 @@ __device__ __forceinline__ void scanline_group(const float4* last, int jend, int
   *o3 = surf ? i3 : -1;
 }
 
+// Picks one of two buffers without indexing the kernel-argument struct (a
+// dynamic index would move the struct to scratch memory).
+__device__ __forceinline__ float4* buf2(float4* const (&a)[2], int k) { return k ? a[1] : a[0]; }
+
+// ---------------------------------------------------------------- LDS layout
+struct SolveWs {  // thread-0 solver workspace (dynamically indexed by the Jacobi sweep)
+  float A[3][3], W[3], V[3][3], V2[3][3], Vi[3][3];
+  int indR[3], indC[3];
+};
+
+struct OdomLds {
+  float4* lastS;     // [kLdsSurf]
+  float4* lastC;     // [kLdsCorner]
+  int* qi;           // [3 * kLdsQ] correspondence indices
+  unsigned* cnt;     // [max(kLdsGridS, kLdsAz)] index-build counters
+  uint16_t *gEndS, *gOrdS, *gEndC, *gOrdC;  // fine grids
+  uint16_t *aEndS, *aOrdS, *aEndC, *aOrdC;  // ring x azimuth lists
+  int *sufS, *preS, *sufC, *preC;           // [kKeyTab] per-key first / last
+  int *kfS, *klS, *kfC, *klC;              // [kMaxRings] per-key first / last index
+  double* red;       // [kOdomWaves * 10]
+  SolveWs* sw;
+  int* wtot;         // [kOdomWaves]
+  int* n;            // [16] flags
+  OdomState* st;     // the stream state, resident for the kernel's lifetime
+};
+enum { N_BREAK = 0, N_IRR_S = 1, N_IRR_C = 2, N_ROUND = 3 };
+
+__host__ __device__ inline size_t odom_lds_bytes() {
+  size_t s = 0;
+  s += (size_t)kLdsSurf * 16 + (size_t)kLdsCorner * 16 + (size_t)kLdsCnt * 4 + (size_t)3 * kLdsQ * 4;
+  s += (size_t)(kLdsGridS + kLdsSurf + kLdsGridC + kLdsCorner) * 2;
+  s += (size_t)(kLdsAz + kLdsSurf + kLdsAz + kLdsCorner) * 2;
+  s += (size_t)4 * kKeyTab * 4 + (size_t)4 * kMaxRings * 4;
+  s += (size_t)kOdomWaves * 10 * 8 + 256 + (size_t)kOdomWaves * 4 + 16 * 4 + 128;
+  return s;
+}
+
+__device__ __forceinline__ OdomLds odom_carve(unsigned char* base) {
+  OdomLds L;
+  size_t o = 0;
+  L.lastS = (float4*)(base + o); o += (size_t)kLdsSurf * 16;
+  L.lastC = (float4*)(base + o); o += (size_t)kLdsCorner * 16;
+  L.cnt = (unsigned*)(base + o); o += (size_t)kLdsCnt * 4;
+  L.qi = (int*)(base + o); o += (size_t)3 * kLdsQ * 4;
+  L.red = (double*)(base + o); o += (size_t)kOdomWaves * 10 * 8;
+  L.sw = (SolveWs*)(base + o); o += 256;
+  L.gEndS = (uint16_t*)(base + o); o += (size_t)kLdsGridS * 2;
+  L.gOrdS = (uint16_t*)(base + o); o += (size_t)kLdsSurf * 2;
+  L.gEndC = (uint16_t*)(base + o); o += (size_t)kLdsGridC * 2;
+  L.gOrdC = (uint16_t*)(base + o); o += (size_t)kLdsCorner * 2;
+  L.aEndS = (uint16_t*)(base + o); o += (size_t)kLdsAz * 2;
+  L.aOrdS = (uint16_t*)(base + o); o += (size_t)kLdsSurf * 2;
+  L.aEndC = (uint16_t*)(base + o); o += (size_t)kLdsAz * 2;
+  L.aOrdC = (uint16_t*)(base + o); o += (size_t)kLdsCorner * 2;
+  L.sufS = (int*)(base + o); o += (size_t)kKeyTab * 4;
+  L.preS = (int*)(base + o); o += (size_t)kKeyTab * 4;
+  L.sufC = (int*)(base + o); o += (size_t)kKeyTab * 4;
+  L.preC = (int*)(base + o); o += (size_t)kKeyTab * 4;
+  L.kfS = (int*)(base + o); o += (size_t)kMaxRings * 4;
+  L.klS = (int*)(base + o); o += (size_t)kMaxRings * 4;
+  L.kfC = (int*)(base + o); o += (size_t)kMaxRings * 4;
+  L.klC = (int*)(base + o); o += (size_t)kMaxRings * 4;
+  L.wtot = (int*)(base + o); o += (size_t)kOdomWaves * 4;
+  L.n = (int*)(base + o); o += 16 * 4;
+  L.st = (OdomState*)(base + o); o += 128;
+  return L;
+}
+
+// The VLP-16-class configuration whose whole working set fits LDS.
+__device__ __forceinline__ bool sensor_resident(const DevCfg& c) {
+  return c.N * kFlatPerRing <= kLdsQ && c.N * az_nb(c.N) <= kLdsAz;
+}
+
+// Views of the current indexes (valid when the snapshot is current).
+__device__ __forceinline__ NNView<uint16_t> view_lds(bool surf, const OdomLds& L, const OdomState* st, const DevCfg& c) {
+  if (surf)
+    return NNView<uint16_t>{L.lastS, st->surfLastNum, L.gEndS, L.gOrdS, fine_T(st->surfLastNum, kLdsGridS),
+                            L.aEndS, L.aOrdS, az_nb(c.N), c.N, L.sufS, L.preS, L.kfS, L.klS, L.n[N_IRR_S]};
+  return NNView<uint16_t>{L.lastC, st->cornerLastNum, L.gEndC, L.gOrdC, fine_T(st->cornerLastNum, kLdsGridC),
+                          L.aEndC, L.aOrdC, az_nb(c.N), c.N, L.sufC, L.preC, L.kfC, L.klC, L.n[N_IRR_C]};
+}
+__device__ __forceinline__ NNView<uint32_t> view_hbm(bool surf, const OdomLds& L, const OdomBufs& ob,
+                                                     const OdomState* st, const DevCfg& c) {
+  if (surf)
+    return NNView<uint32_t>{buf2(ob.surfLast, st->curBuf), st->surfLastNum, ob.nS.gEnd, ob.nS.gOrd,
+                            fine_T(st->surfLastNum, ob.gTS), ob.nS.aEnd, ob.nS.aOrd, az_nb(c.N), c.N, L.sufS,
+                            L.preS, L.kfS, L.klS, L.n[N_IRR_S]};
+  return NNView<uint32_t>{buf2(ob.cornerLast, st->curBuf), st->cornerLastNum, ob.nC.gEnd, ob.nC.gOrd,
+                          fine_T(st->cornerLastNum, ob.gTC), ob.nC.aEnd, ob.nC.aOrd, az_nb(c.N), c.N, L.sufC,
+                          L.preC, L.kfC, L.klC, L.n[N_IRR_C]};
+}
+
+// Rebuilds both clouds' indexes (all threads) over the current last clouds.
+__device__ __forceinline__ void build_indexes(const OdomLds& L, const OdomBufs& ob, const OdomState* st,
+                                              const DevCfg& c) {
+  if (st->resident) {
+    NNStore<uint16_t> sS{L.gEndS, L.gOrdS, L.aEndS, L.aOrdS, L.sufS, L.preS, L.kfS, L.klS, &L.n[N_IRR_S], kLdsGridS};
+    nn_build<uint16_t>(L.lastS, st->surfLastNum, c.N, sS, L.cnt, L.wtot);
+    NNStore<uint16_t> sC{L.gEndC, L.gOrdC, L.aEndC, L.aOrdC, L.sufC, L.preC, L.kfC, L.klC, &L.n[N_IRR_C], kLdsGridC};
+    nn_build<uint16_t>(L.lastC, st->cornerLastNum, c.N, sC, L.cnt, L.wtot);
+  } else {
+    NNStore<uint32_t> sS{ob.nS.gEnd, ob.nS.gOrd, ob.nS.aEnd, ob.nS.aOrd, L.sufS, L.preS, L.kfS, L.klS, &L.n[N_IRR_S], ob.gTS};
+    nn_build<uint32_t>(buf2(ob.surfLast, st->curBuf), st->surfLastNum, c.N, sS, ob.cnt, L.wtot);
+    NNStore<uint32_t> sC{ob.nC.gEnd, ob.nC.gOrd, ob.nC.aEnd, ob.nC.aOrd, L.sufC, L.preC, L.kfC, L.klC, &L.n[N_IRR_C], ob.gTC};
+    nn_build<uint32_t>(buf2(ob.cornerLast, st->curBuf), st->cornerLastNum, c.N, sC, ob.cnt, L.wtot);
+  }
+}
+
 // ---------------------------------------------------------------- reduction
-// 9 doubles (AtA upper triangle 6 + AtB 3) + the row count over the block.
+// 9 doubles (AtA upper triangle 6 + AtB 3) + the row count; thread 0 gets the
+// block totals (waves summed in order).
 __device__ __forceinline__ void block_sum9(double v[9], int m, const OdomLds& L, double out[9], int* mt) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int k = 0; k < 9; ++k)
@@ -477,14 +733,14 @@ __device__ __forceinline__ void block_sum9(double v[9], int m, const OdomLds& L,
     L.red[wave * 10 + 9] = (double)m;
   }
   __syncthreads();
-  for (int k = 0; k < 9; ++k) {
-    double s = 0;
-    for (int w = 0; w < kOdomWaves; ++w) s += L.red[w * 10 + k];
-    out[k] = s;
+  if (threadIdx.x == 0) {
+    for (int k = 0; k < 10; ++k) {
+      double s = 0;
+      for (int w = 0; w < kOdomWaves; ++w) s += L.red[w * 10 + k];
+      if (k < 9) out[k] = s;
+      else *mt = (int)s;
+    }
   }
-  double ms = 0;
-  for (int w = 0; w < kOdomWaves; ++w) ms += L.red[w * 10 + 9];
-  *mt = (int)ms;
 }
 
 struct ScanFeat {
@@ -494,30 +750,32 @@ struct ScanFeat {
   const float4* lflat; int nLF;
 };
 
-// Shared tail of calculateTransformationSurf / Corner.  Thread 0 only.
+// Shared tail of calculateTransformationSurf / Corner.  Thread 0 only; the
+// eigen workspace lives in LDS.
 __device__ __forceinline__ void solve_step(float (&AtA)[3][3], float (&AtB)[3], int iter, OdomState* st,
-                           float (&X)[3]) {
+                                           SolveWs* ws, float (&X)[3]) {
   float Aq[3][3];
-  for (int a = 0; a < 3; ++a) for (int b = 0; b < 3; ++b) Aq[a][b] = AtA[a][b];
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b) Aq[a][b] = AtA[a][b];
   cv_solve_qr<3, 3>(Aq, AtB, X);
   float (&P)[3][3] = *reinterpret_cast<float(*)[3][3]>(st->matP);
   if (iter == 0) {
-    float E[3], V[3][3], V2[3][3], Ae[3][3];
-    for (int a = 0; a < 3; ++a) for (int b = 0; b < 3; ++b) Ae[a][b] = AtA[a][b];
-    cv_eigen_sym<3>(Ae, E, V);
-    for (int a = 0; a < 3; ++a) for (int b = 0; b < 3; ++b) V2[a][b] = V[a][b];
+    for (int a = 0; a < 3; ++a) for (int b = 0; b < 3; ++b) ws->A[a][b] = AtA[a][b];
+    cv_eigen_sym_ws<3>(ws->A, ws->W, ws->V, ws->indR, ws->indC);
+    for (int a = 0; a < 3; ++a) for (int b = 0; b < 3; ++b) ws->V2[a][b] = ws->V[a][b];
     st->isDegenerate = 0;
     for (int i = 2; i >= 0; i--) {
-      if (E[i] < 10) {
-        for (int j = 0; j < 3; j++) V2[i][j] = 0;
+      if (ws->W[i] < 10) {
+        for (int j = 0; j < 3; j++) ws->V2[i][j] = 0;
         st->isDegenerate = 1;
       } else {
         break;
       }
     }
-    float Vi[3][3];
-    cv_inv3(V, Vi);
-    cv_matmul<3>(Vi, V2, P);
+    cv_inv3(ws->V, ws->Vi);
+    cv_matmul<3>(ws->Vi, ws->V2, P);
   }
   if (st->isDegenerate) {
     float X2[3] = {X[0], X[1], X[2]};
@@ -527,23 +785,68 @@ __device__ __forceinline__ void solve_step(float (&AtA)[3][3], float (&AtB)[3], 
 
 __device__ __forceinline__ double r2d(double r) { return r * 180.0 / M_PI; }
 
+// ---------------------------------------------------------------- exchange
+// The workgroups of a launch run the same serial chain on identical inputs
+// and split only the correspondence searches.  Results travel as 8-byte
+// {tag = round + 1, value} granules (MI355X L2s are per XCD: agent-scope
+// relaxed atomics, the data is its own flag), double-buffered by round parity
+// so a fast workgroup cannot overwrite a granule a slow one has yet to read.
+// The granules are zeroed before every launch.  A bounded spin records a
+// timeout in *err instead of hanging.
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+__device__ __forceinline__ void x_publish(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int x_consume(unsigned long long* p, unsigned long long tag, unsigned* err) {
+  for (unsigned spins = 0;; ++spins) {
+    const unsigned long long x = __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((x & 0xffffffff00000000ull) == tag) return (int)(unsigned)x;
+    if ((spins & 1023) == 1023 && __hip_atomic_load((gu32*)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      return -1;  // another wait already timed out: fail fast
+    if (spins > (1u << 20)) {
+      __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return -1;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 // One LM loop (surf: <= 25 x {findCorrespondingSurfFeatures;
-// calculateTransformationSurf}; corner likewise) — updateTransformation :1666-1695.
-__device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const float4* last, int lastN,
-                        const GridView& nn, OdomState* st, const OdomLds& L, int* gqi,
-                        const DevCfg& c, Stamp& S) {
+// calculateTransformationSurf}; corner likewise) — updateTransformation
+// :1666-1695.  R: the last clouds and indexes are LDS-resident.
+template <bool R>
+__device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const OdomLds& L, const OdomBufs& ob,
+                                        const DevCfg& c, Stamp& S) {
+  using Idx = typename std::conditional<R, uint16_t, uint32_t>::type;
+  OdomState* st = L.st;
   const int tid = threadIdx.x;
+  const float4* last;
+  int* qi;
+  int qs;
+  NNView<Idx> nn;
+  if constexpr (R) {
+    last = surf ? L.lastS : L.lastC;
+    qi = L.qi; qs = kLdsQ;
+    nn = view_lds(surf, L, st, c);
+  } else {
+    last = surf ? buf2(ob.surfLast, st->curBuf) : buf2(ob.cornerLast, st->curBuf);
+    qi = ob.qi; qs = ob.capQ;
+    nn = view_hbm(surf, L, ob, st, c);
+  }
+  const int lastN = surf ? st->surfLastNum : st->cornerLastNum;
+  const bool stale = st->curBuf != st->snapBuf;
+  const float4* snap = surf ? buf2(ob.surfLast, st->snapBuf) : buf2(ob.cornerLast, st->snapBuf);
+  const int snapN = surf ? st->nnSurfNum : st->nnCornerNum;
   const float4* qp = surf ? F.flat : F.sharp;
   const int nQ = surf ? F.nFlat : F.nSharp;
   const int jend = min(nQ, lastN);  // the reference bounds by the query count (:1062, :1173)
-  int* qi = (nQ <= kLdsQ) ? L.qi : gqi;
-  const int qs = (nQ <= kLdsQ) ? kLdsQ : nQ;  // stride between the three index arrays
-  const int g = tid & (kG - 1), gbase = tid & 63 & ~(kG - 1), grp = tid / kG;
-  const int ngrp = blockDim.x / kG;
+  const int g = tid & (kGL - 1), grp = tid / kGL;
   for (int it = 0; it < 25; it++) {
     S.start();
     S.count(surf ? P_ITERS_S : P_ITERS_C);
-    if (it % 5 == 0) S.count(P_NNR);
+    const bool nnIter = it % 5 == 0;
+    if (nnIter) S.count(P_NNR);
     float tc[6];
     for (int i = 0; i < 6; ++i) tc[i] = st->transformCur[i];
     const float srx = lego_sinf(tc[0]), crx = lego_cosf(tc[0]);
@@ -552,20 +855,44 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const floa
     const float tx = tc[3], ty = tc[4], tz = tc[5];
     double acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     int mloc = 0;
-    if (it % 5 == 0) {
-      // nearest neighbour + scan-line search, one 32-lane group per query
-      for (int q = grp; q < nQ; q += ngrp) {
+    if (nnIter) {
+      // This workgroup's slice of the queries, one wave per query; the slices
+      // of the other workgroups of the launch arrive through the exchange.
+      const int G = gridDim.x, per = (nQ + G - 1) / G;
+      const int q0 = min(nQ, (int)blockIdx.x * per), q1 = min(nQ, q0 + per);
+      const int round = L.n[N_ROUND];
+      unsigned long long* xg = ob.xg + (size_t)(round & 1) * 3 * ob.capQ;
+      const unsigned long long tag = (unsigned long long)(round + 1) << 32;
+      for (int q = q0 + grp; q < q1; q += kNGrp) {
         const float4 sel = to_start(qp[q], tc);
-        int i1 = grid_nn(nn, sel, c.nn_sq, g, S.prof);
-        if (i1 >= lastN) i1 = -1;  // stale snapshot of a larger cloud
+        int i1 = stale ? nn_brute(snap, snapN, sel, c.nn_sq, g) : nn_i1(nn, sel, c.nn_sq, g, S.prof);
+        if (i1 >= lastN) i1 = -1;  // an index past a stale snapshot's cloud
         int i2 = -1, i3 = -1;
-        if (i1 >= 0) scanline_group(last, jend, i1, sel, surf, c.nn_sq, g, gbase, &i2, &i3);
-        if (g == 0) { qi[q] = i1; qi[qs + q] = i2; qi[2 * qs + q] = i3; }
+        if (i1 >= 0 && (stale || !nn_lines(nn, i1, jend, sel, surf, c.nn_sq, g, &i2, &i3))) {
+          if (S.prof && g == 0) atomicAdd(&S.prof[P_SCANLINE], 1ull);
+          scanline_group(last, jend, i1, sel, surf, c.nn_sq, g, &i2, &i3);
+        }
+        if (g == 0) {
+          qi[q] = i1; qi[qs + q] = i2; qi[2 * qs + q] = i3;
+          if (G > 1) {
+            x_publish(xg + 3 * q + 0, tag | (unsigned)i1);
+            x_publish(xg + 3 * q + 1, tag | (unsigned)i2);
+            x_publish(xg + 3 * q + 2, tag | (unsigned)i3);
+          }
+        }
+      }
+      if (G > 1) {
+        for (int e = tid; e < 3 * nQ; e += kOdomThreads) {
+          const int q = e / 3, k = e - 3 * q;
+          if (q >= q0 && q < q1) continue;
+          qi[k * qs + q] = x_consume(xg + e, tag, ob.xerr);
+        }
       }
       __syncthreads();
+      if (tid == 0) L.n[N_ROUND] = round + 1;
       S.add(P_QUERY);
     }
-    for (int q = tid; q < nQ; q += blockDim.x) {
+    for (int q = tid; q < nQ; q += kOdomThreads) {
       const float4 po = qp[q];
       const float4 sel = to_start(po, tc);
       const int i1 = qi[q], i2 = qi[qs + q], i3 = qi[2 * qs + q];
@@ -648,9 +975,9 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const floa
       }
     }
     double tot[9];
-    int M;
+    int M = 0;
     block_sum9(acc, mloc, L, tot, &M);
-    S.add(surf ? (it % 5 == 0 ? P_SURF_NN : P_SURF) : (it % 5 == 0 ? P_CORN_NN : P_CORN));
+    S.add(surf ? (nnIter ? P_SURF_NN : P_SURF) : (nnIter ? P_CORN_NN : P_CORN));
     if (tid == 0) {
       L.n[N_BREAK] = 0;
       if (M >= 10) {
@@ -659,7 +986,7 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const floa
                            {(float)tot[2], (float)tot[4], (float)tot[5]}};
         float AtB[3] = {(float)tot[6], (float)tot[7], (float)tot[8]};
         float X[3];
-        solve_step(AtA, AtB, it, st, X);
+        solve_step(AtA, AtB, it, st, L.sw, X);
         float* t = st->transformCur;
         double dR, dT;
         if (surf) {
@@ -689,30 +1016,27 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const floa
   }
 }
 
-// Copies the last clouds into LDS when they fit.
-struct Resident {
-  const float4* lastS;
-  const float4* lastC;
-  GridView nnS, nnC;
-};
-
-__device__ __forceinline__ void make_resident(const OdomBufs& ob, const OdomState* st, const OdomLds& L, Resident& R) {
-  const int tid = threadIdx.x;
-  const int ns = st->surfLastNum, nc = st->cornerLastNum;
-  R.lastS = ns <= kLdsSurf ? L.lastS : ob.surfLast;
-  R.lastC = nc <= kLdsCorner ? L.lastC : ob.cornerLast;
-  R.nnS = GridView{ob.gS.keys, ob.gS.cnt, ob.gS.start, ob.gS.pts, ob.gS.idx,
-                   grid_table_size(st->nnSurfNum), st->nnSurfNum};
-  R.nnC = GridView{ob.gC.keys, ob.gC.cnt, ob.gC.start, ob.gC.pts, ob.gC.idx,
-                   grid_table_size(st->nnCornerNum), st->nnCornerNum};
-  if (ns <= kLdsSurf) for (int t = tid; t < ns; t += blockDim.x) L.lastS[t] = ob.surfLast[t];
-  if (nc <= kLdsCorner) for (int t = tid; t < nc; t += blockDim.x) L.lastC[t] = ob.cornerLast[t];
-  __syncthreads();
+// This workgroup's private HBM buffers (the launch's workgroups never share them).
+__device__ __forceinline__ OdomBufs odom_private(OdomBufs ob) {
+  const size_t w = blockIdx.x;
+  ob.cornerLast[0] += w * ob.capCorner;
+  ob.cornerLast[1] += w * ob.capCorner;
+  ob.surfLast[0] += w * ob.capSurf;
+  ob.surfLast[1] += w * ob.capSurf;
+  ob.nC.gEnd += w * ob.gTC; ob.nC.gOrd += w * ob.capCorner;
+  ob.nC.aEnd += w * ob.azB; ob.nC.aOrd += w * ob.capCorner;
+  ob.nS.gEnd += w * ob.gTS; ob.nS.gOrd += w * ob.capSurf;
+  ob.nS.aEnd += w * ob.azB; ob.nS.aOrd += w * ob.capSurf;
+  ob.cnt += w * ob.cntCap;
+  ob.qi += w * 3 * ob.capQ;
+  return ob;
 }
 
-__global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob, DevCfg c, int B,
-                                                      unsigned long long* gkeys, int* gqi,
+__global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs obShared, DevCfg c, int B,
                                                       unsigned long long* prof) {
+  const OdomBufs ob = odom_private(obShared);
+  const bool lead = blockIdx.x == 0;  // writes the outputs and the state
+  if (!lead) prof = nullptr;
   Stamp S{prof, 0};
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   const OdomLds L = odom_carve(lds_raw);
@@ -720,10 +1044,22 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
   static_assert(sizeof(OdomState) <= 128, "OdomState LDS slot");
   OdomState* st = L.st;
   if (tid < (int)(sizeof(OdomState) / 4)) ((int*)st)[tid] = ((const int*)ob.st)[tid];
+  if (tid == 0) L.n[N_ROUND] = 0;
   __syncthreads();
-  Resident R;
+  const bool sensorRes = sensor_resident(c);
+  // LDS does not survive launches: reload the current last clouds and rebuild
+  // the indexes over them (unless the snapshot is stale: brute force then).
   S.start();
-  make_resident(ob, st, L, R);
+  if (st->inited) {
+    if (st->resident) {
+      const float4* gS = buf2(ob.surfLast, st->curBuf);
+      const float4* gC = buf2(ob.cornerLast, st->curBuf);
+      for (int t = tid; t < st->surfLastNum; t += kOdomThreads) L.lastS[t] = gS[t];
+      for (int t = tid; t < st->cornerLastNum; t += kOdomThreads) L.lastC[t] = gC[t];
+      __syncthreads();
+    }
+    if (st->curBuf == st->snapBuf) build_indexes(L, ob, st, c);
+  }
   S.add(P_RESID);
   const ImuEnd im{1.f, 1.f, 1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 1.f, 0.f, 1.f, 0.f};
   for (int b = 0; b < B; ++b) {
@@ -739,8 +1075,13 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     if (!init) {
       // updateInitialGuess is a no-op without IMU
       if (st->cornerLastNum >= 10 && st->surfLastNum >= 100) {
-        lm_loop(true, F, R.lastS, st->surfLastNum, R.nnS, st, L, gqi, c, S);
-        lm_loop(false, F, R.lastC, st->cornerLastNum, R.nnC, st, L, gqi, c, S);
+        if (st->resident) {
+          lm_loop<true>(true, F, L, ob, c, S);
+          lm_loop<true>(false, F, L, ob, c, S);
+        } else {
+          lm_loop<false>(true, F, L, ob, c, S);
+          lm_loop<false>(false, F, L, ob, c, S);
+        }
       }
       // integrateTransformation :1697-1725
       S.start();
@@ -767,33 +1108,36 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     }
     S.start();
     // hand-off: checkSystemInitialization (:1605-1637, no TransformToEnd) or
-    // publishCloudsLast (:1759-1815)
+    // publishCloudsLast (:1759-1815).  The new last clouds go to the HBM
+    // buffer that is not the index snapshot (so a stale snapshot survives),
+    // to the per-scan outputs, and to LDS when they fit.
+    const int nbuf = st->snapBuf ^ 1;
+    float4* gCn = buf2(ob.cornerLast, nbuf);
+    float4* gSn = buf2(ob.surfLast, nbuf);
+    const bool fits = sensorRes && F.nLS <= kLdsCorner && F.nLF <= kLdsSurf;
     float tcur[6];
     for (int i = 0; i < 6; ++i) tcur[i] = st->transformCur[i];
-    for (int t = tid; t < F.nLS; t += blockDim.x) {
+    for (int t = tid; t < F.nLS; t += kOdomThreads) {
       const float4 p = init ? F.lsharp[t] : to_end(F.lsharp[t], tcur, im);
-      ob.cornerLast[t] = p;
-      cEnd[t] = p;
+      gCn[t] = p;
+      if (lead) cEnd[t] = p;
+      if (fits) L.lastC[t] = p;
     }
-    for (int t = tid; t < F.nLF; t += blockDim.x) {
+    for (int t = tid; t < F.nLF; t += kOdomThreads) {
       const float4 p = init ? F.lflat[t] : to_end(F.lflat[t], tcur, im);
-      ob.surfLast[t] = p;
-      sEnd[t] = p;
+      gSn[t] = p;
+      if (lead) sEnd[t] = p;
+      if (fits) L.lastS[t] = p;
     }
     __syncthreads();
     S.add(P_TOEND);
     const bool rebuild = init || (F.nLS > 10 && F.nLF > 100);
-    unsigned long long tb = 0;
-    if (prof && tid == 0) tb = wall_clock64();
-    if (rebuild) {
-      grid_build(ob.cornerLast, F.nLS, ob.gC.keys, ob.gC.cnt, ob.gC.start, ob.gC.slot, ob.gC.pts, ob.gC.idx, L);
-      grid_build(ob.surfLast, F.nLF, ob.gS.keys, ob.gS.cnt, ob.gS.start, ob.gS.slot, ob.gS.pts, ob.gS.idx, L);
-    }
-    if (prof && tid == 0) prof[P_BUILD] += wall_clock64() - tb;
     if (tid == 0) {
       st->cornerLastNum = F.nLS;
       st->surfLastNum = F.nLF;
-      if (rebuild) { st->nnCornerNum = F.nLS; st->nnSurfNum = F.nLF; }
+      st->curBuf = nbuf;
+      st->resident = fits ? 1 : 0;
+      if (rebuild) { st->snapBuf = nbuf; st->nnCornerNum = F.nLS; st->nnSurfNum = F.nLF; }
       int pub = 0;
       if (init) {
         st->transformSum[0] += 0.0f;  // += imuPitchStart
@@ -803,26 +1147,58 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
         st->frameCount++;
         if (st->frameCount >= c.skip + 1) { st->frameCount = 0; pub = 1; }
       }
-      ob.validOut[b] = init ? 0 : 1;
-      ob.pubOut[b] = pub;
-      for (int i = 0; i < 6; ++i) { ob.sumOut[b * 6 + i] = st->transformSum[i]; ob.curOut[b * 6 + i] = st->transformCur[i]; }
+      if (lead) {
+        ob.validOut[b] = init ? 0 : 1;
+        ob.pubOut[b] = pub;
+        for (int i = 0; i < 6; ++i) { ob.sumOut[b * 6 + i] = st->transformSum[i]; ob.curOut[b * 6 + i] = st->transformCur[i]; }
+      }
       __threadfence_block();
     }
     __syncthreads();
-    S.start();
-    make_resident(ob, st, L, R);
-    S.add(P_RESID);
+    unsigned long long tb = 0;
+    if (prof && tid == 0) tb = wall_clock64();
+    if (rebuild) build_indexes(L, ob, st, c);
+    if (prof && tid == 0) prof[P_BUILD] += wall_clock64() - tb;
   }
   __syncthreads();
-  if (tid < (int)(sizeof(OdomState) / 4)) ((int*)ob.st)[tid] = ((const int*)st)[tid];
+  if (lead && tid < (int)(sizeof(OdomState) / 4)) ((int*)ob.st)[tid] = ((const int*)st)[tid];
 }
 
-size_t odom_grid_table(int npts) { return (size_t)grid_table_size(npts); }
+void odom_index_caps(int capCorner, int capSurf, int N, int* gTC, int* gTS, int* azBuckets) {
+  int t = 64;
+  while (t < capCorner / 2) t <<= 1;
+  *gTC = t;
+  t = 64;
+  while (t < capSurf / 2) t <<= 1;
+  *gTS = t;
+  *azBuckets = N * az_nb(N);
+}
 
-void launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int B, hipStream_t s,
-                 StageTimer* tm, unsigned long long* gkeys, int* gqi, unsigned long long* prof) {
+// Workgroups of the odometry launch: LDS-resident sensors split each NN round
+// over one wave per query of the largest round (flat <= 24 N queries).
+int odom_workgroups(int N, int cusAvailable) {
+  if (N * kFlatPerRing > kLdsQ || N * az_nb(N) > kLdsAz) return 1;
+  const int g = (N * kFlatPerRing + kOdomWaves - 1) / kOdomWaves;
+  return g < cusAvailable ? g : cusAvailable;
+}
+
+int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int B, hipStream_t s, StageTimer* tm,
+                unsigned long long* prof) {
   tm->mark("odom.lm", s);
-  k_odom<<<1, kOdomThreads, odom_lds_bytes(), s>>>(bb, ob, c, B, gkeys, gqi, prof);
+  // the exchange granules and the timeout word are zeroed before every launch
+  if (hipMemsetAsync(ob.xblock, 0, ob.xbytes, s) != hipSuccess) return -1;
+  if (ob.G <= 1) {
+    k_odom<<<1, kOdomThreads, odom_lds_bytes(), s>>>(bb, ob, c, B, prof);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
+  BatchBufs a0 = bb;
+  OdomBufs a1 = ob;
+  DevCfg a2 = c;
+  int a3 = B;
+  unsigned long long* a4 = prof;
+  void* args[] = {&a0, &a1, &a2, &a3, &a4};
+  return hipLaunchCooperativeKernel((const void*)k_odom, dim3(ob.G), dim3(kOdomThreads), args,
+                                    (unsigned)odom_lds_bytes(), s) == hipSuccess ? 0 : -1;
 }
 
 }  // namespace lego
