@@ -203,8 +203,8 @@ def main():
                   f"  per scan: nn shell-1 {prof[14] / nsc:.1f}, nn exhaustive {prof[15] / nsc:.1f},"
                   f" scan-line indexed {prof[20] / nsc:.1f}, scan-line literal {prof[13] / nsc:.1f}",
                   file=sys.stderr)
-            print(f"  odom.nn_exhaust {prof[17] / 100.0 / nsc:9.2f} us/scan\n  odom.scan_line  {prof[18] / 100.0 / nsc:9.2f} us/scan",
-                  file=sys.stderr)
+            for i, nm in ((21, "rows (excl. reduce)"), (22, "solve_qr+eig it0"), (23, "solve_qr it>0")):
+                print(f"  odom.{nm:20s} {prof[i] / 100.0 / nsc:9.2f} us/scan", file=sys.stderr)
         if args.stages:
             tot = sum(stage_acc.values())
             for k, v in sorted(stage_acc.items(), key=lambda kv: -kv[1]):

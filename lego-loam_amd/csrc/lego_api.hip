@@ -283,16 +283,13 @@ int lego_create(const lego_sensor_cfg* cfg, int device, int32_t max_points, int3
       A(ob.cornerLast[k], G * ob.capCorner);
       A(ob.surfLast[k], G * ob.capSurf);
     }
-    int gTC = 0, gTS = 0, az = 0;
-    odom_index_caps(ob.capCorner, ob.capSurf, (int)N, &gTC, &gTS, &az);
+    int gTC = 0, gTS = 0;
+    odom_index_caps(ob.capCorner, ob.capSurf, &gTC, &gTS);
     ob.gTC = gTC;
     ob.gTS = gTS;
-    ob.azB = az;
-    ob.cntCap = std::max(std::max(gTC, gTS), az);
+    ob.cntCap = std::max(gTC, gTS);
     A(ob.nC.gEnd, G * gTC); A(ob.nC.gOrd, G * ob.capCorner);
-    A(ob.nC.aEnd, G * az); A(ob.nC.aOrd, G * ob.capCorner);
     A(ob.nS.gEnd, G * gTS); A(ob.nS.gOrd, G * ob.capSurf);
-    A(ob.nS.aEnd, G * az); A(ob.nS.aOrd, G * ob.capSurf);
     A(ob.cnt, G * ob.cntCap);
     ob.capQ = (int)(N * kFlatPerRing);
     A(ob.qi, G * 3 * ob.capQ);

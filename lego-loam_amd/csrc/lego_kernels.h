@@ -67,8 +67,6 @@ class StageTimer {
 struct NNIndexBufs {
   uint32_t* gEnd;  // [gT]        fine-grid bucket ends
   uint32_t* gOrd;  // [cap]       point order
-  uint32_t* aEnd;  // [N * NB]    ring x azimuth bucket ends
-  uint32_t* aOrd;  // [cap]
 };
 
 // Odometry state kept on the device for one stream (featureAssociation.cpp
@@ -97,7 +95,7 @@ struct OdomBufs {
   NNIndexBufs nC, nS;     // [G x] HBM indexes (sensors too large for LDS)
   uint32_t* cnt;          // [G x cntCap] index-build counters
   int* qi;                // [G x 3 * capQ] HBM correspondences
-  int gTC, gTS, azB, cntCap;
+  int gTC, gTS, cntCap;
   int capCorner, capSurf, capQ;
   int G;                  // workgroups per launch
   // exchange (zeroed before each launch): timeout word, then 2 x 3 x capQ granules
@@ -124,6 +122,6 @@ int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int B,
                 StageTimer* tm, unsigned long long* prof);
 int odom_workgroups(int N, int cusAvailable);
 // HBM index sizes for clouds of up to capCorner / capSurf points.
-void odom_index_caps(int capCorner, int capSurf, int N, int* gTC, int* gTS, int* azBuckets);
+void odom_index_caps(int capCorner, int capSurf, int* gTC, int* gTS);
 
 }  // namespace lego

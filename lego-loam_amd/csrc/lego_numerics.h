@@ -416,6 +416,81 @@ LEGO_HD void cv_eigen_sym(float (&A)[N][N], float (&W)[N], float (&V)[N][N]) {
   cv_eigen_sym_ws<N>(A, W, V, indR, indC);
 }
 
+// cv_eigen_sym<3> with every index resolved at compile time, so device code
+// keeps the whole Jacobi state in registers.  Same operations in the same
+// order as the generic form above (tests/native/eigen3_check.cpp compares the
+// two bit for bit): only the pivot bookkeeping is spelled out.  For N = 3 the
+// pivots are (0,1), (0,2), (1,2); indR[1] = 2 and indC[1] = 0 are constant.
+LEGO_HD void cv_eigen_sym3(const float (&Ain)[3][3], float (&W)[3], float (&V)[3][3]) {
+  const float eps = 1.1920928955078125e-07f;
+  float a01 = Ain[0][1], a02 = Ain[0][2], a12 = Ain[1][2];
+  float w0 = Ain[0][0], w1 = Ain[1][1], w2 = Ain[2][2];
+  float v00 = 1.f, v01 = 0.f, v02 = 0.f, v10 = 0.f, v11 = 1.f, v12 = 0.f, v20 = 0.f, v21 = 0.f, v22 = 1.f;
+  int indR0 = (lfabsf(a01) < lfabsf(a02)) ? 2 : 1;
+  int indC2 = (lfabsf(a02) < lfabsf(a12)) ? 1 : 0;
+  for (int iters = 0; iters < 3 * 3 * 30; iters++) {
+    int k = 0, l;
+    float mv = indR0 == 1 ? lfabsf(a01) : lfabsf(a02);
+    float val = lfabsf(a12);
+    if (mv < val) mv = val, k = 1;
+    l = k == 0 ? indR0 : 2;
+    val = lfabsf(a01);
+    if (mv < val) mv = val, k = 0, l = 1;
+    val = indC2 == 0 ? lfabsf(a02) : lfabsf(a12);
+    if (mv < val) mv = val, k = indC2, l = 2;
+    const int pr = k == 0 ? (l == 1 ? 0 : 1) : 2;  // (0,1) (0,2) (1,2)
+    float p = pr == 0 ? a01 : (pr == 1 ? a02 : a12);
+    if (lfabsf(p) <= eps) break;
+    const float wk = pr == 2 ? w1 : w0, wl = pr == 0 ? w1 : w2;
+    float y = (float)((double)(wl - wk) * 0.5);
+    float t = lfabsf(y) + cv_hypot(p, y);
+    float s = cv_hypot(p, t);
+    float c = t / s;
+    s = p / s;
+    t = (p / t) * p;
+    if (y < 0) s = -s, t = -t;
+    float a0, b0;
+#define LEGO_ROT(v0_, v1_) a0 = v0_, b0 = v1_, v0_ = a0 * c - b0 * s, v1_ = a0 * s + b0 * c
+    if (pr == 0) {
+      a01 = 0; w0 -= t; w1 += t;
+      LEGO_ROT(a02, a12);
+      LEGO_ROT(v00, v10); LEGO_ROT(v01, v11); LEGO_ROT(v02, v12);
+    } else if (pr == 1) {
+      a02 = 0; w0 -= t; w2 += t;
+      LEGO_ROT(a01, a12);
+      LEGO_ROT(v00, v20); LEGO_ROT(v01, v21); LEGO_ROT(v02, v22);
+    } else {
+      a12 = 0; w1 -= t; w2 += t;
+      LEGO_ROT(a01, a02);
+      LEGO_ROT(v10, v20); LEGO_ROT(v11, v21); LEGO_ROT(v12, v22);
+    }
+#undef LEGO_ROT
+    // indR / indC of rows and columns k and l (the only ones that change)
+    if (k == 0 || l == 0) indR0 = (lfabsf(a01) < lfabsf(a02)) ? 2 : 1;
+    if (k == 2 || l == 2) indC2 = (lfabsf(a02) < lfabsf(a12)) ? 1 : 0;
+  }
+  // selection sort, descending (strict <), rows of V follow
+  float r0[3] = {v00, v01, v02}, r1[3] = {v10, v11, v12}, r2[3] = {v20, v21, v22};
+  {
+    int m = 0;
+    if (w0 < w1) m = 1;
+    if ((m == 0 ? w0 : w1) < w2) m = 2;
+    if (m == 1) {
+      float tw = w1; w1 = w0; w0 = tw;
+      for (int i = 0; i < 3; i++) { float tv = r1[i]; r1[i] = r0[i]; r0[i] = tv; }
+    } else if (m == 2) {
+      float tw = w2; w2 = w0; w0 = tw;
+      for (int i = 0; i < 3; i++) { float tv = r2[i]; r2[i] = r0[i]; r0[i] = tv; }
+    }
+  }
+  if (w1 < w2) {
+    float tw = w2; w2 = w1; w1 = tw;
+    for (int i = 0; i < 3; i++) { float tv = r2[i]; r2[i] = r1[i]; r1[i] = tv; }
+  }
+  W[0] = w0; W[1] = w1; W[2] = w2;
+  for (int i = 0; i < 3; i++) { V[0][i] = r0[i]; V[1][i] = r1[i]; V[2][i] = r2[i]; }
+}
+
 // cv::solve(A, b, x, DECOMP_QR) for a square float system with one rhs
 // (hal::QR32f, eps = 10*FLT_EPSILON).  A and b are destroyed; x written.
 // On failure OpenCV zeroes dst (lapack.cpp: `if (!result) dst = Scalar(0)`).

@@ -43,9 +43,8 @@ constexpr int kLdsSurf = 4096;                // last surf cloud points
 constexpr int kLdsCorner = 2048;              // last corner cloud points
 constexpr int kLdsQ = 384;                    // queries (flat <= 24 N, sharp <= 12 N)
 constexpr int kLdsGridS = 2048, kLdsGridC = 1024;  // fine-grid buckets
-constexpr int kLdsAz = 2048;                  // ring x azimuth buckets per cloud
 constexpr int kKeyTab = kMaxRings + 4;
-constexpr int kLdsCnt = kLdsGridS > kLdsAz ? kLdsGridS : kLdsAz;
+constexpr int kLdsCnt = kLdsGridS;
 constexpr float kCell = 0.5f;
 
 // ---------------------------------------------------------------- transforms
@@ -199,7 +198,8 @@ __device__ __forceinline__ void plugin_imu_rotation(float bcx, float bcy, float 
 enum { P_SURF_NN = 0, P_SURF = 1, P_CORN_NN = 2, P_CORN = 3, P_SOLVE = 4, P_INTEG = 5,
        P_TOEND = 6, P_BUILD = 7, P_RESID = 8, P_ITERS_S = 9, P_ITERS_C = 10, P_NNR = 11,
        P_QUERY = 12, P_SCANLINE = 13, P_NN_SHELL1 = 14, P_NN_BRUTE = 15,
-       P_G0_TOSTART = 16, P_G0_NN = 17, P_G0_SCAN = 18, P_G0_Q = 19, P_AZLINE = 20, P_NPROF = 32 };
+       P_G0_TOSTART = 16, P_G0_NN = 17, P_G0_SCAN = 18, P_G0_Q = 19, P_AZLINE = 20,
+       P_T_ROWS = 21, P_T_SOLVE0 = 22, P_T_SOLVE = 23, P_NPROF = 32 };
 struct Stamp {
   unsigned long long* prof;
   unsigned long long t;
@@ -210,35 +210,28 @@ struct Stamp {
   __device__ __forceinline__ void count(int k) { if (prof && threadIdx.x == 0) prof[k] += 1; }
 };
 
-// ---------------------------------------------------------------- NN indexes
-// Two bucket indexes over one last cloud, both built by counting sort:
-//   fine grid  0.5 m cells hashed into T buckets;
-//   az lists   bucket = key * NB + azimuth bin, key = int(intensity) (the ring
-//              the scan-line loops test), azimuth about the camera y (up) axis.
-// A bucket array holds END offsets into a point-order array (begin = the
-// previous bucket's end).  Order inside a bucket is arbitrary: every search
-// keeps a lexicographic minimum, so the result does not depend on it.
+// ---------------------------------------------------------------- NN index
+// Fine grid over one last cloud: 0.5 m cells hashed into T buckets, built by
+// counting sort (bucket array = END offsets into a point-order array, begin =
+// the previous bucket's end; order inside a bucket is arbitrary, every search
+// keeps a lexicographic minimum).  Plus per-key first/last tables, key =
+// int(intensity), the ring the scan-line loops test.
 template <class Idx>
 struct NNView {
   const float4* pts;
   int n;
   const Idx* gEnd;
   const Idx* gOrd;
-  int T;
-  const Idx* aEnd;
-  const Idx* aOrd;
-  int NB, NK;
-  const int* sufFirst;  // [NK + 1] first index whose key >= k
-  const int* preLast;   // [NK]     last index whose key <= k
-  const int* kFirst;    // [NK]     first / last index of key k (INT_MAX / -1 if none)
-  const int* kLast;
-  int irregular;        // a key outside [0, NK): the az lists are not built
+  int T, NK;
+  const int* sufFirst;  // [NK + 1] first index whose key >= k (INT_MAX if none)
+  const int* preLast;   // [NK]     last index whose key <= k (-1 if none)
+  int irregular;        // a key outside [0, NK): tables unusable
 };
 
 template <class Idx>
 struct NNStore {
-  Idx *gEnd, *gOrd, *aEnd, *aOrd;
-  int *sufFirst, *preLast, *kFirst, *kLast, *irregular;
+  Idx *gEnd, *gOrd;
+  int *sufFirst, *preLast, *irregular;
   int Tcap;
 };
 
@@ -253,19 +246,6 @@ __device__ __forceinline__ unsigned hash_key(unsigned long long k) {
 __device__ __forceinline__ int cell_of(float v) { return (int)floorf(v * (1.0f / kCell)); }
 __device__ __forceinline__ int fine_bucket(int ix, int iy, int iz, int T) {
   return (int)(hash_key(cell_key(ix, iy, iz)) & (unsigned)(T - 1));
-}
-
-constexpr float kTwoPi = 6.28318530717958647692f;
-// azimuth in [0, 2 pi] about the camera y axis (x = lidar y, z = lidar x)
-__device__ __forceinline__ float az_of(float x, float z) { return atan2f(x, z) + 3.14159265358979323846f; }
-__device__ __forceinline__ int az_bin(float a, int NB) {
-  const int b = (int)(a * ((float)NB / kTwoPi));
-  return b < 0 ? 0 : (b >= NB ? NB - 1 : b);
-}
-__host__ __device__ inline int az_nb(int N) {
-  int nb = 128;
-  while (nb > 32 && N * nb > kLdsAz) nb >>= 1;
-  return nb;
 }
 __host__ __device__ inline int fine_T(int n, int cap) {
   int t = 64;
@@ -297,41 +277,25 @@ __device__ __forceinline__ void block_exscan(unsigned* a, int n, int* wtot) {
   __syncthreads();
 }
 
-// counting sort of point indices 0..n-1 into nb buckets
-template <class Idx, class Bid>
-__device__ __forceinline__ void bucket_build(int n, int nb, const Bid& bid, unsigned* cnt, Idx* E, Idx* Ord,
-                                             int* wtot) {
-  const int tid = threadIdx.x;
-  for (int b = tid; b < nb; b += kOdomThreads) cnt[b] = 0;
-  __syncthreads();
-  for (int i = tid; i < n; i += kOdomThreads) atomicAdd(&cnt[bid(i)], 1u);
-  __syncthreads();
-  block_exscan(cnt, nb, wtot);
-  for (int i = tid; i < n; i += kOdomThreads) Ord[atomicAdd(&cnt[bid(i)], 1u)] = (Idx)i;
-  __syncthreads();
-  for (int b = tid; b < nb; b += kOdomThreads) E[b] = (Idx)cnt[b];
-  __syncthreads();
-}
-
-// Builds both indexes and the per-key first/last tables over pts[0..n).
+// Builds the fine grid and the key tables over pts[0..n) (all threads).
 template <class Idx>
 __device__ __forceinline__ void nn_build(const float4* pts, int n, int NK, const NNStore<Idx>& S, unsigned* cnt,
-                                         int* wtot) {
-  int* kfirst = S.kFirst;
-  int* klast = S.kLast;
+                                         int* wtot, int* kfirst, int* klast) {
   const int tid = threadIdx.x;
-  const int T = fine_T(n, S.Tcap), NB = az_nb(NK);
+  const int T = fine_T(n, S.Tcap);
+  for (int b = tid; b < T; b += kOdomThreads) cnt[b] = 0;
   for (int k = tid; k < NK; k += kOdomThreads) { kfirst[k] = INT_MAX; klast[k] = -1; }
   if (tid == 0) *S.irregular = 0;
   __syncthreads();
   for (int i = tid; i < n; i += kOdomThreads) {
-    const int k = (int)pts[i].w;
+    const float4 p = pts[i];
+    atomicAdd(&cnt[fine_bucket(cell_of(p.x), cell_of(p.y), cell_of(p.z), T)], 1u);
+    const int k = (int)p.w;
     if (k < 0 || k >= NK) { *S.irregular = 1; continue; }
     atomicMin(&kfirst[k], i);
     atomicMax(&klast[k], i);
   }
   __syncthreads();
-  const int irregular = *S.irregular;
   if (tid == 0) {
     int m = INT_MAX;
     S.sufFirst[NK] = INT_MAX;
@@ -339,21 +303,14 @@ __device__ __forceinline__ void nn_build(const float4* pts, int n, int NK, const
     int M = -1;
     for (int k = 0; k < NK; ++k) { M = max(M, klast[k]); S.preLast[k] = M; }
   }
-  bucket_build<Idx>(
-      n, T,
-      [&](int i) {
-        const float4 p = pts[i];
-        return fine_bucket(cell_of(p.x), cell_of(p.y), cell_of(p.z), T);
-      },
-      cnt, S.gEnd, S.gOrd, wtot);
-  if (!irregular)
-    bucket_build<Idx>(
-        n, NK * NB,
-        [&](int i) {
-          const float4 p = pts[i];
-          return (int)p.w * NB + az_bin(az_of(p.x, p.z), NB);
-        },
-        cnt, S.aEnd, S.aOrd, wtot);
+  block_exscan(cnt, T, wtot);
+  for (int i = tid; i < n; i += kOdomThreads) {
+    const float4 p = pts[i];
+    S.gOrd[atomicAdd(&cnt[fine_bucket(cell_of(p.x), cell_of(p.y), cell_of(p.z), T)], 1u)] = (Idx)i;
+  }
+  __syncthreads();
+  for (int b = tid; b < T; b += kOdomThreads) S.gEnd[b] = (Idx)cnt[b];
+  __syncthreads();
 }
 
 template <class Idx>
@@ -394,110 +351,44 @@ __device__ __forceinline__ void group_lex_min3(float& d, int& r, int& j) {
   }
 }
 
-// Walks list k's azimuth buckets outward from the query's bin in one
-// direction (dir 0: bq .. bq + NB/2, dir 1: bq - 1 .. bq - NB/2 + 1, together
-// every bin once), visiting the offsets m = m0 + off, m0 + off + stride, ...
-// (several lanes share one walk), and stops once the angular lower bound on
-// the distance, rq * sin(min(dphi, pi/2)) with rq the query's distance from
-// the y axis, exceeds sqrt(bound()).  Margins absorb the float azimuths.
-template <class Idx, class Visit, class Bound>
-__device__ __forceinline__ void az_walk(const NNView<Idx>& v, int k, float aq, float rq, int dir, int stride, int off,
-                                        const Visit& visit, const Bound& bound) {
-  const int NB = v.NB;
-  const float w = kTwoPi / (float)NB;
-  const int bq = az_bin(aq, NB);
-  const int m0 = dir ? 1 : 0, m1 = dir ? NB / 2 - 1 : NB / 2;
-  for (int m = m0 + off; m <= m1; m += stride) {
-    int b;
-    float lbphi;
-    if (dir == 0) {
-      b = bq + m;
-      lbphi = m == 0 ? 0.f : (float)b * w - aq;
-      if (b >= NB) b -= NB;
-    } else {
-      b = bq - m;
-      lbphi = aq - (float)(b + 1) * w;
-      if (b < 0) b += NB;
-    }
-    const float a = lbphi - 1e-4f;
-    if (a > 0.f) {
-      const float lb = rq * (a >= 1.5707963f ? 1.f : __sinf(a) - 1e-5f) - 1e-4f;
-      if (lb > 0.f && lb * lb > bound()) break;
-    }
-    int lo, hi;
-    bucket_range(v.aEnd, k * NB + b, lo, hi);
-    for (int t = lo; t < hi; ++t) visit((int)v.aOrd[t]);
-  }
-}
-
-// Exact nearest neighbour with d2 < bound, by the calling kGL-lane group: the
-// fine grid's 27-cell and 98-cell shells, each accepted only when the best
-// distance is provably below the radius the shell covers, then every key's
-// azimuth list pruned by the best so far (or every point when the lists are
-// not built).
+// Exact nearest neighbour with d2 < bound, by the calling wave: the fine
+// grid's 27 cells (accepted when the best distance is provably below the one
+// cell they cover), else every point (contiguous, independent loads).
 template <class Idx>
 __device__ __forceinline__ int nn_i1(const NNView<Idx>& v, float4 q, float bound, int g, unsigned long long* prof) {
   if (v.n <= 0) return -1;
   float bd = bound;
   int bi = INT_MAX;
   const int cx = cell_of(q.x), cy = cell_of(q.y), cz = cell_of(q.z);
-  auto scan = [&](int ix, int iy, int iz) {
+  if (g < 27) {
     int lo, hi;
-    bucket_range(v.gEnd, fine_bucket(ix, iy, iz, v.T), lo, hi);
+    bucket_range(v.gEnd, fine_bucket(cx + g % 3 - 1, cy + (g / 3) % 3 - 1, cz + g / 9 - 1, v.T), lo, hi);
     for (int t = lo; t < hi; ++t) {
       const int j = (int)v.gOrd[t];
       lex_min(bd, bi, flann_d2(q, v.pts[j]), j);
     }
-  };
-  for (int c = g; c < 27; c += kGL) scan(cx + c % 3 - 1, cy + (c / 3) % 3 - 1, cz + c / 9 - 1);
+  }
   group_lex_min(bd, bi);
   if (bd < kCell * kCell * 0.99999f) {
     if (prof && g == 0) atomicAdd(&prof[P_NN_SHELL1], 1ull);
-    return (bi != INT_MAX && bd < bound) ? bi : -1;
-  }
-  for (int c = g; c < 125; c += kGL) {
-    const int dx = c % 5 - 2, dy = (c / 5) % 5 - 2, dz = c / 25 - 2;
-    if (abs(dx) == 2 || abs(dy) == 2 || abs(dz) == 2) scan(cx + dx, cy + dy, cz + dz);
-  }
-  group_lex_min(bd, bi);
-  if (bd < 4 * kCell * kCell * 0.99999f) return (bi != INT_MAX && bd < bound) ? bi : -1;
-  if (prof && g == 0) atomicAdd(&prof[P_NN_BRUTE], 1ull);
-  if (v.irregular) {
-    for (int j = g; j < v.n; j += kGL) lex_min(bd, bi, flann_d2(q, v.pts[j]), j);
   } else {
-    const float aq = az_of(q.x, q.z), rq = __builtin_sqrtf(q.x * q.x + q.z * q.z);
-    const int ntask = 2 * v.NK, lpt = ntask >= kGL ? 1 : kGL / ntask;
-    for (int task = g / lpt; task < ntask; task += kGL / lpt)
-      az_walk(
-          v, task >> 1, aq, rq, task & 1, lpt, g % lpt, [&](int j) { lex_min(bd, bi, flann_d2(q, v.pts[j]), j); },
-          [&] { return bd; });
+    if (prof && g == 0) atomicAdd(&prof[P_NN_BRUTE], 1ull);
+    for (int j = g; j < v.n; j += kGL) lex_min(bd, bi, flann_d2(q, v.pts[j]), j);
+    group_lex_min(bd, bi);
   }
-  group_lex_min(bd, bi);
-  return (bi != INT_MAX && bd < bound) ? bi : -1;
-}
-
-// Exact nearest neighbour by brute force (stale snapshot, rare).
-__device__ __forceinline__ int nn_brute(const float4* pts, int n, float4 q, float bound, int g) {
-  float bd = bound;
-  int bi = INT_MAX;
-  for (int j = g; j < n; j += kGL) lex_min(bd, bi, flann_d2(q, pts[j]), j);
-  group_lex_min(bd, bi);
   return (bi != INT_MAX && bd < bound) ? bi : -1;
 }
 
 // Scan-line neighbours of closest point ci (corner :1062-1099, surf
-// :1173-1220), by the calling kGL-lane group.  The forward loop visits
+// :1173-1220), by the calling wave.  The forward loop visits
 // (ci, min(F, jend)) where F is the first index after ci whose key exceeds
-// cScan + 2 (int(I) > cScan + 2.5); the backward loop visits (B, ci) where B
-// is the last index before ci whose key is below cScan - 2.  F and B come from
-// the per-key tables when the keys are ordered enough for that to be exact
-// (otherwise false: the caller runs the loops literally).  Every point of that
-// window is a candidate, classed by its key and side exactly as the loops do;
-// the loops' strict < keeps the first visited among equal distances, i.e. the
-// smallest visit rank.  Only the lists of keys cScan-2 .. cScan+2 can hold
-// candidates: a list partly inside the window is scanned over its index span,
-// a list wholly inside is searched through its azimuth buckets, pruned by the
-// best found so far.
+// cScan + 2 (int(I) > cScan + 2.5); the backward loop visits (B, ci) where B is
+// the last index before ci whose key is below cScan - 2.  With the key tables
+// F and B are known up front (when the keys are ordered enough for that to be
+// exact; otherwise false: the caller runs the loops literally), so the window
+// is scanned with independent contiguous loads.  Every point in it is classed
+// by its key and side exactly as the loops do; their strict < keeps the first
+// visited among equal distances, i.e. the smallest visit rank.
 template <class Idx>
 __device__ __forceinline__ bool nn_lines(const NNView<Idx>& v, int ci, int jend, float4 sel, bool surf, float nn_sq,
                                          int g, int* o2, int* o3) {
@@ -507,16 +398,15 @@ __device__ __forceinline__ bool nn_lines(const NNView<Idx>& v, int ci, int jend,
   const int B = (cScan - 3 >= 0) ? v.preLast[cScan - 3] : -1;
   if (F <= ci || B >= ci) return false;
   const int fwdEnd = min(F, jend);
-  const int hi = fwdEnd > ci ? fwdEnd : ci;  // window = (B, hi) \ {ci}
   float m2 = nn_sq, m3 = nn_sq;
   int r2 = INT_MAX, r3 = INT_MAX, i2 = -1, i3 = -1;
-  auto visit = [&](int j, int kj) {
-    if (j == ci || j <= B || j >= hi) return;
-    const bool fwd = j > ci;
+  auto visit = [&](int j, bool fwd) {
+    const float4 p = v.pts[j];
+    const int kj = (int)p.w;
     bool cls2 = true;
     if (surf) cls2 = fwd ? (kj <= cScan) : (kj >= cScan);
     else if (fwd ? kj <= cScan : kj >= cScan) return;
-    const float d = line_d2(v.pts[j], sel);
+    const float d = line_d2(p, sel);
     if (!(d < nn_sq)) return;
     const int rank = fwd ? j - ci : (jend - ci) + (ci - j);
     // selects, not a branch between the two minima (keeps them in registers)
@@ -525,39 +415,22 @@ __device__ __forceinline__ bool nn_lines(const NNView<Idx>& v, int ci, int jend,
     m2 = u2 ? d : m2; r2 = u2 ? rank : r2; i2 = u2 ? j : i2;
     m3 = u3 ? d : m3; r3 = u3 ? rank : r3; i3 = u3 ? j : i3;
   };
-  int azK[4];
-  int nAz = 0;
-  for (int dk = -2; dk <= 2; ++dk) {
-    const int k = cScan + dk;
-    if (k < 0 || k >= v.NK) continue;
-    if (!surf && dk == 0) continue;  // a corner candidate's key differs from cScan
-    const int kf = v.kFirst[k], kl = v.kLast[k];
-    if (kl <= B || kf >= hi) continue;  // no member inside the window
-    if (dk != 0 && kf > B && kl < hi) { azK[nAz++] = k; continue; }
-    const int lo = max(kf, B + 1), up = min(kl, hi - 1);  // partly inside
-    for (int j = lo + g; j <= up; j += kGL) visit(j, (int)v.pts[j].w);
-  }
-  if (nAz) {
-    // share the scans' minima so the walks prune against them
-    group_lex_min3(m2, r2, i2);
-    if (surf) group_lex_min3(m3, r3, i3);
-    const float aq = az_of(sel.x, sel.z), rq = __builtin_sqrtf(sel.x * sel.x + sel.z * sel.z);
-    const int ntask = 2 * nAz, lpt = kGL / 8;  // <= 8 walks, kGL / 8 lanes each
-    const int task = g / lpt;
-    if (task < ntask) {
-      const int k = azK[task >> 1];
-      const bool fwdP = v.kLast[k] > ci, bwdP = v.kFirst[k] < ci;
-      const bool c2 = surf ? ((fwdP && k <= cScan) || (bwdP && k >= cScan)) : true;
-      const bool c3 = surf && ((fwdP && k > cScan) || (bwdP && k < cScan));
-      az_walk(v, k, aq, rq, task & 1, lpt, g % lpt, [&](int j) { visit(j, k); },
-              [&] { return (c2 && c3) ? fmaxf(m2, m3) : (c2 ? m2 : m3); });
-    }
-  }
+  for (int j = ci + 1 + g; j < fwdEnd; j += kGL) visit(j, true);
+  for (int j = B + 1 + g; j < ci; j += kGL) visit(j, false);
   group_lex_min3(m2, r2, i2);
   if (surf) group_lex_min3(m3, r3, i3);
   *o2 = i2;
   *o3 = surf ? i3 : -1;
   return true;
+}
+
+// Exact nearest neighbour by brute force (stale snapshot, rare).
+__device__ __forceinline__ int nn_brute(const float4* pts, int n, float4 q, float bound, int g) {
+  float bd = bound;
+  int bi = INT_MAX;
+  for (int j = g; j < n; j += kGL) lex_min(bd, bi, flann_d2(q, pts[j]), j);
+  group_lex_min(bd, bi);
+  return (bi != INT_MAX && bd < bound) ? bi : -1;
 }
 
 // The reference's sequential loops, kGL indices per step (fallback).  Every
@@ -626,11 +499,10 @@ struct OdomLds {
   float4* lastS;     // [kLdsSurf]
   float4* lastC;     // [kLdsCorner]
   int* qi;           // [3 * kLdsQ] correspondence indices
-  unsigned* cnt;     // [max(kLdsGridS, kLdsAz)] index-build counters
+  unsigned* cnt;     // [kLdsGridS] index-build counters
   uint16_t *gEndS, *gOrdS, *gEndC, *gOrdC;  // fine grids
-  uint16_t *aEndS, *aOrdS, *aEndC, *aOrdC;  // ring x azimuth lists
   int *sufS, *preS, *sufC, *preC;           // [kKeyTab] per-key first / last
-  int *kfS, *klS, *kfC, *klC;              // [kMaxRings] per-key first / last index
+  int *kfirst, *klast;                      // [kMaxRings] build scratch
   double* red;       // [kOdomWaves * 10]
   SolveWs* sw;
   int* wtot;         // [kOdomWaves]
@@ -643,8 +515,7 @@ __host__ __device__ inline size_t odom_lds_bytes() {
   size_t s = 0;
   s += (size_t)kLdsSurf * 16 + (size_t)kLdsCorner * 16 + (size_t)kLdsCnt * 4 + (size_t)3 * kLdsQ * 4;
   s += (size_t)(kLdsGridS + kLdsSurf + kLdsGridC + kLdsCorner) * 2;
-  s += (size_t)(kLdsAz + kLdsSurf + kLdsAz + kLdsCorner) * 2;
-  s += (size_t)4 * kKeyTab * 4 + (size_t)4 * kMaxRings * 4;
+  s += (size_t)4 * kKeyTab * 4 + (size_t)2 * kMaxRings * 4;
   s += (size_t)kOdomWaves * 10 * 8 + 256 + (size_t)kOdomWaves * 4 + 16 * 4 + 128;
   return s;
 }
@@ -662,18 +533,12 @@ __device__ __forceinline__ OdomLds odom_carve(unsigned char* base) {
   L.gOrdS = (uint16_t*)(base + o); o += (size_t)kLdsSurf * 2;
   L.gEndC = (uint16_t*)(base + o); o += (size_t)kLdsGridC * 2;
   L.gOrdC = (uint16_t*)(base + o); o += (size_t)kLdsCorner * 2;
-  L.aEndS = (uint16_t*)(base + o); o += (size_t)kLdsAz * 2;
-  L.aOrdS = (uint16_t*)(base + o); o += (size_t)kLdsSurf * 2;
-  L.aEndC = (uint16_t*)(base + o); o += (size_t)kLdsAz * 2;
-  L.aOrdC = (uint16_t*)(base + o); o += (size_t)kLdsCorner * 2;
   L.sufS = (int*)(base + o); o += (size_t)kKeyTab * 4;
   L.preS = (int*)(base + o); o += (size_t)kKeyTab * 4;
   L.sufC = (int*)(base + o); o += (size_t)kKeyTab * 4;
   L.preC = (int*)(base + o); o += (size_t)kKeyTab * 4;
-  L.kfS = (int*)(base + o); o += (size_t)kMaxRings * 4;
-  L.klS = (int*)(base + o); o += (size_t)kMaxRings * 4;
-  L.kfC = (int*)(base + o); o += (size_t)kMaxRings * 4;
-  L.klC = (int*)(base + o); o += (size_t)kMaxRings * 4;
+  L.kfirst = (int*)(base + o); o += (size_t)kMaxRings * 4;
+  L.klast = (int*)(base + o); o += (size_t)kMaxRings * 4;
   L.wtot = (int*)(base + o); o += (size_t)kOdomWaves * 4;
   L.n = (int*)(base + o); o += 16 * 4;
   L.st = (OdomState*)(base + o); o += 128;
@@ -682,64 +547,94 @@ __device__ __forceinline__ OdomLds odom_carve(unsigned char* base) {
 
 // The VLP-16-class configuration whose whole working set fits LDS.
 __device__ __forceinline__ bool sensor_resident(const DevCfg& c) {
-  return c.N * kFlatPerRing <= kLdsQ && c.N * az_nb(c.N) <= kLdsAz;
+  return c.N * kFlatPerRing <= kLdsQ;
 }
 
 // Views of the current indexes (valid when the snapshot is current).
 __device__ __forceinline__ NNView<uint16_t> view_lds(bool surf, const OdomLds& L, const OdomState* st, const DevCfg& c) {
   if (surf)
     return NNView<uint16_t>{L.lastS, st->surfLastNum, L.gEndS, L.gOrdS, fine_T(st->surfLastNum, kLdsGridS),
-                            L.aEndS, L.aOrdS, az_nb(c.N), c.N, L.sufS, L.preS, L.kfS, L.klS, L.n[N_IRR_S]};
+                            c.N, L.sufS, L.preS, L.n[N_IRR_S]};
   return NNView<uint16_t>{L.lastC, st->cornerLastNum, L.gEndC, L.gOrdC, fine_T(st->cornerLastNum, kLdsGridC),
-                          L.aEndC, L.aOrdC, az_nb(c.N), c.N, L.sufC, L.preC, L.kfC, L.klC, L.n[N_IRR_C]};
+                          c.N, L.sufC, L.preC, L.n[N_IRR_C]};
 }
 __device__ __forceinline__ NNView<uint32_t> view_hbm(bool surf, const OdomLds& L, const OdomBufs& ob,
                                                      const OdomState* st, const DevCfg& c) {
   if (surf)
     return NNView<uint32_t>{buf2(ob.surfLast, st->curBuf), st->surfLastNum, ob.nS.gEnd, ob.nS.gOrd,
-                            fine_T(st->surfLastNum, ob.gTS), ob.nS.aEnd, ob.nS.aOrd, az_nb(c.N), c.N, L.sufS,
-                            L.preS, L.kfS, L.klS, L.n[N_IRR_S]};
+                            fine_T(st->surfLastNum, ob.gTS), c.N, L.sufS, L.preS, L.n[N_IRR_S]};
   return NNView<uint32_t>{buf2(ob.cornerLast, st->curBuf), st->cornerLastNum, ob.nC.gEnd, ob.nC.gOrd,
-                          fine_T(st->cornerLastNum, ob.gTC), ob.nC.aEnd, ob.nC.aOrd, az_nb(c.N), c.N, L.sufC,
-                          L.preC, L.kfC, L.klC, L.n[N_IRR_C]};
+                          fine_T(st->cornerLastNum, ob.gTC), c.N, L.sufC, L.preC, L.n[N_IRR_C]};
 }
 
 // Rebuilds both clouds' indexes (all threads) over the current last clouds.
 __device__ __forceinline__ void build_indexes(const OdomLds& L, const OdomBufs& ob, const OdomState* st,
                                               const DevCfg& c) {
   if (st->resident) {
-    NNStore<uint16_t> sS{L.gEndS, L.gOrdS, L.aEndS, L.aOrdS, L.sufS, L.preS, L.kfS, L.klS, &L.n[N_IRR_S], kLdsGridS};
-    nn_build<uint16_t>(L.lastS, st->surfLastNum, c.N, sS, L.cnt, L.wtot);
-    NNStore<uint16_t> sC{L.gEndC, L.gOrdC, L.aEndC, L.aOrdC, L.sufC, L.preC, L.kfC, L.klC, &L.n[N_IRR_C], kLdsGridC};
-    nn_build<uint16_t>(L.lastC, st->cornerLastNum, c.N, sC, L.cnt, L.wtot);
+    NNStore<uint16_t> sS{L.gEndS, L.gOrdS, L.sufS, L.preS, &L.n[N_IRR_S], kLdsGridS};
+    nn_build<uint16_t>(L.lastS, st->surfLastNum, c.N, sS, L.cnt, L.wtot, L.kfirst, L.klast);
+    NNStore<uint16_t> sC{L.gEndC, L.gOrdC, L.sufC, L.preC, &L.n[N_IRR_C], kLdsGridC};
+    nn_build<uint16_t>(L.lastC, st->cornerLastNum, c.N, sC, L.cnt, L.wtot, L.kfirst, L.klast);
   } else {
-    NNStore<uint32_t> sS{ob.nS.gEnd, ob.nS.gOrd, ob.nS.aEnd, ob.nS.aOrd, L.sufS, L.preS, L.kfS, L.klS, &L.n[N_IRR_S], ob.gTS};
-    nn_build<uint32_t>(buf2(ob.surfLast, st->curBuf), st->surfLastNum, c.N, sS, ob.cnt, L.wtot);
-    NNStore<uint32_t> sC{ob.nC.gEnd, ob.nC.gOrd, ob.nC.aEnd, ob.nC.aOrd, L.sufC, L.preC, L.kfC, L.klC, &L.n[N_IRR_C], ob.gTC};
-    nn_build<uint32_t>(buf2(ob.cornerLast, st->curBuf), st->cornerLastNum, c.N, sC, ob.cnt, L.wtot);
+    NNStore<uint32_t> sS{ob.nS.gEnd, ob.nS.gOrd, L.sufS, L.preS, &L.n[N_IRR_S], ob.gTS};
+    nn_build<uint32_t>(buf2(ob.surfLast, st->curBuf), st->surfLastNum, c.N, sS, ob.cnt, L.wtot, L.kfirst, L.klast);
+    NNStore<uint32_t> sC{ob.nC.gEnd, ob.nC.gOrd, L.sufC, L.preC, &L.n[N_IRR_C], ob.gTC};
+    nn_build<uint32_t>(buf2(ob.cornerLast, st->curBuf), st->cornerLastNum, c.N, sC, ob.cnt, L.wtot, L.kfirst,
+                       L.klast);
   }
 }
 
 // ---------------------------------------------------------------- reduction
-// 9 doubles (AtA upper triangle 6 + AtB 3) + the row count; thread 0 gets the
-// block totals (waves summed in order).
-__device__ __forceinline__ void block_sum9(double v[9], int m, const OdomLds& L, double out[9], int* mt) {
+// Wave sum of a double through DPP lane moves (VALU, no LDS traffic): quad
+// swaps, half-row and row mirrors give every lane its 16-lane row sum, then
+// the four row sums are read out in a fixed order.  Deterministic.
+template <int kCtrl>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, kCtrl, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), kCtrl, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double rdlane_f64(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double wave_sum_f64(double v) {
+  v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141>(v);  // row_half_mirror
+  v += dpp_f64<0x140>(v);  // row_mirror
+  return (rdlane_f64(v, 0) + rdlane_f64(v, 16)) + (rdlane_f64(v, 32) + rdlane_f64(v, 48));
+}
+
+// 9 doubles (AtA upper triangle 6 + AtB 3) + the row count over the block;
+// thread 0 gets the totals (waves summed in order).  Waves without queries
+// contribute zeros and skip the lane reduction.
+__device__ __forceinline__ void block_sum9(double v[9], int m, int nQ, const OdomLds& L, double out[9], int* mt) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int k = 0; k < 9; ++k)
-    for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
-  for (int o = 32; o > 0; o >>= 1) m += __shfl_xor(m, o, 64);
+  double r[10];
+  if (wave * 64 < nQ) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) r[k] = wave_sum_f64(v[k]);
+    r[9] = wave_sum_f64((double)m);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 10; ++k) r[k] = 0.0;
+  }
   if (lane == 0) {
-    for (int k = 0; k < 9; ++k) L.red[wave * 10 + k] = v[k];
-    L.red[wave * 10 + 9] = (double)m;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) L.red[wave * 10 + k] = r[k];
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int k = 0; k < 10; ++k) {
-      double s = 0;
-      for (int w = 0; w < kOdomWaves; ++w) s += L.red[w * 10 + k];
-      if (k < 9) out[k] = s;
-      else *mt = (int)s;
-    }
+  // lanes 0..9 of wave 0 each sum one quantity over the waves; thread 0 reads them out
+  if (wave == 0) {
+    double sum = 0;
+    if (lane < 10)
+      for (int w = 0; w < kOdomWaves; ++w) sum += L.red[w * 10 + lane];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) out[k] = rdlane_f64(sum, k);
+    *mt = (int)rdlane_f64(sum, 9);
   }
 }
 
@@ -750,10 +645,10 @@ struct ScanFeat {
   const float4* lflat; int nLF;
 };
 
-// Shared tail of calculateTransformationSurf / Corner.  Thread 0 only; the
-// eigen workspace lives in LDS.
+// Shared tail of calculateTransformationSurf / Corner.  Thread 0 only, all in
+// registers (cv_eigen_sym3 is the index-resolved 3x3 Jacobi).
 __device__ __forceinline__ void solve_step(float (&AtA)[3][3], float (&AtB)[3], int iter, OdomState* st,
-                                           SolveWs* ws, float (&X)[3]) {
+                                           float (&X)[3]) {
   float Aq[3][3];
 #pragma unroll
   for (int a = 0; a < 3; ++a)
@@ -762,20 +657,27 @@ __device__ __forceinline__ void solve_step(float (&AtA)[3][3], float (&AtB)[3], 
   cv_solve_qr<3, 3>(Aq, AtB, X);
   float (&P)[3][3] = *reinterpret_cast<float(*)[3][3]>(st->matP);
   if (iter == 0) {
-    for (int a = 0; a < 3; ++a) for (int b = 0; b < 3; ++b) ws->A[a][b] = AtA[a][b];
-    cv_eigen_sym_ws<3>(ws->A, ws->W, ws->V, ws->indR, ws->indC);
-    for (int a = 0; a < 3; ++a) for (int b = 0; b < 3; ++b) ws->V2[a][b] = ws->V[a][b];
-    st->isDegenerate = 0;
+    float E[3], V[3][3], V2[3][3], Vi[3][3];
+    cv_eigen_sym3(AtA, E, V);
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+      for (int b = 0; b < 3; ++b) V2[a][b] = V[a][b];
+    int deg = 0;
+    bool stop = false;
+#pragma unroll
     for (int i = 2; i >= 0; i--) {
-      if (ws->W[i] < 10) {
-        for (int j = 0; j < 3; j++) ws->V2[i][j] = 0;
-        st->isDegenerate = 1;
+      if (!stop && E[i] < 10) {
+#pragma unroll
+        for (int j = 0; j < 3; j++) V2[i][j] = 0;
+        deg = 1;
       } else {
-        break;
+        stop = true;
       }
     }
-    cv_inv3(ws->V, ws->Vi);
-    cv_matmul<3>(ws->Vi, ws->V2, P);
+    st->isDegenerate = deg;
+    cv_inv3(V, Vi);
+    cv_matmul<3>(Vi, V2, P);
   }
   if (st->isDegenerate) {
     float X2[3] = {X[0], X[1], X[2]};
@@ -976,7 +878,8 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
     }
     double tot[9];
     int M = 0;
-    block_sum9(acc, mloc, L, tot, &M);
+    S.add(P_T_ROWS);
+    block_sum9(acc, mloc, nQ, L, tot, &M);
     S.add(surf ? (nnIter ? P_SURF_NN : P_SURF) : (nnIter ? P_CORN_NN : P_CORN));
     if (tid == 0) {
       L.n[N_BREAK] = 0;
@@ -986,7 +889,8 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
                            {(float)tot[2], (float)tot[4], (float)tot[5]}};
         float AtB[3] = {(float)tot[6], (float)tot[7], (float)tot[8]};
         float X[3];
-        solve_step(AtA, AtB, it, st, L.sw, X);
+        solve_step(AtA, AtB, it, st, X);
+        S.add(it == 0 ? P_T_SOLVE0 : P_T_SOLVE);
         float* t = st->transformCur;
         double dR, dT;
         if (surf) {
@@ -1024,9 +928,7 @@ __device__ __forceinline__ OdomBufs odom_private(OdomBufs ob) {
   ob.surfLast[0] += w * ob.capSurf;
   ob.surfLast[1] += w * ob.capSurf;
   ob.nC.gEnd += w * ob.gTC; ob.nC.gOrd += w * ob.capCorner;
-  ob.nC.aEnd += w * ob.azB; ob.nC.aOrd += w * ob.capCorner;
   ob.nS.gEnd += w * ob.gTS; ob.nS.gOrd += w * ob.capSurf;
-  ob.nS.aEnd += w * ob.azB; ob.nS.aOrd += w * ob.capSurf;
   ob.cnt += w * ob.cntCap;
   ob.qi += w * 3 * ob.capQ;
   return ob;
@@ -1164,20 +1066,19 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
   if (lead && tid < (int)(sizeof(OdomState) / 4)) ((int*)ob.st)[tid] = ((const int*)st)[tid];
 }
 
-void odom_index_caps(int capCorner, int capSurf, int N, int* gTC, int* gTS, int* azBuckets) {
+void odom_index_caps(int capCorner, int capSurf, int* gTC, int* gTS) {
   int t = 64;
   while (t < capCorner / 2) t <<= 1;
   *gTC = t;
   t = 64;
   while (t < capSurf / 2) t <<= 1;
   *gTS = t;
-  *azBuckets = N * az_nb(N);
 }
 
 // Workgroups of the odometry launch: LDS-resident sensors split each NN round
 // over one wave per query of the largest round (flat <= 24 N queries).
 int odom_workgroups(int N, int cusAvailable) {
-  if (N * kFlatPerRing > kLdsQ || N * az_nb(N) > kLdsAz) return 1;
+  if (N * kFlatPerRing > kLdsQ) return 1;
   const int g = (N * kFlatPerRing + kOdomWaves - 1) / kOdomWaves;
   return g < cusAvailable ? g : cusAvailable;
 }

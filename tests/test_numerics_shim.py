@@ -33,6 +33,15 @@ def test_introsort_port_matches_std_sort(tmp_path):
     assert r.returncode == 0, r.stdout
 
 
+def test_eigen3_register_form_matches_generic(tmp_path):
+    """The device solver's register-resident 3x3 Jacobi (cv_eigen_sym3) must
+    equal the OpenCV JacobiImpl_ restatement (cv_eigen_sym<3>) bit for bit."""
+    exe = _build(tmp_path, "eigen3_check", REPO / "tests/native/eigen3_check.cpp")
+    r = subprocess.run([str(exe), "300000"], capture_output=True, text=True, timeout=600)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout
+
+
 def test_segmentation_alpha_constants(L):
     """sin/cos of segmentAlphaX/Y (imageProjection.cpp:421) — bit patterns
     recorded in SURVEY.md §9.3 for VLP-16."""
