@@ -203,7 +203,8 @@ def main():
                   f"  per scan: nn shell-1 {prof[14] / nsc:.1f}, nn exhaustive {prof[15] / nsc:.1f},"
                   f" scan-line indexed {prof[20] / nsc:.1f}, scan-line literal {prof[13] / nsc:.1f}",
                   file=sys.stderr)
-            for i, nm in ((21, "rows (excl. reduce)"), (22, "solve_qr+eig it0"), (23, "solve_qr it>0")):
+            for i, nm in ((21, "rows (excl. reduce)"), (22, "solve_qr+eig it0"), (23, "solve_qr it>0"),
+                          (24, "nn local work"), (25, "build surf"), (26, "build corner")):
                 print(f"  odom.{nm:20s} {prof[i] / 100.0 / nsc:9.2f} us/scan", file=sys.stderr)
         if args.stages:
             tot = sum(stage_acc.values())

@@ -76,7 +76,15 @@ struct ImuEnd {
   float cRS, cPS, cYS, sRS, sPS, sYS;  // cosImu*Start / sinImu*Start
   float cYL, sYL, cPL, sPL, cRL, sRL;  // imu*Last
 };
-__device__ __forceinline__ float4 to_end(float4 pi, const float* tc, const ImuEnd& im) {
+// The second half of TransformToEnd rotates by the full transformCur: its
+// sines and cosines are the same for every point, computed once per scan.
+struct EndTrig {
+  float cx, sx, cy, sy, cz, sz;
+};
+__device__ __forceinline__ EndTrig end_trig(const float* tc) {
+  return {lego_cosf(tc[0]), lego_sinf(tc[0]), lego_cosf(tc[1]), lego_sinf(tc[1]), lego_cosf(tc[2]), lego_sinf(tc[2])};
+}
+__device__ __forceinline__ float4 to_end(float4 pi, const float* tc, const EndTrig& et, const ImuEnd& im) {
   const float s = 10 * (pi.w - (float)(int)pi.w);
   float rx = s * tc[0], ry = s * tc[1], rz = s * tc[2];
   float tx = s * tc[3], ty = s * tc[4], tz = s * tc[5];
@@ -91,9 +99,8 @@ __device__ __forceinline__ float4 to_end(float4 pi, const float* tc, const ImuEn
   const float x3 = cy * x2 - sy * z2;
   const float y3 = y2;
   const float z3 = sy * x2 + cy * z2;
-  rx = tc[0]; ry = tc[1]; rz = tc[2]; tx = tc[3]; ty = tc[4]; tz = tc[5];
-  cz = lego_cosf(rz); sz = lego_sinf(rz); cx = lego_cosf(rx); sx = lego_sinf(rx);
-  cy = lego_cosf(ry); sy = lego_sinf(ry);
+  tx = tc[3]; ty = tc[4]; tz = tc[5];
+  cz = et.cz; sz = et.sz; cx = et.cx; sx = et.sx; cy = et.cy; sy = et.sy;
   const float x4 = cy * x3 + sy * z3;
   const float y4 = y3;
   const float z4 = -sy * x3 + cy * z3;
@@ -199,7 +206,8 @@ enum { P_SURF_NN = 0, P_SURF = 1, P_CORN_NN = 2, P_CORN = 3, P_SOLVE = 4, P_INTE
        P_TOEND = 6, P_BUILD = 7, P_RESID = 8, P_ITERS_S = 9, P_ITERS_C = 10, P_NNR = 11,
        P_QUERY = 12, P_SCANLINE = 13, P_NN_SHELL1 = 14, P_NN_BRUTE = 15,
        P_G0_TOSTART = 16, P_G0_NN = 17, P_G0_SCAN = 18, P_G0_Q = 19, P_AZLINE = 20,
-       P_T_ROWS = 21, P_T_SOLVE0 = 22, P_T_SOLVE = 23, P_NPROF = 32 };
+       P_T_ROWS = 21, P_T_SOLVE0 = 22, P_T_SOLVE = 23, P_X_LOCAL = 24, P_B_SURF = 25, P_B_CORN = 26,
+       P_NPROF = 32 };
 struct Stamp {
   unsigned long long* prof;
   unsigned long long t;
@@ -287,13 +295,28 @@ __device__ __forceinline__ void nn_build(const float4* pts, int n, int NK, const
   for (int k = tid; k < NK; k += kOdomThreads) { kfirst[k] = INT_MAX; klast[k] = -1; }
   if (tid == 0) *S.irregular = 0;
   __syncthreads();
-  for (int i = tid; i < n; i += kOdomThreads) {
-    const float4 p = pts[i];
-    atomicAdd(&cnt[fine_bucket(cell_of(p.x), cell_of(p.y), cell_of(p.z), T)], 1u);
-    const int k = (int)p.w;
-    if (k < 0 || k >= NK) { *S.irregular = 1; continue; }
-    atomicMin(&kfirst[k], i);
-    atomicMax(&klast[k], i);
+  const int lane = tid & 63;
+  for (int i0 = tid - lane; i0 < n; i0 += kOdomThreads) {  // wave-uniform loop
+    const int i = i0 + lane;
+    int k = -1;
+    if (i < n) {
+      const float4 p = pts[i];
+      atomicAdd(&cnt[fine_bucket(cell_of(p.x), cell_of(p.y), cell_of(p.z), T)], 1u);
+      k = (int)p.w;
+      if (k < 0 || k >= NK) { *S.irregular = 1; k = -1; }
+    }
+    // per-key first/last: one atomic per distinct key of the wave (keys come in runs)
+    unsigned long long todo = __ballot(k >= 0);
+    while (todo) {
+      const int leader = __ffsll((long long)todo) - 1;
+      const int kk = __builtin_amdgcn_readlane(k, leader);
+      const unsigned long long m = __ballot(k == kk);
+      if (lane == leader) {
+        atomicMin(&kfirst[kk], i0 + leader);
+        atomicMax(&klast[kk], i0 + 63 - __clzll((long long)m));
+      }
+      todo &= ~m;
+    }
   }
   __syncthreads();
   if (tid == 0) {
@@ -334,21 +357,60 @@ __device__ __forceinline__ float line_d2(float4 a, float4 s) {  // the scan-line
 __device__ __forceinline__ void lex_min(float& d, int& i, float d2, int i2) {
   if (d2 < d || (d2 == d && i2 < i)) { d = d2; i = i2; }
 }
+// Wave-wide lexicographic minima through DPP lane moves (VALU, no LDS):
+// quad swaps, half-row and row mirrors leave every lane its 16-lane row
+// minimum; the four row minima are then combined from readlanes.  The
+// order is a total one (ties broken by the second key), so the result does not
+// depend on the pairing.
+template <int kCtrl>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), kCtrl, 0xf, 0xf, false));
+}
+template <int kCtrl>
+__device__ __forceinline__ int dpp_i32(int v) {
+  return __builtin_amdgcn_mov_dpp(v, kCtrl, 0xf, 0xf, false);
+}
+template <int kCtrl>
+__device__ __forceinline__ void lex_step(float& d, int& i) {
+  lex_min(d, i, dpp_f32<kCtrl>(d), dpp_i32<kCtrl>(i));
+}
 __device__ __forceinline__ void group_lex_min(float& d, int& i) {
-  for (int o = kGL / 2; o > 0; o >>= 1) {
-    const float d2 = __shfl_xor(d, o, 64);
-    const int i2 = __shfl_xor(i, o, 64);
-    lex_min(d, i, d2, i2);
-  }
+  static_assert(kGL == 64, "DPP reductions span one wave");
+  lex_step<0xB1>(d, i);
+  lex_step<0x4E>(d, i);
+  lex_step<0x141>(d, i);
+  lex_step<0x140>(d, i);
+  float bd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), 0));
+  int bi = __builtin_amdgcn_readlane(i, 0);
+#pragma unroll
+  for (int r = 16; r < 64; r += 16)
+    lex_min(bd, bi, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), r)), __builtin_amdgcn_readlane(i, r));
+  d = bd;
+  i = bi;
 }
 // (distance, visit rank) minimum carrying the index
+template <int kCtrl>
+__device__ __forceinline__ void lex3_step(float& d, int& r, int& j) {
+  const float d2 = dpp_f32<kCtrl>(d);
+  const int r2 = dpp_i32<kCtrl>(r), j2 = dpp_i32<kCtrl>(j);
+  if (d2 < d || (d2 == d && r2 < r)) { d = d2; r = r2; j = j2; }
+}
 __device__ __forceinline__ void group_lex_min3(float& d, int& r, int& j) {
-  for (int s = kGL / 2; s > 0; s >>= 1) {
-    const float d2 = __shfl_xor(d, s, 64);
-    const int r2 = __shfl_xor(r, s, 64);
-    const int j2 = __shfl_xor(j, s, 64);
-    if (d2 < d || (d2 == d && r2 < r)) { d = d2; r = r2; j = j2; }
+  lex3_step<0xB1>(d, r, j);
+  lex3_step<0x4E>(d, r, j);
+  lex3_step<0x141>(d, r, j);
+  lex3_step<0x140>(d, r, j);
+  float bd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), 0));
+  int br = __builtin_amdgcn_readlane(r, 0), bj = __builtin_amdgcn_readlane(j, 0);
+#pragma unroll
+  for (int q = 16; q < 64; q += 16) {
+    const float d2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), q));
+    const int r2 = __builtin_amdgcn_readlane(r, q), j2 = __builtin_amdgcn_readlane(j, q);
+    if (d2 < bd || (d2 == bd && r2 < br)) { bd = d2; br = r2; bj = j2; }
   }
+  d = bd;
+  r = br;
+  j = bj;
 }
 
 // Exact nearest neighbour with d2 < bound, by the calling wave: the fine
@@ -499,6 +561,8 @@ struct OdomLds {
   float4* lastS;     // [kLdsSurf]
   float4* lastC;     // [kLdsCorner]
   int* qi;           // [3 * kLdsQ] correspondence indices
+  float4* qflat;     // [kLdsQ]      this scan's flat features (LM queries)
+  float4* qsharp;    // [kLdsQ / 2]  this scan's sharp features
   unsigned* cnt;     // [kLdsGridS] index-build counters
   uint16_t *gEndS, *gOrdS, *gEndC, *gOrdC;  // fine grids
   int *sufS, *preS, *sufC, *preC;           // [kKeyTab] per-key first / last
@@ -514,6 +578,7 @@ enum { N_BREAK = 0, N_IRR_S = 1, N_IRR_C = 2, N_ROUND = 3 };
 __host__ __device__ inline size_t odom_lds_bytes() {
   size_t s = 0;
   s += (size_t)kLdsSurf * 16 + (size_t)kLdsCorner * 16 + (size_t)kLdsCnt * 4 + (size_t)3 * kLdsQ * 4;
+  s += (size_t)kLdsQ * 16 + (size_t)(kLdsQ / 2) * 16;
   s += (size_t)(kLdsGridS + kLdsSurf + kLdsGridC + kLdsCorner) * 2;
   s += (size_t)4 * kKeyTab * 4 + (size_t)2 * kMaxRings * 4;
   s += (size_t)kOdomWaves * 10 * 8 + 256 + (size_t)kOdomWaves * 4 + 16 * 4 + 128;
@@ -525,6 +590,8 @@ __device__ __forceinline__ OdomLds odom_carve(unsigned char* base) {
   size_t o = 0;
   L.lastS = (float4*)(base + o); o += (size_t)kLdsSurf * 16;
   L.lastC = (float4*)(base + o); o += (size_t)kLdsCorner * 16;
+  L.qflat = (float4*)(base + o); o += (size_t)kLdsQ * 16;
+  L.qsharp = (float4*)(base + o); o += (size_t)(kLdsQ / 2) * 16;
   L.cnt = (unsigned*)(base + o); o += (size_t)kLdsCnt * 4;
   L.qi = (int*)(base + o); o += (size_t)3 * kLdsQ * 4;
   L.red = (double*)(base + o); o += (size_t)kOdomWaves * 10 * 8;
@@ -547,7 +614,7 @@ __device__ __forceinline__ OdomLds odom_carve(unsigned char* base) {
 
 // The VLP-16-class configuration whose whole working set fits LDS.
 __device__ __forceinline__ bool sensor_resident(const DevCfg& c) {
-  return c.N * kFlatPerRing <= kLdsQ;
+  return c.N * kFlatPerRing <= kLdsQ && c.N * kSharpPerRing <= kLdsQ / 2;
 }
 
 // Views of the current indexes (valid when the snapshot is current).
@@ -569,12 +636,15 @@ __device__ __forceinline__ NNView<uint32_t> view_hbm(bool surf, const OdomLds& L
 
 // Rebuilds both clouds' indexes (all threads) over the current last clouds.
 __device__ __forceinline__ void build_indexes(const OdomLds& L, const OdomBufs& ob, const OdomState* st,
-                                              const DevCfg& c) {
+                                              const DevCfg& c, unsigned long long* prof = nullptr) {
   if (st->resident) {
+    unsigned long long t0 = (prof && threadIdx.x == 0) ? wall_clock64() : 0;
     NNStore<uint16_t> sS{L.gEndS, L.gOrdS, L.sufS, L.preS, &L.n[N_IRR_S], kLdsGridS};
     nn_build<uint16_t>(L.lastS, st->surfLastNum, c.N, sS, L.cnt, L.wtot, L.kfirst, L.klast);
+    if (prof && threadIdx.x == 0) { const unsigned long long t1 = wall_clock64(); prof[P_B_SURF] += t1 - t0; t0 = t1; }
     NNStore<uint16_t> sC{L.gEndC, L.gOrdC, L.sufC, L.preC, &L.n[N_IRR_C], kLdsGridC};
     nn_build<uint16_t>(L.lastC, st->cornerLastNum, c.N, sC, L.cnt, L.wtot, L.kfirst, L.klast);
+    if (prof && threadIdx.x == 0) prof[P_B_CORN] += wall_clock64() - t0;
   } else {
     NNStore<uint32_t> sS{ob.nS.gEnd, ob.nS.gOrd, L.sufS, L.preS, &L.n[N_IRR_S], ob.gTS};
     nn_build<uint32_t>(buf2(ob.surfLast, st->curBuf), st->surfLastNum, c.N, sS, ob.cnt, L.wtot, L.kfirst, L.klast);
@@ -740,7 +810,9 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
   const bool stale = st->curBuf != st->snapBuf;
   const float4* snap = surf ? buf2(ob.surfLast, st->snapBuf) : buf2(ob.cornerLast, st->snapBuf);
   const int snapN = surf ? st->nnSurfNum : st->nnCornerNum;
-  const float4* qp = surf ? F.flat : F.sharp;
+  const float4* qp;
+  if constexpr (R) qp = surf ? L.qflat : L.qsharp;  // staged in LDS at the scan's start
+  else qp = surf ? F.flat : F.sharp;
   const int nQ = surf ? F.nFlat : F.nSharp;
   const int jend = min(nQ, lastN);  // the reference bounds by the query count (:1062, :1173)
   const int g = tid & (kGL - 1), grp = tid / kGL;
@@ -783,6 +855,7 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
           }
         }
       }
+      S.add(P_X_LOCAL);
       if (G > 1) {
         for (int e = tid; e < 3 * nQ; e += kOdomThreads) {
           const int q = e / 3, k = e - 3 * q;
@@ -914,9 +987,9 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
     }
     __syncthreads();
     S.add(P_SOLVE);
-    const int brk = L.n[N_BREAK];
-    __syncthreads();
-    if (brk) break;
+    // thread 0 rewrites the flag only after the next reduction's barrier, which
+    // every thread reaches after this read
+    if (L.n[N_BREAK]) break;
   }
 }
 
@@ -978,6 +1051,9 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
       // updateInitialGuess is a no-op without IMU
       if (st->cornerLastNum >= 10 && st->surfLastNum >= 100) {
         if (st->resident) {
+          for (int t = tid; t < F.nFlat; t += kOdomThreads) L.qflat[t] = F.flat[t];
+          for (int t = tid; t < F.nSharp; t += kOdomThreads) L.qsharp[t] = F.sharp[t];
+          __syncthreads();
           lm_loop<true>(true, F, L, ob, c, S);
           lm_loop<true>(false, F, L, ob, c, S);
         } else {
@@ -1019,14 +1095,15 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     const bool fits = sensorRes && F.nLS <= kLdsCorner && F.nLF <= kLdsSurf;
     float tcur[6];
     for (int i = 0; i < 6; ++i) tcur[i] = st->transformCur[i];
+    const EndTrig et = end_trig(tcur);
     for (int t = tid; t < F.nLS; t += kOdomThreads) {
-      const float4 p = init ? F.lsharp[t] : to_end(F.lsharp[t], tcur, im);
+      const float4 p = init ? F.lsharp[t] : to_end(F.lsharp[t], tcur, et, im);
       gCn[t] = p;
       if (lead) cEnd[t] = p;
       if (fits) L.lastC[t] = p;
     }
     for (int t = tid; t < F.nLF; t += kOdomThreads) {
-      const float4 p = init ? F.lflat[t] : to_end(F.lflat[t], tcur, im);
+      const float4 p = init ? F.lflat[t] : to_end(F.lflat[t], tcur, et, im);
       gSn[t] = p;
       if (lead) sEnd[t] = p;
       if (fits) L.lastS[t] = p;
@@ -1059,7 +1136,7 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     __syncthreads();
     unsigned long long tb = 0;
     if (prof && tid == 0) tb = wall_clock64();
-    if (rebuild) build_indexes(L, ob, st, c);
+    if (rebuild) build_indexes(L, ob, st, c, prof);
     if (prof && tid == 0) prof[P_BUILD] += wall_clock64() - tb;
   }
   __syncthreads();
