@@ -17,6 +17,7 @@
 
 #include "lego_device.h"
 #include "lego_kernels.h"
+#include "lego_mo.h"
 #include "lego_loam.h"
 
 using namespace lego;
@@ -88,6 +89,10 @@ struct lego_ctx {
   std::vector<int8_t> h_gimg;
   lego_ip_out lastIp{};
   bool lastIpDevice = false;  // lastIp describes batch slot 0 on device
+  // scan-to-map (lego_mo_*): buffers allocated by the first lego_mo_set_map
+  MoDev mo{};
+  bool moAlloc = false, moFixed = false;
+  double moTimeLast = -1;
   std::vector<std::string> tnames;
   std::vector<float> tms;
 
@@ -143,6 +148,11 @@ static int ctx_reset(lego_ctx* x) {
   HIPCHK(hipStreamSynchronize(x->stream));
   x->lastIpDevice = false;
   x->lastB = 0;
+  if (x->moAlloc) {
+    HIPCHK(hipMemsetAsync(x->mo.st, 0, sizeof(MoState), x->stream));
+    HIPCHK(hipStreamSynchronize(x->stream));
+  }
+  x->moTimeLast = -1;
   return LEGO_OK;
 }
 
@@ -628,19 +638,140 @@ int lego_batch_fetch(lego_ctx* x, int32_t k, lego_ip_out* ip, lego_fa_out* fa) {
   return LEGO_OK;
 }
 
+// Device buffers of the scan-to-map step for maps of up to nc / ns points.
+static int mo_alloc(lego_ctx* x, int nc, int ns) {
+  MoDev& m = x->mo;
+  const int N = x->dc.N, P = x->dc.P;
+  auto fail = [&](const char* what) {
+    set_err("hipMalloc failed for %s", what);
+    return LEGO_E_DEVICE;
+  };
+#define MA(ptr, n) \
+  if (x->alloc(&(ptr), (size_t)(n)) != hipSuccess) return fail(#ptr);
+  if (!x->moAlloc) {
+    MA(m.st, 1);
+    MA(m.cnt, 1);
+    m.scanCap = P;
+    MA(m.cornerLast, N * kLessSharpPerRing); MA(m.surfLast, P); MA(m.outlierLast, P);
+    MA(m.cornerDS, N * kLessSharpPerRing); MA(m.surfDS, P); MA(m.outlierDS, P);
+    MA(m.surfTotal, 2 * P); MA(m.surfTotalDS, 2 * P);
+    m.rowCap = N * kLessSharpPerRing + 2 * P;
+    MA(m.rows, (size_t)m.rowCap * 8);
+    HIPCHK(hipMemsetAsync(m.st, 0, sizeof(MoState), x->stream));
+    HIPCHK(hipMemsetAsync(m.cnt, 0, sizeof(MoCounts), x->stream));
+    x->moAlloc = true;
+  }
+  const int vcap = std::max(std::max(nc, ns), 2 * P);
+  if (vcap > m.vg.cap) {  // buffers are never freed before the context: grow by reallocating
+    VgScratch& v = m.vg;
+    v.cap = vcap;
+    MA(v.keys, vcap); MA(v.keys2, vcap); MA(v.vals, vcap); MA(v.vals2, vcap);
+    MA(v.heads, vcap); MA(v.scan, vcap); MA(v.mm, 8); MA(v.overflow, 4);
+    v.tmpBytes = voxel_scratch_tmp_bytes(vcap);
+    unsigned char* t = nullptr;
+    MA(t, v.tmpBytes);
+    v.tmp = t;
+  }
+  if (nc > m.mapCornerCap) {
+    m.mapCornerCap = nc;
+    MA(m.cornerMap, nc); MA(m.cornerMapDS, nc);
+    int T = 64;
+    while (T < nc) T <<= 1;
+    MA(m.cornerIx.begin, T); MA(m.cornerIx.end, T); MA(m.cornerIx.sorted, nc);
+    m.cornerIx.cap = nc;
+  }
+  if (ns > m.mapSurfCap) {
+    m.mapSurfCap = ns;
+    MA(m.surfMap, ns); MA(m.surfMapDS, ns);
+    int T = 64;
+    while (T < ns) T <<= 1;
+    MA(m.surfIx.begin, T); MA(m.surfIx.end, T); MA(m.surfIx.sorted, ns);
+    m.surfIx.cap = ns;
+  }
+#undef MA
+  return LEGO_OK;
+}
+
 int lego_mo_set_map(lego_ctx* x, const lego_point_xyzi* corner, int32_t n_corner,
                     const lego_point_xyzi* surf, int32_t n_surf) {
-  (void)corner; (void)n_corner; (void)surf; (void)n_surf;
   if (!x) return LEGO_E_ARG;
-  set_err("scan-to-map is not in this build yet");
-  return LEGO_E_STATE;
+  HIPCHK(hipSetDevice(x->device));
+  if (!corner && !surf) {
+    x->moFixed = false;
+    return LEGO_OK;
+  }
+  if (!corner || !surf || n_corner < 0 || n_surf < 0) return LEGO_E_ARG;
+  int st = mo_alloc(x, std::max(n_corner, 1), std::max(n_surf, 1));
+  if (st != LEGO_OK) return st;
+  MoDev& m = x->mo;
+  HIPCHK(hipMemcpyAsync(m.cornerMap, corner, sizeof(float4) * n_corner, hipMemcpyHostToDevice, x->stream));
+  HIPCHK(hipMemcpyAsync(m.surfMap, surf, sizeof(float4) * n_surf, hipMemcpyHostToDevice, x->stream));
+  if (mo_set_map_device(m, n_corner, n_surf, x->stream) != 0) {
+    set_err("scan-to-map: map voxel filter / index launch failed");
+    return LEGO_E_DEVICE;
+  }
+  HIPCHK(hipStreamSynchronize(x->stream));
+  x->moFixed = true;
+  return LEGO_OK;
 }
 
 int lego_mo_process(lego_ctx* x, const lego_fa_out* in, lego_mo_out* out) {
-  (void)in; (void)out;
-  if (!x) return LEGO_E_ARG;
-  set_err("scan-to-map is not in this build yet");
-  return LEGO_E_STATE;
+  if (!x || !in || !out) return LEGO_E_ARG;
+  std::memset(out, 0, sizeof(*out));
+  if (!x->moFixed) {
+    set_err("scan-to-map needs a map: install one with lego_mo_set_map (keyframe-built maps are not in "
+            "this build)");
+    return LEGO_E_STATE;
+  }
+  // run() gates (mapOptmization.cpp:1487-1499): a new hand-off, then the interval
+  if (!in->publish_to_mapping || !in->odom_valid) return LEGO_OK;
+  if (!(in->stamp - x->moTimeLast >= x->cfg.mapping_process_interval)) return LEGO_OK;
+  x->moTimeLast = in->stamp;
+  MoDev& m = x->mo;
+  const int N = x->dc.N, P = x->dc.P;
+  if (in->n_corner_last < 0 || in->n_corner_last > N * kLessSharpPerRing || in->n_surf_last < 0 ||
+      in->n_surf_last > P || in->n_outlier_last < 0 || in->n_outlier_last > P) {
+    set_err("scan-to-map: cloud larger than the sensor's capacity");
+    return LEGO_E_CAPACITY;
+  }
+  HIPCHK(hipSetDevice(x->device));
+  hipStream_t s = x->stream;
+  if (in->n_corner_last)
+    HIPCHK(hipMemcpyAsync(m.cornerLast, in->corner_last, sizeof(float4) * in->n_corner_last, hipMemcpyHostToDevice, s));
+  if (in->n_surf_last)
+    HIPCHK(hipMemcpyAsync(m.surfLast, in->surf_last, sizeof(float4) * in->n_surf_last, hipMemcpyHostToDevice, s));
+  if (in->n_outlier_last)
+    HIPCHK(hipMemcpyAsync(m.outlierLast, in->outlier_last, sizeof(float4) * in->n_outlier_last,
+                          hipMemcpyHostToDevice, s));
+  MoStepArgs a;
+  for (int i = 0; i < 4; ++i) a.quat[i] = in->odom_quat[i];
+  for (int i = 0; i < 3; ++i) a.pos[i] = in->odom_pos[i];
+  a.nCorner = in->n_corner_last;
+  a.nSurf = in->n_surf_last;
+  a.nOutlier = in->n_outlier_last;
+  if (mo_step_device(m, a, s) != 0) {
+    set_err("scan-to-map launch failed");
+    return LEGO_E_DEVICE;
+  }
+  MoState hs;
+  MoCounts hc;
+  HIPCHK(hipMemcpyAsync(&hs, m.st, sizeof(hs), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(&hc, m.cnt, sizeof(hc), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  out->processed = 1;
+  out->optimized = hs.optimized;
+  out->iterations = hs.iterations;
+  for (int i = 0; i < 6; ++i) {
+    out->transform_tobe_mapped[i] = hs.transformTobeMapped[i];
+    out->transform_aft_mapped[i] = hs.transformAftMapped[i];
+    out->transform_bef_mapped[i] = hs.transformBefMapped[i];
+  }
+  out->n_corner_map_ds = hc.cornerMapDS;
+  out->n_surf_map_ds = hc.surfMapDS;
+  out->n_corner_scan_ds = hc.cornerDS;
+  out->n_surf_scan_ds = hc.surfTotalDS;
+  out->n_rows_last = hs.rowsLast;
+  return LEGO_OK;
 }
 
 int lego_odom_profile(lego_ctx* x, int32_t enable, uint64_t* out32) {

@@ -1,0 +1,684 @@
+// lego_mo.hip — mapOptimization's scan-to-map step on gfx950.
+//
+// Per mapping step (mapOptmization.cpp:1487-1522 with the loop closure off):
+//   k_mo_associate   1 thread: laserOdometryHandler's quaternion -> RPY
+//                    (:629-641), transformAssociateToMap (:376-461)
+//   VoxelGrid        PCL's filter (voxel_grid.hpp) as device passes: min/max,
+//                    voxel index per point, stable radix sort (hipCUB) of
+//                    (index, point), segment heads + scan, one lane per voxel
+//                    summing its points in input order — the map (once per
+//                    installed map) and the scan's corner / surf / outlier /
+//                    surf+outlier clouds (:1067-1091)
+//   NN index         1 m cells hashed into buckets, sorted by bucket (radix
+//                    sort), begin/end per bucket; replaces KdTreeFLANN on the
+//                    map (:1335-1336).  Every use is thresholded (5th nearest
+//                    within 1 m, :1101, :1183), so the 27 cells around a query
+//                    hold every candidate; ties resolve to the lower index.
+//   per LM iteration (<= 10, :1337-1345):
+//     k_mo_rows      one lane per query: pointAssociateToMap (:513-527), 5-NN,
+//                    corner line fit (mean, covariance, 3x3 Jacobi, :1093-1174)
+//                    or surf plane fit (5x3 QR, :1176-1227), weight and
+//                    Jacobian row (:1244-1270)
+//     k_mo_solve     one workgroup: AtA / AtB with double accumulation, 6x6 QR,
+//                    iteration-0 eigen degeneracy projection, update,
+//                    convergence (:1229-1327); later iterations exit at once
+//                    once converged
+//   k_mo_finish      transformUpdate (:463-496, no IMU)
+// The fixed map (config C5, lego_mo_set_map) is voxel-filtered and indexed once
+// per map: the filter of an unchanged cloud is the same cloud every step.
+#include <hipcub/hipcub.hpp>
+
+#include <cfloat>
+#include <climits>
+
+#include "lego_device.h"
+#include "lego_kernels.h"
+#include "lego_mo.h"
+
+namespace lego {
+
+constexpr unsigned kInvalidKey = 0xffffffffu;
+constexpr int kMoSolveThreads = 1024;
+
+// ---------------------------------------------------------------- VoxelGrid
+__device__ __forceinline__ int ord_of(float f) {  // order-preserving float -> int
+  const int o = __float_as_int(f);
+  return o >= 0 ? o : o ^ 0x7fffffff;
+}
+__device__ __forceinline__ float of_ord(int o) { return __int_as_float(o >= 0 ? o : o ^ 0x7fffffff); }
+__device__ __forceinline__ bool finite3(float4 p) {
+  return __builtin_isfinite(p.x) && __builtin_isfinite(p.y) && __builtin_isfinite(p.z);
+}
+
+__global__ void k_vg_init(VgScratch v) {
+  if (threadIdx.x < 3) { v.mm[threadIdx.x] = INT_MAX; v.mm[3 + threadIdx.x] = INT_MIN; }
+  if (threadIdx.x == 0) *v.overflow = 0;
+}
+
+// n: element count (host bound); nDev: actual count on the device, or null
+__global__ void k_vg_minmax(const float4* in, int n, const int* nDev, VgScratch v) {
+  const int nn = nDev ? min(n, *nDev) : n;
+  int mn[3] = {INT_MAX, INT_MAX, INT_MAX}, mx[3] = {INT_MIN, INT_MIN, INT_MIN};
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nn; i += gridDim.x * blockDim.x) {
+    const float4 p = in[i];
+    if (!finite3(p)) continue;
+    const int o[3] = {ord_of(p.x), ord_of(p.y), ord_of(p.z)};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { mn[k] = min(mn[k], o[k]); mx[k] = max(mx[k], o[k]); }
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    for (int off = 32; off > 0; off >>= 1) {
+      mn[k] = min(mn[k], __shfl_xor(mn[k], off, 64));
+      mx[k] = max(mx[k], __shfl_xor(mx[k], off, 64));
+    }
+  }
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { atomicMin(&v.mm[k], mn[k]); atomicMax(&v.mm[3 + k], mx[k]); }
+  }
+}
+
+struct VgGeom {
+  float inv;
+  int minb[3], divb0, divb1;
+  bool overflow;
+};
+// pcl::VoxelGrid::applyFilter: leaf_size -> inverse, integer-overflow guard,
+// min/max voxel, division multipliers (float arithmetic as PCL's Eigen arrays).
+__device__ __forceinline__ VgGeom vg_geom(const VgScratch& v, float leaf) {
+  VgGeom g;
+  g.inv = 1.0f / leaf;
+  float minp[3], maxp[3];
+  for (int k = 0; k < 3; ++k) { minp[k] = of_ord(v.mm[k]); maxp[k] = of_ord(v.mm[3 + k]); }
+  const long long dx = (long long)((maxp[0] - minp[0]) * g.inv) + 1;
+  const long long dy = (long long)((maxp[1] - minp[1]) * g.inv) + 1;
+  const long long dz = (long long)((maxp[2] - minp[2]) * g.inv) + 1;
+  g.overflow = dx * dy * dz > (long long)INT_MAX;
+  int maxb[3];
+  for (int k = 0; k < 3; ++k) {
+    g.minb[k] = (int)floorf(minp[k] * g.inv);
+    maxb[k] = (int)floorf(maxp[k] * g.inv);
+  }
+  g.divb0 = maxb[0] - g.minb[0] + 1;
+  g.divb1 = maxb[1] - g.minb[1] + 1;
+  return g;
+}
+
+__global__ void k_vg_keys(const float4* in, int n, const int* nDev, float leaf, VgScratch v) {
+  const int nn = nDev ? min(n, *nDev) : n;
+  const VgGeom g = vg_geom(v, leaf);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && g.overflow) *v.overflow = 1;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    unsigned key = kInvalidKey;
+    if (i < nn) {
+      const float4 p = in[i];
+      if (finite3(p)) {
+        const int i0 = (int)(floorf(p.x * g.inv) - (float)g.minb[0]);
+        const int i1 = (int)(floorf(p.y * g.inv) - (float)g.minb[1]);
+        const int i2 = (int)(floorf(p.z * g.inv) - (float)g.minb[2]);
+        key = (unsigned)(i0 + i1 * g.divb0 + i2 * g.divb0 * g.divb1);
+      }
+    }
+    v.keys[i] = key;
+    v.vals[i] = i;
+  }
+}
+
+__global__ void k_vg_heads(int n, VgScratch v) {
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+    const unsigned k = v.keys2[t];
+    v.heads[t] = (k != kInvalidKey && (t == 0 || v.keys2[t - 1] != k)) ? 1 : 0;
+  }
+}
+
+// One lane per voxel: the centroid of its points summed in sorted (= input,
+// the sort is stable) order, written at the voxel's rank.  Overflow: copy.
+__global__ void k_vg_emit(const float4* in, int n, const int* nDev, VgScratch v, float4* out, int* nOut) {
+  const int nn = nDev ? min(n, *nDev) : n;
+  if (*v.overflow) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nn; i += gridDim.x * blockDim.x) out[i] = in[i];
+    if (blockIdx.x == 0 && threadIdx.x == 0) *nOut = nn;
+    return;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *nOut = n > 0 ? v.scan[n - 1] + v.heads[n - 1] : 0;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+    if (!v.heads[t]) continue;
+    const unsigned k = v.keys2[t];
+    float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
+    int j = t;
+    for (; j < n && v.keys2[j] == k; ++j) {
+      const float4 p = in[v.vals2[j]];
+      c0 += p.x; c1 += p.y; c2 += p.z; c3 += p.w;
+    }
+    const float cnt = (float)(j - t);
+    out[v.scan[t]] = make_float4(c0 / cnt, c1 / cnt, c2 / cnt, c3 / cnt);
+  }
+}
+
+static int grid_for(int n, int bs = 256) {
+  int g = (n + bs - 1) / bs;
+  return g < 1 ? 1 : (g > 4096 ? 4096 : g);
+}
+
+// in[0 .. min(n, *nDev)) -> out[0 .. *nOut), all on stream s.  n is a host
+// upper bound (the capacity the scratch was sized for).
+int voxel_grid_device(const float4* in, int n, const int* nDev, float leaf, float4* out, int* nOut,
+                      const VgScratch& v, hipStream_t s) {
+  if (n <= 0) {
+    if (hipMemsetAsync(nOut, 0, sizeof(int), s) != hipSuccess) return -1;
+    return 0;
+  }
+  if (n > v.cap) return -1;
+  k_vg_init<<<1, 64, 0, s>>>(v);
+  k_vg_minmax<<<grid_for(n), 256, 0, s>>>(in, n, nDev, v);
+  k_vg_keys<<<grid_for(n), 256, 0, s>>>(in, n, nDev, leaf, v);
+  size_t tb = v.tmpBytes;
+  if (hipcub::DeviceRadixSort::SortPairs(v.tmp, tb, v.keys, v.keys2, v.vals, v.vals2, n, 0, 32, s) != hipSuccess)
+    return -1;
+  k_vg_heads<<<grid_for(n), 256, 0, s>>>(n, v);
+  tb = v.tmpBytes;
+  if (hipcub::DeviceScan::ExclusiveSum(v.tmp, tb, v.heads, v.scan, n, s) != hipSuccess) return -1;
+  k_vg_emit<<<grid_for(n), 256, 0, s>>>(in, n, nDev, v, out, nOut);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+size_t voxel_scratch_tmp_bytes(int cap) {
+  size_t a = 0, b = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (unsigned*)nullptr, (unsigned*)nullptr, (int*)nullptr,
+                                           (int*)nullptr, cap, 0, 32);
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (int*)nullptr, (int*)nullptr, cap);
+  return a > b ? a : b;
+}
+
+// ---------------------------------------------------------------- NN index
+__device__ __forceinline__ unsigned mo_cell_hash(int ix, int iy, int iz) {
+  unsigned long long k = ((unsigned long long)(unsigned)(ix + (1 << 20)) << 42) |
+                         ((unsigned long long)(unsigned)(iy + (1 << 20)) << 21) |
+                         (unsigned long long)(unsigned)(iz + (1 << 20));
+  k ^= k >> 33; k *= 0xff51afd7ed558ccdULL; k ^= k >> 33;
+  return (unsigned)k;
+}
+__device__ __forceinline__ int cell1(float v) { return (int)floorf(v); }  // 1 m cells
+
+__global__ void k_idx_keys(const float4* pts, const int* nDev, int n, int T, VgScratch v) {
+  const int nn = min(n, *nDev);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    unsigned key = kInvalidKey;
+    if (i < nn) {
+      const float4 p = pts[i];
+      key = mo_cell_hash(cell1(p.x), cell1(p.y), cell1(p.z)) & (unsigned)(T - 1);
+    }
+    v.keys[i] = key;
+    v.vals[i] = i;
+  }
+}
+// bucket begin/end (end == begin == 0 for an empty bucket) and the points in
+// bucket order carrying their index in w
+__global__ void k_idx_fill(const float4* pts, int n, VgScratch v, MoIndex ix) {
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+    const unsigned k = v.keys2[t];
+    if (k == kInvalidKey) continue;
+    const int i = v.vals2[t];
+    const float4 p = pts[i];
+    ix.sorted[t] = make_float4(p.x, p.y, p.z, __int_as_float(i));
+    if (t == 0 || v.keys2[t - 1] != k) ix.begin[k] = t;
+    if (t == n - 1 || v.keys2[t + 1] != k) ix.end[k] = t + 1;
+  }
+}
+
+int index_build_device(const float4* pts, int n, const int* nDev, MoIndex& ix, const VgScratch& v, hipStream_t s) {
+  if (n > v.cap || n > ix.cap) return -1;
+  int T = 64;
+  while (T < n) T <<= 1;
+  ix.T = T;
+  if (hipMemsetAsync(ix.begin, 0, sizeof(int) * T, s) != hipSuccess) return -1;
+  if (hipMemsetAsync(ix.end, 0, sizeof(int) * T, s) != hipSuccess) return -1;
+  if (n <= 0) return 0;
+  k_idx_keys<<<grid_for(n), 256, 0, s>>>(pts, nDev, n, T, v);
+  size_t tb = v.tmpBytes;
+  if (hipcub::DeviceRadixSort::SortPairs(v.tmp, tb, v.keys, v.keys2, v.vals, v.vals2, n, 0, 32, s) != hipSuccess)
+    return -1;
+  k_idx_fill<<<grid_for(n), 256, 0, s>>>(pts, n, v, ix);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// The 5 nearest map points with squared distance < 1 (FLANN L2_Simple order),
+// sorted by (distance, index).  Returns how many were found (<= 5).
+__device__ __forceinline__ int knn5(const MoIndex& ix, float4 q, int* oi, float* od) {
+  int n = 0;
+  const int cx = cell1(q.x), cy = cell1(q.y), cz = cell1(q.z);
+  for (int dz = -1; dz <= 1; ++dz)
+    for (int dy = -1; dy <= 1; ++dy)
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int bx = cx + dx, by = cy + dy, bz = cz + dz;
+        const unsigned b = mo_cell_hash(bx, by, bz) & (unsigned)(ix.T - 1);
+        const int lo = ix.begin[b], hi = ix.end[b];
+        for (int t = lo; t < hi; ++t) {
+          const float4 p = ix.sorted[t];
+          if (cell1(p.x) != bx || cell1(p.y) != by || cell1(p.z) != bz) continue;  // another cell's bucket mate
+          float d2 = 0.f, d;
+          d = q.x - p.x; d2 += d * d;
+          d = q.y - p.y; d2 += d * d;
+          d = q.z - p.z; d2 += d * d;
+          if (!(d2 < 1.0f)) continue;
+          const int id = __float_as_int(p.w);
+          if (n == 5 && !(d2 < od[4] || (d2 == od[4] && id < oi[4]))) continue;
+          int pos = n < 5 ? n++ : 4;
+          while (pos > 0 && (d2 < od[pos - 1] || (d2 == od[pos - 1] && id < oi[pos - 1]))) {
+            od[pos] = od[pos - 1];
+            oi[pos] = oi[pos - 1];
+            --pos;
+          }
+          od[pos] = d2;
+          oi[pos] = id;
+        }
+      }
+  return n;
+}
+
+// ---------------------------------------------------------------- state
+__device__ __forceinline__ void quat_from_rpy(double roll, double pitch, double yaw, double q[4]) {
+  const double hy = yaw * 0.5, hp = pitch * 0.5, hr = roll * 0.5;
+  const double cy = cos(hy), sy = sin(hy), cp = cos(hp), sp = sin(hp), cr = cos(hr), sr = sin(hr);
+  q[0] = sr * cp * cy - cr * sp * sy;
+  q[1] = cr * sp * cy + sr * cp * sy;
+  q[2] = cr * cp * sy - sr * sp * cy;
+  q[3] = cr * cp * cy + sr * sp * sy;
+}
+// tf::Matrix3x3(q).getRPY, solution 1
+__device__ __forceinline__ void rpy_from_quat(double x, double y, double z, double w, double* roll, double* pitch,
+                                              double* yaw) {
+  const double d = x * x + y * y + z * z + w * w;
+  const double s = 2.0 / d;
+  const double xs = x * s, ys = y * s, zs = z * s;
+  const double wx = w * xs, wy = w * ys, wz = w * zs;
+  const double xx = x * xs, xy = x * ys, xz = x * zs;
+  const double yy = y * ys, yz = y * zs, zz = z * zs;
+  const double m00 = 1.0 - (yy + zz), m10 = xy + wz, m20 = xz - wy, m21 = yz + wx, m22 = 1.0 - (xx + yy);
+  if (fabs(m20) >= 1) {
+    *yaw = 0;
+    const double delta = atan2(m21, m22);
+    *pitch = m20 < 0 ? M_PI / 2.0 : -M_PI / 2.0;
+    *roll = delta;
+  } else {
+    *pitch = -asin(m20);
+    const double cp = cos(*pitch);
+    *roll = atan2(m21 / cp, m22 / cp);
+    *yaw = atan2(m10 / cp, m00 / cp);
+  }
+}
+
+__device__ __forceinline__ void mo_update_trig(MoState* st) {  // updatePointAssociateToMapSinCos :498-511
+  const float* t = st->transformTobeMapped;
+  st->cRoll = lego_cosf(t[0]); st->sRoll = lego_sinf(t[0]);
+  st->cPitch = lego_cosf(t[1]); st->sPitch = lego_sinf(t[1]);
+  st->cYaw = lego_cosf(t[2]); st->sYaw = lego_sinf(t[2]);
+}
+
+// laserOdometryHandler (:629-641) and transformAssociateToMap (:376-461)
+__global__ void k_mo_associate(MoState* st, MoCounts* cnt, double qx, double qy, double qz, double qw, double px,
+                               double py, double pz) {
+  if (threadIdx.x != 0) return;
+  double roll, pitch, yaw;
+  rpy_from_quat(qz, -qx, -qy, qw, &roll, &pitch, &yaw);
+  float* ts = st->transformSum;
+  ts[0] = (float)-pitch; ts[1] = (float)-yaw; ts[2] = (float)roll;
+  ts[3] = (float)px; ts[4] = (float)py; ts[5] = (float)pz;
+  const float* bef = st->transformBefMapped;
+  const float* aft = st->transformAftMapped;
+  float* tbm = st->transformTobeMapped;
+  float* inc = st->transformIncre;
+  float x1 = lego_cosf(ts[1]) * (bef[3] - ts[3]) - lego_sinf(ts[1]) * (bef[5] - ts[5]);
+  float y1 = bef[4] - ts[4];
+  float z1 = lego_sinf(ts[1]) * (bef[3] - ts[3]) + lego_cosf(ts[1]) * (bef[5] - ts[5]);
+  float x2 = x1;
+  float y2 = lego_cosf(ts[0]) * y1 + lego_sinf(ts[0]) * z1;
+  float z2 = -lego_sinf(ts[0]) * y1 + lego_cosf(ts[0]) * z1;
+  inc[3] = lego_cosf(ts[2]) * x2 + lego_sinf(ts[2]) * y2;
+  inc[4] = -lego_sinf(ts[2]) * x2 + lego_cosf(ts[2]) * y2;
+  inc[5] = z2;
+  const float sbcx = lego_sinf(ts[0]), cbcx = lego_cosf(ts[0]);
+  const float sbcy = lego_sinf(ts[1]), cbcy = lego_cosf(ts[1]);
+  const float sbcz = lego_sinf(ts[2]), cbcz = lego_cosf(ts[2]);
+  const float sblx = lego_sinf(bef[0]), cblx = lego_cosf(bef[0]);
+  const float sbly = lego_sinf(bef[1]), cbly = lego_cosf(bef[1]);
+  const float sblz = lego_sinf(bef[2]), cblz = lego_cosf(bef[2]);
+  const float salx = lego_sinf(aft[0]), calx = lego_cosf(aft[0]);
+  const float saly = lego_sinf(aft[1]), caly = lego_cosf(aft[1]);
+  const float salz = lego_sinf(aft[2]), calz = lego_cosf(aft[2]);
+  const float srx = -sbcx * (salx * sblx + calx * cblx * salz * sblz + calx * calz * cblx * cblz) -
+                    cbcx * sbcy * (calx * calz * (cbly * sblz - cblz * sblx * sbly) -
+                                   calx * salz * (cbly * cblz + sblx * sbly * sblz) + cblx * salx * sbly) -
+                    cbcx * cbcy * (calx * salz * (cblz * sbly - cbly * sblx * sblz) -
+                                   calx * calz * (sbly * sblz + cbly * cblz * sblx) + cblx * cbly * salx);
+  tbm[0] = -lego_asinf(srx);
+  const float srycrx = sbcx * (cblx * cblz * (caly * salz - calz * salx * saly) -
+                               cblx * sblz * (caly * calz + salx * saly * salz) + calx * saly * sblx) -
+                       cbcx * cbcy * ((caly * calz + salx * saly * salz) * (cblz * sbly - cbly * sblx * sblz) +
+                                      (caly * salz - calz * salx * saly) * (sbly * sblz + cbly * cblz * sblx) -
+                                      calx * cblx * cbly * saly) +
+                       cbcx * sbcy * ((caly * calz + salx * saly * salz) * (cbly * cblz + sblx * sbly * sblz) +
+                                      (caly * salz - calz * salx * saly) * (cbly * sblz - cblz * sblx * sbly) +
+                                      calx * cblx * saly * sbly);
+  const float crycrx = sbcx * (cblx * sblz * (calz * saly - caly * salx * salz) -
+                               cblx * cblz * (saly * salz + caly * calz * salx) + calx * caly * sblx) +
+                       cbcx * cbcy * ((saly * salz + caly * calz * salx) * (sbly * sblz + cbly * cblz * sblx) +
+                                      (calz * saly - caly * salx * salz) * (cblz * sbly - cbly * sblx * sblz) +
+                                      calx * caly * cblx * cbly) -
+                       cbcx * sbcy * ((saly * salz + caly * calz * salx) * (cbly * sblz - cblz * sblx * sbly) +
+                                      (calz * saly - caly * salx * salz) * (cbly * cblz + sblx * sbly * sblz) -
+                                      calx * caly * cblx * sbly);
+  tbm[1] = lego_atan2f(srycrx / lego_cosf(tbm[0]), crycrx / lego_cosf(tbm[0]));
+  const float srzcrx = (cbcz * sbcy - cbcy * sbcx * sbcz) *
+                           (calx * salz * (cblz * sbly - cbly * sblx * sblz) -
+                            calx * calz * (sbly * sblz + cbly * cblz * sblx) + cblx * cbly * salx) -
+                       (cbcy * cbcz + sbcx * sbcy * sbcz) *
+                           (calx * calz * (cbly * sblz - cblz * sblx * sbly) -
+                            calx * salz * (cbly * cblz + sblx * sbly * sblz) + cblx * salx * sbly) +
+                       cbcx * sbcz * (salx * sblx + calx * cblx * salz * sblz + calx * calz * cblx * cblz);
+  const float crzcrx = (cbcy * sbcz - cbcz * sbcx * sbcy) *
+                           (calx * calz * (cbly * sblz - cblz * sblx * sbly) -
+                            calx * salz * (cbly * cblz + sblx * sbly * sblz) + cblx * salx * sbly) -
+                       (sbcy * sbcz + cbcy * cbcz * sbcx) *
+                           (calx * salz * (cblz * sbly - cbly * sblx * sblz) -
+                            calx * calz * (sbly * sblz + cbly * cblz * sblx) + cblx * cbly * salx) +
+                       cbcx * cbcz * (salx * sblx + calx * cblx * salz * sblz + calx * calz * cblx * cblz);
+  tbm[2] = lego_atan2f(srzcrx / lego_cosf(tbm[0]), crzcrx / lego_cosf(tbm[0]));
+  x1 = lego_cosf(tbm[2]) * inc[3] - lego_sinf(tbm[2]) * inc[4];
+  y1 = lego_sinf(tbm[2]) * inc[3] + lego_cosf(tbm[2]) * inc[4];
+  z1 = inc[5];
+  x2 = x1;
+  y2 = lego_cosf(tbm[0]) * y1 - lego_sinf(tbm[0]) * z1;
+  z2 = lego_sinf(tbm[0]) * y1 + lego_cosf(tbm[0]) * z1;
+  tbm[3] = aft[3] - (lego_cosf(tbm[1]) * x2 + lego_sinf(tbm[1]) * z2);
+  tbm[4] = aft[4] - y2;
+  tbm[5] = aft[5] - (-lego_sinf(tbm[1]) * x2 + lego_cosf(tbm[1]) * z2);
+  mo_update_trig(st);
+  st->converged = 0;
+  st->iterations = 0;
+  // scan2MapOptimization's guard (:1331)
+  st->optimized = (cnt->cornerMapDS > 10 && cnt->surfMapDS > 100) ? 1 : 0;
+}
+
+// surfTotalLast = surfLastDS + outlierLastDS (:1084-1086)
+__global__ void k_mo_concat(const float4* a, const float4* b, MoCounts* cnt, float4* out) {
+  const int na = cnt->surfDS, nb = cnt->outlierDS;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < na + nb; i += gridDim.x * blockDim.x)
+    out[i] = i < na ? a[i] : b[i - na];
+  if (blockIdx.x == 0 && threadIdx.x == 0) cnt->surfTotal = na + nb;
+}
+
+// ---------------------------------------------------------------- LM rows
+__device__ __forceinline__ float4 associate_to_map(float4 pi, const MoState* st) {  // :513-527
+  const float x1 = st->cYaw * pi.x - st->sYaw * pi.y;
+  const float y1 = st->sYaw * pi.x + st->cYaw * pi.y;
+  const float z1 = pi.z;
+  const float x2 = x1;
+  const float y2 = st->cRoll * y1 - st->sRoll * z1;
+  const float z2 = st->sRoll * y1 + st->cRoll * z1;
+  const float* t = st->transformTobeMapped;
+  return make_float4(st->cPitch * x2 + st->sPitch * z2 + t[3], y2 + t[4], -st->sPitch * x2 + st->cPitch * z2 + t[5],
+                     pi.w);
+}
+
+// One lane per query: corner queries [0, nCornerDS), then surf+outlier
+// queries.  Row r = {arx, ary, arz, cf.x, cf.y, cf.z, B, valid}.
+__global__ void k_mo_rows(MoState* st, const MoCounts* cnt, const float4* cornerDS, const float4* surfTotalDS,
+                          MoIndex cornerIx, MoIndex surfIx, const float4* cornerMap, const float4* surfMap,
+                          float* rows, int qcap) {
+  if (!st->optimized || st->converged) return;
+  const int nC = cnt->cornerDS, nS = cnt->surfTotalDS;
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nC + nS || q >= qcap) return;
+  float* row = rows + (size_t)q * 8;
+  row[7] = 0.f;
+  const bool corner = q < nC;
+  const float4 po = corner ? cornerDS[q] : surfTotalDS[q - nC];
+  const float4 sel = associate_to_map(po, st);
+  int ind[5];
+  float sq[5];
+  if (knn5(corner ? cornerIx : surfIx, sel, ind, sq) < 5) return;
+  float4 cf;
+  if (corner) {  // cornerOptimization :1093-1174
+    float cx = 0, cy = 0, cz = 0;
+    for (int j = 0; j < 5; j++) {
+      const float4 m = cornerMap[ind[j]];
+      cx += m.x; cy += m.y; cz += m.z;
+    }
+    cx /= 5; cy /= 5; cz /= 5;
+    float a11 = 0, a12 = 0, a13 = 0, a22 = 0, a23 = 0, a33 = 0;
+    for (int j = 0; j < 5; j++) {
+      const float4 m = cornerMap[ind[j]];
+      const float ax = m.x - cx, ay = m.y - cy, az = m.z - cz;
+      a11 += ax * ax; a12 += ax * ay; a13 += ax * az;
+      a22 += ay * ay; a23 += ay * az; a33 += az * az;
+    }
+    a11 /= 5; a12 /= 5; a13 /= 5; a22 /= 5; a23 /= 5; a33 /= 5;
+    const float A1[3][3] = {{a11, a12, a13}, {a12, a22, a23}, {a13, a23, a33}};
+    float D1[3], V1[3][3];
+    cv_eigen_sym3(A1, D1, V1);
+    if (!(D1[0] > 3 * D1[1])) return;
+    const float x0 = sel.x, y0 = sel.y, z0 = sel.z;
+    const float x1 = (float)(cx + 0.1 * (double)V1[0][0]);
+    const float y1 = (float)(cy + 0.1 * (double)V1[0][1]);
+    const float z1 = (float)(cz + 0.1 * (double)V1[0][2]);
+    const float x2 = (float)(cx - 0.1 * (double)V1[0][0]);
+    const float y2 = (float)(cy - 0.1 * (double)V1[0][1]);
+    const float z2 = (float)(cz - 0.1 * (double)V1[0][2]);
+    const float m11 = (x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1);
+    const float m22 = (x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1);
+    const float m33 = (y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1);
+    const float a012 = __builtin_sqrtf(m11 * m11 + m22 * m22 + m33 * m33);
+    const float l12 = __builtin_sqrtf((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2));
+    const float la = ((y1 - y2) * m11 + (z1 - z2) * m22) / a012 / l12;
+    const float lb = -((x1 - x2) * m11 - (z1 - z2) * m33) / a012 / l12;
+    const float lc = -((x1 - x2) * m22 + (y1 - y2) * m33) / a012 / l12;
+    const float ld2 = a012 / l12;
+    const float s = (float)(1 - 0.9 * (double)lfabsf(ld2));
+    if (!((double)s > 0.1)) return;
+    cf = make_float4(s * la, s * lb, s * lc, s * ld2);
+  } else {  // surfOptimization :1176-1227
+    float A0[5][3];
+    const float B0[5] = {-1, -1, -1, -1, -1};
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+      const float4 m = surfMap[ind[j]];
+      A0[j][0] = m.x; A0[j][1] = m.y; A0[j][2] = m.z;
+    }
+    float X0[3];
+    cv_solve_qr<5, 3>(A0, B0, X0);
+    float pa = X0[0], pb = X0[1], pc = X0[2], pd = 1;
+    const float ps = __builtin_sqrtf(pa * pa + pb * pb + pc * pc);
+    pa /= ps; pb /= ps; pc /= ps; pd /= ps;
+    for (int j = 0; j < 5; j++) {
+      const float4 m = surfMap[ind[j]];
+      if ((double)lfabsf(pa * m.x + pb * m.y + pc * m.z + pd) > 0.2) return;
+    }
+    const float pd2 = pa * sel.x + pb * sel.y + pc * sel.z + pd;
+    const float s = (float)(1 - 0.9 * (double)lfabsf(pd2) /
+                                    (double)__builtin_sqrtf(__builtin_sqrtf(sel.x * sel.x + sel.y * sel.y + sel.z * sel.z)));
+    if (!((double)s > 0.1)) return;
+    cf = make_float4(s * pa, s * pb, s * pc, s * pd2);
+  }
+  // LMOptimization's Jacobian row (:1244-1270)
+  const float* t = st->transformTobeMapped;
+  const float srx = st->sRoll, crx = st->cRoll, sry = st->sPitch, cry = st->cPitch, srz = st->sYaw, crz = st->cYaw;
+  (void)t;
+  const float arx = (crx * sry * srz * po.x + crx * crz * sry * po.y - srx * sry * po.z) * cf.x +
+                    (-srx * srz * po.x - crz * srx * po.y - crx * po.z) * cf.y +
+                    (crx * cry * srz * po.x + crx * cry * crz * po.y - cry * srx * po.z) * cf.z;
+  const float ary = ((cry * srx * srz - crz * sry) * po.x + (sry * srz + cry * crz * srx) * po.y + crx * cry * po.z) * cf.x +
+                    ((-cry * crz - srx * sry * srz) * po.x + (cry * srz - crz * srx * sry) * po.y - crx * sry * po.z) * cf.z;
+  const float arz = ((crz * srx * sry - cry * srz) * po.x + (-cry * crz - srx * sry * srz) * po.y) * cf.x +
+                    (crx * crz * po.x - crx * srz * po.y) * cf.y +
+                    ((sry * srz + cry * crz * srx) * po.x + (crz * sry - cry * srx * srz) * po.y) * cf.z;
+  row[0] = arx; row[1] = ary; row[2] = arz;
+  row[3] = cf.x; row[4] = cf.y; row[5] = cf.z;
+  row[6] = -cf.w;
+  row[7] = 1.f;
+}
+
+// ---------------------------------------------------------------- LM solve
+// Wave sum of a double through DPP (see lego_odom.hip).
+template <int kCtrl>
+__device__ __forceinline__ double mo_dpp(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, kCtrl, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), kCtrl, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double mo_rdlane(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double mo_wave_sum(double v) {
+  v += mo_dpp<0xB1>(v);
+  v += mo_dpp<0x4E>(v);
+  v += mo_dpp<0x141>(v);
+  v += mo_dpp<0x140>(v);
+  return (mo_rdlane(v, 0) + mo_rdlane(v, 16)) + (mo_rdlane(v, 32) + mo_rdlane(v, 48));
+}
+
+constexpr int kMoSums = 21 + 6 + 1;  // AtA upper triangle, AtB, row count
+
+__global__ void __launch_bounds__(kMoSolveThreads) k_mo_solve(MoState* st, const MoCounts* cnt, const float* rows,
+                                                             int qcap, int iterCount) {
+  if (!st->optimized || st->converged) return;
+  __shared__ double red[kMoSolveThreads / 64][kMoSums];
+  __shared__ float ws[6 * 6 * 6 + 16];  // eigen / inverse workspace (thread 0)
+  __shared__ int wsi[16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int Q = min(cnt->cornerDS + cnt->surfTotalDS, qcap);
+  double acc[kMoSums];
+#pragma unroll
+  for (int k = 0; k < kMoSums; ++k) acc[k] = 0.0;
+  for (int r = tid; r < Q; r += kMoSolveThreads) {
+    const float* row = rows + (size_t)r * 8;
+    if (row[7] == 0.f) continue;
+    double a[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) a[k] = row[k];
+    int o = 0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = i; j < 6; ++j) acc[o++] += a[i] * a[j];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) acc[21 + i] += a[i] * a[6];
+    acc[27] += 1.0;
+  }
+#pragma unroll
+  for (int k = 0; k < kMoSums; ++k) {
+    const double w = mo_wave_sum(acc[k]);
+    if (lane == 0) red[wave][k] = w;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  double tot[kMoSums];
+  for (int k = 0; k < kMoSums; ++k) {
+    double sum = 0;
+    for (int w = 0; w < kMoSolveThreads / 64; ++w) sum += red[w][k];
+    tot[k] = sum;
+  }
+  const int M = (int)tot[27];
+  st->rowsLast = M;
+  st->iterations = iterCount + 1;
+  if (M < 50) return;  // LMOptimization returns false: not converged
+  float AtA[6][6], AtB[6];
+  int o = 0;
+  for (int i = 0; i < 6; ++i)
+    for (int j = i; j < 6; ++j) { AtA[i][j] = AtA[j][i] = (float)tot[o++]; }
+  for (int i = 0; i < 6; ++i) AtB[i] = (float)tot[21 + i];
+  float Aq[6][6], X[6];
+  for (int i = 0; i < 6; ++i)
+    for (int j = 0; j < 6; ++j) Aq[i][j] = AtA[i][j];
+  cv_solve_qr<6, 6>(Aq, AtB, X);
+  float (&P)[6][6] = *reinterpret_cast<float(*)[6][6]>(st->matP);
+  if (iterCount == 0) {
+    // eigen / inverse on LDS arrays (their loops index dynamically)
+    float (&Ae)[6][6] = *reinterpret_cast<float(*)[6][6]>(ws);
+    float (&V)[6][6] = *reinterpret_cast<float(*)[6][6]>(ws + 36);
+    float (&V2)[6][6] = *reinterpret_cast<float(*)[6][6]>(ws + 72);
+    float (&Vi)[6][6] = *reinterpret_cast<float(*)[6][6]>(ws + 108);
+    float (&E)[6] = *reinterpret_cast<float(*)[6]>(ws + 144);
+    int (&indR)[6] = *reinterpret_cast<int(*)[6]>(wsi);
+    int (&indC)[6] = *reinterpret_cast<int(*)[6]>(wsi + 6);
+    for (int i = 0; i < 6; ++i)
+      for (int j = 0; j < 6; ++j) Ae[i][j] = AtA[i][j];
+    cv_eigen_sym_ws<6>(Ae, E, V, indR, indC);
+    for (int i = 0; i < 6; ++i)
+      for (int j = 0; j < 6; ++j) V2[i][j] = V[i][j];
+    st->isDegenerate = 0;
+    for (int i = 5; i >= 0; i--) {
+      if (E[i] < 100) {
+        for (int j = 0; j < 6; j++) V2[i][j] = 0;
+        st->isDegenerate = 1;
+      } else {
+        break;
+      }
+    }
+    cv_inv_lu<6>(V, Vi);
+    cv_matmul<6>(Vi, V2, P);
+  }
+  if (st->isDegenerate) {
+    float X2[6];
+    for (int i = 0; i < 6; ++i) X2[i] = X[i];
+    cv_matvec<6>(P, X2, X);
+  }
+  float* t = st->transformTobeMapped;
+  for (int i = 0; i < 6; i++) t[i] += X[i];
+  // pcl::rad2deg(float) = a * 57.29578f
+  const double d0 = X[0] * 57.29578f, d1 = X[1] * 57.29578f, d2 = X[2] * 57.29578f;
+  const double t0 = X[3] * 100, t1 = X[4] * 100, t2 = X[5] * 100;
+  const float deltaR = (float)sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+  const float deltaT = (float)sqrt(t0 * t0 + t1 * t1 + t2 * t2);
+  mo_update_trig(st);
+  if ((double)deltaR < 0.05 && (double)deltaT < 0.05) st->converged = 1;
+}
+
+__global__ void k_mo_finish(MoState* st) {  // transformUpdate :463-496 (no IMU)
+  if (threadIdx.x != 0 || !st->optimized) return;
+  for (int i = 0; i < 6; i++) {
+    st->transformBefMapped[i] = st->transformSum[i];
+    st->transformAftMapped[i] = st->transformTobeMapped[i];
+  }
+}
+
+int mo_step_device(const MoDev& m, const MoStepArgs& a, hipStream_t s) {
+  k_mo_associate<<<1, 64, 0, s>>>(m.st, m.cnt, a.quat[0], a.quat[1], a.quat[2], a.quat[3], a.pos[0], a.pos[1],
+                                  a.pos[2]);
+  if (hipGetLastError() != hipSuccess) return -1;
+  // downsampleCurrentScan :1067-1091
+  if (voxel_grid_device(m.cornerLast, a.nCorner, nullptr, 0.2f, m.cornerDS, &m.cnt->cornerDS, m.vg, s)) return -1;
+  if (voxel_grid_device(m.surfLast, a.nSurf, nullptr, 0.4f, m.surfDS, &m.cnt->surfDS, m.vg, s)) return -1;
+  if (voxel_grid_device(m.outlierLast, a.nOutlier, nullptr, 0.4f, m.outlierDS, &m.cnt->outlierDS, m.vg, s)) return -1;
+  k_mo_concat<<<grid_for(a.nSurf + a.nOutlier), 256, 0, s>>>(m.surfDS, m.outlierDS, m.cnt, m.surfTotal);
+  if (voxel_grid_device(m.surfTotal, a.nSurf + a.nOutlier, &m.cnt->surfTotal, 0.4f, m.surfTotalDS,
+                        &m.cnt->surfTotalDS, m.vg, s))
+    return -1;
+  // scan2MapOptimization :1329-1350 — the iterations exit on the device once converged
+  const int qcap = a.nCorner + a.nSurf + a.nOutlier;
+  if (qcap > m.rowCap) return -1;
+  for (int it = 0; it < 10; ++it) {
+    if (qcap > 0)
+      k_mo_rows<<<grid_for(qcap, 128), 128, 0, s>>>(m.st, m.cnt, m.cornerDS, m.surfTotalDS, m.cornerIx, m.surfIx,
+                                                   m.cornerMapDS, m.surfMapDS, m.rows, qcap);
+    k_mo_solve<<<1, kMoSolveThreads, 0, s>>>(m.st, m.cnt, m.rows, qcap, it);
+  }
+  k_mo_finish<<<1, 64, 0, s>>>(m.st);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// Installs a fixed map: voxel filter (corner 0.2 m, surf 0.4 m, :1062-1064) and
+// NN index, once.
+int mo_set_map_device(MoDev& m, int nCornerMap, int nSurfMap, hipStream_t s) {
+  if (voxel_grid_device(m.cornerMap, nCornerMap, nullptr, 0.2f, m.cornerMapDS, &m.cnt->cornerMapDS, m.vg, s)) return -1;
+  if (voxel_grid_device(m.surfMap, nSurfMap, nullptr, 0.4f, m.surfMapDS, &m.cnt->surfMapDS, m.vg, s)) return -1;
+  if (index_build_device(m.cornerMapDS, nCornerMap, &m.cnt->cornerMapDS, m.cornerIx, m.vg, s)) return -1;
+  if (index_build_device(m.surfMapDS, nSurfMap, &m.cnt->surfMapDS, m.surfIx, m.vg, s)) return -1;
+  return 0;
+}
+
+}  // namespace lego

@@ -368,6 +368,19 @@ class Lego:
               "lego_fa_process", self.lib)
         return fa_to_dict(self._fa)
 
+    def mo_set_map(self, corner: np.ndarray, surf: np.ndarray) -> None:
+        corner = np.ascontiguousarray(corner, dtype=XYZI_DTYPE)
+        surf = np.ascontiguousarray(surf, dtype=XYZI_DTYPE)
+        check(self.lib.lego_mo_set_map(self.h, corner.ctypes.data, len(corner), surf.ctypes.data, len(surf)),
+              "lego_mo_set_map", self.lib)
+
+    def mo(self) -> dict:
+        """Scan-to-map on the last fa() output (mapOptimization::run)."""
+        out = MoOut()
+        check(self.lib.lego_mo_process(self.h, C.byref(self._fa), C.byref(out)), "lego_mo_process", self.lib)
+        return {k: (np.array(list(getattr(out, k)), dtype=np.float32)
+                    if k.startswith("transform") else getattr(out, k)) for k, _ in MoOut._fields_}
+
     def odom_batch(self, pts: np.ndarray, offsets: np.ndarray, stamps: np.ndarray) -> np.ndarray:
         pts = np.ascontiguousarray(pts, dtype=XYZIR_DTYPE)
         offsets = np.ascontiguousarray(offsets, dtype=np.int64)

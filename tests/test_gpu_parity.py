@@ -167,3 +167,52 @@ def test_batch_argument_checks(L):
     gpu.reset()
     assert call(pts, two, 1) == L.LEGO_OK
     gpu.close()
+
+
+@pytest.mark.parametrize("sensor,seed,nscans,n_surf,n_corner", [
+    ("VLP-16", 3, 14, 200000, 40000),
+])
+def test_scan_to_map_parity(L, sensor, seed, nscans, n_surf, n_corner):
+    """mapOptimization's scan-to-map step against a fixed synthetic map (config
+    C5 shape, smaller): voxel-filtered sizes bit-exact, the same processed /
+    optimized decisions and iteration counts, poses within 1e-4."""
+    sc = L.synth_cfg(sensor, seed)
+    surf, corner = L.synth_map(seed, 50.0, n_surf, n_corner)
+    ora = L.Oracle(L.sensor_cfg(sensor))
+    ora.mo_set_map(corner, surf)
+    gpu = L.Lego(L.sensor_cfg(sensor, L.hip_lib()), max_points=40000)
+    gpu.mo_set_map(corner, surf)
+    steps = optimized = 0
+    worst = 0.0
+    for k in range(nscans):
+        pts, stamp = L.synth_scan(sc, k)
+        ora.ip(pts, stamp)
+        ora.fa()
+        o = ora.mo()
+        gpu.ip(pts, stamp)
+        gpu.fa()
+        g = gpu.mo()
+        assert g["processed"] == o["processed"], k
+        if not o["processed"]:
+            continue
+        steps += 1
+        for key in ("optimized", "n_corner_map_ds", "n_surf_map_ds", "n_corner_scan_ds", "n_surf_scan_ds"):
+            assert g[key] == o[key], (k, key, g[key], o[key])
+        optimized += int(o["optimized"])
+        d = np.max(np.abs(g["transform_aft_mapped"].astype(np.float64) - o["transform_aft_mapped"]))
+        worst = max(worst, float(d))
+        assert d <= POSE_TOL, (k, g["transform_aft_mapped"], o["transform_aft_mapped"], g["iterations"],
+                               o["iterations"], g["n_rows_last"], o["n_rows_last"])
+    print(f"scan-to-map: {steps} steps, {optimized} optimized, worst |dpose| = {worst:.3g}")
+    assert steps >= 2 and optimized >= 1
+    gpu.close()
+
+
+def test_scan_to_map_needs_a_map(L):
+    gpu = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=40000)
+    sc = L.synth_cfg("VLP-16", 0)
+    gpu.ip(*L.synth_scan(sc, 0))
+    gpu.fa()
+    with pytest.raises(RuntimeError, match="status 5"):
+        gpu.mo()
+    gpu.close()
