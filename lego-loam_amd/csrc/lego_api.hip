@@ -150,6 +150,10 @@ static int ctx_reset(lego_ctx* x) {
   x->lastB = 0;
   if (x->moAlloc) {
     HIPCHK(hipMemsetAsync(x->mo.st, 0, sizeof(MoState), x->stream));
+    if (x->mo.kf.kcap) {
+      HIPCHK(hipMemsetAsync(x->mo.kf.meta, 0, sizeof(int) * kKfMeta, x->stream));
+      HIPCHK(hipMemsetAsync(x->mo.kf.robot, 0, sizeof(float) * 8, x->stream));
+    }
     HIPCHK(hipStreamSynchronize(x->stream));
   }
   x->moTimeLast = -1;
@@ -692,6 +696,30 @@ static int mo_alloc(lego_ctx* x, int nc, int ns) {
   return LEGO_OK;
 }
 
+// Keyframe store for the keyframe-built map (first use without a fixed map).
+static int mo_alloc_keyframes(lego_ctx* x) {
+  MoDev& m = x->mo;
+  if (m.kf.kcap) return LEGO_OK;
+  const int fromCap = 2 << 20;
+  int st = mo_alloc(x, fromCap, fromCap);
+  if (st != LEGO_OK) return st;
+  MoKeyframes& kf = m.kf;
+  const int kcap = 16384, acap = 16 << 20;
+#define MA(ptr, n) \
+  if (x->alloc(&(ptr), (size_t)(n)) != hipSuccess) { set_err("hipMalloc failed for %s", #ptr); return LEGO_E_DEVICE; }
+  MA(kf.pos3, kcap); MA(kf.pose6, kcap * 6); MA(kf.seg, kcap * 6); MA(kf.arena, acap);
+  MA(kf.exID, kcap); MA(kf.plan, kcap * 4); MA(kf.sur, kcap); MA(kf.surDS, kcap); MA(kf.sortKeys, kcap);
+  MA(kf.meta, kKfMeta); MA(kf.robot, 8);
+  MA(m.cornerFromMap, fromCap); MA(m.surfFromMap, fromCap);
+#undef MA
+  m.fromMapCap = fromCap;
+  HIPCHK(hipMemsetAsync(kf.meta, 0, sizeof(int) * kKfMeta, x->stream));
+  HIPCHK(hipMemsetAsync(kf.robot, 0, sizeof(float) * 8, x->stream));
+  kf.kcap = kcap;
+  kf.acap = acap;
+  return LEGO_OK;
+}
+
 int lego_mo_set_map(lego_ctx* x, const lego_point_xyzi* corner, int32_t n_corner,
                     const lego_point_xyzi* surf, int32_t n_surf) {
   if (!x) return LEGO_E_ARG;
@@ -718,14 +746,13 @@ int lego_mo_set_map(lego_ctx* x, const lego_point_xyzi* corner, int32_t n_corner
 int lego_mo_process(lego_ctx* x, const lego_fa_out* in, lego_mo_out* out) {
   if (!x || !in || !out) return LEGO_E_ARG;
   std::memset(out, 0, sizeof(*out));
-  if (!x->moFixed) {
-    set_err("scan-to-map needs a map: install one with lego_mo_set_map (keyframe-built maps are not in "
-            "this build)");
-    return LEGO_E_STATE;
-  }
   // run() gates (mapOptmization.cpp:1487-1499): a new hand-off, then the interval
   if (!in->publish_to_mapping || !in->odom_valid) return LEGO_OK;
   if (!(in->stamp - x->moTimeLast >= x->cfg.mapping_process_interval)) return LEGO_OK;
+  if (!x->moFixed) {
+    const int st = mo_alloc_keyframes(x);
+    if (st != LEGO_OK) return st;
+  }
   x->moTimeLast = in->stamp;
   MoDev& m = x->mo;
   const int N = x->dc.N, P = x->dc.P;
@@ -749,7 +776,12 @@ int lego_mo_process(lego_ctx* x, const lego_fa_out* in, lego_mo_out* out) {
   a.nCorner = in->n_corner_last;
   a.nSurf = in->n_surf_last;
   a.nOutlier = in->n_outlier_last;
-  if (mo_step_device(m, a, s) != 0) {
+  const int rs = mo_step_device(m, a, x->moFixed, x->cfg.surrounding_keyframe_search_radius, s);
+  if (rs == -2) {
+    set_err("scan-to-map: keyframe store full");
+    return LEGO_E_CAPACITY;
+  }
+  if (rs != 0) {
     set_err("scan-to-map launch failed");
     return LEGO_E_DEVICE;
   }

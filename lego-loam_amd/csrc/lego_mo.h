@@ -48,6 +48,26 @@ struct MoIndex {
   int T, cap;
 };
 
+// Keyframe store (saveKeyFramesAndFactor :1353-1454 without iSAM2: the chain
+// estimate equals the initial values when there are no loop factors) and the
+// surrounding-map bookkeeping of extractSurroundingKeyFrames (:1001-1065).
+struct MoKeyframes {
+  float4* pos3;      // [kcap] x, y, z, intensity = key index (cloudKeyPoses3D)
+  float* pose6;      // [kcap * 6] x, y, z, roll, pitch, yaw (cloudKeyPoses6D)
+  int* seg;          // [kcap * 6] arena offset / count of corner, surf, outlier DS clouds
+  float4* arena;     // [acap] keyframe clouds
+  int* exID;         // [kcap] surroundingExistingKeyPosesID
+  int* plan;         // [kcap * 4] per existing key: key, corner offset, surf offset, -
+  float4* sur;       // [kcap] surrounding key poses (radius hits, distance order)
+  float4* surDS;     // [kcap] their 1 m voxel filter
+  unsigned long long* sortKeys;  // [kcap] (distance bits, index) of the hits
+  int* meta;         // [kKfMeta] K, arenaTop, nEx, nSur, nSurDS, nCornerFromMap, nSurfFromMap, overflow, saved
+  float* robot;      // previousRobotPos xyz, currentRobotPos xyz
+  int kcap, acap;
+};
+enum { KF_K = 0, KF_TOP = 1, KF_NEX = 2, KF_NSUR = 3, KF_NSURDS = 4, KF_NCM = 5, KF_NSM = 6, KF_OVF = 7,
+       kKfMeta = 16 };
+
 struct MoDev {
   MoState* st;
   MoCounts* cnt;
@@ -62,6 +82,10 @@ struct MoDev {
   int scanCap;
   float* rows;  // [rowCap x 8]
   int rowCap;
+  // keyframe-built map (when no fixed map is installed)
+  MoKeyframes kf;
+  float4 *cornerFromMap, *surfFromMap;  // [fromMapCap]
+  int fromMapCap;
 };
 
 struct MoStepArgs {
@@ -74,6 +98,8 @@ size_t voxel_scratch_tmp_bytes(int cap);
 int voxel_grid_device(const float4* in, int n, const int* nDev, float leaf, float4* out, int* nOut,
                       const VgScratch& v, hipStream_t s);
 int mo_set_map_device(MoDev& m, int nCornerMap, int nSurfMap, hipStream_t s);
-int mo_step_device(const MoDev& m, const MoStepArgs& a, hipStream_t s);
+// One mapping step.  fixedMap: the installed map; otherwise the keyframe map.
+// Returns 0, -1 on a launch failure, -2 when the keyframe store is full.
+int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, hipStream_t s);
 
 }  // namespace lego

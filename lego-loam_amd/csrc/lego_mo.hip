@@ -317,7 +317,7 @@ __device__ __forceinline__ void mo_update_trig(MoState* st) {  // updatePointAss
 }
 
 // laserOdometryHandler (:629-641) and transformAssociateToMap (:376-461)
-__global__ void k_mo_associate(MoState* st, MoCounts* cnt, double qx, double qy, double qz, double qw, double px,
+__global__ void k_mo_associate(MoState* st, double qx, double qy, double qz, double qw, double px,
                                double py, double pz) {
   if (threadIdx.x != 0) return;
   double roll, pitch, yaw;
@@ -397,8 +397,12 @@ __global__ void k_mo_associate(MoState* st, MoCounts* cnt, double qx, double qy,
   mo_update_trig(st);
   st->converged = 0;
   st->iterations = 0;
-  // scan2MapOptimization's guard (:1331)
-  st->optimized = (cnt->cornerMapDS > 10 && cnt->surfMapDS > 100) ? 1 : 0;
+  st->optimized = 0;
+}
+
+// scan2MapOptimization's guard (:1331), once the map is filtered
+__global__ void k_mo_guard(MoState* st, const MoCounts* cnt) {
+  if (threadIdx.x == 0) st->optimized = (cnt->cornerMapDS > 10 && cnt->surfMapDS > 100) ? 1 : 0;
 }
 
 // surfTotalLast = surfLastDS + outlierLastDS (:1084-1086)
@@ -646,10 +650,188 @@ __global__ void k_mo_finish(MoState* st) {  // transformUpdate :463-496 (no IMU)
   }
 }
 
-int mo_step_device(const MoDev& m, const MoStepArgs& a, hipStream_t s) {
-  k_mo_associate<<<1, 64, 0, s>>>(m.st, m.cnt, a.quat[0], a.quat[1], a.quat[2], a.quat[3], a.pos[0], a.pos[1],
-                                  a.pos[2]);
+// ---------------------------------------------------------------- keyframe map
+// extractSurroundingKeyFrames (:1001-1065), radius search part: key poses
+// within surroundingKeyframeSearchRadius of the last saved position, in
+// (distance, index) order (the kd-tree's sorted radius search; ties unpinned).
+constexpr int kKfSortCap = 8192;
+__global__ void __launch_bounds__(1024) k_kf_select(MoKeyframes kf, float radius) {
+  __shared__ unsigned long long keys[kKfSortCap];
+  __shared__ int nHit;
+  const int tid = threadIdx.x;
+  const int K = kf.meta[KF_K];
+  if (tid == 0) nHit = 0;
+  __syncthreads();
+  const float cx = kf.robot[3], cy = kf.robot[4], cz = kf.robot[5];
+  const double r = (double)radius;
+  for (int i = tid; i < K; i += blockDim.x) {
+    const float4 p = kf.pos3[i];
+    float d = 0.f, e;
+    e = cx - p.x; d += e * e;
+    e = cy - p.y; d += e * e;
+    e = cz - p.z; d += e * e;
+    if ((double)d <= r * r) {
+      const int j = atomicAdd(&nHit, 1);
+      if (j < kKfSortCap) keys[j] = ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)i;
+    }
+  }
+  __syncthreads();
+  const int n = min(nHit, kKfSortCap);
+  int np = 1;
+  while (np < n) np <<= 1;
+  for (int i = n + tid; i < np; i += blockDim.x) keys[i] = ~0ull;
+  __syncthreads();
+  for (int k = 2; k <= np; k <<= 1)  // bitonic sort, ascending (distance >= 0: bits order = value order)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < np; i += blockDim.x) {
+        const int l = i ^ j;
+        if (l > i) {
+          const unsigned long long a = keys[i], b = keys[l];
+          if (((i & k) == 0) == (a > b)) { keys[i] = b; keys[l] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  for (int i = tid; i < n; i += blockDim.x) kf.sur[i] = kf.pos3[(int)(keys[i] & 0xffffffffu)];
+  if (tid == 0) {
+    kf.meta[KF_NSUR] = n;
+    if (nHit > kKfSortCap) kf.meta[KF_OVF] = 1;
+  }
+}
+
+// The existing-key bookkeeping (erase the keys no longer around, append the
+// new ones in filtered order) and the concatenation plan: per existing key its
+// corner offset and its surf + outlier offset in the map clouds.
+__global__ void k_kf_plan(MoKeyframes kf) {
+  if (threadIdx.x != 0) return;
+  const int nSurDS = kf.meta[KF_NSURDS];
+  int nEx = kf.meta[KF_NEX], w = 0;
+  for (int i = 0; i < nEx; ++i) {
+    const int id = kf.exID[i];
+    bool exist = false;
+    for (int j = 0; j < nSurDS && !exist; ++j) exist = (int)kf.surDS[j].w == id;
+    if (exist) kf.exID[w++] = id;
+  }
+  nEx = w;
+  for (int j = 0; j < nSurDS; ++j) {
+    const int key = (int)kf.surDS[j].w;
+    bool exist = false;
+    for (int i = 0; i < nEx && !exist; ++i) exist = kf.exID[i] == key;
+    if (!exist && nEx < kf.kcap) kf.exID[nEx++] = key;
+  }
+  int oc = 0, os = 0;
+  for (int i = 0; i < nEx; ++i) {
+    const int key = kf.exID[i];
+    kf.plan[4 * i + 0] = key;
+    kf.plan[4 * i + 1] = oc;
+    kf.plan[4 * i + 2] = os;
+    oc += kf.seg[6 * key + 1];
+    os += kf.seg[6 * key + 3] + kf.seg[6 * key + 5];
+  }
+  kf.meta[KF_NEX] = nEx;
+  kf.meta[KF_NCM] = oc;
+  kf.meta[KF_NSM] = os;
+}
+
+// transformPointCloud (:529-575) of every existing key's clouds into the map
+// clouds, one workgroup per key: corner, then surf followed by outlier.
+__global__ void k_kf_gather(MoKeyframes kf, float4* cornerFromMap, float4* surfFromMap) {
+  const int i = blockIdx.x;
+  const int key = kf.plan[4 * i + 0], oc = kf.plan[4 * i + 1], os = kf.plan[4 * i + 2];
+  const float* pose = kf.pose6 + 6 * key;
+  const float ctRoll = lego_cosf(pose[3]), stRoll = lego_sinf(pose[3]);
+  const float ctPitch = lego_cosf(pose[4]), stPitch = lego_sinf(pose[4]);
+  const float ctYaw = lego_cosf(pose[5]), stYaw = lego_sinf(pose[5]);
+  const float tx = pose[0], ty = pose[1], tz = pose[2];
+  auto tf = [&](float4 p) {
+    const float x1 = ctYaw * p.x - stYaw * p.y;
+    const float y1 = stYaw * p.x + ctYaw * p.y;
+    const float z1 = p.z;
+    const float x2 = x1;
+    const float y2 = ctRoll * y1 - stRoll * z1;
+    const float z2 = stRoll * y1 + ctRoll * z1;
+    return make_float4(ctPitch * x2 + stPitch * z2 + tx, y2 + ty, -stPitch * x2 + ctPitch * z2 + tz, p.w);
+  };
+  const int* sg = kf.seg + 6 * key;
+  for (int j = threadIdx.x; j < sg[1]; j += blockDim.x) cornerFromMap[oc + j] = tf(kf.arena[sg[0] + j]);
+  for (int j = threadIdx.x; j < sg[3]; j += blockDim.x) surfFromMap[os + j] = tf(kf.arena[sg[2] + j]);
+  for (int j = threadIdx.x; j < sg[5]; j += blockDim.x) surfFromMap[os + sg[3] + j] = tf(kf.arena[sg[4] + j]);
+}
+
+// saveKeyFramesAndFactor (:1353-1454) with iSAM2's chain estimate: keyframe
+// decision, pose append, arena slots for this step's filtered clouds.
+__global__ void k_kf_save(MoKeyframes kf, MoState* st, const MoCounts* cnt) {
+  if (threadIdx.x != 0) return;
+  float* prev = kf.robot;
+  float* cur = kf.robot + 3;
+  const float* aft = st->transformAftMapped;
+  cur[0] = aft[3]; cur[1] = aft[4]; cur[2] = aft[5];
+  const float dx = prev[0] - cur[0], dy = prev[1] - cur[1], dz = prev[2] - cur[2];
+  const bool save = !(__builtin_sqrtf(dx * dx + dy * dy + dz * dz) < 0.3f);
+  const int K = kf.meta[KF_K];
+  kf.meta[KF_OVF + 1] = 0;  // no copy unless saved
+  if (!save && K > 0) return;
+  const int top = kf.meta[KF_TOP];
+  const int nc = cnt->cornerDS, ns = cnt->surfDS, no = cnt->outlierDS;
+  if (K >= kf.kcap || top + nc + ns + no > kf.acap) {
+    kf.meta[KF_OVF] = 1;
+    return;
+  }
+  prev[0] = cur[0]; prev[1] = cur[1]; prev[2] = cur[2];
+  const float* est = K == 0 ? st->transformTobeMapped : aft;
+  float e[6];
+  for (int i = 0; i < 6; ++i) e[i] = est[i];
+  kf.pos3[K] = make_float4(e[3], e[4], e[5], (float)K);
+  float* p6 = kf.pose6 + 6 * K;
+  p6[0] = e[3]; p6[1] = e[4]; p6[2] = e[5]; p6[3] = e[0]; p6[4] = e[1]; p6[5] = e[2];
+  if (K + 1 > 1)
+    for (int i = 0; i < 6; ++i) st->transformTobeMapped[i] = aft[i];
+  int* sg = kf.seg + 6 * K;
+  sg[0] = top; sg[1] = nc; sg[2] = top + nc; sg[3] = ns; sg[4] = top + nc + ns; sg[5] = no;
+  kf.meta[KF_TOP] = top + nc + ns + no;
+  kf.meta[KF_K] = K + 1;
+  kf.meta[KF_OVF + 1] = 1;
+}
+__global__ void k_kf_copy(MoKeyframes kf, const float4* cornerDS, const float4* surfDS, const float4* outlierDS) {
+  if (!kf.meta[KF_OVF + 1]) return;
+  const int* sg = kf.seg + 6 * (kf.meta[KF_K] - 1);
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < sg[1] + sg[3] + sg[5]; j += gridDim.x * blockDim.x) {
+    float4 p;
+    if (j < sg[1]) p = cornerDS[j];
+    else if (j < sg[1] + sg[3]) p = surfDS[j - sg[1]];
+    else p = outlierDS[j - sg[1] - sg[3]];
+    kf.arena[sg[0] + j] = p;
+  }
+}
+
+// The surrounding map of the keyframe store, filtered and indexed.
+static int kf_map(MoDev& m, float radius, hipStream_t s) {
+  MoKeyframes& kf = m.kf;
+  k_kf_select<<<1, 1024, 0, s>>>(kf, radius);
+  if (voxel_grid_device(kf.sur, kf.kcap, &kf.meta[KF_NSUR], 1.0f, kf.surDS, &kf.meta[KF_NSURDS], m.vg, s))
+    return -1;
+  k_kf_plan<<<1, 64, 0, s>>>(kf);
+  int meta[kKfMeta];
+  if (hipMemcpyAsync(meta, kf.meta, sizeof(meta), hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
+  if (hipStreamSynchronize(s) != hipSuccess) return -1;
+  if (meta[KF_OVF] || meta[KF_NCM] > m.fromMapCap || meta[KF_NSM] > m.fromMapCap) return -2;
+  if (meta[KF_NEX] > 0) k_kf_gather<<<meta[KF_NEX], 256, 0, s>>>(kf, m.cornerFromMap, m.surfFromMap);
+  if (voxel_grid_device(m.cornerFromMap, meta[KF_NCM], nullptr, 0.2f, m.cornerMapDS, &m.cnt->cornerMapDS, m.vg, s))
+    return -1;
+  if (voxel_grid_device(m.surfFromMap, meta[KF_NSM], nullptr, 0.4f, m.surfMapDS, &m.cnt->surfMapDS, m.vg, s))
+    return -1;
+  if (index_build_device(m.cornerMapDS, meta[KF_NCM], &m.cnt->cornerMapDS, m.cornerIx, m.vg, s)) return -1;
+  if (index_build_device(m.surfMapDS, meta[KF_NSM], &m.cnt->surfMapDS, m.surfIx, m.vg, s)) return -1;
+  return 0;
+}
+
+int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, hipStream_t s) {
+  k_mo_associate<<<1, 64, 0, s>>>(m.st, a.quat[0], a.quat[1], a.quat[2], a.quat[3], a.pos[0], a.pos[1], a.pos[2]);
   if (hipGetLastError() != hipSuccess) return -1;
+  if (!fixedMap) {  // extractSurroundingKeyFrames :1001-1065
+    const int st = kf_map(m, radius, s);
+    if (st) return st;
+  }
   // downsampleCurrentScan :1067-1091
   if (voxel_grid_device(m.cornerLast, a.nCorner, nullptr, 0.2f, m.cornerDS, &m.cnt->cornerDS, m.vg, s)) return -1;
   if (voxel_grid_device(m.surfLast, a.nSurf, nullptr, 0.4f, m.surfDS, &m.cnt->surfDS, m.vg, s)) return -1;
@@ -658,6 +840,7 @@ int mo_step_device(const MoDev& m, const MoStepArgs& a, hipStream_t s) {
   if (voxel_grid_device(m.surfTotal, a.nSurf + a.nOutlier, &m.cnt->surfTotal, 0.4f, m.surfTotalDS,
                         &m.cnt->surfTotalDS, m.vg, s))
     return -1;
+  k_mo_guard<<<1, 64, 0, s>>>(m.st, m.cnt);
   // scan2MapOptimization :1329-1350 — the iterations exit on the device once converged
   const int qcap = a.nCorner + a.nSurf + a.nOutlier;
   if (qcap > m.rowCap) return -1;
@@ -668,6 +851,10 @@ int mo_step_device(const MoDev& m, const MoStepArgs& a, hipStream_t s) {
     k_mo_solve<<<1, kMoSolveThreads, 0, s>>>(m.st, m.cnt, m.rows, qcap, it);
   }
   k_mo_finish<<<1, 64, 0, s>>>(m.st);
+  if (!fixedMap) {  // saveKeyFramesAndFactor :1353-1454
+    k_kf_save<<<1, 64, 0, s>>>(m.kf, m.st, m.cnt);
+    k_kf_copy<<<grid_for(qcap), 256, 0, s>>>(m.kf, m.cornerDS, m.surfDS, m.outlierDS);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -208,11 +208,46 @@ def test_scan_to_map_parity(L, sensor, seed, nscans, n_surf, n_corner):
     gpu.close()
 
 
-def test_scan_to_map_needs_a_map(L):
+def test_scan_to_map_gates(L):
+    """run()'s gates (mapOptmization.cpp:1487-1499): nothing is processed
+    before the first odometry hand-off (the initialisation scan)."""
     gpu = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=40000)
     sc = L.synth_cfg("VLP-16", 0)
     gpu.ip(*L.synth_scan(sc, 0))
-    gpu.fa()
-    with pytest.raises(RuntimeError, match="status 5"):
-        gpu.mo()
+    fa = gpu.fa()
+    assert fa["odom_valid"] == 0
+    assert gpu.mo()["processed"] == 0
+    gpu.close()
+
+
+def test_scan_to_map_keyframe_parity(L):
+    """The reference's default mapping mode: the surrounding map is built from
+    the saved keyframes (radius search, 1 m key-pose filter, existing-key
+    bookkeeping, transformed clouds, map voxel filter).  Same decisions, sizes
+    bit-exact, poses within 1e-4 over a 40-scan stream."""
+    sc = L.synth_cfg("VLP-16", 6)
+    ora = L.Oracle(L.sensor_cfg("VLP-16"))
+    gpu = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=40000)
+    steps = optimized = 0
+    worst = 0.0
+    for k in range(40):
+        pts, stamp = L.synth_scan(sc, k)
+        ora.ip(pts, stamp)
+        ora.fa()
+        o = ora.mo()
+        gpu.ip(pts, stamp)
+        gpu.fa()
+        g = gpu.mo()
+        assert g["processed"] == o["processed"], k
+        if not o["processed"]:
+            continue
+        steps += 1
+        for key in ("optimized", "n_corner_map_ds", "n_surf_map_ds", "n_corner_scan_ds", "n_surf_scan_ds"):
+            assert g[key] == o[key], (k, key, g[key], o[key])
+        optimized += int(o["optimized"])
+        d = np.max(np.abs(g["transform_aft_mapped"].astype(np.float64) - o["transform_aft_mapped"]))
+        worst = max(worst, float(d))
+        assert d <= POSE_TOL, (k, g["transform_aft_mapped"], o["transform_aft_mapped"])
+    print(f"keyframe scan-to-map: {steps} steps, {optimized} optimized, worst |dpose| = {worst:.3g}")
+    assert steps >= 5 and optimized >= 3
     gpu.close()
