@@ -74,11 +74,35 @@ def stream_fixture(L, sensor, seed, n, name):
                         seed=np.int64(seed))
 
 
+def mapping_fixture(L, sensor, seed, n, name, fixed_map):
+    """Scan-to-map after every scan of a stream: the keyframe-built map
+    (fixed_map None) or a fixed synthetic map (seed, radius, n_surf, n_corner)."""
+    sc = L.synth_cfg(sensor, seed)
+    ora = L.Oracle(L.sensor_cfg(sensor))
+    if fixed_map:
+        surf, corner = L.synth_map(*fixed_map)
+        ora.mo_set_map(corner, surf)
+    aft, info = [], []
+    for k in range(n):
+        pts, stamp = L.synth_scan(sc, k)
+        ora.ip(pts, stamp)
+        ora.fa()
+        o = ora.mo()
+        aft.append(o["transform_aft_mapped"])
+        info.append([o["processed"], o["optimized"], o["iterations"], o["n_rows_last"], o["n_corner_map_ds"],
+                     o["n_surf_map_ds"], o["n_corner_scan_ds"], o["n_surf_scan_ds"]])
+    np.savez_compressed(OUT / f"{name}.npz", transform_aft_mapped=np.array(aft, np.float32),
+                        info=np.array(info, np.int32), sensor=np.bytes_(sensor), seed=np.int64(seed),
+                        fixed_map=np.array(fixed_map or [], np.float64))
+
+
 def main():
     L = ffi()
     scan_fixture(L, "VLP-16", 0, 0, "vlp16_seed0_scan0", full=True)
     scan_fixture(L, "HDL-64E", 2, 0, "hdl64_seed2_scan0", full=False)
     stream_fixture(L, "VLP-16", 1, 20, "vlp16_seed1_stream20")
+    mapping_fixture(L, "VLP-16", 6, 24, "vlp16_seed6_keyframe_map24", None)
+    mapping_fixture(L, "VLP-16", 3, 10, "vlp16_seed3_fixed_map10", (3, 50.0, 200000, 40000))
     for p in sorted(OUT.glob("*.npz")):
         print(p.name, p.stat().st_size)
 

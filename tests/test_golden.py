@@ -103,3 +103,53 @@ def test_product_reproduces_stream_fixture(L):
         exact += int(np.array_equal(fa["transform_sum"].view(np.uint32), s["transform_sum"][k].view(np.uint32)))
     print(f"bit-exact poses: {exact}/{len(s['counts'])}")
     gpu.close()
+
+
+def _run_mapping(L, g, engine_factory, gpu):
+    sensor = g["sensor"].item().decode()
+    sc = L.synth_cfg(sensor, int(g["seed"]))
+    eng = engine_factory(sensor)
+    fm = g["fixed_map"]
+    if len(fm):
+        surf, corner = L.synth_map(int(fm[0]), float(fm[1]), int(fm[2]), int(fm[3]))
+        eng.mo_set_map(corner, surf)
+    out = []
+    for k in range(len(g["info"])):
+        pts, stamp = L.synth_scan(sc, k)
+        eng.ip(pts, stamp)
+        eng.fa()
+        out.append(eng.mo())
+    if gpu:
+        eng.close()
+    return out
+
+
+@pytest.mark.parametrize("name", ["vlp16_seed6_keyframe_map24", "vlp16_seed3_fixed_map10"])
+def test_oracle_reproduces_mapping_fixture(L, name):
+    g = load(name)
+    out = _run_mapping(L, g, lambda s: L.Oracle(L.sensor_cfg(s)), False)
+    for k, o in enumerate(out):
+        info = [o["processed"], o["optimized"], o["iterations"], o["n_rows_last"], o["n_corner_map_ds"],
+                o["n_surf_map_ds"], o["n_corner_scan_ds"], o["n_surf_scan_ds"]]
+        np.testing.assert_array_equal(info, g["info"][k], err_msg=str(k))
+        np.testing.assert_array_equal(o["transform_aft_mapped"].view(np.uint32),
+                                      g["transform_aft_mapped"][k].view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["vlp16_seed6_keyframe_map24", "vlp16_seed3_fixed_map10"])
+def test_product_reproduces_mapping_fixture(L, name):
+    """Decisions and filtered sizes exact, mapped pose within 1e-4 (north star);
+    the number of bit-exact poses is reported."""
+    g = load(name)
+    out = _run_mapping(L, g, lambda s: L.Lego(L.sensor_cfg(s, L.hip_lib()), max_points=40000), True)
+    exact = 0
+    for k, o in enumerate(out):
+        info = [o["processed"], o["optimized"], o["n_corner_map_ds"], o["n_surf_map_ds"], o["n_corner_scan_ds"],
+                o["n_surf_scan_ds"]]
+        np.testing.assert_array_equal(info, g["info"][k][[0, 1, 4, 5, 6, 7]], err_msg=str(k))
+        d = np.abs(o["transform_aft_mapped"].astype(np.float64) - g["transform_aft_mapped"][k])
+        assert d.max() <= 1e-4, (k, d)
+        exact += int(np.array_equal(o["transform_aft_mapped"].view(np.uint32),
+                                    g["transform_aft_mapped"][k].view(np.uint32)))
+    print(f"{name}: bit-exact mapped poses {exact}/{len(out)}")
