@@ -90,6 +90,60 @@ def cpu_baseline(L, sensor, seed, nscans, budget_s):
     return done / dt, done, passes
 
 
+def mapping_bench(L, steps: int, cpu: bool):
+    """Auxiliary (not the headline metric): config C5 scan-to-map — a VLS-128
+    scan against a fixed synthetic map of 1.0 M surf / 200 k corner points
+    (SURVEY.md §8d C5).  Each step is one mapOptimization::run on the same
+    hand-off with the stamp advanced past the 0.3 s gate, so the state (pose,
+    degeneracy) evolves as in a stream.  GPU: host wall clock around
+    lego_mo_process (includes the scan upload and the pose read-back)."""
+    sensor = "VLS-128"
+    sc = L.synth_cfg(sensor, 3)
+    surf, corner = L.synth_map(3, 50.0, 1_000_000, 200_000)
+    res = {"workload": "C5: VLS-128 scan vs fixed map 1.0M surf + 200k corner, <= 10 LM iterations per step",
+           "steps": steps}
+    gpu = L.Lego(L.sensor_cfg(sensor, L.hip_lib()), max_points=260000)
+    t0 = time.perf_counter()
+    gpu.mo_set_map(corner, surf)
+    res["map_install_ms"] = (time.perf_counter() - t0) * 1e3
+    k = 0
+    while True:  # scans until one is handed to mapping
+        pts, stamp = L.synth_scan(sc, k)
+        gpu.ip(pts, stamp)
+        fa = gpu.fa()
+        k += 1
+        if fa["publish_to_mapping"] and fa["odom_valid"]:
+            break
+    base = gpu._fa.stamp
+    g = gpu.mo()  # warm-up step
+    t0 = time.perf_counter()
+    for i in range(steps):
+        gpu._fa.stamp = base + 0.5 * (i + 1)
+        g = gpu.mo()
+    res["gpu_ms_per_step"] = (time.perf_counter() - t0) * 1e3 / steps
+    res["iterations_last"] = g["iterations"]
+    res["rows_last"] = g["n_rows_last"]
+    res["map_ds"] = [g["n_corner_map_ds"], g["n_surf_map_ds"]]
+    gpu.close()
+    if cpu:
+        ora = L.Oracle(L.sensor_cfg(sensor))
+        ora.mo_set_map(corner, surf)
+        for j in range(k):
+            pts, stamp = L.synth_scan(sc, j)
+            ora.ip(pts, stamp)
+            ora.fa()
+        base = ora._fa.stamp
+        ora.mo()
+        n = 2
+        t0 = time.perf_counter()
+        for i in range(n):
+            ora._fa.stamp = base + 0.5 * (i + 1)
+            ora.mo()
+        res["cpu_ms_per_step"] = (time.perf_counter() - t0) * 1e3 / n
+        res["cpu_sample"] = f"{n} steps of the oracle (1 thread; map filter + kd-tree build every step, as the reference)"
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -102,6 +156,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
     ap.add_argument("--odom-profile", action="store_true", help="in-kernel phase stamps (diagnostic)")
+    ap.add_argument("--mapping-steps", type=int, default=5, help="C5 scan-to-map steps (aux; 0 = skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -211,6 +266,9 @@ def main():
             for k, v in sorted(stage_acc.items(), key=lambda kv: -kv[1]):
                 print(f"  {k:14s} {v / args.steps:9.3f} ms/step  {100 * v / max(tot, 1e-9):5.1f}%",
                       file=sys.stderr)
+        aux = None
+        if args.mapping_steps > 0:
+            aux = {"scan_to_map_c5": mapping_bench(L, args.mapping_steps, not args.no_cpu)}
         line = {
             "metric": "scans/sec (projection+seg+feat+LM) VLP-16 16x1800",
             "value": value,
@@ -233,6 +291,7 @@ def main():
                          "kernel": "k_odom", "launch_ms": odom_ms},
             "cpu_baseline": cpu,
             "stages_ms_per_step": {k: v / args.steps for k, v in stage_acc.items()},
+            "aux": aux,
         }
         print(json.dumps(line))
     gpu.close()
