@@ -1238,6 +1238,7 @@ extern "C" int lego_oracle_mo_process(lego_oracle* o, const lego_fa_out* in, leg
   if (st != LEGO_OK) return st;
   std::memset(out, 0, sizeof(*out));
   out->processed = mo.processed;
+  if (!mo.processed) return LEGO_OK;  // nothing published this call (the product's ABI too)
   out->optimized = mo.processed && mo.optimized;
   out->iterations = mo.iterations;
   for (int i = 0; i < 6; ++i) {
