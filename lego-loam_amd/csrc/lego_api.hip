@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -292,6 +293,11 @@ int lego_create(const lego_sensor_cfg* cfg, int device, int32_t max_points, int3
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 1;
     if (hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device) != hipSuccess) coop = 0;
     ob.G = coop ? odom_workgroups((int)N, cus) : 1;
+    // diagnostic override (profiling / scaling studies); never above the default
+    if (const char* e = std::getenv("LEGO_ODOM_WORKGROUPS")) {
+      const int g = std::atoi(e);
+      if (g >= 1 && g < ob.G) ob.G = g;
+    }
     const size_t G = ob.G;
     for (int k = 0; k < 2; ++k) {
       A(ob.cornerLast[k], G * ob.capCorner);
