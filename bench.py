@@ -162,6 +162,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal knobs for the N > 1 path on a one-GPU box (never used by the
+    # driver): every rank on device 0, the pose gather over gloo on the host.
+    if os.environ.get("LEGO_BENCH_SHARE_GPU"):
+        local = 0
+    backend = os.environ.get("LEGO_BENCH_BACKEND", "nccl")  # nccl = RCCL on ROCm
     import torch
 
     dist = None
@@ -169,7 +174,7 @@ def main():
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(backend)
     dev = torch.device("cuda", local)
 
     L = load_ffi()
@@ -216,13 +221,13 @@ def main():
             stage_acc[k] = stage_acc.get(k, 0.0) + v
         alg_bytes += odom_alg_bytes(recs)
         if dist:  # hand-off of the step's pose records to the serial consumer on rank 0
-            gathered = ms.gather_pose_records(ms.recs_to_bytes(recs), dist, dev)
+            gathered = ms.gather_pose_records(ms.recs_to_bytes(recs), dist, dev if backend == "nccl" else None)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        t = torch.tensor([dt], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     total_scans = args.steps * B * world

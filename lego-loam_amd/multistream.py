@@ -28,7 +28,7 @@ def stream_seed(stream: int) -> int:
 
 def recs_to_bytes(recs) -> np.ndarray:
     """ctypes array of lego_pose_rec -> uint8[K*64] (no copy of semantics)."""
-    raw = np.frombuffer(bytes(recs), dtype=np.uint8)
+    raw = np.frombuffer(bytearray(bytes(recs)), dtype=np.uint8)
     assert raw.size == len(recs) * POSE_REC_BYTES
     return raw
 
