@@ -567,7 +567,7 @@ struct OdomLds {
   uint16_t *gEndS, *gOrdS, *gEndC, *gOrdC;  // fine grids
   int *sufS, *preS, *sufC, *preC;           // [kKeyTab] per-key first / last
   int *kfirst, *klast;                      // [kMaxRings] build scratch
-  double* red;       // [kOdomWaves * 10]
+  double* red;       // [2][kOdomWaves * 10] reduction partials (iteration parity)
   SolveWs* sw;
   int* wtot;         // [kOdomWaves]
   int* n;            // [16] flags
@@ -581,7 +581,7 @@ __host__ __device__ inline size_t odom_lds_bytes() {
   s += (size_t)kLdsQ * 16 + (size_t)(kLdsQ / 2) * 16;
   s += (size_t)(kLdsGridS + kLdsSurf + kLdsGridC + kLdsCorner) * 2;
   s += (size_t)4 * kKeyTab * 4 + (size_t)2 * kMaxRings * 4;
-  s += (size_t)kOdomWaves * 10 * 8 + 256 + (size_t)kOdomWaves * 4 + 16 * 4 + 128;
+  s += (size_t)2 * kOdomWaves * 10 * 8 + 256 + (size_t)kOdomWaves * 4 + 16 * 4 + 128;
   return s;
 }
 
@@ -594,7 +594,7 @@ __device__ __forceinline__ OdomLds odom_carve(unsigned char* base) {
   L.qsharp = (float4*)(base + o); o += (size_t)(kLdsQ / 2) * 16;
   L.cnt = (unsigned*)(base + o); o += (size_t)kLdsCnt * 4;
   L.qi = (int*)(base + o); o += (size_t)3 * kLdsQ * 4;
-  L.red = (double*)(base + o); o += (size_t)kOdomWaves * 10 * 8;
+  L.red = (double*)(base + o); o += (size_t)2 * kOdomWaves * 10 * 8;
   L.sw = (SolveWs*)(base + o); o += 256;
   L.gEndS = (uint16_t*)(base + o); o += (size_t)kLdsGridS * 2;
   L.gOrdS = (uint16_t*)(base + o); o += (size_t)kLdsSurf * 2;
@@ -678,11 +678,16 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
   return (rdlane_f64(v, 0) + rdlane_f64(v, 16)) + (rdlane_f64(v, 32) + rdlane_f64(v, 48));
 }
 
-// 9 doubles (AtA upper triangle 6 + AtB 3) + the row count over the block;
-// thread 0 gets the totals (waves summed in order).  Waves without queries
-// contribute zeros and skip the lane reduction.
-__device__ __forceinline__ void block_sum9(double v[9], int m, int nQ, const OdomLds& L, double out[9], int* mt) {
+// 9 doubles (AtA upper triangle 6 + AtB 3) + the row count over the block.
+// Every wave gets the totals (waves summed in order, identically in each), so
+// the solve that follows runs redundantly in every wave without a second
+// barrier.  The partials are double-buffered by iteration parity: a wave can
+// run at most one iteration ahead of the slowest reader.  Waves without
+// queries contribute zeros and skip the lane reduction.
+__device__ __forceinline__ void block_sum9(double v[9], int m, int nQ, int parity, const OdomLds& L, double out[9],
+                                           int* mt) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double* red = L.red + parity * kOdomWaves * 10;
   double r[10];
   if (wave * 64 < nQ) {
 #pragma unroll
@@ -694,18 +699,16 @@ __device__ __forceinline__ void block_sum9(double v[9], int m, int nQ, const Odo
   }
   if (lane == 0) {
 #pragma unroll
-    for (int k = 0; k < 10; ++k) L.red[wave * 10 + k] = r[k];
+    for (int k = 0; k < 10; ++k) red[wave * 10 + k] = r[k];
   }
   __syncthreads();
-  // lanes 0..9 of wave 0 each sum one quantity over the waves; thread 0 reads them out
-  if (wave == 0) {
-    double sum = 0;
-    if (lane < 10)
-      for (int w = 0; w < kOdomWaves; ++w) sum += L.red[w * 10 + lane];
+  // lanes 0..9 of every wave each sum one quantity over the waves
+  double sum = 0;
+  if (lane < 10)
+    for (int w = 0; w < kOdomWaves; ++w) sum += red[w * 10 + lane];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) out[k] = rdlane_f64(sum, k);
-    *mt = (int)rdlane_f64(sum, 9);
-  }
+  for (int k = 0; k < 9; ++k) out[k] = rdlane_f64(sum, k);
+  *mt = (int)rdlane_f64(sum, 9);
 }
 
 struct ScanFeat {
@@ -717,15 +720,14 @@ struct ScanFeat {
 
 // Shared tail of calculateTransformationSurf / Corner.  Thread 0 only, all in
 // registers (cv_eigen_sym3 is the index-resolved 3x3 Jacobi).
-__device__ __forceinline__ void solve_step(float (&AtA)[3][3], float (&AtB)[3], int iter, OdomState* st,
-                                           float (&X)[3]) {
+__device__ __forceinline__ void solve_step(float (&AtA)[3][3], float (&AtB)[3], int iter, float (&P)[3][3],
+                                           int& isDeg, float (&X)[3]) {
   float Aq[3][3];
 #pragma unroll
   for (int a = 0; a < 3; ++a)
 #pragma unroll
     for (int b = 0; b < 3; ++b) Aq[a][b] = AtA[a][b];
   cv_solve_qr<3, 3>(Aq, AtB, X);
-  float (&P)[3][3] = *reinterpret_cast<float(*)[3][3]>(st->matP);
   if (iter == 0) {
     float E[3], V[3][3], V2[3][3], Vi[3][3];
     cv_eigen_sym3(AtA, E, V);
@@ -745,11 +747,11 @@ __device__ __forceinline__ void solve_step(float (&AtA)[3][3], float (&AtB)[3], 
         stop = true;
       }
     }
-    st->isDegenerate = deg;
+    isDeg = deg;
     cv_inv3(V, Vi);
     cv_matmul<3>(Vi, V2, P);
   }
-  if (st->isDegenerate) {
+  if (isDeg) {
     float X2[3] = {X[0], X[1], X[2]};
     cv_matvec<3>(P, X2, X);
   }
@@ -816,13 +818,19 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
   const int nQ = surf ? F.nFlat : F.nSharp;
   const int jend = min(nQ, lastN);  // the reference bounds by the query count (:1062, :1173)
   const int g = tid & (kGL - 1), grp = tid / kGL;
+  // transformCur, matP and isDegenerate live in registers for the loop: every
+  // wave computes the same solve (st is written back once at the end)
+  float tc[6], Pm[3][3];
+  int isDeg = st->isDegenerate;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) tc[i] = st->transformCur[i];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) Pm[i / 3][i % 3] = st->matP[i];
   for (int it = 0; it < 25; it++) {
     S.start();
     S.count(surf ? P_ITERS_S : P_ITERS_C);
     const bool nnIter = it % 5 == 0;
     if (nnIter) S.count(P_NNR);
-    float tc[6];
-    for (int i = 0; i < 6; ++i) tc[i] = st->transformCur[i];
     const float srx = lego_sinf(tc[0]), crx = lego_cosf(tc[0]);
     const float sry = lego_sinf(tc[1]), cry = lego_cosf(tc[1]);
     const float srz = lego_sinf(tc[2]), crz = lego_cosf(tc[2]);
@@ -952,45 +960,48 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
     double tot[9];
     int M = 0;
     S.add(P_T_ROWS);
-    block_sum9(acc, mloc, nQ, L, tot, &M);
+    block_sum9(acc, mloc, nQ, it & 1, L, tot, &M);
     S.add(surf ? (nnIter ? P_SURF_NN : P_SURF) : (nnIter ? P_CORN_NN : P_CORN));
-    if (tid == 0) {
-      L.n[N_BREAK] = 0;
-      if (M >= 10) {
-        float AtA[3][3] = {{(float)tot[0], (float)tot[1], (float)tot[2]},
-                           {(float)tot[1], (float)tot[3], (float)tot[4]},
-                           {(float)tot[2], (float)tot[4], (float)tot[5]}};
-        float AtB[3] = {(float)tot[6], (float)tot[7], (float)tot[8]};
-        float X[3];
-        solve_step(AtA, AtB, it, st, X);
-        S.add(it == 0 ? P_T_SOLVE0 : P_T_SOLVE);
-        float* t = st->transformCur;
-        double dR, dT;
-        if (surf) {
-          t[0] += X[0]; t[2] += X[1]; t[4] += X[2];
-        } else {
-          t[1] += X[0]; t[3] += X[1]; t[5] += X[2];
-        }
-        for (int i = 0; i < 6; i++) if (__builtin_isnan(t[i])) t[i] = 0;
-        if (surf) {
-          const double r0 = r2d(X[0]), r1 = r2d(X[1]), t2 = (double)(X[2] * 100);
-          dR = (double)(float)__builtin_sqrt(r0 * r0 + r1 * r1);
-          dT = (double)(float)__builtin_sqrt(t2 * t2);
-        } else {
-          const double r0 = r2d(X[0]), t1 = (double)(X[1] * 100), t2 = (double)(X[2] * 100);
-          dR = (double)(float)__builtin_sqrt(r0 * r0);
-          dT = (double)(float)__builtin_sqrt(t1 * t1 + t2 * t2);
-        }
-        if (dR < 0.1 && dT < 0.1) L.n[N_BREAK] = 1;
+    bool brk = false;
+    if (M >= 10) {
+      float AtA[3][3] = {{(float)tot[0], (float)tot[1], (float)tot[2]},
+                         {(float)tot[1], (float)tot[3], (float)tot[4]},
+                         {(float)tot[2], (float)tot[4], (float)tot[5]}};
+      float AtB[3] = {(float)tot[6], (float)tot[7], (float)tot[8]};
+      float X[3];
+      solve_step(AtA, AtB, it, Pm, isDeg, X);
+      S.add(it == 0 ? P_T_SOLVE0 : P_T_SOLVE);
+      double dR, dT;
+      if (surf) {
+        tc[0] += X[0]; tc[2] += X[1]; tc[4] += X[2];
+      } else {
+        tc[1] += X[0]; tc[3] += X[1]; tc[5] += X[2];
       }
-      __threadfence_block();
+#pragma unroll
+      for (int i = 0; i < 6; i++) if (__builtin_isnan(tc[i])) tc[i] = 0;
+      if (surf) {
+        const double r0 = r2d(X[0]), r1 = r2d(X[1]), t2 = (double)(X[2] * 100);
+        dR = (double)(float)__builtin_sqrt(r0 * r0 + r1 * r1);
+        dT = (double)(float)__builtin_sqrt(t2 * t2);
+      } else {
+        const double r0 = r2d(X[0]), t1 = (double)(X[1] * 100), t2 = (double)(X[2] * 100);
+        dR = (double)(float)__builtin_sqrt(r0 * r0);
+        dT = (double)(float)__builtin_sqrt(t1 * t1 + t2 * t2);
+      }
+      brk = dR < 0.1 && dT < 0.1;
     }
-    __syncthreads();
     S.add(P_SOLVE);
-    // thread 0 rewrites the flag only after the next reduction's barrier, which
-    // every thread reaches after this read
-    if (L.n[N_BREAK]) break;
+    if (brk) break;
   }
+  // write the loop's state back once (all waves hold the same values)
+  if (tid == 0) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) st->transformCur[i] = tc[i];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) st->matP[i] = Pm[i / 3][i % 3];
+    st->isDegenerate = isDeg;
+  }
+  __syncthreads();
 }
 
 // This workgroup's private HBM buffers (the launch's workgroups never share them).
