@@ -266,6 +266,10 @@ def main():
             for i, nm in ((21, "rows (excl. reduce)"), (22, "solve_qr+eig it0"), (23, "solve_qr it>0"),
                           (24, "nn local work"), (25, "build surf"), (26, "build corner")):
                 print(f"  odom.{nm:20s} {prof[i] / 100.0 / nsc:9.2f} us/scan", file=sys.stderr)
+            nq0 = max(prof[30], 1)
+            for i, nm in ((27, "wave0 q: to_start"), (28, "wave0 q: nn i1"), (29, "wave0 q: scan-line")):
+                print(f"  odom.{nm:20s} {prof[i] / 100.0 / nq0:9.2f} us/query ({prof[30] / nsc:.1f} q/scan)",
+                      file=sys.stderr)
         if args.stages:
             tot = sum(stage_acc.values())
             for k, v in sorted(stage_acc.items(), key=lambda kv: -kv[1]):

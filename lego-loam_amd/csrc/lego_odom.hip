@@ -422,10 +422,12 @@ __device__ __forceinline__ int nn_i1(const NNView<Idx>& v, float4 q, float bound
   float bd = bound;
   int bi = INT_MAX;
   const int cx = cell_of(q.x), cy = cell_of(q.y), cz = cell_of(q.z);
-  if (g < 27) {
+  if (g < 54) {  // two lanes per cell, alternate points of the bucket
+    const int cc = g % 27, half = g / 27;
     int lo, hi;
-    bucket_range(v.gEnd, fine_bucket(cx + g % 3 - 1, cy + (g / 3) % 3 - 1, cz + g / 9 - 1, v.T), lo, hi);
-    for (int t = lo; t < hi; ++t) {
+    bucket_range(v.gEnd, fine_bucket(cx + cc % 3 - 1, cy + (cc / 3) % 3 - 1, cz + cc / 9 - 1, v.T), lo, hi);
+#pragma unroll 2
+    for (int t = lo + half; t < hi; t += 2) {
       const int j = (int)v.gOrd[t];
       lex_min(bd, bi, flann_d2(q, v.pts[j]), j);
     }
@@ -435,6 +437,7 @@ __device__ __forceinline__ int nn_i1(const NNView<Idx>& v, float4 q, float bound
     if (prof && g == 0) atomicAdd(&prof[P_NN_SHELL1], 1ull);
   } else {
     if (prof && g == 0) atomicAdd(&prof[P_NN_BRUTE], 1ull);
+#pragma unroll 4
     for (int j = g; j < v.n; j += kGL) lex_min(bd, bi, flann_d2(q, v.pts[j]), j);
     group_lex_min(bd, bi);
   }
@@ -477,7 +480,9 @@ __device__ __forceinline__ bool nn_lines(const NNView<Idx>& v, int ci, int jend,
     m2 = u2 ? d : m2; r2 = u2 ? rank : r2; i2 = u2 ? j : i2;
     m3 = u3 ? d : m3; r3 = u3 ? rank : r3; i3 = u3 ? j : i3;
   };
+#pragma unroll 2
   for (int j = ci + 1 + g; j < fwdEnd; j += kGL) visit(j, true);
+#pragma unroll 4
   for (int j = B + 1 + g; j < ci; j += kGL) visit(j, false);
   group_lex_min3(m2, r2, i2);
   if (surf) group_lex_min3(m3, r3, i3);
@@ -831,9 +836,19 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
     S.count(surf ? P_ITERS_S : P_ITERS_C);
     const bool nnIter = it % 5 == 0;
     if (nnIter) S.count(P_NNR);
-    const float srx = lego_sinf(tc[0]), crx = lego_cosf(tc[0]);
-    const float sry = lego_sinf(tc[1]), cry = lego_cosf(tc[1]);
-    const float srz = lego_sinf(tc[2]), crz = lego_cosf(tc[2]);
+    // sin / cos of the three angles: lanes 0-2 and 3-5 of each wave, then broadcast
+    float trig;
+    {
+      const int l = tid & 63;
+      const float a = tc[l % 3];
+      trig = l < 3 ? lego_sinf(a) : lego_cosf(a);
+    }
+    const float srx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(trig), 0));
+    const float sry = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(trig), 1));
+    const float srz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(trig), 2));
+    const float crx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(trig), 3));
+    const float cry = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(trig), 4));
+    const float crz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(trig), 5));
     const float tx = tc[3], ty = tc[4], tz = tc[5];
     double acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     int mloc = 0;
@@ -845,14 +860,22 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
       const int round = L.n[N_ROUND];
       unsigned long long* xg = ob.xg + (size_t)(round & 1) * 3 * ob.capQ;
       const unsigned long long tag = (unsigned long long)(round + 1) << 32;
+      const bool w0 = S.prof && tid == 0;
       for (int q = q0 + grp; q < q1; q += kNGrp) {
+        unsigned long long ta = w0 ? wall_clock64() : 0;
         const float4 sel = to_start(qp[q], tc);
+        unsigned long long tb = w0 ? wall_clock64() : 0;
         int i1 = stale ? nn_brute(snap, snapN, sel, c.nn_sq, g) : nn_i1(nn, sel, c.nn_sq, g, S.prof);
         if (i1 >= lastN) i1 = -1;  // an index past a stale snapshot's cloud
+        unsigned long long tcn = w0 ? wall_clock64() : 0;
         int i2 = -1, i3 = -1;
         if (i1 >= 0 && (stale || !nn_lines(nn, i1, jend, sel, surf, c.nn_sq, g, &i2, &i3))) {
           if (S.prof && g == 0) atomicAdd(&S.prof[P_SCANLINE], 1ull);
           scanline_group(last, jend, i1, sel, surf, c.nn_sq, g, &i2, &i3);
+        }
+        if (w0) {
+          const unsigned long long td = wall_clock64();
+          S.prof[27] += tb - ta; S.prof[28] += tcn - tb; S.prof[29] += td - tcn; S.prof[30] += 1;
         }
         if (g == 0) {
           qi[q] = i1; qi[qs + q] = i2; qi[2 * qs + q] = i3;
