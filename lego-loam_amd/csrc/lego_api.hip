@@ -307,7 +307,7 @@ int lego_create(const lego_sensor_cfg* cfg, int device, int32_t max_points, int3
     odom_index_caps(ob.capCorner, ob.capSurf, &gTC, &gTS);
     ob.gTC = gTC;
     ob.gTS = gTS;
-    ob.cntCap = std::max(gTC, gTS);
+    ob.cntCap = gTC + gTS;
     A(ob.nC.gEnd, G * gTC); A(ob.nC.gOrd, G * ob.capCorner);
     A(ob.nS.gEnd, G * gTS); A(ob.nS.gOrd, G * ob.capSurf);
     A(ob.cnt, G * ob.cntCap);

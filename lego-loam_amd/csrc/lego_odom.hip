@@ -44,7 +44,7 @@ constexpr int kLdsCorner = 2048;              // last corner cloud points
 constexpr int kLdsQ = 384;                    // queries (flat <= 24 N, sharp <= 12 N)
 constexpr int kLdsGridS = 2048, kLdsGridC = 1024;  // fine-grid buckets
 constexpr int kKeyTab = kMaxRings + 4;
-constexpr int kLdsCnt = kLdsGridS;
+constexpr int kLdsCnt = kLdsGridS + kLdsGridC;
 constexpr float kCell = 0.5f;
 
 // ---------------------------------------------------------------- transforms
@@ -200,6 +200,102 @@ __device__ __forceinline__ void plugin_imu_rotation(float bcx, float bcy, float 
   acz = lego_atan2f(srzcrx / lego_cosf(acx), crzcrx / lego_cosf(acx));
 }
 
+// integrateTransformation (:1697-1725) by one wave: the same expressions as
+// accumulate_rotation / plugin_imu_rotation above, with their independent
+// sines and cosines evaluated on separate lanes and broadcast by readlane, and
+// the two atan2f of each step on two lanes.  The IMU angles are zero here
+// (sin 0 = 0, cos 0 = 1 exactly, as lego_sinf / lego_cosf return).
+__device__ __forceinline__ float rl_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ float sel6(int m, float a0, float a1, float a2, float a3, float a4, float a5) {
+  return m == 0 ? a0 : m == 1 ? a1 : m == 2 ? a2 : m == 3 ? a3 : m == 4 ? a4 : a5;
+}
+__device__ __forceinline__ void integrate_wave(float* ts, const float* tc) {
+  const int lane = threadIdx.x & 63;
+  // accumulate_rotation(ts[0..2], -tc[0..2]): lanes 0-5 sin, 6-11 cos of {lx, ly, lz, cx, cy, cz}
+  float v = 0.f;
+  if (lane < 12) {
+    const float a = sel6(lane % 6, -tc[0], -tc[1], -tc[2], ts[0], ts[1], ts[2]);
+    v = lane < 6 ? lego_sinf(a) : lego_cosf(a);
+  }
+  const float slx = rl_f(v, 0), sly = rl_f(v, 1), slz = rl_f(v, 2), scx = rl_f(v, 3), scy = rl_f(v, 4), scz = rl_f(v, 5);
+  const float clx = rl_f(v, 6), cly = rl_f(v, 7), clz = rl_f(v, 8), ccx = rl_f(v, 9), ccy = rl_f(v, 10), ccz = rl_f(v, 11);
+  const float srx = clx * ccx * sly * scz - ccx * ccz * slx - clx * cly * scx;
+  const float ox = -lego_asinf(srx);
+  const float cox = lego_cosf(ox);
+  const float srycrx = slx * (ccy * scz - ccz * scx * scy) + clx * sly * (ccy * ccz + scx * scy * scz) +
+                       clx * cly * ccx * scy;
+  const float crycrx = clx * cly * ccx * ccy - clx * sly * (ccz * scy - ccy * scx * scz) -
+                       slx * (scy * scz + ccy * ccz * scx);
+  const float srzcrx = scx * (clz * sly - cly * slx * slz) + ccx * scz * (cly * clz + slx * sly * slz) +
+                       clx * ccx * ccz * slz;
+  const float crzcrx = clx * clz * ccx * ccz - ccx * scz * (cly * slz - clz * slx * sly) -
+                       scx * (sly * slz + cly * clz * slx);
+  const float at = lane == 0 ? lego_atan2f(srycrx / cox, crycrx / cox) : lego_atan2f(srzcrx / cox, crzcrx / cox);
+  const float rx = ox, ry = rl_f(at, 0), rz = rl_f(at, 1);
+  // sin / cos of the accumulated angles: the translation and plugin_imu_rotation's bc terms
+  float w = 0.f;
+  if (lane < 6) {
+    const float a = sel6(lane % 3, rx, ry, rz, rx, ry, rz);
+    w = lane < 3 ? lego_sinf(a) : lego_cosf(a);
+  }
+  const float sbcx = rl_f(w, 0), sbcy = rl_f(w, 1), sbcz = rl_f(w, 2);
+  const float cbcx = rl_f(w, 3), cbcy = rl_f(w, 4), cbcz = rl_f(w, 5);
+  const float x1 = cbcz * (tc[3] - 0.0f) - sbcz * (tc[4] - 0.0f);
+  const float y1 = sbcz * (tc[3] - 0.0f) + cbcz * (tc[4] - 0.0f);
+  const float z1 = tc[5] - 0.0f;
+  const float x2 = x1;
+  const float y2 = cbcx * y1 - sbcx * z1;
+  const float z2 = sbcx * y1 + cbcx * z1;
+  const float tx = ts[3] - (cbcy * x2 + sbcy * z2);
+  const float ty = ts[4] - y2;
+  const float tz = ts[5] - (-sbcy * x2 + cbcy * z2);
+  // plugin_imu_rotation(rx, ry, rz, 0, 0, 0, 0, 0, 0)
+  const float sblx = 0.f, cblx = 1.f, sbly = 0.f, cbly = 1.f, sblz = 0.f, cblz = 1.f;
+  const float salx = 0.f, calx = 1.f, saly = 0.f, caly = 1.f, salz = 0.f, calz = 1.f;
+  const float psrx = -sbcx * (salx * sblx + calx * caly * cblx * cbly + calx * cblx * saly * sbly) -
+                     cbcx * cbcz * (calx * saly * (cbly * sblz - cblz * sblx * sbly) -
+                                    calx * caly * (sbly * sblz + cbly * cblz * sblx) + cblx * cblz * salx) -
+                     cbcx * sbcz * (calx * caly * (cblz * sbly - cbly * sblx * sblz) -
+                                    calx * saly * (cbly * cblz + sblx * sbly * sblz) + cblx * salx * sblz);
+  const float acx = -lego_asinf(psrx);
+  const float cacx = lego_cosf(acx);
+  const float psrycrx = (cbcy * sbcz - cbcz * sbcx * sbcy) *
+                            (calx * saly * (cbly * sblz - cblz * sblx * sbly) -
+                             calx * caly * (sbly * sblz + cbly * cblz * sblx) + cblx * cblz * salx) -
+                        (cbcy * cbcz + sbcx * sbcy * sbcz) *
+                            (calx * caly * (cblz * sbly - cbly * sblx * sblz) -
+                             calx * saly * (cbly * cblz + sblx * sbly * sblz) + cblx * salx * sblz) +
+                        cbcx * sbcy * (salx * sblx + calx * caly * cblx * cbly + calx * cblx * saly * sbly);
+  const float pcrycrx = (cbcz * sbcy - cbcy * sbcx * sbcz) *
+                            (calx * caly * (cblz * sbly - cbly * sblx * sblz) -
+                             calx * saly * (cbly * cblz + sblx * sbly * sblz) + cblx * salx * sblz) -
+                        (sbcy * sbcz + cbcy * cbcz * sbcx) *
+                            (calx * saly * (cbly * sblz - cblz * sblx * sbly) -
+                             calx * caly * (sbly * sblz + cbly * cblz * sblx) + cblx * cblz * salx) +
+                        cbcx * cbcy * (salx * sblx + calx * caly * cblx * cbly + calx * cblx * saly * sbly);
+  const float psrzcrx = sbcx * (cblx * cbly * (calz * saly - caly * salx * salz) -
+                                cblx * sbly * (caly * calz + salx * saly * salz) + calx * salz * sblx) -
+                        cbcx * cbcz * ((caly * calz + salx * saly * salz) * (cbly * sblz - cblz * sblx * sbly) +
+                                       (calz * saly - caly * salx * salz) * (sbly * sblz + cbly * cblz * sblx) -
+                                       calx * cblx * cblz * salz) +
+                        cbcx * sbcz * ((caly * calz + salx * saly * salz) * (cbly * cblz + sblx * sbly * sblz) +
+                                       (calz * saly - caly * salx * salz) * (cblz * sbly - cbly * sblx * sblz) +
+                                       calx * cblx * salz * sblz);
+  const float pcrzcrx = sbcx * (cblx * sbly * (caly * salz - calz * salx * saly) -
+                                cblx * cbly * (saly * salz + caly * calz * salx) + calx * calz * sblx) +
+                        cbcx * cbcz * ((saly * salz + caly * calz * salx) * (sbly * sblz + cbly * cblz * sblx) +
+                                       (caly * salz - calz * salx * saly) * (cbly * sblz - cblz * sblx * sbly) +
+                                       calx * calz * cblx * cblz) -
+                        cbcx * sbcz * ((saly * salz + caly * calz * salx) * (cblz * sbly - cbly * sblx * sblz) +
+                                       (caly * salz - calz * salx * saly) * (cbly * cblz + sblx * sbly * sblz) -
+                                       calx * calz * cblx * sblz);
+  const float pt = lane == 0 ? lego_atan2f(psrycrx / cacx, pcrycrx / cacx) : lego_atan2f(psrzcrx / cacx, pcrzcrx / cacx);
+  const float acy = rl_f(pt, 0), acz = rl_f(pt, 1);
+  if (lane == 0) { ts[0] = acx; ts[1] = acy; ts[2] = acz; ts[3] = tx; ts[4] = ty; ts[5] = tz; }
+}
+
 // In-kernel phase stamps (diagnostic; enabled per launch).  Thread 0 adds
 // wall_clock64 deltas (100 MHz) into prof[k].
 enum { P_SURF_NN = 0, P_SURF = 1, P_CORN_NN = 2, P_CORN = 3, P_SOLVE = 4, P_INTEG = 5,
@@ -285,54 +381,71 @@ __device__ __forceinline__ void block_exscan(unsigned* a, int n, int* wtot) {
   __syncthreads();
 }
 
-// Builds the fine grid and the key tables over pts[0..n) (all threads).
+// Builds both clouds' fine grids and key tables in shared passes (all
+// threads; half the barriers of two builds): ptsS[0..nS) then ptsC[0..nC) as
+// one index range, surf buckets [0, TS) then corner buckets [TS, TS + TC) in
+// one counter array (>= TS + TC entries), kfirst / klast [2 * NK].
 template <class Idx>
-__device__ __forceinline__ void nn_build(const float4* pts, int n, int NK, const NNStore<Idx>& S, unsigned* cnt,
-                                         int* wtot, int* kfirst, int* klast) {
-  const int tid = threadIdx.x;
-  const int T = fine_T(n, S.Tcap);
-  for (int b = tid; b < T; b += kOdomThreads) cnt[b] = 0;
-  for (int k = tid; k < NK; k += kOdomThreads) { kfirst[k] = INT_MAX; klast[k] = -1; }
-  if (tid == 0) *S.irregular = 0;
+__device__ __forceinline__ void nn_build2(const float4* ptsS, int nS, const NNStore<Idx>& S, const float4* ptsC,
+                                          int nC, const NNStore<Idx>& Cs, int NK, unsigned* cnt, int* wtot,
+                                          int* kfirst, int* klast) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int TS = fine_T(nS, S.Tcap), TC = fine_T(nC, Cs.Tcap), n = nS + nC;
+  for (int b = tid; b < TS + TC; b += kOdomThreads) cnt[b] = 0;
+  for (int k = tid; k < 2 * NK; k += kOdomThreads) { kfirst[k] = INT_MAX; klast[k] = -1; }
+  if (tid == 0) { *S.irregular = 0; *Cs.irregular = 0; }
   __syncthreads();
-  const int lane = tid & 63;
   for (int i0 = tid - lane; i0 < n; i0 += kOdomThreads) {  // wave-uniform loop
     const int i = i0 + lane;
-    int k = -1;
+    int kk = -1;
     if (i < n) {
-      const float4 p = pts[i];
-      atomicAdd(&cnt[fine_bucket(cell_of(p.x), cell_of(p.y), cell_of(p.z), T)], 1u);
-      k = (int)p.w;
-      if (k < 0 || k >= NK) { *S.irregular = 1; k = -1; }
+      const bool corner = i >= nS;
+      const float4 p = corner ? ptsC[i - nS] : ptsS[i];
+      const int T = corner ? TC : TS;
+      atomicAdd(&cnt[(corner ? TS : 0) + fine_bucket(cell_of(p.x), cell_of(p.y), cell_of(p.z), T)], 1u);
+      const int k = (int)p.w;
+      if (k < 0 || k >= NK) *(corner ? Cs.irregular : S.irregular) = 1;
+      else kk = k + (corner ? NK : 0);
     }
-    // per-key first/last: one atomic per distinct key of the wave (keys come in runs)
-    unsigned long long todo = __ballot(k >= 0);
+    // per-key first/last: one atomic per distinct (cloud, key) of the wave
+    unsigned long long todo = __ballot(kk >= 0);
     while (todo) {
       const int leader = __ffsll((long long)todo) - 1;
-      const int kk = __builtin_amdgcn_readlane(k, leader);
-      const unsigned long long m = __ballot(k == kk);
+      const int key = __builtin_amdgcn_readlane(kk, leader);
+      const unsigned long long m = __ballot(kk == key);
       if (lane == leader) {
-        atomicMin(&kfirst[kk], i0 + leader);
-        atomicMax(&klast[kk], i0 + 63 - __clzll((long long)m));
+        const int base = key >= NK ? nS : 0;
+        atomicMin(&kfirst[key], i0 + leader - base);
+        atomicMax(&klast[key], i0 + 63 - __clzll((long long)m) - base);
       }
       todo &= ~m;
     }
   }
   __syncthreads();
-  if (tid == 0) {
-    int m = INT_MAX;
-    S.sufFirst[NK] = INT_MAX;
-    for (int k = NK - 1; k >= 0; --k) { m = min(m, kfirst[k]); S.sufFirst[k] = m; }
-    int M = -1;
-    for (int k = 0; k < NK; ++k) { M = max(M, klast[k]); S.preLast[k] = M; }
+  // suffix-min of first / prefix-max of last, one thread per (cloud, key)
+  for (int t = tid; t < 2 * NK; t += kOdomThreads) {
+    const int c0 = t >= NK ? NK : 0, k = t - c0;
+    int m = INT_MAX, M = -1;
+    for (int j = k; j < NK; ++j) m = min(m, kfirst[c0 + j]);
+    for (int j = 0; j <= k; ++j) M = max(M, klast[c0 + j]);
+    (c0 ? Cs : S).sufFirst[k] = m;
+    (c0 ? Cs : S).preLast[k] = M;
   }
-  block_exscan(cnt, T, wtot);
+  if (tid == 0) { S.sufFirst[NK] = INT_MAX; Cs.sufFirst[NK] = INT_MAX; }
+  block_exscan(cnt, TS + TC, wtot);  // corner starts come out offset by nS
   for (int i = tid; i < n; i += kOdomThreads) {
-    const float4 p = pts[i];
-    S.gOrd[atomicAdd(&cnt[fine_bucket(cell_of(p.x), cell_of(p.y), cell_of(p.z), T)], 1u)] = (Idx)i;
+    const bool corner = i >= nS;
+    const float4 p = corner ? ptsC[i - nS] : ptsS[i];
+    const int T = corner ? TC : TS;
+    const unsigned pos = atomicAdd(&cnt[(corner ? TS : 0) + fine_bucket(cell_of(p.x), cell_of(p.y), cell_of(p.z), T)], 1u);
+    if (corner) Cs.gOrd[pos - nS] = (Idx)(i - nS);
+    else S.gOrd[pos] = (Idx)i;
   }
   __syncthreads();
-  for (int b = tid; b < T; b += kOdomThreads) S.gEnd[b] = (Idx)cnt[b];
+  for (int b = tid; b < TS + TC; b += kOdomThreads) {
+    if (b < TS) S.gEnd[b] = (Idx)cnt[b];
+    else Cs.gEnd[b - TS] = (Idx)(cnt[b] - nS);
+  }
   __syncthreads();
 }
 
@@ -571,7 +684,7 @@ struct OdomLds {
   unsigned* cnt;     // [kLdsGridS] index-build counters
   uint16_t *gEndS, *gOrdS, *gEndC, *gOrdC;  // fine grids
   int *sufS, *preS, *sufC, *preC;           // [kKeyTab] per-key first / last
-  int *kfirst, *klast;                      // [kMaxRings] build scratch
+  int *kfirst, *klast;                      // [2 * kMaxRings] build scratch
   double* red;       // [2][kOdomWaves * 10] reduction partials (iteration parity)
   SolveWs* sw;
   int* wtot;         // [kOdomWaves]
@@ -585,7 +698,7 @@ __host__ __device__ inline size_t odom_lds_bytes() {
   s += (size_t)kLdsSurf * 16 + (size_t)kLdsCorner * 16 + (size_t)kLdsCnt * 4 + (size_t)3 * kLdsQ * 4;
   s += (size_t)kLdsQ * 16 + (size_t)(kLdsQ / 2) * 16;
   s += (size_t)(kLdsGridS + kLdsSurf + kLdsGridC + kLdsCorner) * 2;
-  s += (size_t)4 * kKeyTab * 4 + (size_t)2 * kMaxRings * 4;
+  s += (size_t)4 * kKeyTab * 4 + (size_t)4 * kMaxRings * 4;
   s += (size_t)2 * kOdomWaves * 10 * 8 + 256 + (size_t)kOdomWaves * 4 + 16 * 4 + 128;
   return s;
 }
@@ -609,8 +722,8 @@ __device__ __forceinline__ OdomLds odom_carve(unsigned char* base) {
   L.preS = (int*)(base + o); o += (size_t)kKeyTab * 4;
   L.sufC = (int*)(base + o); o += (size_t)kKeyTab * 4;
   L.preC = (int*)(base + o); o += (size_t)kKeyTab * 4;
-  L.kfirst = (int*)(base + o); o += (size_t)kMaxRings * 4;
-  L.klast = (int*)(base + o); o += (size_t)kMaxRings * 4;
+  L.kfirst = (int*)(base + o); o += (size_t)2 * kMaxRings * 4;
+  L.klast = (int*)(base + o); o += (size_t)2 * kMaxRings * 4;
   L.wtot = (int*)(base + o); o += (size_t)kOdomWaves * 4;
   L.n = (int*)(base + o); o += 16 * 4;
   L.st = (OdomState*)(base + o); o += 128;
@@ -642,21 +755,19 @@ __device__ __forceinline__ NNView<uint32_t> view_hbm(bool surf, const OdomLds& L
 // Rebuilds both clouds' indexes (all threads) over the current last clouds.
 __device__ __forceinline__ void build_indexes(const OdomLds& L, const OdomBufs& ob, const OdomState* st,
                                               const DevCfg& c, unsigned long long* prof = nullptr) {
+  const unsigned long long t0 = (prof && threadIdx.x == 0) ? wall_clock64() : 0;
   if (st->resident) {
-    unsigned long long t0 = (prof && threadIdx.x == 0) ? wall_clock64() : 0;
     NNStore<uint16_t> sS{L.gEndS, L.gOrdS, L.sufS, L.preS, &L.n[N_IRR_S], kLdsGridS};
-    nn_build<uint16_t>(L.lastS, st->surfLastNum, c.N, sS, L.cnt, L.wtot, L.kfirst, L.klast);
-    if (prof && threadIdx.x == 0) { const unsigned long long t1 = wall_clock64(); prof[P_B_SURF] += t1 - t0; t0 = t1; }
     NNStore<uint16_t> sC{L.gEndC, L.gOrdC, L.sufC, L.preC, &L.n[N_IRR_C], kLdsGridC};
-    nn_build<uint16_t>(L.lastC, st->cornerLastNum, c.N, sC, L.cnt, L.wtot, L.kfirst, L.klast);
-    if (prof && threadIdx.x == 0) prof[P_B_CORN] += wall_clock64() - t0;
+    nn_build2<uint16_t>(L.lastS, st->surfLastNum, sS, L.lastC, st->cornerLastNum, sC, c.N, L.cnt, L.wtot,
+                        L.kfirst, L.klast);
   } else {
     NNStore<uint32_t> sS{ob.nS.gEnd, ob.nS.gOrd, L.sufS, L.preS, &L.n[N_IRR_S], ob.gTS};
-    nn_build<uint32_t>(buf2(ob.surfLast, st->curBuf), st->surfLastNum, c.N, sS, ob.cnt, L.wtot, L.kfirst, L.klast);
     NNStore<uint32_t> sC{ob.nC.gEnd, ob.nC.gOrd, L.sufC, L.preC, &L.n[N_IRR_C], ob.gTC};
-    nn_build<uint32_t>(buf2(ob.cornerLast, st->curBuf), st->cornerLastNum, c.N, sC, ob.cnt, L.wtot, L.kfirst,
-                       L.klast);
+    nn_build2<uint32_t>(buf2(ob.surfLast, st->curBuf), st->surfLastNum, sS, buf2(ob.cornerLast, st->curBuf),
+                        st->cornerLastNum, sC, c.N, ob.cnt, L.wtot, L.kfirst, L.klast);
   }
+  if (prof && threadIdx.x == 0) prof[P_B_SURF] += wall_clock64() - t0;
 }
 
 // ---------------------------------------------------------------- reduction
@@ -1097,24 +1208,7 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
       }
       // integrateTransformation :1697-1725
       S.start();
-      if (tid == 0) {
-        float* ts = st->transformSum;
-        const float* tc = st->transformCur;
-        float rx, ry, rz;
-        accumulate_rotation(ts[0], ts[1], ts[2], -tc[0], -tc[1], -tc[2], rx, ry, rz);
-        const float x1 = lego_cosf(rz) * (tc[3] - 0.0f) - lego_sinf(rz) * (tc[4] - 0.0f);
-        const float y1 = lego_sinf(rz) * (tc[3] - 0.0f) + lego_cosf(rz) * (tc[4] - 0.0f);
-        const float z1 = tc[5] - 0.0f;
-        const float x2 = x1;
-        const float y2 = lego_cosf(rx) * y1 - lego_sinf(rx) * z1;
-        const float z2 = lego_sinf(rx) * y1 + lego_cosf(rx) * z1;
-        const float tx = ts[3] - (lego_cosf(ry) * x2 + lego_sinf(ry) * z2);
-        const float ty = ts[4] - y2;
-        const float tz = ts[5] - (-lego_sinf(ry) * x2 + lego_cosf(ry) * z2);
-        plugin_imu_rotation(rx, ry, rz, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, rx, ry, rz);
-        ts[0] = rx; ts[1] = ry; ts[2] = rz; ts[3] = tx; ts[4] = ty; ts[5] = tz;
-        __threadfence_block();
-      }
+      if (tid < 64) integrate_wave(st->transformSum, st->transformCur);
       __syncthreads();
       S.add(P_INTEG);
     }
