@@ -173,6 +173,16 @@ typedef struct lego_ctx lego_ctx;
  * max_points points and batches of up to max_batch scans. */
 int lego_create(const lego_sensor_cfg* cfg, int device, int32_t max_points,
                 int32_t max_batch, lego_ctx** out);
+/* A fleet: n_streams independent lidar streams in one context on one device,
+ * run together by lego_odom_batch (one launch per stage for all of them; the
+ * device's CUs split between the streams' odometry chains).  Batches are
+ * stream-major: nscans = n_streams x K, scans [s*K, s*K + K) are K consecutive
+ * scans of stream s, K <= scans_per_stream.  Each stream's results equal those
+ * of its own lego_create context.  The node-shaped calls (lego_fa_process,
+ * lego_mo_*) need a single-stream context (LEGO_E_ARG otherwise).
+ * No reference counterpart: the reference runs one stream per process. */
+int lego_fleet_create(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
+                      int32_t max_points, int32_t scans_per_stream, lego_ctx** out);
 int lego_destroy(lego_ctx* ctx);
 /* Resets the per-stream state (odometry, residues) to construction values. */
 int lego_reset(lego_ctx* ctx);
@@ -184,7 +194,9 @@ int lego_fa_process(lego_ctx* ctx, const lego_ip_out* in, lego_fa_out* out);
 /* Device-resident batch: scans k=0..nscans-1 are the points
  * pts[offsets[k] .. offsets[k+1]).  pts/offsets are device pointers when
  * on_device != 0, host pointers otherwise.  Runs ip + fa + odometry for every
- * scan in stream order and writes one record per scan to recs (host).
+ * scan in stream order and writes one record per scan to recs (host).  On a
+ * fleet context the batch is stream-major (lego_fleet_create) and nscans a
+ * multiple of n_streams (LEGO_E_ARG otherwise).
  * offsets[k+1] > offsets[k] (an empty scan is LEGO_E_ARG, nothing runs) and
  * every scan <= max_points (LEGO_E_CAPACITY).  A non-finite point anywhere in
  * the batch is LEGO_E_NOT_DENSE, detected on the device after the batch ran:

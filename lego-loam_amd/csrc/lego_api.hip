@@ -66,7 +66,8 @@ struct lego_ctx {
   lego_sensor_cfg cfg;
   DevCfg dc;
   int device = 0;
-  int maxPoints = 0, maxBatch = 0;
+  int maxPoints = 0, maxBatch = 0;  // maxBatch: scans per call over all streams
+  int nStreams = 1;                   // a fleet context carries nStreams independent streams
   hipStream_t stream = nullptr;
   BatchBufs bb{};
   OdomBufs ob{};
@@ -143,9 +144,12 @@ static int ctx_reset(lego_ctx* x) {
   OdomState st;
   std::memset(&st, 0, sizeof(st));
   st.frameCount = x->cfg.skip_frame_num;  // frameCount = skipFrameNum (:314)
-  HIPCHK(hipMemcpyAsync(x->ob.st, &st, sizeof(st), hipMemcpyHostToDevice, x->stream));
-  FaCarry cz{0, 0, 0, 0};  // fresh member arrays: phantom {0.0f, 0}, picked[0] = 0
-  HIPCHK(hipMemcpyAsync(x->d_carry, &cz, sizeof(cz), hipMemcpyHostToDevice, x->stream));
+  const std::vector<OdomState> sts(x->nStreams, st);
+  HIPCHK(hipMemcpyAsync(x->ob.st, sts.data(), sizeof(st) * x->nStreams, hipMemcpyHostToDevice, x->stream));
+  // fresh member arrays: phantom {0.0f, 0}, picked[0] = 0
+  const std::vector<FaCarry> cz(x->nStreams, FaCarry{0, 0, 0, 0});
+  HIPCHK(hipMemcpyAsync(x->d_carry, cz.data(), sizeof(FaCarry) * x->nStreams, hipMemcpyHostToDevice,
+                        x->stream));
   HIPCHK(hipStreamSynchronize(x->stream));
   x->lastIpDevice = false;
   x->lastB = 0;
@@ -210,9 +214,9 @@ int lego_sensor_preset(const char* name, lego_sensor_cfg* o) {
   return LEGO_OK;
 }
 
-int lego_create(const lego_sensor_cfg* cfg, int device, int32_t max_points, int32_t max_batch,
-                lego_ctx** out) {
-  if (!cfg || !out || max_points <= 0 || max_batch <= 0) return LEGO_E_ARG;
+static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams, int32_t max_points,
+                      int32_t max_batch, lego_ctx** out) {
+  if (!cfg || !out || max_points <= 0 || max_batch <= 0 || n_streams <= 0) return LEGO_E_ARG;
   DevCfg dc;
   if (make_devcfg(cfg, &dc) != LEGO_OK) {
     set_err("unsupported sensor configuration");
@@ -230,6 +234,7 @@ int lego_create(const lego_sensor_cfg* cfg, int device, int32_t max_points, int3
   x->device = device;
   x->maxPoints = max_points;
   x->maxBatch = max_batch;
+  x->nStreams = n_streams;
   auto fail = [&](int st) { delete x; return st; };
   if (hipSetDevice(device) != hipSuccess) return fail(LEGO_E_DEVICE);
   if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess) return fail(LEGO_E_DEVICE);
@@ -286,19 +291,23 @@ int lego_create(const lego_sensor_cfg* cfg, int device, int32_t max_points, int3
   ob.capLS = (int)(N * kLessSharpPerRing);
   ob.capCorner = ob.capLS;
   ob.capSurf = (int)P;
-  A(ob.st, 1);
+  const size_t S = n_streams;
+  ob.S = n_streams;
+  A(ob.st, S);
   {
     // workgroups of the odometry launch (cooperative: all resident at once)
     int cus = 0, coop = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 1;
     if (hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device) != hipSuccess) coop = 0;
     ob.G = coop ? odom_workgroups((int)N, cus) : 1;
+    // a fleet's streams share the device: S x G workgroups, all resident
+    if (n_streams > 1) ob.G = std::max(1, std::min(ob.G, cus / n_streams));
     // diagnostic override (profiling / scaling studies); never above the default
     if (const char* e = std::getenv("LEGO_ODOM_WORKGROUPS")) {
       const int g = std::atoi(e);
       if (g >= 1 && g < ob.G) ob.G = g;
     }
-    const size_t G = ob.G;
+    const size_t G = S * ob.G;  // private copies over all streams' workgroups
     for (int k = 0; k < 2; ++k) {
       A(ob.cornerLast[k], G * ob.capCorner);
       A(ob.surfLast[k], G * ob.capSurf);
@@ -313,8 +322,8 @@ int lego_create(const lego_sensor_cfg* cfg, int device, int32_t max_points, int3
     A(ob.cnt, G * ob.cntCap);
     ob.capQ = (int)(N * kFlatPerRing);
     A(ob.qi, G * 3 * ob.capQ);
-    // exchange block: 16-byte timeout word, then 2 x 3 x capQ granules
-    ob.xbytes = 16 + sizeof(unsigned long long) * 2 * 3 * (size_t)ob.capQ;
+    // exchange block: 16-byte timeout word, then per stream 2 x 3 x capQ granules
+    ob.xbytes = 16 + S * sizeof(unsigned long long) * 2 * 3 * (size_t)ob.capQ;
     unsigned char* xb = nullptr;
     A(xb, ob.xbytes);
     ob.xblock = xb;
@@ -327,7 +336,7 @@ int lego_create(const lego_sensor_cfg* cfg, int device, int32_t max_points, int3
   A(ob.pubOut, B);
   A(ob.cornerEnd, B * ob.capLS);
   A(ob.surfEnd, B * P);
-  A(x->d_carry, 1);
+  A(x->d_carry, S);
   A(x->d_prof, 32);
 #undef A
   bb.pts = x->d_pts;
@@ -343,6 +352,18 @@ int lego_create(const lego_sensor_cfg* cfg, int device, int32_t max_points, int3
   if (st != LEGO_OK) return fail(st);
   *out = x;
   return LEGO_OK;
+}
+
+int lego_create(const lego_sensor_cfg* cfg, int device, int32_t max_points, int32_t max_batch,
+                lego_ctx** out) {
+  return create_ctx(cfg, device, 1, max_points, max_batch, out);
+}
+
+int lego_fleet_create(const lego_sensor_cfg* cfg, int device, int32_t n_streams, int32_t max_points,
+                      int32_t scans_per_stream, lego_ctx** out) {
+  if (n_streams <= 0 || scans_per_stream <= 0 || (int64_t)n_streams * scans_per_stream > (1 << 24))
+    return LEGO_E_ARG;
+  return create_ctx(cfg, device, n_streams, max_points, n_streams * scans_per_stream, out);
 }
 
 int lego_destroy(lego_ctx* x) {
@@ -405,8 +426,8 @@ static int run_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* of
   x->tm.begin();
   launch_ip(bb, x->dc, B, want_labels, x->stream, &x->tm);
   if (with_fa) {
-    launch_fa(bb, x->dc, B, x->d_carry, x->stream, &x->tm);
-    if (launch_odom(bb, x->ob, x->dc, B, x->stream, &x->tm, x->profOn ? x->d_prof : nullptr) != 0) {
+    launch_fa(bb, x->dc, B, x->nStreams, x->d_carry, x->stream, &x->tm);
+    if (launch_odom(bb, x->ob, x->dc, B / x->nStreams, x->stream, &x->tm, x->profOn ? x->d_prof : nullptr) != 0) {
       set_err("odometry launch failed (%d workgroups)", x->ob.G);
       return LEGO_E_DEVICE;
     }
@@ -572,6 +593,10 @@ static int upload_ip(lego_ctx* x, const lego_ip_out* in) {
 
 int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
   if (!x || !in || !out) return LEGO_E_ARG;
+  if (x->nStreams != 1) {
+    set_err("lego_fa_process needs a single-stream context");
+    return LEGO_E_ARG;
+  }
   HIPCHK(hipSetDevice(x->device));
   const bool resident = x->lastIpDevice && in->segmented_cloud == x->h_seg.data() &&
                         in->n_segmented == x->lastIp.n_segmented;
@@ -581,7 +606,7 @@ int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
   }
   x->stamps.assign(1, in->info.stamp);
   x->tm.begin();
-  launch_fa(x->bb, x->dc, 1, x->d_carry, x->stream, &x->tm);
+  launch_fa(x->bb, x->dc, 1, 1, x->d_carry, x->stream, &x->tm);
   if (launch_odom(x->bb, x->ob, x->dc, 1, x->stream, &x->tm, x->profOn ? x->d_prof : nullptr) != 0) {
     set_err("odometry launch failed (%d workgroups)", x->ob.G);
     return LEGO_E_DEVICE;
@@ -606,6 +631,10 @@ int lego_odom_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* off
   if (nscans > x->maxBatch) {
     set_err("batch of %d scans > context capacity %d", nscans, x->maxBatch);
     return LEGO_E_CAPACITY;
+  }
+  if (nscans % x->nStreams) {
+    set_err("batch of %d scans is not %d streams x K scans", nscans, x->nStreams);
+    return LEGO_E_ARG;
   }
   x->stamps.assign(stamps ? stamps : nullptr, stamps ? stamps + nscans : nullptr);
   if (!stamps) x->stamps.assign(nscans, 0.0);
@@ -728,6 +757,10 @@ static int mo_alloc_keyframes(lego_ctx* x) {
 
 int lego_mo_set_map(lego_ctx* x, const lego_point_xyzi* corner, int32_t n_corner,
                     const lego_point_xyzi* surf, int32_t n_surf) {
+  if (x && x->nStreams != 1) {
+    set_err("mapping needs a single-stream context");
+    return LEGO_E_ARG;
+  }
   if (!x) return LEGO_E_ARG;
   HIPCHK(hipSetDevice(x->device));
   if (!corner && !surf) {
@@ -750,6 +783,10 @@ int lego_mo_set_map(lego_ctx* x, const lego_point_xyzi* corner, int32_t n_corner
 }
 
 int lego_mo_process(lego_ctx* x, const lego_fa_out* in, lego_mo_out* out) {
+  if (x && x->nStreams != 1) {
+    set_err("mapping needs a single-stream context");
+    return LEGO_E_ARG;
+  }
   if (!x || !in || !out) return LEGO_E_ARG;
   std::memset(out, 0, sizeof(*out));
   // run() gates (mapOptmization.cpp:1487-1499): a new hand-off, then the interval

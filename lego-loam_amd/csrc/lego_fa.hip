@@ -503,16 +503,18 @@ __global__ void __launch_bounds__(kExtractThreads) k_extract(BatchBufs bb, DevCf
   }
 }
 
-// Walks the batch in stream order; re-runs ring 0 wherever the real carry is
-// not S* (the first scan of a stream, or after a 0.0-curvature tie).
-__global__ void __launch_bounds__(kExtractThreads) k_fa_fixup(BatchBufs bb, DevCfg c, int B,
-                                                             FaCarry* carry) {
+// Walks each stream's scans in order (block s: scans [s*K, s*K + K), carry
+// d_carry[s]); re-runs ring 0 wherever the real carry is not S* (the first
+// scan of a stream, or after a 0.0-curvature tie).
+__global__ void __launch_bounds__(kExtractThreads) k_fa_fixup(BatchBufs bb, DevCfg c, int K,
+                                                             FaCarry* carries) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   const ExtractLds L = carve(lds_raw, c.H);
   __shared__ FaCarry cs;
+  FaCarry* carry = carries + blockIdx.x;
   if (threadIdx.x == 0) cs = *carry;
   __syncthreads();
-  for (int b = 0; b < B; ++b) {
+  for (int b = blockIdx.x * K; b < (int)(blockIdx.x + 1) * K; ++b) {
     const bool steady = cs.phantom_ind == 0 && cs.picked0 == 1;
     if (steady) {
       __syncthreads();
@@ -558,7 +560,7 @@ __global__ void k_fa_compact(BatchBufs bb, DevCfg c) {
   }
 }
 
-void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, FaCarry* d_carry, hipStream_t s,
+void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_carry, hipStream_t s,
                StageTimer* tm) {
   tm->mark("fa.deskew", s);
   (void)hipMemsetAsync(bb.firsthalf, 0x7f, sizeof(int) * B, s);
@@ -570,7 +572,7 @@ void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, FaCarry* d_carry, hi
   const size_t lds = extract_lds_bytes(c.H);
   k_extract<<<dim3(c.N, B), kExtractThreads, lds, s>>>(bb, c);
   tm->mark("fa.fixup", s);
-  k_fa_fixup<<<1, kExtractThreads, lds, s>>>(bb, c, B, d_carry);
+  k_fa_fixup<<<S, kExtractThreads, lds, s>>>(bb, c, B / S, d_carry);
   tm->mark("fa.compact", s);
   k_fa_compact<<<B, 256, 0, s>>>(bb, c);
 }

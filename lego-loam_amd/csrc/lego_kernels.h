@@ -85,11 +85,13 @@ struct OdomState {
   int resident;  // current last clouds (and indexes) are LDS-resident
 };
 
-// Device buffers of the odometry kernel.  Arrays marked [G x] hold one private
-// copy per workgroup of the launch (the workgroups redundantly run the same
-// serial chain and split only the NN searches); the kernel offsets them.
+// Device buffers of the odometry kernel for S independent streams (a fleet;
+// S = 1 for a plain context).  Arrays marked [G x] hold one private copy per
+// workgroup of the launch (the G workgroups of a stream redundantly run the
+// same serial chain and split only the NN searches); they and st are [S x]
+// over the streams.  The kernel offsets them.
 struct OdomBufs {
-  OdomState* st;
+  OdomState* st;          // [S]
   float4* cornerLast[2];  // [G x capCorner] double-buffered: current / stale snapshot
   float4* surfLast[2];    // [G x capSurf]
   NNIndexBufs nC, nS;     // [G x] HBM indexes (sensors too large for LDS)
@@ -97,8 +99,11 @@ struct OdomBufs {
   int* qi;                // [G x 3 * capQ] HBM correspondences
   int gTC, gTS, cntCap;
   int capCorner, capSurf, capQ;
-  int G;                  // workgroups per launch
-  // exchange (zeroed before each launch): timeout word, then 2 x 3 x capQ granules
+  int G;                  // workgroups per stream
+  int S;                  // streams
+  int wg;                 // set in the kernel: this workgroup's index within its stream
+  // exchange (zeroed before each launch): timeout word shared by the streams,
+  // then per stream 2 x 3 x capQ granules
   void* xblock;
   size_t xbytes;
   unsigned* xerr;
@@ -115,10 +120,12 @@ struct OdomBufs {
 
 void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hipStream_t s,
                StageTimer* tm);
-void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, FaCarry* d_carry, hipStream_t s,
+// B = S x K scans, stream-major (scans [s*K, s*K + K) are stream s's, in
+// order); d_carry[S].
+void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_carry, hipStream_t s,
                StageTimer* tm);
-// Returns 0 on a successful launch.
-int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int B, hipStream_t s,
+// K scans per stream over ob.S streams.  Returns 0 on a successful launch.
+int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int K, hipStream_t s,
                 StageTimer* tm, unsigned long long* prof);
 int odom_workgroups(int N, int cusAvailable);
 // HBM index sizes for clouds of up to capCorner / capSurf points.

@@ -966,10 +966,10 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
     if (nnIter) {
       // This workgroup's slice of the queries, one wave per query; the slices
       // of the other workgroups of the launch arrive through the exchange.
-      const int G = gridDim.x, per = (nQ + G - 1) / G;
-      const int q0 = min(nQ, (int)blockIdx.x * per), q1 = min(nQ, q0 + per);
+      const int G = ob.G, per = (nQ + G - 1) / G;
+      const int q0 = min(nQ, ob.wg * per), q1 = min(nQ, q0 + per);
       const int round = L.n[N_ROUND];
-      unsigned long long* xg = ob.xg + (size_t)(round & 1) * 3 * ob.capQ;
+      unsigned long long* xg = ob.xg + (size_t)(round & 1) * 3 * ob.capQ;  // this stream's (odom_private)
       const unsigned long long tag = (unsigned long long)(round + 1) << 32;
       const bool w0 = S.prof && tid == 0;
       for (int q = q0 + grp; q < q1; q += kNGrp) {
@@ -1138,9 +1138,15 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
   __syncthreads();
 }
 
-// This workgroup's private HBM buffers (the launch's workgroups never share them).
+// This workgroup's private HBM buffers (the launch's workgroups never share
+// them) and its stream's state and exchange granules.  Block i of the launch
+// is workgroup i % G of stream i / G.
 __device__ __forceinline__ OdomBufs odom_private(OdomBufs ob) {
-  const size_t w = blockIdx.x;
+  const int s = blockIdx.x / ob.G;
+  ob.wg = blockIdx.x - s * ob.G;
+  const size_t w = blockIdx.x;  // index into the [S x G x] arrays
+  ob.st += s;
+  ob.xg += (size_t)s * 2 * 3 * ob.capQ;
   ob.cornerLast[0] += w * ob.capCorner;
   ob.cornerLast[1] += w * ob.capCorner;
   ob.surfLast[0] += w * ob.capSurf;
@@ -1152,11 +1158,14 @@ __device__ __forceinline__ OdomBufs odom_private(OdomBufs ob) {
   return ob;
 }
 
-__global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs obShared, DevCfg c, int B,
+// K scans of each of the ob.S streams: block i runs stream i / G's scans
+// [s*K, s*K + K) of the batch.
+__global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs obShared, DevCfg c, int K,
                                                       unsigned long long* prof) {
   const OdomBufs ob = odom_private(obShared);
-  const bool lead = blockIdx.x == 0;  // writes the outputs and the state
-  if (!lead) prof = nullptr;
+  const int b0 = (int)(blockIdx.x / ob.G) * K;
+  const bool lead = ob.wg == 0;  // writes the stream's outputs and state
+  if (blockIdx.x != 0) prof = nullptr;
   Stamp S{prof, 0};
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   const OdomLds L = odom_carve(lds_raw);
@@ -1182,7 +1191,7 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
   }
   S.add(P_RESID);
   const ImuEnd im{1.f, 1.f, 1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 1.f, 0.f, 1.f, 0.f};
-  for (int b = 0; b < B; ++b) {
+  for (int b = b0; b < b0 + K; ++b) {
     ScanFeat F;
     const int* fc = bb.f_cnt + b * 4;
     F.sharp = bb.f_sharp + (size_t)b * c.N * kSharpPerRing; F.nSharp = fc[0];
@@ -1288,22 +1297,23 @@ int odom_workgroups(int N, int cusAvailable) {
   return g < cusAvailable ? g : cusAvailable;
 }
 
-int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int B, hipStream_t s, StageTimer* tm,
+int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int K, hipStream_t s, StageTimer* tm,
                 unsigned long long* prof) {
   tm->mark("odom.lm", s);
   // the exchange granules and the timeout word are zeroed before every launch
   if (hipMemsetAsync(ob.xblock, 0, ob.xbytes, s) != hipSuccess) return -1;
-  if (ob.G <= 1) {
-    k_odom<<<1, kOdomThreads, odom_lds_bytes(), s>>>(bb, ob, c, B, prof);
+  const int blocks = ob.S * ob.G;
+  if (ob.G <= 1) {  // no exchange: the streams' workgroups need not be co-resident
+    k_odom<<<blocks, kOdomThreads, odom_lds_bytes(), s>>>(bb, ob, c, K, prof);
     return hipGetLastError() == hipSuccess ? 0 : -1;
   }
   BatchBufs a0 = bb;
   OdomBufs a1 = ob;
   DevCfg a2 = c;
-  int a3 = B;
+  int a3 = K;
   unsigned long long* a4 = prof;
   void* args[] = {&a0, &a1, &a2, &a3, &a4};
-  return hipLaunchCooperativeKernel((const void*)k_odom, dim3(ob.G), dim3(kOdomThreads), args,
+  return hipLaunchCooperativeKernel((const void*)k_odom, dim3(blocks), dim3(kOdomThreads), args,
                                     (unsigned)odom_lds_bytes(), s) == hipSuccess ? 0 : -1;
 }
 

@@ -166,7 +166,7 @@ def oracle_lib() -> C.CDLL:
     return lib
 
 
-HIP_EXPORTS = ["lego_sensor_preset", "lego_create", "lego_destroy", "lego_reset",
+HIP_EXPORTS = ["lego_sensor_preset", "lego_create", "lego_fleet_create", "lego_destroy", "lego_reset",
                "lego_ip_process", "lego_fa_process", "lego_odom_batch", "lego_batch_fetch",
                "lego_mo_set_map", "lego_mo_process", "lego_last_error", "lego_stage_times",
                "lego_odom_profile"]
@@ -178,6 +178,8 @@ def hip_lib() -> C.CDLL:
     lib.lego_sensor_preset.argtypes = [C.c_char_p, C.POINTER(SensorCfg)]
     lib.lego_create.argtypes = [C.POINTER(SensorCfg), C.c_int, C.c_int32, C.c_int32,
                                 C.POINTER(C.c_void_p)]
+    lib.lego_fleet_create.argtypes = [C.POINTER(SensorCfg), C.c_int, C.c_int32, C.c_int32, C.c_int32,
+                                      C.POINTER(C.c_void_p)]
     lib.lego_destroy.argtypes = [C.c_void_p]
     lib.lego_reset.argtypes = [C.c_void_p]
     lib.lego_ip_process.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_double, C.c_uint32,
@@ -336,12 +338,18 @@ class Lego:
     """The product pipeline (HIP) behind the C-ABI, one stream per context."""
 
     def __init__(self, cfg: SensorCfg, device: int = 0, max_points: int = 300000,
-                 max_batch: int = 1):
+                 max_batch: int = 1, streams: int = 0):
+        """streams > 0: a fleet context (lego_fleet_create) of that many
+        streams, max_batch scans per stream; batches are stream-major."""
         self.lib = hip_lib()
         self.cfg = cfg
         self.h = C.c_void_p()
-        check(self.lib.lego_create(C.byref(cfg), device, max_points, max_batch, C.byref(self.h)),
-              "lego_create", self.lib)
+        if streams > 0:
+            check(self.lib.lego_fleet_create(C.byref(cfg), device, streams, max_points, max_batch,
+                                             C.byref(self.h)), "lego_fleet_create", self.lib)
+        else:
+            check(self.lib.lego_create(C.byref(cfg), device, max_points, max_batch, C.byref(self.h)),
+                  "lego_create", self.lib)
         self._ip = IpOut()
         self._fa = FaOut()
 

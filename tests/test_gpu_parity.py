@@ -251,3 +251,113 @@ def test_scan_to_map_keyframe_parity(L):
     print(f"keyframe scan-to-map: {steps} steps, {optimized} optimized, worst |dpose| = {worst:.3g}")
     assert steps >= 5 and optimized >= 3
     gpu.close()
+
+
+def test_concurrent_streams_identical(L):
+    """Contexts on one device driven concurrently (one host thread and HIP
+    stream each) give the same pose records, byte for byte, as one context at
+    a time — also with fewer odometry workgroups than the default (the
+    redundant per-workgroup solve makes the count invisible)."""
+    import os
+    import threading
+
+    cfg = L.sensor_cfg("VLP-16", L.hip_lib())
+    K = 10
+    streams = []
+    for seed in (4, 5, 6, 7):
+        sc = L.synth_cfg("VLP-16", seed)
+        scans = [L.synth_scan(sc, k) for k in range(K)]
+        pts = np.concatenate([s[0] for s in scans])
+        off = np.zeros(K + 1, np.int64)
+        off[1:] = np.cumsum([len(s[0]) for s in scans])
+        streams.append((pts, off, np.array([s[1] for s in scans])))
+
+    def run(ctx, st):
+        pts, off, stamps = st
+        h = K // 2  # two batches: the odometry state crosses a launch boundary
+        a = bytes(ctx.odom_batch(pts[:off[h]], off[:h + 1], stamps[:h]))
+        b = bytes(ctx.odom_batch(pts[off[h]:], off[h:] - off[h], stamps[h:]))
+        raw = a + b
+        return [raw[64 * k:64 * k + 60] for k in range(K)]  # every field but the pad word
+
+    ref = []
+    for st in streams:
+        g = L.Lego(cfg, max_points=40000, max_batch=K)
+        ref.append(run(g, st))
+        g.close()
+    ctxs = []
+    for wg in (None, "16", "4", "1"):
+        if wg:
+            os.environ["LEGO_ODOM_WORKGROUPS"] = wg
+        try:
+            ctxs.append(L.Lego(cfg, max_points=40000, max_batch=K))
+        finally:
+            os.environ.pop("LEGO_ODOM_WORKGROUPS", None)
+    got = [None] * len(ctxs)
+    errs = []
+
+    def worker(i):
+        try:
+            got[i] = run(ctxs[i], streams[i])
+        except Exception as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(len(ctxs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for c in ctxs:
+        c.close()
+    assert not errs, errs
+    for i in range(len(ctxs)):
+        assert got[i] == ref[i], i
+
+
+@pytest.mark.parametrize("workgroups", [None, "1"])
+def test_fleet_equals_single_streams(L, workgroups):
+    """A fleet context (lego_fleet_create: S streams, one launch per stage for
+    all of them) gives each stream the same pose records, byte for byte, as
+    the stream's own context, across two stream-major batches (the states
+    and the FA carries cross the launch boundary per stream)."""
+    import os
+
+    cfg = L.sensor_cfg("VLP-16", L.hip_lib())
+    K, S = 8, 3
+    streams = []
+    for seed in (4, 8, 9):
+        sc = L.synth_cfg("VLP-16", seed)
+        streams.append([L.synth_scan(sc, k) for k in range(K)])
+
+    def pack(scans):
+        pts = np.concatenate([p for p, _ in scans])
+        off = np.zeros(len(scans) + 1, np.int64)
+        off[1:] = np.cumsum([len(p) for p, _ in scans])
+        return pts, off, np.array([t for _, t in scans])
+
+    ref = []
+    for scans in streams:
+        g = L.Lego(cfg, max_points=40000, max_batch=K)
+        raw = bytes(g.odom_batch(*pack(scans[:K // 2]))) + bytes(g.odom_batch(*pack(scans[K // 2:])))
+        g.close()
+        ref.append([raw[64 * k:64 * k + 60] for k in range(K)])
+    if workgroups:
+        os.environ["LEGO_ODOM_WORKGROUPS"] = workgroups
+    try:
+        fl = L.Lego(cfg, max_points=40000, max_batch=K // 2, streams=S)
+    finally:
+        os.environ.pop("LEGO_ODOM_WORKGROUPS", None)
+    got = [[] for _ in range(S)]
+    for h in (slice(0, K // 2), slice(K // 2, K)):
+        batch = [sc for scans in streams for sc in scans[h]]  # stream-major
+        raw = bytes(fl.odom_batch(*pack(batch)))
+        for s in range(S):
+            for k in range(K // 2):
+                r = s * (K // 2) + k
+                got[s].append(raw[64 * r:64 * r + 60])
+    # a batch that is not S x K scans is refused
+    with pytest.raises(RuntimeError):
+        fl.odom_batch(*pack([streams[0][0], streams[1][0]]))
+    fl.close()
+    for s in range(S):
+        assert got[s] == ref[s], s
