@@ -90,6 +90,58 @@ def cpu_baseline(L, sensor, seed, nscans, budget_s):
     return done / dt, done, passes
 
 
+def cpu_all_cores(L, sensor, threads, nscans, budget_s):
+    """The oracle on `threads` host threads, thread t running its own stream
+    (seed 10 + t; the oracle releases the GIL inside its C++ calls), each
+    repeating its stream until ~budget_s.  SURVEY.md §8d's "all cores" line:
+    the CPU counterpart of several streams per host."""
+    import threading
+
+    cfg = L.sensor_cfg(sensor)
+    streams = [None] * threads
+    done = [0] * threads
+
+    def synth(t):
+        sc = L.synth_cfg(sensor, 10 + t)
+        streams[t] = [L.synth_scan(sc, k) for k in range(nscans)]
+
+    def work(t, t0):
+        while time.perf_counter() - t0 < budget_s:
+            ora = L.Oracle(cfg)
+            for pts, st in streams[t]:
+                ora.ip(pts, st)
+                ora.fa()
+                done[t] += 1
+
+    th = [threading.Thread(target=synth, args=(t,)) for t in range(threads)]
+    [x.start() for x in th]
+    [x.join() for x in th]
+    t0 = time.perf_counter()
+    th = [threading.Thread(target=work, args=(t, t0)) for t in range(threads)]
+    [x.start() for x in th]
+    [x.join() for x in th]
+    dt = time.perf_counter() - t0
+    return {"value": sum(done) / dt, "unit": "scans/s", "cores": threads, "kind": "port",
+            "sample": f"{sum(done)} scans: {threads} threads, each its own {nscans}-scan {sensor} stream "
+                      f"(seeds 10..{9 + threads}) through oracle ip+fa incl. LM, ~{budget_s:.0f} s"}
+
+
+def host_info():
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        share = len(os.sched_getaffinity(0))
+    except AttributeError:
+        share = os.cpu_count() or 1
+    return {"nproc": os.cpu_count(), "affinity": share, "cpu_model": model}
+
+
 def mapping_bench(L, steps: int, cpu: bool):
     """Auxiliary (not the headline metric): config C5 scan-to-map — a VLS-128
     scan against a fixed synthetic map of 1.0 M surf / 200 k corner points
@@ -144,6 +196,46 @@ def mapping_bench(L, steps: int, cpu: bool):
     return res
 
 
+def fleet_bench(L, streams: int, k: int, steps: int, device: int):
+    """Auxiliary (not the headline metric): `streams` independent VLP-16
+    streams in one fleet context (lego_fleet_create) on one GPU, k scans per
+    stream per call, the stream-major batch resident in HBM.  Whole-GPU
+    scans/s over `steps` calls (host wall clock, like the headline).  Four
+    distinct synthetic streams are reused round-robin."""
+    import torch
+
+    cfg = L.sensor_cfg("VLP-16", L.hip_lib())
+    nwin = steps + 1
+    src = []
+    for d in range(min(4, streams)):
+        sc = L.synth_cfg("VLP-16", 10 + d)
+        src.append([L.synth_scan(sc, j)[0] for j in range(k * nwin)])
+    maxn = max(len(p) for s in src for p in s)
+    wins = []
+    for w in range(nwin):
+        scans = [src[s % len(src)][w * k + j] for s in range(streams) for j in range(k)]
+        off = np.zeros(len(scans) + 1, np.int64)
+        off[1:] = np.cumsum([len(p) for p in scans])
+        st = np.concatenate([np.arange(w * k, (w + 1) * k) * 0.1] * streams)
+        wins.append((torch.from_numpy(np.concatenate(scans).view(np.uint8)).to(device),
+                     torch.from_numpy(off).to(device), st))
+    fl = L.Lego(cfg, device=device, max_points=maxn + 16, max_batch=k, streams=streams)
+    recs = (L.PoseRec * (streams * k))()
+    run = lambda w: fl.odom_batch_device(w[0].data_ptr(), w[1].data_ptr(), w[2], streams * k, recs)  # noqa: E731
+    run(wins[0])  # warm-up (initialises every stream)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        run(wins[1 + i])
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    fl.close()
+    return {"workload": f"fleet: {streams} independent VLP-16 streams x {k} scans per call on one GPU "
+                        "(lego_fleet_create), full per-scan pipeline incl. LM odometry",
+            "streams": streams, "scans_per_stream_per_call": k, "calls": steps,
+            "scans_per_s": streams * k * steps / dt, "ms_per_call": dt / steps * 1e3}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -157,6 +249,7 @@ def main():
     ap.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
     ap.add_argument("--odom-profile", action="store_true", help="in-kernel phase stamps (diagnostic)")
     ap.add_argument("--mapping-steps", type=int, default=5, help="C5 scan-to-map steps (aux; 0 = skip)")
+    ap.add_argument("--fleet-streams", type=int, default=64, help="streams of the fleet aux line (0 = skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -245,11 +338,15 @@ def main():
             except Exception:  # noqa: BLE001
                 traffic = None
         cpu = None
+        cpu_all = None
         if not args.no_cpu:
             v, n, passes = cpu_baseline(L, args.sensor, seed, args.stream_len, args.cpu_budget)
             cpu = {"value": v, "unit": "scans/s", "cores": 1, "kind": "port",
                    "sample": f"{n} scans ({passes} pass(es) over the {args.stream_len}-scan "
                              f"{args.sensor} stream, seed {seed}) through oracle ip+fa incl. LM, 1 thread"}
+            # the box's CPU share is 16 cores per GPU (the machine's nproc is larger)
+            thr = max(1, min(16, host_info()["affinity"]))
+            cpu_all = cpu_all_cores(L, args.sensor, thr, 60, args.cpu_budget)
         if args.odom_profile:
             prof = (C.c_uint64 * 32)()
             lib.lego_odom_profile(gpu.h, -1, prof)
@@ -275,9 +372,14 @@ def main():
             for k, v in sorted(stage_acc.items(), key=lambda kv: -kv[1]):
                 print(f"  {k:14s} {v / args.steps:9.3f} ms/step  {100 * v / max(tot, 1e-9):5.1f}%",
                       file=sys.stderr)
-        aux = None
+        aux = {}
         if args.mapping_steps > 0:
-            aux = {"scan_to_map_c5": mapping_bench(L, args.mapping_steps, not args.no_cpu)}
+            aux["scan_to_map_c5"] = mapping_bench(L, args.mapping_steps, not args.no_cpu)
+        if args.fleet_streams > 0 and world == 1:
+            aux["fleet_vlp16"] = fleet_bench(L, args.fleet_streams, 20, 3, local)
+        if cpu_all:
+            aux["cpu_all_cores"] = cpu_all
+        aux["host"] = host_info()
         line = {
             "metric": "scans/sec (projection+seg+feat+LM) VLP-16 16x1800",
             "value": value,
