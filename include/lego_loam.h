@@ -155,6 +155,16 @@ typedef struct lego_mo_out {
   int32_t n_rows_last;        /* laserCloudOri size at the last iteration */
 } lego_mo_out;
 
+/* /imu_raw message (sensor_msgs/Imu; utility.h:54): the fields the
+ * reference's imuHandlers read (featureAssociation.cpp:431-458,
+ * mapOptmization.cpp:643-652). */
+typedef struct lego_imu_msg {
+  double stamp;                  /* header.stamp.toSec() */
+  double orientation[4];         /* x, y, z, w */
+  double angular_velocity[3];    /* x, y, z */
+  double linear_acceleration[3]; /* x, y, z */
+} lego_imu_msg;
+
 /* One record per scan from the batch path (64 bytes, also the RCCL gather
  * unit of the multi-GPU bench). */
 typedef struct lego_pose_rec {
@@ -205,6 +215,21 @@ int lego_fa_process(lego_ctx* ctx, const lego_ip_out* in, lego_fa_out* out);
 int lego_odom_batch(lego_ctx* ctx, const lego_point_xyzir* pts,
                     const int64_t* offsets, const double* stamps,
                     int32_t nscans, int32_t on_device, lego_pose_rec* recs);
+/* /imu_raw: delivers messages to the featureAssociation and mapOptimization
+ * IMU queues in order (featureAssociation.cpp:431-458 imuHandler +
+ * AccumulateIMUShiftAndRotation :392-429; mapOptmization.cpp:643-652), as
+ * the ROS callbacks would between two scans.  Single-stream contexts. */
+int lego_imu_push(lego_ctx* ctx, const lego_imu_msg* msgs, int32_t n);
+/* lego_odom_batch with the IMU messages that arrive during the batch:
+ * imu[0 .. imu_before[k]) are delivered before scan k is processed
+ * (imu_before non-decreasing, <= n_imu), the rest after the last scan.
+ * Deskew (adjustDistortion :525-614), the initial guess (updateInitialGuess
+ * :1639-1664), integration and the hand-off then use the IMU terms once the
+ * stream has received a message.  Single-stream contexts. */
+int lego_odom_batch_imu(lego_ctx* ctx, const lego_point_xyzir* pts,
+                        const int64_t* offsets, const double* stamps,
+                        int32_t nscans, int32_t on_device, const lego_imu_msg* imu,
+                        int32_t n_imu, const int32_t* imu_before, lego_pose_rec* recs);
 /* After lego_odom_batch: fetch full per-scan outputs of scan k of that batch. */
 int lego_batch_fetch(lego_ctx* ctx, int32_t k, lego_ip_out* ip, lego_fa_out* fa);
 

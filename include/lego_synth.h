@@ -39,6 +39,12 @@ int32_t lego_synth_max_points(const lego_synth_cfg* cfg);
 int lego_synth_scan(const lego_synth_cfg* cfg, int32_t scan_index,
                     lego_point_xyzir* out, int32_t cap, int32_t* n_out,
                     double* stamp);
+/* /imu_raw messages of the same ego motion at rate_hz, stamps
+ * phase + i / rate_hz within [t0, t1): orientation (ego yaw plus a small
+ * roll / pitch sway), gyro and accelerometer (specific force incl. gravity)
+ * in the ROS body frame (x forward, y left, z up), with seeded noise. */
+int lego_synth_imu(const lego_synth_cfg* cfg, double t0, double t1, double rate_hz, double phase,
+                   lego_imu_msg* out, int32_t cap, int32_t* n_out);
 /* Config-5 surrounding map: planes (surf, ~0.4 m spacing) and vertical edges
  * (corner, ~0.2 m spacing) within `radius` of the origin, in the mapping
  * frame (camera convention: x left, y up, z forward as in

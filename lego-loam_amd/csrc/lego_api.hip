@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "lego_device.h"
+#include "lego_imu_host.h"
 #include "lego_kernels.h"
 #include "lego_mo.h"
 #include "lego_loam.h"
@@ -91,6 +92,12 @@ struct lego_ctx {
   std::vector<int8_t> h_gimg;
   lego_ip_out lastIp{};
   bool lastIpDevice = false;  // lastIp describes batch slot 0 on device
+  // /imu_raw: featureAssociation's and mapOptimization's queues (host), the
+  // per-scan snapshots of the former for a batch
+  FaImuQueue faImu;
+  MoImuQueue moImu;
+  std::vector<ImuSnap> h_imu;
+  ImuSnap* d_imu = nullptr;
   // scan-to-map (lego_mo_*): buffers allocated by the first lego_mo_set_map
   MoDev mo{};
   bool moAlloc = false, moFixed = false;
@@ -147,12 +154,14 @@ static int ctx_reset(lego_ctx* x) {
   const std::vector<OdomState> sts(x->nStreams, st);
   HIPCHK(hipMemcpyAsync(x->ob.st, sts.data(), sizeof(st) * x->nStreams, hipMemcpyHostToDevice, x->stream));
   // fresh member arrays: phantom {0.0f, 0}, picked[0] = 0
-  const std::vector<FaCarry> cz(x->nStreams, FaCarry{0, 0, 0, 0});
+  const std::vector<FaCarry> cz(x->nStreams, FaCarry{});
   HIPCHK(hipMemcpyAsync(x->d_carry, cz.data(), sizeof(FaCarry) * x->nStreams, hipMemcpyHostToDevice,
                         x->stream));
   HIPCHK(hipStreamSynchronize(x->stream));
   x->lastIpDevice = false;
   x->lastB = 0;
+  x->faImu = FaImuQueue{};
+  x->moImu = MoImuQueue{};
   if (x->moAlloc) {
     HIPCHK(hipMemsetAsync(x->mo.st, 0, sizeof(MoState), x->stream));
     if (x->mo.kf.kcap) {
@@ -287,6 +296,9 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
   A(bb.f_flat, B * N * kFlatPerRing);
   A(bb.f_lflat, B * P);
   A(bb.f_cnt, B * 4);
+  A(bb.imuScan, B);
+  A(x->d_imu, B);
+  bb.imu = nullptr;
   OdomBufs& ob = x->ob;
   ob.capLS = (int)(N * kLessSharpPerRing);
   ob.capCorner = ob.capLS;
@@ -377,8 +389,44 @@ int lego_reset(lego_ctx* x) {
   return ctx_reset(x);
 }
 
+// Delivers /imu_raw messages to both nodes' queues (host imuHandlers).
+static void imu_deliver(lego_ctx* x, const lego_imu_msg* m, int n) {
+  for (int i = 0; i < n; ++i) {
+    x->faImu.push(m[i], x->cfg.scan_period);
+    x->moImu.push(m[i]);
+  }
+}
+
+// The featureAssociation queue of scans 0..B-1 (x->stamps): messages
+// imu[0 .. before[k]) are delivered before scan k, the rest after the last
+// scan.  Returns the device snapshots, or null while the stream has never
+// received a message (adjustDistortion's imuPointerLast < 0 branch).
+static int imu_stage(lego_ctx* x, int B, const lego_imu_msg* imu, int n_imu, const int32_t* before,
+                     const ImuSnap** out) {
+  *out = nullptr;
+  const bool any = x->faImu.last >= 0 || (n_imu > 0 && before && before[B - 1] > 0);
+  if (!any) {  // adjustDistortion still ends with imuPointerLastIteration = imuPointerLast (-1)
+    x->faImu.lastIter = x->faImu.last;
+    imu_deliver(x, imu, n_imu);
+    return LEGO_OK;
+  }
+  x->h_imu.resize(B);
+  int j = 0;
+  for (int k = 0; k < B; ++k) {
+    const int upto = before ? before[k] : 0;
+    imu_deliver(x, imu + j, upto - j);
+    j = upto;
+    x->faImu.snapshot(x->stamps[k], &x->h_imu[k]);
+  }
+  imu_deliver(x, imu + j, n_imu - j);
+  HIPCHK(hipMemcpyAsync(x->d_imu, x->h_imu.data(), sizeof(ImuSnap) * B, hipMemcpyHostToDevice, x->stream));
+  *out = x->d_imu;
+  return LEGO_OK;
+}
+
 static int run_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offsets, int B,
-                     int on_device, int want_labels, bool with_fa) {
+                     int on_device, int want_labels, bool with_fa, const lego_imu_msg* imu = nullptr,
+                     int n_imu = 0, const int32_t* imu_before = nullptr) {
   HIPCHK(hipSetDevice(x->device));
   BatchBufs bb = x->bb;
   // Per-scan sizes are validated on the host in both modes: an empty scan is
@@ -422,6 +470,10 @@ static int run_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* of
     bb.off = x->d_off;
   }
   bb.Nmax = mx;
+  if (with_fa) {
+    const int st = imu_stage(x, B, imu, n_imu, imu_before, &bb.imu);
+    if (st != LEGO_OK) return st;
+  }
   HIPCHK(hipMemsetAsync(bb.bad, 0, sizeof(int) * B, x->stream));
   x->tm.begin();
   launch_ip(bb, x->dc, B, want_labels, x->stream, &x->tm);
@@ -605,9 +657,14 @@ int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
     if (st != LEGO_OK) return st;
   }
   x->stamps.assign(1, in->info.stamp);
+  BatchBufs bb = x->bb;
+  {
+    const int st = imu_stage(x, 1, nullptr, 0, nullptr, &bb.imu);
+    if (st != LEGO_OK) return st;
+  }
   x->tm.begin();
-  launch_fa(x->bb, x->dc, 1, 1, x->d_carry, x->stream, &x->tm);
-  if (launch_odom(x->bb, x->ob, x->dc, 1, x->stream, &x->tm, x->profOn ? x->d_prof : nullptr) != 0) {
+  launch_fa(bb, x->dc, 1, 1, x->d_carry, x->stream, &x->tm);
+  if (launch_odom(bb, x->ob, x->dc, 1, x->stream, &x->tm, x->profOn ? x->d_prof : nullptr) != 0) {
     set_err("odometry launch failed (%d workgroups)", x->ob.G);
     return LEGO_E_DEVICE;
   }
@@ -627,7 +684,35 @@ int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
 
 int lego_odom_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offsets,
                     const double* stamps, int32_t nscans, int32_t on_device, lego_pose_rec* recs) {
+  return lego_odom_batch_imu(x, pts, offsets, stamps, nscans, on_device, nullptr, 0, nullptr, recs);
+}
+
+int lego_imu_push(lego_ctx* x, const lego_imu_msg* msgs, int32_t n) {
+  if (!x || n < 0 || (n > 0 && !msgs)) return LEGO_E_ARG;
+  if (x->nStreams != 1) {
+    set_err("IMU input needs a single-stream context");
+    return LEGO_E_ARG;
+  }
+  imu_deliver(x, msgs, n);
+  return LEGO_OK;
+}
+
+int lego_odom_batch_imu(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offsets,
+                        const double* stamps, int32_t nscans, int32_t on_device, const lego_imu_msg* imu,
+                        int32_t n_imu, const int32_t* imu_before, lego_pose_rec* recs) {
   if (!x || !pts || !offsets || nscans <= 0 || !recs) return LEGO_E_ARG;
+  if (n_imu < 0 || (n_imu > 0 && (!imu || !imu_before))) return LEGO_E_ARG;
+  if (n_imu > 0) {
+    if (x->nStreams != 1) {
+      set_err("IMU input needs a single-stream context");
+      return LEGO_E_ARG;
+    }
+    for (int k = 0; k < nscans; ++k)
+      if (imu_before[k] < (k ? imu_before[k - 1] : 0) || imu_before[k] > n_imu) {
+        set_err("imu_before must be non-decreasing within [0, n_imu]");
+        return LEGO_E_ARG;
+      }
+  }
   if (nscans > x->maxBatch) {
     set_err("batch of %d scans > context capacity %d", nscans, x->maxBatch);
     return LEGO_E_CAPACITY;
@@ -638,7 +723,7 @@ int lego_odom_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* off
   }
   x->stamps.assign(stamps ? stamps : nullptr, stamps ? stamps + nscans : nullptr);
   if (!stamps) x->stamps.assign(nscans, 0.0);
-  int st = run_batch(x, pts, offsets, nscans, on_device, 0, true);
+  int st = run_batch(x, pts, offsets, nscans, on_device, 0, true, imu, n_imu, imu_before);
   if (st != LEGO_OK) return st;
   x->lastIpDevice = false;
   std::vector<float> sum(6 * nscans);
@@ -819,6 +904,9 @@ int lego_mo_process(lego_ctx* x, const lego_fa_out* in, lego_mo_out* out) {
   a.nCorner = in->n_corner_last;
   a.nSurf = in->n_surf_last;
   a.nOutlier = in->n_outlier_last;
+  int moFront = x->moImu.front;
+  a.imuOn = x->moImu.at(in->stamp, x->cfg.scan_period, &a.imuRoll, &a.imuPitch, &moFront) ? 1 : 0;
+  if (!a.imuOn) a.imuRoll = a.imuPitch = 0.f;
   const int rs = mo_step_device(m, a, x->moFixed, x->cfg.surrounding_keyframe_search_radius, s);
   if (rs == -2) {
     set_err("scan-to-map: keyframe store full");
@@ -833,6 +921,7 @@ int lego_mo_process(lego_ctx* x, const lego_fa_out* in, lego_mo_out* out) {
   HIPCHK(hipMemcpyAsync(&hs, m.st, sizeof(hs), hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(&hc, m.cnt, sizeof(hc), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  if (hs.optimized) x->moImu.front = moFront;  // transformUpdate ran (:1345)
   out->processed = 1;
   out->optimized = hs.optimized;
   out->iterations = hs.iterations;

@@ -34,19 +34,58 @@ struct DevCfg {
   int skip;  // skipFrameNum (featureAssociation.cpp:284)
 };
 
+// ---- IMU (featureAssociation.cpp:84-159, 317-459, 525-614)
+constexpr int kImuQ = 200;  // imuQueLength, utility.h:109
+enum { IV_ROLL, IV_PITCH, IV_YAW, IV_VX, IV_VY, IV_VZ, IV_SX, IV_SY, IV_SZ, IV_AX, IV_AY, IV_AZ, kImuV };
+
+// featureAssociation's IMU queue as adjustDistortion sees it for one scan
+// (the host runs imuHandler / AccumulateIMUShiftAndRotation as messages are
+// delivered and snapshots the queue per scan).
+struct ImuSnap {
+  double stamp;           // timeScanCur
+  double time[kImuQ];
+  float v[kImuV][kImuQ];  // imuRoll, imuPitch, imuYaw, imuVelo*, imuShift*, imuAngularRotation*
+  int last;               // imuPointerLast (-1: no message yet)
+  int lastIter;           // imuPointerLastIteration
+  int _pad[2];
+};
+
+// Per-scan IMU terms.  k_fa_imu_start / k_fa_point write this scan's raw
+// values; k_fa_fixup resolves the members that persist across scans (a scan
+// with no IMU message yet, or too few points, leaves them as they were) in
+// stream order; the odometry reads the resolved values.
+struct ImuScan {
+  int active;    // imuPointerLast >= 0
+  int hasFirst;  // the loop reached point 0 (ns >= 1)
+  int hasLast;   // ... and a later point (ns >= 2)
+  int _pad;
+  float rollStart, pitchStart, yawStart;
+  float veloStart[3];
+  float cRS, cPS, cYS, sRS, sPS, sYS;  // updateImuRollPitchYawStartSinCos
+  float ar0[3];                        // imuAngularRotation*Cur at point 0
+  float rollCur, pitchCur, yawCur;     // at the last point
+  float vfs[3];                        // imuVeloFromStart*Cur at the last point
+  float angFromStart[3];               // imuAngularFromStart* (resolved)
+};
+
 // Per-stream feature-extraction carry: the stale
 // cloudSmoothness[4] entry (value is always 0.0f, only its index moves) and the
-// sticky cloudNeighborPicked[0].  S* = {0, 1} is the steady state.
+// sticky cloudNeighborPicked[0].  S* = {0, 1} is the steady state.  Then the
+// featureAssociation IMU members that persist from scan to scan.
 struct FaCarry {
   int phantom_ind;
   int picked0;
   int flags;
   int _pad;
+  float rollStart, pitchStart, yawStart, rollCur, pitchCur, yawCur;
+  float vfs[3], arLast[3], angFromStart[3];
 };
 
 // Batch-wide device pointers (filled by the host, passed by value).
 struct BatchBufs {
   int B;
+  const ImuSnap* imu;        // [B] or null: no IMU message delivered to this batch's stream(s)
+  ImuScan* imuScan;          // [B]
   int Nmax;                  // max input points per scan
   // ---- image projection
   const void* pts;           // lego_point_xyzir [*]

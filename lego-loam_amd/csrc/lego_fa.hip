@@ -56,6 +56,102 @@ __device__ __forceinline__ bool occ_par(const float* r, int i, int ns) {
   return (double)d1 > 0.02 * (double)r[i] && (double)d2 > 0.02 * (double)r[i];
 }
 
+// ---------------------------------------------------------------- IMU
+// adjustDistortion's queue lookup (:526-566) for the point at timeScanCur +
+// pointTime: the first entry after imuPointerLastIteration stamped later than
+// the point (or imuPointerLast), interpolated with the entry before it.
+struct ImuAt {
+  float roll, pitch, yaw, vx, vy, vz;
+  float rf, rb;  // ratioFront / ratioBack (interpolated case)
+  int f, b;
+  bool exact;    // timeScanCur + pointTime > imuTime[front]: no interpolation
+};
+__device__ __forceinline__ void imu_lookup(const ImuSnap& S, float pointTime, ImuAt& a) {
+  const double t = S.stamp + pointTime;
+  int f = S.lastIter;
+  while (f != S.last) {
+    if (t < S.time[f]) break;
+    f = (f + 1) % kImuQ;
+  }
+  a.f = f;
+  a.exact = t > S.time[f];
+  if (a.exact) {
+    a.roll = S.v[IV_ROLL][f]; a.pitch = S.v[IV_PITCH][f]; a.yaw = S.v[IV_YAW][f];
+    a.vx = S.v[IV_VX][f]; a.vy = S.v[IV_VY][f]; a.vz = S.v[IV_VZ][f];
+    return;
+  }
+  const int b = (f + kImuQ - 1) % kImuQ;
+  a.b = b;
+  a.rf = (float)((S.stamp + pointTime - S.time[b]) / (S.time[f] - S.time[b]));
+  a.rb = (float)((S.time[f] - S.stamp - pointTime) / (S.time[f] - S.time[b]));
+  a.roll = S.v[IV_ROLL][f] * a.rf + S.v[IV_ROLL][b] * a.rb;
+  a.pitch = S.v[IV_PITCH][f] * a.rf + S.v[IV_PITCH][b] * a.rb;
+  const float yf = S.v[IV_YAW][f], yb = S.v[IV_YAW][b];
+  if ((double)(yf - yb) > M_PI) a.yaw = (float)(yf * a.rf + (yb + 2 * M_PI) * a.rb);
+  else if ((double)(yf - yb) < -M_PI) a.yaw = (float)(yf * a.rf + (yb - 2 * M_PI) * a.rb);
+  else a.yaw = yf * a.rf + yb * a.rb;
+  a.vx = S.v[IV_VX][f] * a.rf + S.v[IV_VX][b] * a.rb;
+  a.vy = S.v[IV_VY][f] * a.rf + S.v[IV_VY][b] * a.rb;
+  a.vz = S.v[IV_VZ][f] * a.rf + S.v[IV_VZ][b] * a.rb;
+}
+
+// Point 0 of each scan (the i == 0 branch of :568-610): the start attitude and
+// velocity, their sines / cosines, and the angular rotation at point 0.  One
+// lane per scan.  Defaults rollCur.. to the start values (a one-point scan).
+__global__ void k_fa_imu_start(BatchBufs bb, DevCfg c) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= bb.B) return;
+  const ImuSnap& S = bb.imu[b];
+  ImuScan o = {};
+  const int ns = bb.ns[b];
+  o.active = S.last >= 0;
+  o.hasFirst = o.active && ns >= 1;
+  o.hasLast = o.active && ns >= 2;
+  if (o.hasFirst) {
+    const float4 p = bb.seg[(size_t)b * c.P];
+    const float so = bb.orient[3 * b], od = bb.orient[3 * b + 2];
+    const float ori = ori_not_half(-lego_atan2f(p.y, p.x), so);
+    const float relTime = (ori - so) / od;
+    ImuAt a;
+    imu_lookup(S, relTime * c.scan_period, a);
+    o.rollStart = a.roll; o.pitchStart = a.pitch; o.yawStart = a.yaw;
+    o.veloStart[0] = a.vx; o.veloStart[1] = a.vy; o.veloStart[2] = a.vz;
+    if (a.exact) {
+      for (int k = 0; k < 3; ++k) o.ar0[k] = S.v[IV_AX + k][a.f];
+    } else {
+      for (int k = 0; k < 3; ++k) o.ar0[k] = S.v[IV_AX + k][a.f] * a.rf + S.v[IV_AX + k][a.b] * a.rb;
+    }
+    o.cRS = lego_cosf(o.rollStart); o.cPS = lego_cosf(o.pitchStart); o.cYS = lego_cosf(o.yawStart);
+    o.sRS = lego_sinf(o.rollStart); o.sPS = lego_sinf(o.pitchStart); o.sYS = lego_sinf(o.yawStart);
+    o.rollCur = o.rollStart; o.pitchCur = o.pitchStart; o.yawCur = o.yawStart;
+  }
+  bb.imuScan[b] = o;
+}
+
+// TransformToStartIMU :365-390 (imuShiftFromStart*Cur stays 0: ShiftToStartIMU
+// is never called)
+__device__ __forceinline__ float4 to_start_imu(float4 p, const ImuAt& a, const ImuScan& s) {
+  const float cr = lego_cosf(a.roll), sr = lego_sinf(a.roll);
+  const float cp = lego_cosf(a.pitch), sp = lego_sinf(a.pitch);
+  const float cy = lego_cosf(a.yaw), sy = lego_sinf(a.yaw);
+  const float x1 = cr * p.x - sr * p.y;
+  const float y1 = sr * p.x + cr * p.y;
+  const float z1 = p.z;
+  const float x2 = x1;
+  const float y2 = cp * y1 - sp * z1;
+  const float z2 = sp * y1 + cp * z1;
+  const float x3 = cy * x2 + sy * z2;
+  const float y3 = y2;
+  const float z3 = -sy * x2 + cy * z2;
+  const float x4 = s.cYS * x3 - s.sYS * z3;
+  const float y4 = y3;
+  const float z4 = s.sYS * x3 + s.cYS * z3;
+  const float x5 = x4;
+  const float y5 = s.cPS * y4 + s.sPS * z4;
+  const float z5 = -s.sPS * y4 + s.cPS * z4;
+  return make_float4(s.cRS * x5 + s.sRS * y5 + 0.0f, -s.sRS * x5 + s.cRS * y5 + 0.0f, z5 + 0.0f, p.w);
+}
+
 __global__ void k_fa_point(BatchBufs bb, DevCfg c) {
   const int b = blockIdx.y;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -75,7 +171,30 @@ __global__ void k_fa_point(BatchBufs bb, DevCfg c) {
   }
   const float relTime = (ori - so) / od;
   const float inten = (float)(int)p.w + c.scan_period * relTime;
-  bb.dsk[base + i] = make_float4(p.y, p.z, p.x, inten);
+  float4 q = make_float4(p.y, p.z, p.x, inten);
+  if (bb.imu && i > 0) {
+    ImuScan& is = bb.imuScan[b];
+    if (is.active) {
+      ImuAt a;
+      imu_lookup(bb.imu[b], relTime * c.scan_period, a);
+      if (i == ns - 1) {  // the members the scan leaves behind: the last point's
+        // VeloToStartIMU :346-363
+        float vx = a.vx - is.veloStart[0], vy = a.vy - is.veloStart[1], vz = a.vz - is.veloStart[2];
+        const float x1 = is.cYS * vx - is.sYS * vz;
+        const float y1 = vy;
+        const float z1 = is.sYS * vx + is.cYS * vz;
+        const float x2 = x1;
+        const float y2 = is.cPS * y1 + is.sPS * z1;
+        const float z2 = -is.sPS * y1 + is.cPS * z1;
+        is.vfs[0] = is.cRS * x2 + is.sRS * y2;
+        is.vfs[1] = -is.sRS * x2 + is.cRS * y2;
+        is.vfs[2] = z2;
+        is.rollCur = a.roll; is.pitchCur = a.pitch; is.yawCur = a.yaw;
+      }
+      q = to_start_imu(q, a, is);
+    }
+  }
+  bb.dsk[base + i] = q;
   // calculateSmoothness :624-640
   const float* r = bb.srange + base;
   float cv = 0.f;
@@ -529,6 +648,22 @@ __global__ void __launch_bounds__(kExtractThreads) k_fa_fixup(BatchBufs bb, DevC
       extract_ring(bb, c, b, 0, &cs, L);
       if (threadIdx.x == 0) bb.fa_flags[b] |= 2;  // ring 0 recomputed with the real carry
     }
+    if (bb.imu && threadIdx.x == 0) {  // the IMU members in stream order (:568-612, 1641-1651)
+      ImuScan& o = bb.imuScan[b];
+      if (o.hasFirst) {
+        cs.rollStart = o.rollStart; cs.pitchStart = o.pitchStart; cs.yawStart = o.yawStart;
+        for (int k = 0; k < 3; ++k) {
+          cs.angFromStart[k] = o.ar0[k] - cs.arLast[k];
+          cs.arLast[k] = o.ar0[k];
+        }
+        cs.rollCur = o.rollCur; cs.pitchCur = o.pitchCur; cs.yawCur = o.yawCur;
+        if (o.hasLast)
+          for (int k = 0; k < 3; ++k) cs.vfs[k] = o.vfs[k];
+      }
+      o.rollStart = cs.rollStart; o.pitchStart = cs.pitchStart; o.yawStart = cs.yawStart;
+      o.rollCur = cs.rollCur; o.pitchCur = cs.pitchCur; o.yawCur = cs.yawCur;
+      for (int k = 0; k < 3; ++k) { o.vfs[k] = cs.vfs[k]; o.angFromStart[k] = cs.angFromStart[k]; }
+    }
   }
   if (threadIdx.x == 0) *carry = cs;
 }
@@ -567,6 +702,7 @@ void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_ca
   (void)hipMemsetAsync(bb.fa_flags, 0, sizeof(int) * B, s);
   dim3 gpts((c.P + 255) / 256, B);
   k_fa_half<<<gpts, 256, 0, s>>>(bb, c);
+  if (bb.imu) k_fa_imu_start<<<(B + 63) / 64, 64, 0, s>>>(bb, c);
   k_fa_point<<<gpts, 256, 0, s>>>(bb, c);
   tm->mark("fa.extract", s);
   const size_t lds = extract_lds_bytes(c.H);

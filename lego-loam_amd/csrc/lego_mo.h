@@ -92,6 +92,8 @@ struct MoStepArgs {
   double quat[4];  // /laser_odom_to_init orientation (x, y, z, w)
   double pos[3];
   int nCorner, nSurf, nOutlier;
+  int imuOn;              // transformUpdate's IMU blend (:465-490), roll / pitch from the host queue
+  float imuRoll, imuPitch;
 };
 
 size_t voxel_scratch_tmp_bytes(int cap);

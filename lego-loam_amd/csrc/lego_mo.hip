@@ -23,7 +23,7 @@
 //                    iteration-0 eigen degeneracy projection, update,
 //                    convergence (:1229-1327); later iterations exit at once
 //                    once converged
-//   k_mo_finish      transformUpdate (:463-496, no IMU)
+//   k_mo_finish      transformUpdate (:463-496)
 // The fixed map (config C5, lego_mo_set_map) is voxel-filtered and indexed once
 // per map: the filter of an unchanged cloud is the same cloud every step.
 #include <hipcub/hipcub.hpp>
@@ -642,8 +642,16 @@ __global__ void __launch_bounds__(kMoSolveThreads) k_mo_solve(MoState* st, const
   if ((double)deltaR < 0.05 && (double)deltaT < 0.05) st->converged = 1;
 }
 
-__global__ void k_mo_finish(MoState* st) {  // transformUpdate :463-496 (no IMU)
+// transformUpdate :463-496.  imuOn: the host's mapOptimization IMU queue had a
+// message; imuRoll / imuPitch are imuRollLast / imuPitchLast at
+// timeLaserOdometry + scanPeriod.
+__global__ void k_mo_finish(MoState* st, int imuOn, float imuRoll, float imuPitch) {
   if (threadIdx.x != 0 || !st->optimized) return;
+  if (imuOn) {
+    float* t = st->transformTobeMapped;
+    t[0] = (float)(0.998 * t[0] + 0.002 * imuPitch);
+    t[2] = (float)(0.998 * t[2] + 0.002 * imuRoll);
+  }
   for (int i = 0; i < 6; i++) {
     st->transformBefMapped[i] = st->transformSum[i];
     st->transformAftMapped[i] = st->transformTobeMapped[i];
@@ -850,7 +858,7 @@ int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, h
                                                    m.cornerMapDS, m.surfMapDS, m.rows, qcap);
     k_mo_solve<<<1, kMoSolveThreads, 0, s>>>(m.st, m.cnt, m.rows, qcap, it);
   }
-  k_mo_finish<<<1, 64, 0, s>>>(m.st);
+  k_mo_finish<<<1, 64, 0, s>>>(m.st, a.imuOn, a.imuRoll, a.imuPitch);
   if (!fixedMap) {  // saveKeyFramesAndFactor :1353-1454
     k_kf_save<<<1, 64, 0, s>>>(m.kf, m.st, m.cnt);
     k_kf_copy<<<grid_for(qcap), 256, 0, s>>>(m.kf, m.cornerDS, m.surfDS, m.outlierDS);

@@ -203,21 +203,26 @@ __device__ __forceinline__ void plugin_imu_rotation(float bcx, float bcy, float 
 // integrateTransformation (:1697-1725) by one wave: the same expressions as
 // accumulate_rotation / plugin_imu_rotation above, with their independent
 // sines and cosines evaluated on separate lanes and broadcast by readlane, and
-// the two atan2f of each step on two lanes.  The IMU angles are zero here
-// (sin 0 = 0, cos 0 = 1 exactly, as lego_sinf / lego_cosf return).
+// the two atan2f of each step on two lanes.  bl / al: the IMU angles
+// (imuPitchStart, imuYawStart, imuRollStart) / (imuPitchLast, imuYawLast,
+// imuRollLast); all zero without an IMU.
 __device__ __forceinline__ float rl_f(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 __device__ __forceinline__ float sel6(int m, float a0, float a1, float a2, float a3, float a4, float a5) {
   return m == 0 ? a0 : m == 1 ? a1 : m == 2 ? a2 : m == 3 ? a3 : m == 4 ? a4 : a5;
 }
-__device__ __forceinline__ void integrate_wave(float* ts, const float* tc) {
+__device__ __forceinline__ void integrate_wave(float* ts, const float* tc, const float bl[3], const float al[3]) {
   const int lane = threadIdx.x & 63;
-  // accumulate_rotation(ts[0..2], -tc[0..2]): lanes 0-5 sin, 6-11 cos of {lx, ly, lz, cx, cy, cz}
+  // accumulate_rotation(ts[0..2], -tc[0..2]): lanes 0-5 sin, 6-11 cos of {lx, ly, lz, cx, cy, cz};
+  // plugin_imu_rotation's bl / al: lanes 12-17 sin, 18-23 cos
   float v = 0.f;
   if (lane < 12) {
     const float a = sel6(lane % 6, -tc[0], -tc[1], -tc[2], ts[0], ts[1], ts[2]);
     v = lane < 6 ? lego_sinf(a) : lego_cosf(a);
+  } else if (lane < 24) {
+    const float a = sel6(lane % 6, bl[0], bl[1], bl[2], al[0], al[1], al[2]);
+    v = lane < 18 ? lego_sinf(a) : lego_cosf(a);
   }
   const float slx = rl_f(v, 0), sly = rl_f(v, 1), slz = rl_f(v, 2), scx = rl_f(v, 3), scy = rl_f(v, 4), scz = rl_f(v, 5);
   const float clx = rl_f(v, 6), cly = rl_f(v, 7), clz = rl_f(v, 8), ccx = rl_f(v, 9), ccy = rl_f(v, 10), ccz = rl_f(v, 11);
@@ -251,9 +256,11 @@ __device__ __forceinline__ void integrate_wave(float* ts, const float* tc) {
   const float tx = ts[3] - (cbcy * x2 + sbcy * z2);
   const float ty = ts[4] - y2;
   const float tz = ts[5] - (-sbcy * x2 + cbcy * z2);
-  // plugin_imu_rotation(rx, ry, rz, 0, 0, 0, 0, 0, 0)
-  const float sblx = 0.f, cblx = 1.f, sbly = 0.f, cbly = 1.f, sblz = 0.f, cblz = 1.f;
-  const float salx = 0.f, calx = 1.f, saly = 0.f, caly = 1.f, salz = 0.f, calz = 1.f;
+  // plugin_imu_rotation(rx, ry, rz, bl, al)
+  const float sblx = rl_f(v, 12), sbly = rl_f(v, 13), sblz = rl_f(v, 14);
+  const float salx = rl_f(v, 15), saly = rl_f(v, 16), salz = rl_f(v, 17);
+  const float cblx = rl_f(v, 18), cbly = rl_f(v, 19), cblz = rl_f(v, 20);
+  const float calx = rl_f(v, 21), caly = rl_f(v, 22), calz = rl_f(v, 23);
   const float psrx = -sbcx * (salx * sblx + calx * caly * cblx * cbly + calx * cblx * saly * sbly) -
                      cbcx * cbcz * (calx * saly * (cbly * sblz - cblz * sblx * sbly) -
                                     calx * caly * (sbly * sblz + cbly * cblz * sblx) + cblx * cblz * salx) -
@@ -1190,7 +1197,6 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     if (st->curBuf == st->snapBuf) build_indexes(L, ob, st, c);
   }
   S.add(P_RESID);
-  const ImuEnd im{1.f, 1.f, 1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 1.f, 0.f, 1.f, 0.f};
   for (int b = b0; b < b0 + K; ++b) {
     ScanFeat F;
     const int* fc = bb.f_cnt + b * 4;
@@ -1201,8 +1207,25 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     float4* cEnd = ob.cornerEnd + (size_t)b * ob.capLS;
     float4* sEnd = ob.surfEnd + (size_t)b * c.P;
     const bool init = !st->inited;
+    // this scan's IMU terms (all zero without an IMU message: cos 0 = 1)
+    ImuScan iq = {};
+    if (bb.imu) iq = bb.imuScan[b];
     if (!init) {
-      // updateInitialGuess is a no-op without IMU
+      // updateInitialGuess :1639-1664 (imuShiftFromStart* stays 0)
+      if (tid == 0) {
+        float* tc = st->transformCur;
+        if (iq.angFromStart[0] != 0 || iq.angFromStart[1] != 0 || iq.angFromStart[2] != 0) {
+          tc[0] = -iq.angFromStart[1];
+          tc[1] = -iq.angFromStart[2];
+          tc[2] = -iq.angFromStart[0];
+        }
+        if (iq.vfs[0] != 0 || iq.vfs[1] != 0 || iq.vfs[2] != 0) {
+          tc[3] -= iq.vfs[0] * c.scan_period;
+          tc[4] -= iq.vfs[1] * c.scan_period;
+          tc[5] -= iq.vfs[2] * c.scan_period;
+        }
+      }
+      __syncthreads();
       if (st->cornerLastNum >= 10 && st->surfLastNum >= 100) {
         if (st->resident) {
           for (int t = tid; t < F.nFlat; t += kOdomThreads) L.qflat[t] = F.flat[t];
@@ -1217,7 +1240,11 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
       }
       // integrateTransformation :1697-1725
       S.start();
-      if (tid < 64) integrate_wave(st->transformSum, st->transformCur);
+      if (tid < 64) {
+        const float bl[3] = {iq.pitchStart, iq.yawStart, iq.rollStart};
+        const float al[3] = {iq.pitchCur, iq.yawCur, iq.rollCur};  // imu*Last = imu*Cur (:1641-1643)
+        integrate_wave(st->transformSum, st->transformCur, bl, al);
+      }
       __syncthreads();
       S.add(P_INTEG);
     }
@@ -1233,6 +1260,11 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     float tcur[6];
     for (int i = 0; i < 6; ++i) tcur[i] = st->transformCur[i];
     const EndTrig et = end_trig(tcur);
+    // updateImuRollPitchYawStartSinCos (:1761) and the imu*Last terms of TransformToEnd
+    const ImuEnd im{lego_cosf(iq.rollStart), lego_cosf(iq.pitchStart), lego_cosf(iq.yawStart),
+                    lego_sinf(iq.rollStart), lego_sinf(iq.pitchStart), lego_sinf(iq.yawStart),
+                    lego_cosf(iq.yawCur), lego_sinf(iq.yawCur), lego_cosf(iq.pitchCur),
+                    lego_sinf(iq.pitchCur), lego_cosf(iq.rollCur), lego_sinf(iq.rollCur)};
     for (int t = tid; t < F.nLS; t += kOdomThreads) {
       const float4 p = init ? F.lsharp[t] : to_end(F.lsharp[t], tcur, et, im);
       gCn[t] = p;
@@ -1256,8 +1288,8 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
       if (rebuild) { st->snapBuf = nbuf; st->nnCornerNum = F.nLS; st->nnSurfNum = F.nLF; }
       int pub = 0;
       if (init) {
-        st->transformSum[0] += 0.0f;  // += imuPitchStart
-        st->transformSum[2] += 0.0f;  // += imuRollStart
+        st->transformSum[0] += iq.pitchStart;  // checkSystemInitialization :1633-1634
+        st->transformSum[2] += iq.rollStart;
         st->inited = 1;
       } else {
         st->frameCount++;

@@ -246,6 +246,52 @@ extern "C" int lego_synth_scan(const lego_synth_cfg* c, int32_t k, lego_point_xy
   return LEGO_OK;
 }
 
+extern "C" int lego_synth_imu(const lego_synth_cfg* c, double t0, double t1, double rate_hz, double phase,
+                              lego_imu_msg* out, int32_t cap, int32_t* n_out) {
+  if (!c || !out || !n_out || !(rate_hz > 0) || !(t1 >= t0)) return LEGO_E_ARG;
+  const double v = c->speed_mps, w = c->yaw_rate_dps * M_PI / 180.0, g = 9.81;
+  const double dt = 1.0 / rate_hz;
+  int32_t n = 0;
+  for (int64_t i = (int64_t)std::ceil((t0 - phase) * rate_hz - 1e-9);; ++i) {
+    const double t = phase + (double)i * dt;
+    if (t < t0) continue;
+    if (t >= t1) break;
+    if (n >= cap) return LEGO_E_CAPACITY;
+    // attitude: the ego yaw plus a gentle roll / pitch sway
+    const double a1 = 2.0 * M_PI * 0.5, a2 = 2.0 * M_PI * 0.3;
+    const double roll = 0.01 * std::sin(a1 * t), pitch = 0.008 * std::sin(a2 * t + 1.0);
+    double px, py, yaw;
+    ego_pose(*c, t, &px, &py, &yaw);
+    const double droll = 0.01 * a1 * std::cos(a1 * t), dpitch = 0.008 * a2 * std::cos(a2 * t + 1.0);
+    // quaternion of R = Rz(yaw) Ry(pitch) Rx(roll) (tf setRPY)
+    const double hr = roll / 2, hp = pitch / 2, hy = yaw / 2;
+    const double cr = std::cos(hr), sr = std::sin(hr), cp = std::cos(hp), sp = std::sin(hp);
+    const double cy = std::cos(hy), sy = std::sin(hy);
+    lego_imu_msg& m = out[n++];
+    std::memset(&m, 0, sizeof(m));
+    m.stamp = t;
+    m.orientation[0] = sr * cp * cy - cr * sp * sy;
+    m.orientation[1] = cr * sp * cy + sr * cp * sy;
+    m.orientation[2] = cr * cp * sy - sr * sp * cy;
+    m.orientation[3] = cr * cp * cy + sr * sp * sy;
+    const uint64_t key = c->seed * 0xA24BAED4963EE407ULL + (uint64_t)i * 0x9FB21C651E98DF25ULL;
+    m.angular_velocity[0] = droll + 0.002 * hash_gauss(key ^ 0x71);
+    m.angular_velocity[1] = dpitch + 0.002 * hash_gauss(key ^ 0x72);
+    m.angular_velocity[2] = w + 0.002 * hash_gauss(key ^ 0x73);
+    // specific force: centripetal acceleration plus the gravity reaction, in the body frame
+    const double fw[3] = {-v * w * std::sin(yaw), v * w * std::cos(yaw), g};
+    const double Cy = std::cos(yaw), Sy = std::sin(yaw), Cp = std::cos(pitch), Sp = std::sin(pitch);
+    const double Cr = std::cos(roll), Sr = std::sin(roll);
+    // R^T f, R = Rz Ry Rx
+    const double a0 = Cy * fw[0] + Sy * fw[1], b0 = -Sy * fw[0] + Cy * fw[1], z0 = fw[2];
+    const double a1x = Cp * a0 - Sp * z0, z1 = Sp * a0 + Cp * z0;
+    const double fb[3] = {a1x, Cr * b0 + Sr * z1, -Sr * b0 + Cr * z1};
+    for (int k = 0; k < 3; ++k) m.linear_acceleration[k] = fb[k] + 0.02 * hash_gauss(key ^ (0x80 + k));
+  }
+  *n_out = n;
+  return LEGO_OK;
+}
+
 extern "C" int lego_synth_map(uint64_t seed, float radius, int32_t n_surf, int32_t n_corner,
                               lego_point_xyzi* surf, lego_point_xyzi* corner) {
   if ((n_surf && !surf) || (n_corner && !corner) || radius <= 0) return LEGO_E_ARG;

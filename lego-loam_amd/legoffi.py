@@ -108,6 +108,12 @@ class PoseRec(C.Structure):
 assert C.sizeof(PoseRec) == 64
 
 
+# lego_imu_msg (include/lego_loam.h): the sensor_msgs/Imu fields the handlers read
+IMU_DTYPE = np.dtype([("stamp", np.float64), ("orientation", np.float64, 4),
+                      ("angular_velocity", np.float64, 3), ("linear_acceleration", np.float64, 3)])
+assert IMU_DTYPE.itemsize == 88
+
+
 class SynthCfg(C.Structure):
     _fields_ = [("n_scan", C.c_int32), ("horizon_scan", C.c_int32), ("vert_min_deg", C.c_float),
                 ("vert_max_deg", C.c_float), ("mount_height", C.c_float),
@@ -139,6 +145,8 @@ def synth_lib() -> C.CDLL:
                                     C.POINTER(C.c_int32), C.POINTER(C.c_double)]
     lib.lego_synth_map.argtypes = [C.c_uint64, C.c_float, C.c_int32, C.c_int32, C.c_void_p,
                                    C.c_void_p]
+    lib.lego_synth_imu.argtypes = [C.POINTER(SynthCfg), C.c_double, C.c_double, C.c_double, C.c_double,
+                                   C.c_void_p, C.c_int32, C.POINTER(C.c_int32)]
     return lib
 
 
@@ -155,6 +163,7 @@ def oracle_lib() -> C.CDLL:
     lib.lego_oracle_fa_process.argtypes = [C.c_void_p, C.POINTER(IpOut), C.POINTER(FaOut)]
     lib.lego_oracle_mo_set_map.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32]
     lib.lego_oracle_mo_process.argtypes = [C.c_void_p, C.POINTER(FaOut), C.POINTER(MoOut)]
+    lib.lego_oracle_imu_push.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
     lib.lego_oracle_voxel_grid.argtypes = [C.c_void_p, C.c_int32, C.c_float, C.c_int32,
                                            C.c_void_p, C.POINTER(C.c_int32)]
     for fn in ("atan2f",):
@@ -167,7 +176,8 @@ def oracle_lib() -> C.CDLL:
 
 
 HIP_EXPORTS = ["lego_sensor_preset", "lego_create", "lego_fleet_create", "lego_destroy", "lego_reset",
-               "lego_ip_process", "lego_fa_process", "lego_odom_batch", "lego_batch_fetch",
+               "lego_ip_process", "lego_fa_process", "lego_odom_batch", "lego_odom_batch_imu",
+               "lego_imu_push", "lego_batch_fetch",
                "lego_mo_set_map", "lego_mo_process", "lego_last_error", "lego_stage_times",
                "lego_odom_profile"]
 
@@ -187,6 +197,9 @@ def hip_lib() -> C.CDLL:
     lib.lego_fa_process.argtypes = [C.c_void_p, C.POINTER(IpOut), C.POINTER(FaOut)]
     lib.lego_odom_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
                                     C.c_int32, C.c_void_p]
+    lib.lego_odom_batch_imu.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
+                                        C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
+    lib.lego_imu_push.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
     lib.lego_batch_fetch.argtypes = [C.c_void_p, C.c_int32, C.POINTER(IpOut), C.POINTER(FaOut)]
     lib.lego_mo_set_map.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32]
     lib.lego_mo_process.argtypes = [C.c_void_p, C.POINTER(FaOut), C.POINTER(MoOut)]
@@ -227,6 +240,18 @@ def synth_scan(cfg: SynthCfg, k: int) -> tuple[np.ndarray, float]:
     check(lib.lego_synth_scan(C.byref(cfg), k, buf.ctypes.data, cap, C.byref(n), C.byref(st)),
           "synth_scan")
     return buf[: n.value].copy(), st.value
+
+
+def synth_imu(cfg: SynthCfg, t0: float, t1: float, rate_hz: float = 100.0,
+              phase: float = 0.0037) -> np.ndarray:
+    """/imu_raw messages of the synthetic ego motion with stamps in [t0, t1)."""
+    lib = synth_lib()
+    cap = int((t1 - t0) * rate_hz) + 2
+    buf = np.zeros(cap, dtype=IMU_DTYPE)
+    n = C.c_int32()
+    check(lib.lego_synth_imu(C.byref(cfg), t0, t1, rate_hz, phase, buf.ctypes.data, cap, C.byref(n)),
+          "synth_imu")
+    return buf[: n.value].copy()
 
 
 def synth_map(seed: int, radius: float, n_surf: int, n_corner: int):
@@ -318,6 +343,12 @@ class Oracle:
               "oracle_ip")
         return ip_to_dict(self._ip, self.cfg, images)
 
+    def imu(self, msgs: np.ndarray) -> None:
+        """Delivers /imu_raw messages to the featureAssociation and
+        mapOptimization handlers, in order."""
+        msgs = np.ascontiguousarray(msgs, dtype=IMU_DTYPE)
+        check(self.lib.lego_oracle_imu_push(self.h, msgs.ctypes.data, len(msgs)), "oracle_imu")
+
     def fa(self) -> dict:
         check(self.lib.lego_oracle_fa_process(self.h, C.byref(self._ip), C.byref(self._fa)),
               "oracle_fa")
@@ -389,15 +420,31 @@ class Lego:
         return {k: (np.array(list(getattr(out, k)), dtype=np.float32)
                     if k.startswith("transform") else getattr(out, k)) for k, _ in MoOut._fields_}
 
-    def odom_batch(self, pts: np.ndarray, offsets: np.ndarray, stamps: np.ndarray) -> np.ndarray:
+    def odom_batch(self, pts: np.ndarray, offsets: np.ndarray, stamps: np.ndarray,
+                   imu: np.ndarray | None = None, imu_before: np.ndarray | None = None) -> np.ndarray:
+        """imu / imu_before: lego_odom_batch_imu (messages imu[:imu_before[k]]
+        delivered before scan k, the rest after the batch)."""
         pts = np.ascontiguousarray(pts, dtype=XYZIR_DTYPE)
         offsets = np.ascontiguousarray(offsets, dtype=np.int64)
         stamps = np.ascontiguousarray(stamps, dtype=np.float64)
         k = len(offsets) - 1
         recs = (PoseRec * k)()
-        check(self.lib.lego_odom_batch(self.h, pts.ctypes.data, offsets.ctypes.data,
-                                       stamps.ctypes.data, k, 0, recs), "lego_odom_batch", self.lib)
+        if imu is None:
+            check(self.lib.lego_odom_batch(self.h, pts.ctypes.data, offsets.ctypes.data,
+                                           stamps.ctypes.data, k, 0, recs), "lego_odom_batch", self.lib)
+        else:
+            imu = np.ascontiguousarray(imu, dtype=IMU_DTYPE)
+            before = np.ascontiguousarray(imu_before, dtype=np.int32)
+            check(self.lib.lego_odom_batch_imu(self.h, pts.ctypes.data, offsets.ctypes.data,
+                                               stamps.ctypes.data, k, 0, imu.ctypes.data, len(imu),
+                                               before.ctypes.data, recs), "lego_odom_batch_imu", self.lib)
         return recs
+
+    def imu(self, msgs: np.ndarray) -> None:
+        """Delivers /imu_raw messages to the featureAssociation and
+        mapOptimization queues (lego_imu_push)."""
+        msgs = np.ascontiguousarray(msgs, dtype=IMU_DTYPE)
+        check(self.lib.lego_imu_push(self.h, msgs.ctypes.data, len(msgs)), "lego_imu_push", self.lib)
 
     def odom_batch_device(self, pts_ptr: int, offsets_ptr: int, stamps: np.ndarray, k: int, recs):
         check(self.lib.lego_odom_batch(self.h, C.c_void_p(pts_ptr), C.c_void_p(offsets_ptr),

@@ -417,6 +417,11 @@ struct ImageProjection {
 };
 
 // ============================================================ FeatureAssociation
+// tf::Matrix3x3(q).getRPY, defined with the mapping restatement (oracle_mo.inc)
+inline void rpy_from_quat(double x, double y, double z, double w, double* roll, double* pitch, double* yaw);
+
+static constexpr int kImuQ = 200;  // imuQueLength, utility.h:109
+
 struct Smooth { float value; size_t ind; };           // utility.h:139-142
 struct ByValue {                                       // utility.h:144-148
   bool operator()(Smooth const& l, Smooth const& r) const { return l.value < r.value; }
@@ -451,12 +456,32 @@ struct FeatureAssociation {
   bool isDegenerate = false;
   float matP[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
   int frameCount;
-  // IMU terms: all zero without an IMU topic (imuPointerLast = -1, :251)
+  // IMU state (:84-159, initialised :251-295); all zero until the first
+  // /imu_raw message (imuPointerLast = -1)
   float cosImuRollStart = 0, cosImuPitchStart = 0, cosImuYawStart = 0;
   float sinImuRollStart = 0, sinImuPitchStart = 0, sinImuYawStart = 0;
   float imuRollStart = 0, imuPitchStart = 0, imuYawStart = 0;
   float imuRollLast = 0, imuPitchLast = 0, imuYawLast = 0;
   float imuShiftFromStartX = 0, imuShiftFromStartY = 0, imuShiftFromStartZ = 0;
+  float imuVeloFromStartX = 0, imuVeloFromStartY = 0, imuVeloFromStartZ = 0;
+  int imuPointerFront = 0, imuPointerLast = -1, imuPointerLastIteration = 0;
+  double imuTime[kImuQ] = {};
+  float imuRoll[kImuQ] = {}, imuPitch[kImuQ] = {}, imuYaw[kImuQ] = {};
+  float imuAccX[kImuQ] = {}, imuAccY[kImuQ] = {}, imuAccZ[kImuQ] = {};
+  float imuVeloX[kImuQ] = {}, imuVeloY[kImuQ] = {}, imuVeloZ[kImuQ] = {};
+  float imuShiftX[kImuQ] = {}, imuShiftY[kImuQ] = {}, imuShiftZ[kImuQ] = {};
+  float imuAngularVeloX[kImuQ] = {}, imuAngularVeloY[kImuQ] = {}, imuAngularVeloZ[kImuQ] = {};
+  float imuAngularRotationX[kImuQ] = {}, imuAngularRotationY[kImuQ] = {}, imuAngularRotationZ[kImuQ] = {};
+  float imuRollCur = 0, imuPitchCur = 0, imuYawCur = 0;
+  float imuVeloXStart = 0, imuVeloYStart = 0, imuVeloZStart = 0;
+  float imuShiftXStart = 0, imuShiftYStart = 0, imuShiftZStart = 0;
+  float imuVeloXCur = 0, imuVeloYCur = 0, imuVeloZCur = 0;
+  float imuShiftXCur = 0, imuShiftYCur = 0, imuShiftZCur = 0;
+  float imuShiftFromStartXCur = 0, imuShiftFromStartYCur = 0, imuShiftFromStartZCur = 0;
+  float imuVeloFromStartXCur = 0, imuVeloFromStartYCur = 0, imuVeloFromStartZCur = 0;
+  float imuAngularRotationXCur = 0, imuAngularRotationYCur = 0, imuAngularRotationZCur = 0;
+  float imuAngularRotationXLast = 0, imuAngularRotationYLast = 0, imuAngularRotationZLast = 0;
+  float imuAngularFromStartX = 0, imuAngularFromStartY = 0, imuAngularFromStartZ = 0;
   // outputs
   bool odomValid = false, publishToMapping = false;
   std::vector<Pt> outCornerLast, outSurfLast, outOutlierLast;
@@ -471,7 +496,99 @@ struct FeatureAssociation {
     frameCount = c.skip_frame_num;
   }
 
-  // adjustDistortion :491-619 (imuPointerLast < 0 branch)
+  // updateImuRollPitchYawStartSinCos :317-324
+  void updateImuStartSinCos() {
+    cosImuRollStart = lego_cosf(imuRollStart); cosImuPitchStart = lego_cosf(imuPitchStart);
+    cosImuYawStart = lego_cosf(imuYawStart); sinImuRollStart = lego_sinf(imuRollStart);
+    sinImuPitchStart = lego_sinf(imuPitchStart); sinImuYawStart = lego_sinf(imuYawStart);
+  }
+
+  // AccumulateIMUShiftAndRotation :392-429
+  void accumulateIMUShiftAndRotation() {
+    const int l = imuPointerLast;
+    const float roll = imuRoll[l], pitch = imuPitch[l], yaw = imuYaw[l];
+    float accX = imuAccX[l], accY = imuAccY[l], accZ = imuAccZ[l];
+    const float x1 = lego_cosf(roll) * accX - lego_sinf(roll) * accY;
+    const float y1 = lego_sinf(roll) * accX + lego_cosf(roll) * accY;
+    const float z1 = accZ;
+    const float x2 = x1;
+    const float y2 = lego_cosf(pitch) * y1 - lego_sinf(pitch) * z1;
+    const float z2 = lego_sinf(pitch) * y1 + lego_cosf(pitch) * z1;
+    accX = lego_cosf(yaw) * x2 + lego_sinf(yaw) * z2;
+    accY = y2;
+    accZ = -lego_sinf(yaw) * x2 + lego_cosf(yaw) * z2;
+    const int b = (l + kImuQ - 1) % kImuQ;
+    const double timeDiff = imuTime[l] - imuTime[b];
+    if (timeDiff < c.scan_period) {
+      imuShiftX[l] = (float)(imuShiftX[b] + imuVeloX[b] * timeDiff + accX * timeDiff * timeDiff / 2);
+      imuShiftY[l] = (float)(imuShiftY[b] + imuVeloY[b] * timeDiff + accY * timeDiff * timeDiff / 2);
+      imuShiftZ[l] = (float)(imuShiftZ[b] + imuVeloZ[b] * timeDiff + accZ * timeDiff * timeDiff / 2);
+      imuVeloX[l] = (float)(imuVeloX[b] + accX * timeDiff);
+      imuVeloY[l] = (float)(imuVeloY[b] + accY * timeDiff);
+      imuVeloZ[l] = (float)(imuVeloZ[b] + accZ * timeDiff);
+      imuAngularRotationX[l] = (float)(imuAngularRotationX[b] + imuAngularVeloX[b] * timeDiff);
+      imuAngularRotationY[l] = (float)(imuAngularRotationY[b] + imuAngularVeloY[b] * timeDiff);
+      imuAngularRotationZ[l] = (float)(imuAngularRotationZ[b] + imuAngularVeloZ[b] * timeDiff);
+    }
+  }
+
+  // imuHandler :431-458
+  void imuHandler(const lego_imu_msg& m) {
+    double roll, pitch, yaw;
+    rpy_from_quat(m.orientation[0], m.orientation[1], m.orientation[2], m.orientation[3], &roll, &pitch, &yaw);
+    const float accX = (float)(m.linear_acceleration[1] - std::sin(roll) * std::cos(pitch) * 9.81);
+    const float accY = (float)(m.linear_acceleration[2] - std::cos(roll) * std::cos(pitch) * 9.81);
+    const float accZ = (float)(m.linear_acceleration[0] + std::sin(pitch) * 9.81);
+    imuPointerLast = (imuPointerLast + 1) % kImuQ;
+    const int l = imuPointerLast;
+    imuTime[l] = m.stamp;
+    imuRoll[l] = (float)roll; imuPitch[l] = (float)pitch; imuYaw[l] = (float)yaw;
+    imuAccX[l] = accX; imuAccY[l] = accY; imuAccZ[l] = accZ;
+    imuAngularVeloX[l] = (float)m.angular_velocity[0];
+    imuAngularVeloY[l] = (float)m.angular_velocity[1];
+    imuAngularVeloZ[l] = (float)m.angular_velocity[2];
+    accumulateIMUShiftAndRotation();
+  }
+
+  // VeloToStartIMU :346-363
+  void veloToStartIMU() {
+    imuVeloFromStartXCur = imuVeloXCur - imuVeloXStart;
+    imuVeloFromStartYCur = imuVeloYCur - imuVeloYStart;
+    imuVeloFromStartZCur = imuVeloZCur - imuVeloZStart;
+    const float x1 = cosImuYawStart * imuVeloFromStartXCur - sinImuYawStart * imuVeloFromStartZCur;
+    const float y1 = imuVeloFromStartYCur;
+    const float z1 = sinImuYawStart * imuVeloFromStartXCur + cosImuYawStart * imuVeloFromStartZCur;
+    const float x2 = x1;
+    const float y2 = cosImuPitchStart * y1 + sinImuPitchStart * z1;
+    const float z2 = -sinImuPitchStart * y1 + cosImuPitchStart * z1;
+    imuVeloFromStartXCur = cosImuRollStart * x2 + sinImuRollStart * y2;
+    imuVeloFromStartYCur = -sinImuRollStart * x2 + cosImuRollStart * y2;
+    imuVeloFromStartZCur = z2;
+  }
+
+  // TransformToStartIMU :365-390
+  void transformToStartIMU(Pt* p) const {
+    const float x1 = lego_cosf(imuRollCur) * p->x - lego_sinf(imuRollCur) * p->y;
+    const float y1 = lego_sinf(imuRollCur) * p->x + lego_cosf(imuRollCur) * p->y;
+    const float z1 = p->z;
+    const float x2 = x1;
+    const float y2 = lego_cosf(imuPitchCur) * y1 - lego_sinf(imuPitchCur) * z1;
+    const float z2 = lego_sinf(imuPitchCur) * y1 + lego_cosf(imuPitchCur) * z1;
+    const float x3 = lego_cosf(imuYawCur) * x2 + lego_sinf(imuYawCur) * z2;
+    const float y3 = y2;
+    const float z3 = -lego_sinf(imuYawCur) * x2 + lego_cosf(imuYawCur) * z2;
+    const float x4 = cosImuYawStart * x3 - sinImuYawStart * z3;
+    const float y4 = y3;
+    const float z4 = sinImuYawStart * x3 + cosImuYawStart * z3;
+    const float x5 = x4;
+    const float y5 = cosImuPitchStart * y4 + sinImuPitchStart * z4;
+    const float z5 = -sinImuPitchStart * y4 + cosImuPitchStart * z4;
+    p->x = cosImuRollStart * x5 + sinImuRollStart * y5 + imuShiftFromStartXCur;
+    p->y = -sinImuRollStart * x5 + cosImuRollStart * y5 + imuShiftFromStartYCur;
+    p->z = z5 + imuShiftFromStartZCur;
+  }
+
+  // adjustDistortion :491-619
   void adjustDistortion() {
     bool halfPassed = false;
     const int n = (int)segmentedCloud.size();
@@ -492,7 +609,92 @@ struct FeatureAssociation {
       }
       float relTime = (ori - startOri) / oriDiff;
       point.intensity = (float)(int)segmentedCloud[i].intensity + c.scan_period * relTime;
+      if (imuPointerLast >= 0) {
+        const float pointTime = relTime * c.scan_period;
+        imuPointerFront = imuPointerLastIteration;
+        // imuPointerLastIteration is -1 when the previous scan saw no message:
+        // the reference then reads imuTime[-1] (undefined; SURVEY.md §9.7
+        // policy) — restated as a zero slot, which the scan time passes.
+        if (imuPointerFront < 0) imuPointerFront = 0;
+        while (imuPointerFront != imuPointerLast) {
+          if (stamp + pointTime < imuTime[imuPointerFront]) break;
+          imuPointerFront = (imuPointerFront + 1) % kImuQ;
+        }
+        const int f = imuPointerFront;
+        if (stamp + pointTime > imuTime[f]) {
+          imuRollCur = imuRoll[f]; imuPitchCur = imuPitch[f]; imuYawCur = imuYaw[f];
+          imuVeloXCur = imuVeloX[f]; imuVeloYCur = imuVeloY[f]; imuVeloZCur = imuVeloZ[f];
+          imuShiftXCur = imuShiftX[f]; imuShiftYCur = imuShiftY[f]; imuShiftZCur = imuShiftZ[f];
+        } else {
+          const int b = (f + kImuQ - 1) % kImuQ;
+          const float ratioFront = (float)((stamp + pointTime - imuTime[b]) / (imuTime[f] - imuTime[b]));
+          const float ratioBack = (float)((imuTime[f] - stamp - pointTime) / (imuTime[f] - imuTime[b]));
+          imuRollCur = imuRoll[f] * ratioFront + imuRoll[b] * ratioBack;
+          imuPitchCur = imuPitch[f] * ratioFront + imuPitch[b] * ratioBack;
+          if ((double)(imuYaw[f] - imuYaw[b]) > M_PI)
+            imuYawCur = (float)(imuYaw[f] * ratioFront + (imuYaw[b] + 2 * M_PI) * ratioBack);
+          else if ((double)(imuYaw[f] - imuYaw[b]) < -M_PI)
+            imuYawCur = (float)(imuYaw[f] * ratioFront + (imuYaw[b] - 2 * M_PI) * ratioBack);
+          else
+            imuYawCur = imuYaw[f] * ratioFront + imuYaw[b] * ratioBack;
+          imuVeloXCur = imuVeloX[f] * ratioFront + imuVeloX[b] * ratioBack;
+          imuVeloYCur = imuVeloY[f] * ratioFront + imuVeloY[b] * ratioBack;
+          imuVeloZCur = imuVeloZ[f] * ratioFront + imuVeloZ[b] * ratioBack;
+          imuShiftXCur = imuShiftX[f] * ratioFront + imuShiftX[b] * ratioBack;
+          imuShiftYCur = imuShiftY[f] * ratioFront + imuShiftY[b] * ratioBack;
+          imuShiftZCur = imuShiftZ[f] * ratioFront + imuShiftZ[b] * ratioBack;
+        }
+        if (i == 0) {
+          imuRollStart = imuRollCur; imuPitchStart = imuPitchCur; imuYawStart = imuYawCur;
+          imuVeloXStart = imuVeloXCur; imuVeloYStart = imuVeloYCur; imuVeloZStart = imuVeloZCur;
+          imuShiftXStart = imuShiftXCur; imuShiftYStart = imuShiftYCur; imuShiftZStart = imuShiftZCur;
+          if (stamp + pointTime > imuTime[f]) {
+            imuAngularRotationXCur = imuAngularRotationX[f];
+            imuAngularRotationYCur = imuAngularRotationY[f];
+            imuAngularRotationZCur = imuAngularRotationZ[f];
+          } else {
+            const int b = (f + kImuQ - 1) % kImuQ;
+            const float ratioFront = (float)((stamp + pointTime - imuTime[b]) / (imuTime[f] - imuTime[b]));
+            const float ratioBack = (float)((imuTime[f] - stamp - pointTime) / (imuTime[f] - imuTime[b]));
+            imuAngularRotationXCur = imuAngularRotationX[f] * ratioFront + imuAngularRotationX[b] * ratioBack;
+            imuAngularRotationYCur = imuAngularRotationY[f] * ratioFront + imuAngularRotationY[b] * ratioBack;
+            imuAngularRotationZCur = imuAngularRotationZ[f] * ratioFront + imuAngularRotationZ[b] * ratioBack;
+          }
+          imuAngularFromStartX = imuAngularRotationXCur - imuAngularRotationXLast;
+          imuAngularFromStartY = imuAngularRotationYCur - imuAngularRotationYLast;
+          imuAngularFromStartZ = imuAngularRotationZCur - imuAngularRotationZLast;
+          imuAngularRotationXLast = imuAngularRotationXCur;
+          imuAngularRotationYLast = imuAngularRotationYCur;
+          imuAngularRotationZLast = imuAngularRotationZCur;
+          updateImuStartSinCos();
+        } else {
+          veloToStartIMU();
+          transformToStartIMU(&point);
+        }
+      }
       segmentedCloud[i] = point;
+    }
+    imuPointerLastIteration = imuPointerLast;
+  }
+
+  // updateInitialGuess :1639-1664
+  void updateInitialGuess() {
+    imuPitchLast = imuPitchCur; imuYawLast = imuYawCur; imuRollLast = imuRollCur;
+    imuShiftFromStartX = imuShiftFromStartXCur;
+    imuShiftFromStartY = imuShiftFromStartYCur;
+    imuShiftFromStartZ = imuShiftFromStartZCur;
+    imuVeloFromStartX = imuVeloFromStartXCur;
+    imuVeloFromStartY = imuVeloFromStartYCur;
+    imuVeloFromStartZ = imuVeloFromStartZCur;
+    if (imuAngularFromStartX != 0 || imuAngularFromStartY != 0 || imuAngularFromStartZ != 0) {
+      transformCur[0] = -imuAngularFromStartY;
+      transformCur[1] = -imuAngularFromStartZ;
+      transformCur[2] = -imuAngularFromStartX;
+    }
+    if (imuVeloFromStartX != 0 || imuVeloFromStartY != 0 || imuVeloFromStartZ != 0) {
+      transformCur[3] -= imuVeloFromStartX * c.scan_period;
+      transformCur[4] -= imuVeloFromStartY * c.scan_period;
+      transformCur[5] -= imuVeloFromStartZ * c.scan_period;
     }
   }
 
@@ -1028,9 +1230,7 @@ struct FeatureAssociation {
 
   // publishCloudsLast :1759-1815
   void publishCloudsLast() {
-    cosImuRollStart = lego_cosf(imuRollStart); cosImuPitchStart = lego_cosf(imuPitchStart);
-    cosImuYawStart = lego_cosf(imuYawStart); sinImuRollStart = lego_sinf(imuRollStart);
-    sinImuPitchStart = lego_sinf(imuPitchStart); sinImuYawStart = lego_sinf(imuYawStart);
+    updateImuStartSinCos();
     for (Pt& p : lessSharp) toEnd(p, p);
     for (Pt& p : lessFlat) toEnd(p, p);
     std::swap(lessSharp, cornerLast);
@@ -1093,6 +1293,7 @@ struct FeatureAssociation {
       odomValid = false;
       return LEGO_OK;
     }
+    updateInitialGuess();
     updateTransformation();
     integrateTransformation();
     odomValid = true;
@@ -1196,6 +1397,15 @@ extern "C" int lego_oracle_fa_process(lego_oracle* o, const lego_ip_out* in, leg
     out->corner_last = fa.outCornerLast.data(); out->n_corner_last = (int32_t)fa.outCornerLast.size();
     out->surf_last = fa.outSurfLast.data(); out->n_surf_last = (int32_t)fa.outSurfLast.size();
     out->outlier_last = fa.outOutlierLast.data(); out->n_outlier_last = (int32_t)fa.outOutlierLast.size();
+  }
+  return LEGO_OK;
+}
+
+extern "C" int lego_oracle_imu_push(lego_oracle* o, const lego_imu_msg* msgs, int32_t n) {
+  if (!o || n < 0 || (n > 0 && !msgs)) return LEGO_E_ARG;
+  for (int i = 0; i < n; ++i) {  // both nodes subscribe to /imu_raw
+    o->fa->imuHandler(msgs[i]);
+    o->mo->imuHandler(msgs[i]);
   }
   return LEGO_OK;
 }

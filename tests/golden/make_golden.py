@@ -96,6 +96,47 @@ def mapping_fixture(L, sensor, seed, n, name, fixed_map):
                         fixed_map=np.array(fixed_map or [], np.float64))
 
 
+def imu_before(imu, stamps, period):
+    """Delivery rule of the IMU fixtures: the messages stamped before the end
+    of scan k's sweep (stamp + scan period) reach the handlers before scan k
+    is processed."""
+    return np.searchsorted(imu["stamp"], np.asarray(stamps) + period, side="left").astype(np.int32)
+
+
+def imu_fixture(L, sensor, seed, n, name, imu_t0, rate_hz):
+    """The VLP-16 stream with /imu_raw from imu_t0 on (the first scans see no
+    message: the imuPointerLast < 0 branch, then the switch-over), odometry
+    and keyframe scan-to-map after every scan."""
+    sc = L.synth_cfg(sensor, seed)
+    ora = L.Oracle(L.sensor_cfg(sensor))
+    period = float(sc.scan_period)
+    imu = L.synth_imu(sc, imu_t0, n * period + period, rate_hz)
+    stamps = [L.synth_scan(sc, k)[1] for k in range(n)]
+    before = imu_before(imu, stamps, period)
+    sums, counts, shas, aft, info = [], [], [], [], []
+    j = 0
+    for k in range(n):
+        pts, stamp = L.synth_scan(sc, k)
+        ora.imu(imu[j:before[k]])
+        j = before[k]
+        ip = ora.ip(pts, stamp)
+        fa = ora.fa()
+        o = ora.mo()
+        sums.append(fa["transform_sum"])
+        counts.append([len(ip["segmented"]), len(fa["sharp"]), len(fa["less_sharp"]), len(fa["flat"]),
+                       len(fa["less_flat"]), fa["odom_valid"], fa["publish_to_mapping"]])
+        shas.append(sha(np.concatenate([fa[k2].view(np.uint8) for k2 in
+                                        ("sharp", "less_sharp", "flat", "less_flat")])))
+        aft.append(o["transform_aft_mapped"])
+        info.append([o["processed"], o["optimized"], o["iterations"], o["n_rows_last"], o["n_corner_map_ds"],
+                     o["n_surf_map_ds"], o["n_corner_scan_ds"], o["n_surf_scan_ds"]])
+    np.savez_compressed(OUT / f"{name}.npz", transform_sum=np.array(sums, np.float32),
+                        counts=np.array(counts, np.int32), feat_sha=np.array(shas, dtype="S64"),
+                        transform_aft_mapped=np.array(aft, np.float32), info=np.array(info, np.int32),
+                        imu=imu.view(np.uint8), imu_before=before, sensor=np.bytes_(sensor),
+                        seed=np.int64(seed))
+
+
 def main():
     L = ffi()
     scan_fixture(L, "VLP-16", 0, 0, "vlp16_seed0_scan0", full=True)
@@ -103,6 +144,7 @@ def main():
     stream_fixture(L, "VLP-16", 1, 20, "vlp16_seed1_stream20")
     mapping_fixture(L, "VLP-16", 6, 24, "vlp16_seed6_keyframe_map24", None)
     mapping_fixture(L, "VLP-16", 3, 10, "vlp16_seed3_fixed_map10", (3, 50.0, 200000, 40000))
+    imu_fixture(L, "VLP-16", 6, 24, "vlp16_seed6_imu100_map24", 0.25, 100.0)
     for p in sorted(OUT.glob("*.npz")):
         print(p.name, p.stat().st_size)
 

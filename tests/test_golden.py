@@ -153,3 +153,92 @@ def test_product_reproduces_mapping_fixture(L, name):
         exact += int(np.array_equal(o["transform_aft_mapped"].view(np.uint32),
                                     g["transform_aft_mapped"][k].view(np.uint32)))
     print(f"{name}: bit-exact mapped poses {exact}/{len(out)}")
+
+
+# ---------------------------------------------------------------- /imu_raw
+def _imu_fixture_run(L, g, eng, gpu):
+    """Node-shaped replay of the IMU fixture: the messages before each scan,
+    then ip -> fa -> mo."""
+    sensor = g["sensor"].item().decode()
+    sc = L.synth_cfg(sensor, int(g["seed"]))
+    imu = g["imu"].view(L.IMU_DTYPE)
+    before = g["imu_before"]
+    outs = []
+    j = 0
+    for k in range(len(before)):
+        pts, stamp = L.synth_scan(sc, k)
+        eng.imu(imu[j:before[k]])
+        j = int(before[k])
+        ip = eng.ip(pts, stamp)
+        fa = eng.fa()
+        outs.append((ip, fa, eng.mo()))
+    return outs
+
+
+def _check_imu_fixture(g, outs, pose_exact):
+    for k, (ip, fa, mo) in enumerate(outs):
+        c = [len(ip["segmented"]), len(fa["sharp"]), len(fa["less_sharp"]), len(fa["flat"]),
+             len(fa["less_flat"]), fa["odom_valid"], fa["publish_to_mapping"]]
+        np.testing.assert_array_equal(c, g["counts"][k], err_msg=str(k))
+        feats = np.concatenate([fa[key].view(np.uint8) for key in ("sharp", "less_sharp", "flat", "less_flat")])
+        assert sha(feats) == g["feat_sha"][k].decode(), k
+        if pose_exact:
+            np.testing.assert_array_equal(np.asarray(fa["transform_sum"], np.float32).view(np.uint32),
+                                          g["transform_sum"][k].view(np.uint32), err_msg=str(k))
+        else:
+            assert np.abs(np.asarray(fa["transform_sum"], np.float64) - g["transform_sum"][k]).max() <= 1e-4, k
+        info = [mo["processed"], mo["optimized"], mo["iterations"], mo["n_rows_last"], mo["n_corner_map_ds"],
+                mo["n_surf_map_ds"], mo["n_corner_scan_ds"], mo["n_surf_scan_ds"]]
+        if pose_exact:
+            np.testing.assert_array_equal(info, g["info"][k], err_msg=str(k))
+            np.testing.assert_array_equal(mo["transform_aft_mapped"].view(np.uint32),
+                                          g["transform_aft_mapped"][k].view(np.uint32), err_msg=str(k))
+        else:
+            np.testing.assert_array_equal(np.array(info)[[0, 1, 4, 5, 6, 7]], g["info"][k][[0, 1, 4, 5, 6, 7]],
+                                          err_msg=str(k))
+            assert np.abs(mo["transform_aft_mapped"].astype(np.float64) - g["transform_aft_mapped"][k]).max() <= 1e-4
+
+
+def test_oracle_reproduces_imu_fixture(L):
+    g = load("vlp16_seed6_imu100_map24")
+    outs = _imu_fixture_run(L, g, L.Oracle(L.sensor_cfg("VLP-16")), False)
+    _check_imu_fixture(g, outs, True)
+
+
+@pytest.mark.gpu
+def test_product_reproduces_imu_fixture(L):
+    """/imu_raw through lego_imu_push + the node calls: IMU deskew, initial
+    guess, integration, hand-off and the mapping blend."""
+    g = load("vlp16_seed6_imu100_map24")
+    eng = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=40000)
+    outs = _imu_fixture_run(L, g, eng, True)
+    eng.close()
+    _check_imu_fixture(g, outs, False)
+
+
+@pytest.mark.gpu
+def test_product_reproduces_imu_fixture_batched(L):
+    """The same stream through lego_odom_batch_imu in three batches, the
+    messages of each batch scheduled by imu_before."""
+    g = load("vlp16_seed6_imu100_map24")
+    sc = L.synth_cfg("VLP-16", int(g["seed"]))
+    imu = g["imu"].view(L.IMU_DTYPE)
+    before = g["imu_before"].astype(np.int64)
+    n = len(before)
+    scans = [L.synth_scan(sc, k) for k in range(n)]
+    eng = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=40000, max_batch=10)
+    recs = []
+    j0 = 0
+    for lo, hi in ((0, 7), (7, 15), (15, n)):
+        pts = np.concatenate([p for p, _ in scans[lo:hi]])
+        off = np.zeros(hi - lo + 1, np.int64)
+        off[1:] = np.cumsum([len(p) for p, _ in scans[lo:hi]])
+        j1 = int(before[hi]) if hi < n else len(imu)  # this batch's messages end where the next scan's start
+        b = (before[lo:hi] - j0).astype(np.int32)
+        recs += list(eng.odom_batch(pts, off, np.array([s for _, s in scans[lo:hi]]), imu[j0:j1], b))
+        j0 = j1
+    eng.close()
+    for k, r in enumerate(recs):
+        c = [r.n_segmented, r.n_sharp, r.n_less_sharp, r.n_flat, r.n_less_flat, r.odom_valid]
+        np.testing.assert_array_equal(c, g["counts"][k][:6], err_msg=str(k))
+        assert np.abs(np.array(list(r.transform_sum), np.float64) - g["transform_sum"][k]).max() <= 1e-4, k

@@ -224,3 +224,45 @@ def test_voxel_order_deviation_bounded(L):
         assert len(fa["less_flat"]) == len(fb["less_flat"])
         worst = max(worst, float(np.max(np.abs(fa["transform_sum"].astype(np.float64) - fb["transform_sum"]))))
     assert worst <= 1e-4, worst
+
+
+def test_level_stationary_imu(L):
+    """KAT: an IMU that reads level, still and gravity only (identity
+    orientation, zero gyro, a = +g) leaves every de-skewed point and the
+    odometry exactly as without an IMU — all IMU angles, velocities and
+    angular increments are 0, so TransformToStartIMU / PluginIMURotation /
+    TransformToEnd reduce to identities (sin 0 = 0, cos 0 = 1).  Mapping
+    differs only by transformUpdate's blend toward the level attitude
+    (mapOptmization.cpp:488-489): at the first optimized step
+    aft[0] = (float)(0.998 * aft_noimu[0] + 0.002 * 0), likewise aft[2]."""
+    sc = L.synth_cfg("VLP-16", 2)
+    cfg = L.sensor_cfg("VLP-16")
+    a, b = L.Oracle(cfg), L.Oracle(cfg)
+    imu = np.zeros(60, dtype=L.IMU_DTYPE)
+    imu["stamp"] = 0.005 + 0.01 * np.arange(60)
+    imu["orientation"][:, 3] = 1.0
+    imu["linear_acceleration"][:, 2] = 9.81
+    j = 0
+    blended = False
+    for k in range(6):
+        pts, st = L.synth_scan(sc, k)
+        n = int(np.searchsorted(imu["stamp"], st + 0.1))
+        b.imu(imu[j:n])
+        j = n
+        a.ip(pts, st); fa_a = a.fa(); mo_a = a.mo()
+        b.ip(pts, st); fa_b = b.fa(); mo_b = b.mo()
+        assert np.array_equal(fa_a["transform_sum"].view(np.uint32), fa_b["transform_sum"].view(np.uint32)), k
+        for key in ("sharp", "less_sharp", "flat", "less_flat"):
+            assert np.array_equal(fa_a[key].view(np.float32), fa_b[key].view(np.float32)), (k, key)
+        if blended:
+            continue
+        if mo_a["optimized"]:
+            ta, tb = mo_a["transform_aft_mapped"], mo_b["transform_aft_mapped"]
+            for i in (0, 2):
+                assert tb[i] == np.float32(0.998 * np.float64(ta[i]) + 0.002 * 0.0), (k, i)
+            for i in (1, 3, 4, 5):
+                assert tb[i] == ta[i], (k, i)
+            blended = True
+        else:
+            assert np.array_equal(mo_a["transform_aft_mapped"], mo_b["transform_aft_mapped"]), k
+    assert blended
