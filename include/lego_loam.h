@@ -233,6 +233,63 @@ int lego_odom_batch_imu(lego_ctx* ctx, const lego_point_xyzir* pts,
 /* After lego_odom_batch: fetch full per-scan outputs of scan k of that batch. */
 int lego_batch_fetch(lego_ctx* ctx, int32_t k, lego_ip_out* ip, lego_fa_out* fa);
 
+/* ---- Wire formats: sensor_msgs/PointCloud2 and
+ * cloud_msgs/cloud_info as they travel between the ROS nodes. */
+
+/* sensor_msgs/PointField datatypes. */
+enum { LEGO_PF_INT8 = 1, LEGO_PF_UINT8 = 2, LEGO_PF_INT16 = 3, LEGO_PF_UINT16 = 4,
+       LEGO_PF_INT32 = 5, LEGO_PF_UINT32 = 6, LEGO_PF_FLOAT32 = 7, LEGO_PF_FLOAT64 = 8 };
+
+typedef struct lego_pc2_field {
+  char name[16];
+  uint32_t offset;
+  uint8_t datatype;
+  uint32_t count;
+} lego_pc2_field;
+
+/* A sensor_msgs/PointCloud2 (header stamp as seconds).  data holds
+ * height x row_step bytes; host or device memory as the call says. */
+typedef struct lego_pc2_msg {
+  double stamp;
+  uint32_t height, width, point_step, row_step;
+  uint8_t is_bigendian, is_dense;
+  int32_t n_fields;
+  const lego_pc2_field* fields;
+  const uint8_t* data;
+} lego_pc2_msg;
+
+/* pcl::fromROSMsg into PointXYZIR (imageProjection.cpp:166, 172): each of
+ * x, y, z, intensity (FLOAT32) and ring (UINT16) is copied from the field of
+ * that name, datatype and count 1; a field without a match stays 0 (PCL
+ * warns and skips it).  Big-endian data is LEGO_E_ARG.  is_dense == 0 is
+ * LEGO_E_NOT_DENSE (:173-176).  Decoding runs on the device; out is host
+ * memory with room for height x width points. */
+int lego_pc2_decode(lego_ctx* ctx, const lego_pc2_msg* msg, lego_point_xyzir* out,
+                    int32_t cap, int32_t* n_out);
+/* cloudHandler on a raw /velodyne_points message (decode + lego_ip_process). */
+int lego_ip_process_pc2(lego_ctx* ctx, const lego_pc2_msg* msg, uint32_t flags, lego_ip_out* out);
+/* lego_odom_batch over nscans raw messages (msgs[k].data: device pointers
+ * when on_device != 0, host otherwise); stamps from the messages. */
+int lego_odom_batch_pc2(lego_ctx* ctx, const lego_pc2_msg* msgs, int32_t nscans,
+                        int32_t on_device, lego_pose_rec* recs);
+
+/* pcl::toROSMsg of a PointXYZI cloud (the /segmented_cloud, /outlier_cloud,
+ * /laser_cloud_* payloads): fields x@0 y@4 z@8 intensity@16 FLOAT32,
+ * point_step 32, height 1, dense.  Writes 32 * n bytes to data (bytes 12-15
+ * carry PCL's data[3] = 1.0f, the rest of the padding is 0) and the 4
+ * fields to fields4. */
+int lego_pc2_encode_xyzi(const lego_point_xyzi* pts, int32_t n, uint8_t* data,
+                         lego_pc2_field* fields4);
+/* ROS1 wire bytes of a cloud_msgs/cloud_info (cloud_info.msg:1-12):
+ * Header {seq, stamp = ros::Time::fromSec(info->stamp), frame_id}, then the
+ * arrays with their uint32 lengths — startRingIndex / endRingIndex n_scan,
+ * the three per-point arrays P = n_scan x horizon_scan (the reference
+ * publishes them at full length, imageProjection.cpp:125-130).  *len gets
+ * the size; with buf == NULL only the size is computed. */
+int lego_cloud_info_serialize(const lego_cloud_info* info, int32_t n_scan, int32_t horizon_scan,
+                              uint32_t seq, const char* frame_id, uint8_t* buf, uint64_t cap,
+                              uint64_t* len);
+
 /* Mapping (scan-to-map).  lego_mo_set_map installs a fixed surrounding map
  * (config 5) instead of the keyframe-built one; pass NULLs to go back to the
  * keyframe map of mapOptmization.cpp:1001-1056. */

@@ -21,6 +21,7 @@
 #include "lego_kernels.h"
 #include "lego_mo.h"
 #include "lego_loam.h"
+#include "lego_wire.h"
 
 using namespace lego;
 
@@ -94,6 +95,11 @@ struct lego_ctx {
   bool lastIpDevice = false;  // lastIp describes batch slot 0 on device
   // /imu_raw: featureAssociation's and mapOptimization's queues (host), the
   // per-scan snapshots of the former for a batch
+  // raw PointCloud2 staging (lego_*_pc2): grown on demand
+  uint8_t* d_raw = nullptr;
+  size_t rawCap = 0;
+  Pc2Desc* d_desc = nullptr;
+  std::vector<Pc2Desc> h_desc;
   FaImuQueue faImu;
   MoImuQueue moImu;
   std::vector<ImuSnap> h_imu;
@@ -113,6 +119,7 @@ struct lego_ctx {
   }
   ~lego_ctx() {
     if (device >= 0) (void)hipSetDevice(device);
+    if (d_raw) (void)hipFree(d_raw);
     for (void* p : allocs) (void)hipFree(p);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -297,6 +304,7 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
   A(bb.f_lflat, B * P);
   A(bb.f_cnt, B * 4);
   A(bb.imuScan, B);
+  A(x->d_desc, B);
   A(x->d_imu, B);
   bb.imu = nullptr;
   OdomBufs& ob = x->ob;
@@ -936,6 +944,109 @@ int lego_mo_process(lego_ctx* x, const lego_fa_out* in, lego_mo_out* out) {
   out->n_surf_scan_ds = hc.surfTotalDS;
   out->n_rows_last = hs.rowsLast;
   return LEGO_OK;
+}
+
+// ---------------------------------------------------------------- PointCloud2
+// Decodes K messages (pcl::fromROSMsg, lego_wire.hip) into the context's
+// point buffer, scan k at points [off[k], off[k+1]).  Host data is staged
+// through one device copy per message.
+static int pc2_stage(lego_ctx* x, const lego_pc2_msg* msgs, int K, bool onDevice, std::vector<int64_t>& off) {
+  x->h_desc.resize(K);
+  off.assign(K + 1, 0);
+  size_t raw = 0;
+  uint64_t maxPts = 0;
+  for (int k = 0; k < K; ++k) {
+    if (pc2_plan(&msgs[k], &x->h_desc[k]) != LEGO_OK) {
+      set_err("PointCloud2 %d: bad layout (big-endian, point_step, row_step or a field past point_step)", k);
+      return LEGO_E_ARG;
+    }
+    if (!msgs[k].is_dense) {  // imageProjection.cpp:173-176
+      set_err("PointCloud2 %d is not dense (is_dense = false)", k);
+      return LEGO_E_NOT_DENSE;
+    }
+    const uint64_t n = (uint64_t)msgs[k].height * msgs[k].width;
+    if (n == 0) {
+      set_err("PointCloud2 %d is empty", k);
+      return LEGO_E_ARG;
+    }
+    if (n > (uint64_t)x->maxPoints) {
+      set_err("PointCloud2 %d has %llu points > capacity %d", k, (unsigned long long)n, x->maxPoints);
+      return LEGO_E_CAPACITY;
+    }
+    if (!msgs[k].data) return LEGO_E_ARG;
+    x->h_desc[k].outBase = (uint64_t)off[k];
+    off[k + 1] = off[k] + (int64_t)n;
+    raw += (size_t)msgs[k].height * msgs[k].row_step;
+    maxPts = std::max(maxPts, n);
+  }
+  if (!onDevice) {
+    if (raw > x->rawCap) {
+      if (x->d_raw) HIPCHK(hipFree(x->d_raw));
+      x->d_raw = nullptr;
+      x->rawCap = 0;
+      HIPCHK(hipMalloc(&x->d_raw, raw));
+      x->rawCap = raw;
+    }
+    size_t o = 0;
+    for (int k = 0; k < K; ++k) {
+      const size_t bytes = (size_t)msgs[k].height * msgs[k].row_step;
+      HIPCHK(hipMemcpyAsync(x->d_raw + o, msgs[k].data, bytes, hipMemcpyHostToDevice, x->stream));
+      x->h_desc[k].data = x->d_raw + o;
+      o += bytes;
+    }
+  }
+  HIPCHK(hipMemcpyAsync(x->d_desc, x->h_desc.data(), sizeof(Pc2Desc) * K, hipMemcpyHostToDevice, x->stream));
+  if (launch_pc2_decode(x->d_desc, K, maxPts, x->d_pts, x->stream) != 0) {
+    set_err("PointCloud2 decode launch failed");
+    return LEGO_E_DEVICE;
+  }
+  HIPCHK(hipMemcpyAsync(x->d_off, off.data(), sizeof(int64_t) * (K + 1), hipMemcpyHostToDevice, x->stream));
+  return LEGO_OK;
+}
+
+int lego_pc2_decode(lego_ctx* x, const lego_pc2_msg* msg, lego_point_xyzir* out, int32_t cap, int32_t* n_out) {
+  if (!x || !msg || !out || !n_out) return LEGO_E_ARG;
+  HIPCHK(hipSetDevice(x->device));
+  std::vector<int64_t> off;
+  const int st = pc2_stage(x, msg, 1, false, off);
+  if (st != LEGO_OK) return st;
+  if (off[1] > cap) return LEGO_E_CAPACITY;
+  HIPCHK(hipMemcpyAsync(out, x->d_pts, sizeof(lego_point_xyzir) * off[1], hipMemcpyDeviceToHost, x->stream));
+  HIPCHK(hipStreamSynchronize(x->stream));
+  *n_out = (int32_t)off[1];
+  return LEGO_OK;
+}
+
+int lego_ip_process_pc2(lego_ctx* x, const lego_pc2_msg* msg, uint32_t flags, lego_ip_out* out) {
+  if (!x || !msg || !out) return LEGO_E_ARG;
+  HIPCHK(hipSetDevice(x->device));
+  std::vector<int64_t> off;
+  int st = pc2_stage(x, msg, 1, false, off);
+  if (st != LEGO_OK) return st;
+  x->stamps.assign(1, msg->stamp);
+  st = run_batch(x, x->d_pts, x->d_off, 1, 1, (flags & LEGO_IP_IMAGES) ? 1 : 0, false);
+  if (st != LEGO_OK) return st;
+  st = fetch_ip(x, 0, (flags & LEGO_IP_IMAGES) != 0, out);
+  if (st != LEGO_OK) return st;
+  x->lastIp = *out;
+  x->lastIpDevice = true;
+  return LEGO_OK;
+}
+
+int lego_odom_batch_pc2(lego_ctx* x, const lego_pc2_msg* msgs, int32_t nscans, int32_t on_device,
+                        lego_pose_rec* recs) {
+  if (!x || !msgs || nscans <= 0 || !recs) return LEGO_E_ARG;
+  if (nscans > x->maxBatch) {
+    set_err("batch of %d scans > context capacity %d", nscans, x->maxBatch);
+    return LEGO_E_CAPACITY;
+  }
+  HIPCHK(hipSetDevice(x->device));
+  std::vector<int64_t> off;
+  const int st = pc2_stage(x, msgs, nscans, on_device != 0, off);
+  if (st != LEGO_OK) return st;
+  std::vector<double> stamps(nscans);
+  for (int k = 0; k < nscans; ++k) stamps[k] = msgs[k].stamp;
+  return lego_odom_batch(x, x->d_pts, x->d_off, stamps.data(), nscans, 1, recs);
 }
 
 int lego_odom_profile(lego_ctx* x, int32_t enable, uint64_t* out32) {

@@ -114,6 +114,44 @@ IMU_DTYPE = np.dtype([("stamp", np.float64), ("orientation", np.float64, 4),
 assert IMU_DTYPE.itemsize == 88
 
 
+class Pc2Field(C.Structure):  # lego_pc2_field (sensor_msgs/PointField)
+    _fields_ = [("name", C.c_char * 16), ("offset", C.c_uint32), ("datatype", C.c_uint8),
+                ("count", C.c_uint32)]
+
+
+class Pc2Msg(C.Structure):  # lego_pc2_msg (sensor_msgs/PointCloud2)
+    _fields_ = [("stamp", C.c_double), ("height", C.c_uint32), ("width", C.c_uint32),
+                ("point_step", C.c_uint32), ("row_step", C.c_uint32), ("is_bigendian", C.c_uint8),
+                ("is_dense", C.c_uint8), ("n_fields", C.c_int32), ("fields", C.POINTER(Pc2Field)),
+                ("data", C.c_void_p)]
+
+
+PF = {"INT8": 1, "UINT8": 2, "INT16": 3, "UINT16": 4, "INT32": 5, "UINT32": 6, "FLOAT32": 7, "FLOAT64": 8}
+
+
+def pc2_msg(data: np.ndarray, fields: list[tuple[str, int, int, int]], point_step: int, width: int,
+            height: int = 1, row_step: int | None = None, stamp: float = 0.0, is_dense: int = 1,
+            is_bigendian: int = 0):
+    """A Pc2Msg over the uint8 buffer `data` (kept alive by the caller);
+    fields: (name, offset, datatype, count)."""
+    arr = (Pc2Field * max(1, len(fields)))()
+    for i, (nm, off, dt, cnt) in enumerate(fields):
+        arr[i].name = nm.encode()
+        arr[i].offset = off
+        arr[i].datatype = dt
+        arr[i].count = cnt
+    m = Pc2Msg()
+    m.stamp = stamp
+    m.height, m.width, m.point_step = height, width, point_step
+    m.row_step = row_step if row_step is not None else width * point_step
+    m.is_bigendian, m.is_dense = is_bigendian, is_dense
+    m.n_fields = len(fields)
+    m.fields = C.cast(arr, C.POINTER(Pc2Field))
+    m.data = data.ctypes.data
+    m._keep = (arr, data)
+    return m
+
+
 class SynthCfg(C.Structure):
     _fields_ = [("n_scan", C.c_int32), ("horizon_scan", C.c_int32), ("vert_min_deg", C.c_float),
                 ("vert_max_deg", C.c_float), ("mount_height", C.c_float),
@@ -177,7 +215,8 @@ def oracle_lib() -> C.CDLL:
 
 HIP_EXPORTS = ["lego_sensor_preset", "lego_create", "lego_fleet_create", "lego_destroy", "lego_reset",
                "lego_ip_process", "lego_fa_process", "lego_odom_batch", "lego_odom_batch_imu",
-               "lego_imu_push", "lego_batch_fetch",
+               "lego_imu_push", "lego_batch_fetch", "lego_pc2_decode", "lego_ip_process_pc2",
+               "lego_odom_batch_pc2", "lego_pc2_encode_xyzi", "lego_cloud_info_serialize",
                "lego_mo_set_map", "lego_mo_process", "lego_last_error", "lego_stage_times",
                "lego_odom_profile"]
 
@@ -200,6 +239,12 @@ def hip_lib() -> C.CDLL:
     lib.lego_odom_batch_imu.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
                                         C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
     lib.lego_imu_push.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
+    lib.lego_pc2_decode.argtypes = [C.c_void_p, C.POINTER(Pc2Msg), C.c_void_p, C.c_int32, C.POINTER(C.c_int32)]
+    lib.lego_ip_process_pc2.argtypes = [C.c_void_p, C.POINTER(Pc2Msg), C.c_uint32, C.POINTER(IpOut)]
+    lib.lego_odom_batch_pc2.argtypes = [C.c_void_p, C.POINTER(Pc2Msg), C.c_int32, C.c_int32, C.c_void_p]
+    lib.lego_pc2_encode_xyzi.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(Pc2Field)]
+    lib.lego_cloud_info_serialize.argtypes = [C.POINTER(CloudInfo), C.c_int32, C.c_int32, C.c_uint32,
+                                              C.c_char_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
     lib.lego_batch_fetch.argtypes = [C.c_void_p, C.c_int32, C.POINTER(IpOut), C.POINTER(FaOut)]
     lib.lego_mo_set_map.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32]
     lib.lego_mo_process.argtypes = [C.c_void_p, C.POINTER(FaOut), C.POINTER(MoOut)]
