@@ -230,6 +230,19 @@ int lego_odom_batch_imu(lego_ctx* ctx, const lego_point_xyzir* pts,
                         const int64_t* offsets, const double* stamps,
                         int32_t nscans, int32_t on_device, const lego_imu_msg* imu,
                         int32_t n_imu, const int32_t* imu_before, lego_pose_rec* recs);
+/* Asynchronous form: lego_odom_batch_submit enqueues a batch (arguments as
+ * lego_odom_batch_imu; pass imu = NULL, n_imu = 0 without IMU) and returns;
+ * lego_odom_batch_wait blocks for the oldest submitted batch and writes its
+ * cap >= nscans records.  At most two batches are in flight (LEGO_E_STATE
+ * otherwise): the second one's projection and extraction run while the
+ * first one's odometry chain does.  The node-shaped calls and lego_reset
+ * need no batch in flight.  Host input arrays may be reused once submit
+ * returns; device inputs must stay valid until the wait. */
+int lego_odom_batch_submit(lego_ctx* ctx, const lego_point_xyzir* pts,
+                           const int64_t* offsets, const double* stamps,
+                           int32_t nscans, int32_t on_device, const lego_imu_msg* imu,
+                           int32_t n_imu, const int32_t* imu_before);
+int lego_odom_batch_wait(lego_ctx* ctx, lego_pose_rec* recs, int32_t cap, int32_t* nscans);
 /* After lego_odom_batch: fetch full per-scan outputs of scan k of that batch. */
 int lego_batch_fetch(lego_ctx* ctx, int32_t k, lego_ip_out* ip, lego_fa_out* fa);
 

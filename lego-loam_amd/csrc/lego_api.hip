@@ -11,6 +11,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <atomic>
 #include <cstring>
 #include <new>
 #include <string>
@@ -70,7 +71,18 @@ struct lego_ctx {
   int device = 0;
   int maxPoints = 0, maxBatch = 0;  // maxBatch: scans per call over all streams
   int nStreams = 1;                   // a fleet context carries nStreams independent streams
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;   // image projection + feature extraction (and everything else)
+  hipStream_t ostream = nullptr;  // the odometry chain (overlaps the next batch's extraction)
+  // Two batch slots: the per-scan buffers hold 2 x maxBatch scans; batch n
+  // uses slot n % 2, so batch n + 1's projection + extraction (stream) run
+  // while batch n's odometry (ostream) still reads its slot.
+  hipEvent_t faDone[2] = {nullptr, nullptr};    // extraction of the slot's batch finished
+  hipEvent_t recsDone[2] = {nullptr, nullptr};  // the slot's packed records are on the host
+  hipEvent_t oJoin = nullptr;                   // ostream work so far (node calls order after it)
+  int nextSlot = 0, inflight = 0, oldest = 0;
+  int slotB[2] = {0, 0};
+  std::vector<double> slotStamps[2];
+  int lastBase = 0;  // first scan slot of the batch lego_batch_fetch reads
   BatchBufs bb{};
   OdomBufs ob{};
   FaCarry* d_carry = nullptr;
@@ -79,7 +91,8 @@ struct lego_ctx {
   lego_point_xyzir* d_pts = nullptr;
   int64_t* d_off = nullptr;
   std::vector<void*> allocs;
-  StageTimer tm;
+  StageTimer tm, otm;            // node-shaped calls
+  StageTimer stm[2], sotm[2];    // per batch slot: extraction / odometry stages
   // last batch
   int lastB = 0;
   std::vector<double> stamps;
@@ -100,6 +113,11 @@ struct lego_ctx {
   size_t rawCap = 0;
   Pc2Desc* d_desc = nullptr;
   std::vector<Pc2Desc> h_desc;
+  PackedRec* d_pack = nullptr;  // [maxBatch + 1]
+  PackedRec* h_pack = nullptr;  // pinned
+  int64_t* h_offp = nullptr;    // pinned [maxBatch + 1]: device offsets read back for validation
+  OdomState* h_resetSt = nullptr;   // pinned [S]: construction state (ctx_reset)
+  FaCarry* h_resetCarry = nullptr;  // pinned [S]
   FaImuQueue faImu;
   MoImuQueue moImu;
   std::vector<ImuSnap> h_imu;
@@ -119,8 +137,20 @@ struct lego_ctx {
   }
   ~lego_ctx() {
     if (device >= 0) (void)hipSetDevice(device);
+    if (stream) (void)hipStreamSynchronize(stream);  // batches still in flight
+    if (ostream) (void)hipStreamSynchronize(ostream);
     if (d_raw) (void)hipFree(d_raw);
+    if (h_pack) (void)hipHostFree(h_pack);
+    if (h_offp) (void)hipHostFree(h_offp);
+    if (h_resetSt) (void)hipHostFree(h_resetSt);
+    if (h_resetCarry) (void)hipHostFree(h_resetCarry);
     for (void* p : allocs) (void)hipFree(p);
+    if (oJoin) (void)hipEventDestroy(oJoin);
+    for (int i = 0; i < 2; ++i) {
+      if (faDone[i]) (void)hipEventDestroy(faDone[i]);
+      if (recsDone[i]) (void)hipEventDestroy(recsDone[i]);
+    }
+    if (ostream) (void)hipStreamDestroy(ostream);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -154,17 +184,17 @@ static int make_devcfg(const lego_sensor_cfg* c, DevCfg* d) {
   return LEGO_OK;
 }
 
+// Back to construction state.  The device state is reset in stream order —
+// the odometry state on the odometry stream, the FA carry on the extraction
+// stream — so batches already submitted finish with the old state and the
+// next one starts fresh (from a constant pinned image).
 static int ctx_reset(lego_ctx* x) {
-  OdomState st;
-  std::memset(&st, 0, sizeof(st));
-  st.frameCount = x->cfg.skip_frame_num;  // frameCount = skipFrameNum (:314)
-  const std::vector<OdomState> sts(x->nStreams, st);
-  HIPCHK(hipMemcpyAsync(x->ob.st, sts.data(), sizeof(st) * x->nStreams, hipMemcpyHostToDevice, x->stream));
-  // fresh member arrays: phantom {0.0f, 0}, picked[0] = 0
-  const std::vector<FaCarry> cz(x->nStreams, FaCarry{});
-  HIPCHK(hipMemcpyAsync(x->d_carry, cz.data(), sizeof(FaCarry) * x->nStreams, hipMemcpyHostToDevice,
+  HIPCHK(hipMemcpyAsync(x->ob.st, x->h_resetSt, sizeof(OdomState) * x->nStreams, hipMemcpyHostToDevice,
+                        x->ostream));
+  HIPCHK(hipMemcpyAsync(x->d_carry, x->h_resetCarry, sizeof(FaCarry) * x->nStreams, hipMemcpyHostToDevice,
                         x->stream));
-  HIPCHK(hipStreamSynchronize(x->stream));
+  // the next batch's odometry must also follow the reset of its own stream's
+  // carry: it already waits for that batch's extraction (faDone)
   x->lastIpDevice = false;
   x->lastB = 0;
   x->faImu = FaImuQueue{};
@@ -254,7 +284,14 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
   auto fail = [&](int st) { delete x; return st; };
   if (hipSetDevice(device) != hipSuccess) return fail(LEGO_E_DEVICE);
   if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess) return fail(LEGO_E_DEVICE);
-  const size_t B = max_batch, P = dc.P, N = dc.N;
+  if (hipStreamCreateWithFlags(&x->ostream, hipStreamNonBlocking) != hipSuccess) return fail(LEGO_E_DEVICE);
+  if (hipEventCreateWithFlags(&x->oJoin, hipEventDisableTiming) != hipSuccess) return fail(LEGO_E_DEVICE);
+  for (int i = 0; i < 2; ++i)
+    if (hipEventCreateWithFlags(&x->faDone[i], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&x->recsDone[i], hipEventDisableTiming) != hipSuccess)
+      return fail(LEGO_E_DEVICE);
+  // B: per-scan slots (two batches); input staging is one batch
+  const size_t B = 2 * (size_t)max_batch, B1 = max_batch, P = dc.P, N = dc.N;
   BatchBufs& bb = x->bb;
   bb.B = max_batch;
   bb.Nmax = max_points;
@@ -263,8 +300,8 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
     set_err("hipMalloc failed for %s", #ptr);               \
     return fail(LEGO_E_DEVICE);                             \
   }
-  A(x->d_pts, B * max_points);
-  A(x->d_off, B + 1);
+  A(x->d_pts, B1 * max_points);
+  A(x->d_off, B1 + 1);
   A(bb.owner, B * P);
   A(bb.range, B * P);
   A(bb.full, B * P);
@@ -305,7 +342,18 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
   A(bb.f_cnt, B * 4);
   A(bb.imuScan, B);
   A(x->d_desc, B);
-  A(x->d_imu, B);
+  A(x->d_pack, 2 * (B1 + 1));
+  if (hipHostMalloc(&x->h_pack, sizeof(PackedRec) * 2 * (B1 + 1), hipHostMallocDefault) != hipSuccess) {
+    x->h_pack = nullptr;
+    set_err("hipHostMalloc failed for the record buffer");
+    return fail(LEGO_E_DEVICE);
+  }
+  if (hipHostMalloc(&x->h_offp, sizeof(int64_t) * (B1 + 1), hipHostMallocDefault) != hipSuccess) {
+    x->h_offp = nullptr;
+    set_err("hipHostMalloc failed for the offsets buffer");
+    return fail(LEGO_E_DEVICE);
+  }
+  A(x->d_imu, B1);
   bb.imu = nullptr;
   OdomBufs& ob = x->ob;
   ob.capLS = (int)(N * kLessSharpPerRing);
@@ -315,11 +363,10 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
   ob.S = n_streams;
   A(ob.st, S);
   {
-    // workgroups of the odometry launch (cooperative: all resident at once)
-    int cus = 0, coop = 0;
+    // workgroups of the odometry launch
+    int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 1;
-    if (hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device) != hipSuccess) coop = 0;
-    ob.G = coop ? odom_workgroups((int)N, cus) : 1;
+    ob.G = odom_workgroups((int)N, cus);
     // a fleet's streams share the device: S x G workgroups, all resident
     if (n_streams > 1) ob.G = std::max(1, std::min(ob.G, cus / n_streams));
     // diagnostic override (profiling / scaling studies); never above the default
@@ -342,8 +389,10 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
     A(ob.cnt, G * ob.cntCap);
     ob.capQ = (int)(N * kFlatPerRing);
     A(ob.qi, G * 3 * ob.capQ);
-    // exchange block: 16-byte timeout word, then per stream 2 x 3 x capQ granules
-    ob.xbytes = 16 + S * sizeof(unsigned long long) * 2 * 3 * (size_t)ob.capQ;
+    // exchange block: 16-byte error word, then per stream one slot of 3 x capQ
+    // granules per NN round a launch can run (10 per scan)
+    ob.roundsCap = 10 * (int)((B1 + S - 1) / S);
+    ob.xbytes = 16 + S * sizeof(unsigned long long) * (size_t)ob.roundsCap * 3 * (size_t)ob.capQ;
     unsigned char* xb = nullptr;
     A(xb, ob.xbytes);
     ob.xblock = xb;
@@ -357,6 +406,16 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
   A(ob.cornerEnd, B * ob.capLS);
   A(ob.surfEnd, B * P);
   A(x->d_carry, S);
+  if (hipHostMalloc(&x->h_resetSt, sizeof(OdomState) * S, hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc(&x->h_resetCarry, sizeof(FaCarry) * S, hipHostMallocDefault) != hipSuccess) {
+    set_err("hipHostMalloc failed for the reset image");
+    return fail(LEGO_E_DEVICE);
+  }
+  for (size_t i = 0; i < S; ++i) {
+    std::memset(&x->h_resetSt[i], 0, sizeof(OdomState));
+    x->h_resetSt[i].frameCount = cfg->skip_frame_num;  // frameCount = skipFrameNum (:314)
+    x->h_resetCarry[i] = FaCarry{};  // fresh member arrays: phantom {0.0f, 0}, picked[0] = 0
+  }
   A(x->d_prof, 32);
 #undef A
   bb.pts = x->d_pts;
@@ -432,20 +491,63 @@ static int imu_stage(lego_ctx* x, int B, const lego_imu_msg* imu, int n_imu, con
   return LEGO_OK;
 }
 
-static int run_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offsets, int B,
-                     int on_device, int want_labels, bool with_fa, const lego_imu_msg* imu = nullptr,
-                     int n_imu = 0, const int32_t* imu_before = nullptr) {
+// ---------------------------------------------------------------- batch slots
+// The per-scan device views of scan slots [c0, c0 + n).
+static BatchBufs bb_slice(const BatchBufs& a, const DevCfg& c, int c0, int n) {
+  BatchBufs b = a;
+  const size_t k = (size_t)c0, P = c.P, N = c.N;
+  b.B = n;
+  if (b.imu) b.imu += k;
+  b.imuScan += k;
+  b.off += k;
+  b.owner += k * P; b.range += k * P; b.full += k * P; b.ground += k * P; b.label += k * P;
+  b.parent += k * P; b.root += k * P; b.edges += k * P; b.csize += k * P;
+  b.rowmask += k * P * 2; b.rawang += k * 2; b.bad += k;
+  b.seg += k * P; b.gflag += k * P; b.col += k * P; b.srange += k * P; b.outl += k * P;
+  b.ns += k; b.nout += k; b.sri += k * N; b.eri += k * N; b.orient += k * 3;
+  b.firsthalf += k; b.dsk += k * P; b.curv += k * P; b.pick0 += k * P;
+  b.r_sharp += k * N * kSharpPerRing; b.r_lsharp += k * N * kLessSharpPerRing;
+  b.r_flat += k * N * kFlatPerRing; b.r_lflat += k * P; b.r_cnt += k * N * 4;
+  b.spec_out += k; b.fa_flags += k;
+  b.f_sharp += k * N * kSharpPerRing; b.f_lsharp += k * N * kLessSharpPerRing;
+  b.f_flat += k * N * kFlatPerRing; b.f_lflat += k * P; b.f_cnt += k * 4;
+  return b;
+}
+
+// The odometry view of streams [s0, s0 + S) whose scans are the slots from c0.
+static OdomBufs ob_slice(const OdomBufs& a, const DevCfg& c, int c0, int s0, int S) {
+  OdomBufs o = a;
+  o.S = S;
+  o.st += s0;
+  const size_t w = (size_t)s0 * a.G, k = (size_t)c0;
+  for (int i = 0; i < 2; ++i) {
+    o.cornerLast[i] += w * a.capCorner;
+    o.surfLast[i] += w * a.capSurf;
+  }
+  o.nC.gEnd += w * a.gTC; o.nC.gOrd += w * a.capCorner;
+  o.nS.gEnd += w * a.gTS; o.nS.gOrd += w * a.capSurf;
+  o.cnt += w * a.cntCap;
+  o.qi += w * 3 * a.capQ;
+  o.xg += (size_t)s0 * a.roundsCap * 3 * a.capQ;
+  o.sumOut += k * 6; o.curOut += k * 6; o.validOut += k; o.pubOut += k;
+  o.cornerEnd += k * a.capLS; o.surfEnd += k * c.P;
+  return o;
+}
+
+// Validates a batch and points bb (a slot view) at its input points: the
+// caller's device arrays, or a copy of host arrays in the staging buffer.
+static int stage_inputs(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offsets, int B,
+                        int on_device, BatchBufs& bb) {
   HIPCHK(hipSetDevice(x->device));
-  BatchBufs bb = x->bb;
   // Per-scan sizes are validated on the host in both modes: an empty scan is
   // undefined upstream (findStartEndAngle reads points[0] and points[size-1],
   // imageProjection.cpp:201-203) and a scan above capacity would overrun the
   // per-point work buffers.
   std::vector<int64_t> off(B + 1);
   if (on_device) {
-    HIPCHK(hipMemcpyAsync(off.data(), offsets, sizeof(int64_t) * (B + 1), hipMemcpyDeviceToHost,
-                          x->stream));
+    HIPCHK(hipMemcpyAsync(x->h_offp, offsets, sizeof(int64_t) * (B + 1), hipMemcpyDeviceToHost, x->stream));
     HIPCHK(hipStreamSynchronize(x->stream));
+    for (int k = 0; k <= B; ++k) off[k] = x->h_offp[k];
   } else {
     for (int k = 0; k <= B; ++k) off[k] = offsets[k];
   }
@@ -478,39 +580,144 @@ static int run_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* of
     bb.off = x->d_off;
   }
   bb.Nmax = mx;
-  if (with_fa) {
-    const int st = imu_stage(x, B, imu, n_imu, imu_before, &bb.imu);
-    if (st != LEGO_OK) return st;
+  return LEGO_OK;
+}
+
+// Image projection only (lego_ip_process*): slot 0, synchronous.
+static int run_ip(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offsets, int B, int on_device,
+                  int want_labels) {
+  if (x->inflight) {
+    set_err("node-shaped call while batches are in flight (lego_odom_batch_wait first)");
+    return LEGO_E_STATE;
   }
+  BatchBufs bb = x->bb;
+  int st = stage_inputs(x, pts, offsets, B, on_device, bb);
+  if (st != LEGO_OK) return st;
   HIPCHK(hipMemsetAsync(bb.bad, 0, sizeof(int) * B, x->stream));
   x->tm.begin();
   launch_ip(bb, x->dc, B, want_labels, x->stream, &x->tm);
-  if (with_fa) {
-    launch_fa(bb, x->dc, B, x->nStreams, x->d_carry, x->stream, &x->tm);
-    if (launch_odom(bb, x->ob, x->dc, B / x->nStreams, x->stream, &x->tm, x->profOn ? x->d_prof : nullptr) != 0) {
-      set_err("odometry launch failed (%d workgroups)", x->ob.G);
-      return LEGO_E_DEVICE;
-    }
-  }
   x->tm.end(x->stream);
   HIPCHK(hipGetLastError());
   x->h_bad.resize(B);
   HIPCHK(hipMemcpyAsync(x->h_bad.data(), bb.bad, sizeof(int) * B, hipMemcpyDeviceToHost, x->stream));
-  unsigned xerr = 0;
-  if (with_fa) HIPCHK(hipMemcpyAsync(&xerr, x->ob.xerr, sizeof(xerr), hipMemcpyDeviceToHost, x->stream));
   HIPCHK(hipStreamSynchronize(x->stream));
-  if (xerr) {
-    set_err("odometry workgroup exchange timed out");
-    return LEGO_E_DEVICE;
-  }
-  x->tm.collect(x->tnames, x->tms);
+  x->tnames.clear();
+  x->tms.clear();
+  std::vector<int> cnt;
+  x->tm.collect(x->tnames, x->tms, cnt);
   x->lastB = B;
+  x->lastBase = 0;
   for (int k = 0; k < B; ++k)
     if (x->h_bad[k]) {
       x->lastB = 0;
       set_err("scan %d of the batch has non-finite xyz (the cloud must be dense)", k);
       return LEGO_E_NOT_DENSE;
     }
+  return LEGO_OK;
+}
+
+// Enqueues ip + fa + odometry for a batch (x->stamps) in the next slot and
+// returns.  Projection and extraction run on x->stream, the odometry on
+// x->ostream after them, so they overlap the previous batch's odometry.
+static int submit_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offsets, int B, int on_device,
+                        const lego_imu_msg* imu, int n_imu, const int32_t* imu_before) {
+  if (x->inflight >= 2) {
+    set_err("two batches in flight: lego_odom_batch_wait before submitting another");
+    return LEGO_E_STATE;
+  }
+  const int h = x->nextSlot, base = h * x->maxBatch;
+  BatchBufs bb = bb_slice(x->bb, x->dc, base, B);
+  int st = stage_inputs(x, pts, offsets, B, on_device, bb);
+  if (st != LEGO_OK) return st;
+  st = imu_stage(x, B, imu, n_imu, imu_before, &bb.imu);
+  if (st != LEGO_OK) return st;
+  const int S = x->nStreams;
+  StageTimer& tm = x->stm[h];
+  StageTimer& otm = x->sotm[h];
+  tm.enabled = otm.enabled = x->tm.enabled;
+  HIPCHK(hipMemsetAsync(bb.bad, 0, sizeof(int) * B, x->stream));
+  tm.begin();
+  otm.begin();
+  launch_ip(bb, x->dc, B, 0, x->stream, &tm);
+  launch_fa(bb, x->dc, B, S, x->d_carry, x->stream, &tm);
+  tm.end(x->stream);
+  HIPCHK(hipEventRecord(x->faDone[h], x->stream));
+  HIPCHK(hipStreamWaitEvent(x->ostream, x->faDone[h], 0));
+  HIPCHK(hipMemsetAsync(x->ob.xerr, 0, sizeof(unsigned), x->ostream));
+  const OdomBufs ob = ob_slice(x->ob, x->dc, base, 0, S);
+  if (launch_odom(bb, ob, x->dc, B / S, x->ostream, &otm, x->profOn ? x->d_prof : nullptr) != 0) {
+    set_err("odometry launch failed (%d workgroups)", x->ob.G);
+    return LEGO_E_DEVICE;
+  }
+  otm.end(x->ostream);
+  // the batch's records, non-dense flags and the error word in one copy
+  PackedRec* dp = x->d_pack + (size_t)h * (x->maxBatch + 1);
+  launch_pack_recs(bb, ob, B, dp, x->ostream);
+  HIPCHK(hipMemcpyAsync(x->h_pack + (size_t)h * (x->maxBatch + 1), dp, sizeof(PackedRec) * (B + 1),
+                        hipMemcpyDeviceToHost, x->ostream));
+  HIPCHK(hipEventRecord(x->recsDone[h], x->ostream));
+  HIPCHK(hipGetLastError());
+  x->slotB[h] = B;
+  x->slotStamps[h] = x->stamps;
+  if (x->inflight == 0) x->oldest = h;
+  x->inflight++;
+  x->nextSlot = h ^ 1;
+  return LEGO_OK;
+}
+
+// Waits for the oldest batch in flight and writes its pose records.
+static int wait_batch(lego_ctx* x, lego_pose_rec* recs, int cap, int* nOut) {
+  if (!x->inflight) {
+    set_err("no batch in flight");
+    return LEGO_E_STATE;
+  }
+  const int h = x->oldest, B = x->slotB[h];
+  HIPCHK(hipEventSynchronize(x->recsDone[h]));
+  x->inflight--;
+  x->oldest = h ^ 1;
+  const PackedRec* pk = x->h_pack + (size_t)h * (x->maxBatch + 1);
+  x->tnames.clear();
+  x->tms.clear();
+  std::vector<int> cnt;
+  x->stm[h].collect(x->tnames, x->tms, cnt);
+  x->sotm[h].collect(x->tnames, x->tms, cnt);
+  for (size_t i = 0, m = x->tnames.size(); i < m; ++i) {  // launches per stage, as "n:<stage>"
+    x->tnames.push_back("n:" + x->tnames[i]);
+    x->tms.push_back((float)cnt[i]);
+  }
+  x->lastB = 0;
+  if (pk[B].bad) {
+    set_err("odometry exchange overflow (more NN rounds than slots)");
+    return LEGO_E_DEVICE;
+  }
+  for (int k = 0; k < B; ++k)
+    if (pk[k].bad) {
+      set_err("scan %d of the batch has non-finite xyz (the cloud must be dense)", k);
+      return LEGO_E_NOT_DENSE;
+    }
+  if (cap < B) {
+    set_err("record buffer of %d < %d scans", cap, B);
+    return LEGO_E_ARG;
+  }
+  const std::vector<double>& stamps = x->slotStamps[h];
+  for (int k = 0; k < B; ++k) {
+    const PackedRec& p = pk[k];
+    lego_pose_rec& r = recs[k];
+    std::memset(&r, 0, sizeof(r));
+    r.stamp = k < (int)stamps.size() ? stamps[k] : 0.0;
+    for (int i = 0; i < 6; ++i) r.transform_sum[i] = p.sum[i];
+    r.n_segmented = p.ns;
+    r.n_sharp = p.cnt[0];
+    r.n_less_sharp = p.cnt[1];
+    r.n_flat = p.cnt[2];
+    r.n_less_flat = p.cnt[3];
+    r.odom_valid = p.valid;
+    r.flags = p.flags;
+  }
+  x->stamps = stamps;
+  x->lastB = B;
+  x->lastBase = h * x->maxBatch;
+  if (nOut) *nOut = B;
   return LEGO_OK;
 }
 
@@ -540,7 +747,8 @@ static int fetch_ip(lego_ctx* x, int k, bool images, lego_ip_out* o) {
   }
   HIPCHK(hipStreamSynchronize(s));
   std::memset(o, 0, sizeof(*o));
-  o->info.stamp = (k < (int)x->stamps.size()) ? x->stamps[k] : 0.0;
+  const int kr = k - x->lastBase;  // index within the batch
+  o->info.stamp = (kr < (int)x->stamps.size()) ? x->stamps[kr] : 0.0;
   o->info.start_ring_index = x->h_sri.data();
   o->info.end_ring_index = x->h_eri.data();
   o->info.start_orientation = orient[0];
@@ -589,7 +797,8 @@ static int fetch_fa(lego_ctx* x, int k, lego_fa_out* o) {
     x->h_outlLast[i] = {p.y, p.z, p.x, p.intensity};
   }
   std::memset(o, 0, sizeof(*o));
-  o->stamp = (k < (int)x->stamps.size()) ? x->stamps[k] : 0.0;
+  const int kr = k - x->lastBase;
+  o->stamp = (kr < (int)x->stamps.size()) ? x->stamps[kr] : 0.0;
   o->sharp = x->h_sharp.data(); o->n_sharp = cnt[0];
   o->less_sharp = x->h_lsharp.data(); o->n_less_sharp = cnt[1];
   o->flat = x->h_flat.data(); o->n_flat = cnt[2];
@@ -615,7 +824,7 @@ int lego_ip_process(lego_ctx* x, const lego_point_xyzir* pts, int32_t n, double 
       return LEGO_E_NOT_DENSE;
   int64_t off[2] = {0, n};
   x->stamps.assign(1, stamp);
-  int st = run_batch(x, pts, off, 1, 0, (flags & LEGO_IP_IMAGES) ? 1 : 0, false);
+  int st = run_ip(x, pts, off, 1, 0, (flags & LEGO_IP_IMAGES) ? 1 : 0);
   if (st != LEGO_OK) return st;
   st = fetch_ip(x, 0, (flags & LEGO_IP_IMAGES) != 0, out);
   if (st != LEGO_OK) return st;
@@ -653,6 +862,10 @@ static int upload_ip(lego_ctx* x, const lego_ip_out* in) {
 
 int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
   if (!x || !in || !out) return LEGO_E_ARG;
+  if (x->inflight) {
+    set_err("node-shaped call while batches are in flight (lego_odom_batch_wait first)");
+    return LEGO_E_STATE;
+  }
   if (x->nStreams != 1) {
     set_err("lego_fa_process needs a single-stream context");
     return LEGO_E_ARG;
@@ -666,11 +879,14 @@ int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
   }
   x->stamps.assign(1, in->info.stamp);
   BatchBufs bb = x->bb;
+  HIPCHK(hipEventRecord(x->oJoin, x->ostream));  // e.g. a reset of the odometry state
+  HIPCHK(hipStreamWaitEvent(x->stream, x->oJoin, 0));
   {
     const int st = imu_stage(x, 1, nullptr, 0, nullptr, &bb.imu);
     if (st != LEGO_OK) return st;
   }
   x->tm.begin();
+  HIPCHK(hipMemsetAsync(x->ob.xerr, 0, sizeof(unsigned), x->stream));
   launch_fa(bb, x->dc, 1, 1, x->d_carry, x->stream, &x->tm);
   if (launch_odom(bb, x->ob, x->dc, 1, x->stream, &x->tm, x->profOn ? x->d_prof : nullptr) != 0) {
     set_err("odometry launch failed (%d workgroups)", x->ob.G);
@@ -682,10 +898,11 @@ int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
   HIPCHK(hipMemcpyAsync(&xerr, x->ob.xerr, sizeof(xerr), hipMemcpyDeviceToHost, x->stream));
   HIPCHK(hipStreamSynchronize(x->stream));
   if (xerr) {
-    set_err("odometry workgroup exchange timed out");
+    set_err("odometry exchange overflow (more NN rounds than slots)");
     return LEGO_E_DEVICE;
   }
   x->lastB = 1;
+  x->lastBase = 0;
   x->lastIpDevice = false;
   return fetch_fa(x, 0, out);
 }
@@ -705,10 +922,10 @@ int lego_imu_push(lego_ctx* x, const lego_imu_msg* msgs, int32_t n) {
   return LEGO_OK;
 }
 
-int lego_odom_batch_imu(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offsets,
-                        const double* stamps, int32_t nscans, int32_t on_device, const lego_imu_msg* imu,
-                        int32_t n_imu, const int32_t* imu_before, lego_pose_rec* recs) {
-  if (!x || !pts || !offsets || nscans <= 0 || !recs) return LEGO_E_ARG;
+int lego_odom_batch_submit(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offsets,
+                           const double* stamps, int32_t nscans, int32_t on_device, const lego_imu_msg* imu,
+                           int32_t n_imu, const int32_t* imu_before) {
+  if (!x || !pts || !offsets || nscans <= 0) return LEGO_E_ARG;
   if (n_imu < 0 || (n_imu > 0 && (!imu || !imu_before))) return LEGO_E_ARG;
   if (n_imu > 0) {
     if (x->nStreams != 1) {
@@ -729,44 +946,43 @@ int lego_odom_batch_imu(lego_ctx* x, const lego_point_xyzir* pts, const int64_t*
     set_err("batch of %d scans is not %d streams x K scans", nscans, x->nStreams);
     return LEGO_E_ARG;
   }
+  HIPCHK(hipSetDevice(x->device));
   x->stamps.assign(stamps ? stamps : nullptr, stamps ? stamps + nscans : nullptr);
   if (!stamps) x->stamps.assign(nscans, 0.0);
-  int st = run_batch(x, pts, offsets, nscans, on_device, 0, true, imu, n_imu, imu_before);
-  if (st != LEGO_OK) return st;
   x->lastIpDevice = false;
-  std::vector<float> sum(6 * nscans);
-  std::vector<int> valid(nscans), fcnt(4 * nscans), ns(nscans), flags(nscans);
-  hipStream_t s = x->stream;
-  HIPCHK(hipMemcpyAsync(sum.data(), x->ob.sumOut, sizeof(float) * 6 * nscans, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(valid.data(), x->ob.validOut, sizeof(int) * nscans, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(fcnt.data(), x->bb.f_cnt, sizeof(int) * 4 * nscans, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(ns.data(), x->bb.ns, sizeof(int) * nscans, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(flags.data(), x->bb.fa_flags, sizeof(int) * nscans, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  for (int k = 0; k < nscans; ++k) {
-    lego_pose_rec& r = recs[k];
-    std::memset(&r, 0, sizeof(r));
-    r.stamp = x->stamps[k];
-    for (int i = 0; i < 6; ++i) r.transform_sum[i] = sum[6 * k + i];
-    r.n_segmented = ns[k];
-    r.n_sharp = fcnt[4 * k];
-    r.n_less_sharp = fcnt[4 * k + 1];
-    r.n_flat = fcnt[4 * k + 2];
-    r.n_less_flat = fcnt[4 * k + 3];
-    r.odom_valid = valid[k];
-    r.flags = flags[k];
+  return submit_batch(x, pts, offsets, nscans, on_device, imu, n_imu, imu_before);
+}
+
+int lego_odom_batch_wait(lego_ctx* x, lego_pose_rec* recs, int32_t cap, int32_t* nscans) {
+  if (!x || !recs) return LEGO_E_ARG;
+  HIPCHK(hipSetDevice(x->device));
+  int n = 0;
+  const int st = wait_batch(x, recs, cap, &n);
+  if (nscans) *nscans = n;
+  return st;
+}
+
+int lego_odom_batch_imu(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offsets,
+                        const double* stamps, int32_t nscans, int32_t on_device, const lego_imu_msg* imu,
+                        int32_t n_imu, const int32_t* imu_before, lego_pose_rec* recs) {
+  if (!x || !recs) return LEGO_E_ARG;
+  if (x->inflight) {
+    set_err("lego_odom_batch with batches in flight (lego_odom_batch_wait first)");
+    return LEGO_E_STATE;
   }
-  return LEGO_OK;
+  const int st = lego_odom_batch_submit(x, pts, offsets, stamps, nscans, on_device, imu, n_imu, imu_before);
+  if (st != LEGO_OK) return st;
+  return lego_odom_batch_wait(x, recs, nscans, nullptr);
 }
 
 int lego_batch_fetch(lego_ctx* x, int32_t k, lego_ip_out* ip, lego_fa_out* fa) {
   if (!x || k < 0 || k >= x->lastB) return LEGO_E_ARG;
   HIPCHK(hipSetDevice(x->device));
   if (ip) {
-    int st = fetch_ip(x, k, false, ip);
+    int st = fetch_ip(x, x->lastBase + k, false, ip);
     if (st != LEGO_OK) return st;
   }
-  if (fa) return fetch_fa(x, k, fa);
+  if (fa) return fetch_fa(x, x->lastBase + k, fa);
   return LEGO_OK;
 }
 
@@ -1024,7 +1240,7 @@ int lego_ip_process_pc2(lego_ctx* x, const lego_pc2_msg* msg, uint32_t flags, le
   int st = pc2_stage(x, msg, 1, false, off);
   if (st != LEGO_OK) return st;
   x->stamps.assign(1, msg->stamp);
-  st = run_batch(x, x->d_pts, x->d_off, 1, 1, (flags & LEGO_IP_IMAGES) ? 1 : 0, false);
+  st = run_ip(x, x->d_pts, x->d_off, 1, 1, (flags & LEGO_IP_IMAGES) ? 1 : 0);
   if (st != LEGO_OK) return st;
   st = fetch_ip(x, 0, (flags & LEGO_IP_IMAGES) != 0, out);
   if (st != LEGO_OK) return st;
@@ -1065,7 +1281,7 @@ int lego_odom_profile(lego_ctx* x, int32_t enable, uint64_t* out32) {
 int lego_stage_times(lego_ctx* x, const char** names, float* ms, int32_t cap, int32_t* n) {
   if (!x || !n) return LEGO_E_ARG;
   if (cap == 0) {  // toggle: cap 0 with names == NULL enables/disables the timer
-    x->tm.enabled = ms != nullptr;
+    x->tm.enabled = x->otm.enabled = ms != nullptr;
     *n = 0;
     return LEGO_OK;
   }

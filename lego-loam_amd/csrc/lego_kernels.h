@@ -35,11 +35,12 @@ class StageTimer {
     names_.push_back(name);
   }
   void end(hipStream_t s) { mark("__end__", s); }
-  // Collapses repeated names into totals.  Call after a stream sync.
-  void collect(std::vector<std::string>& names, std::vector<float>& ms) const {
-    names.clear();
-    ms.clear();
+  // Collapses repeated names into totals (appended to names / ms, with the
+  // number of intervals per name in counts; "__gap__" marks time that belongs
+  // to no stage).  Call after a stream sync.
+  void collect(std::vector<std::string>& names, std::vector<float>& ms, std::vector<int>& counts) const {
     for (size_t i = 0; i + 1 < used_; ++i) {
+      if (names_[i] == "__gap__") continue;
       float t = 0;
       if (hipEventElapsedTime(&t, events_[i], events_[i + 1]) != hipSuccess) t = 0;
       size_t k = 0;
@@ -48,8 +49,10 @@ class StageTimer {
       if (k == names.size()) {
         names.push_back(names_[i]);
         ms.push_back(0);
+        counts.push_back(0);
       }
       ms[k] += t;
+      counts[k] += 1;
     }
   }
   ~StageTimer() {
@@ -101,9 +104,10 @@ struct OdomBufs {
   int capCorner, capSurf, capQ;
   int G;                  // workgroups per stream
   int S;                  // streams
+  int roundsCap;          // exchange slots (NN rounds) per stream and launch
   int wg;                 // set in the kernel: this workgroup's index within its stream
-  // exchange (zeroed before each launch): timeout word shared by the streams,
-  // then per stream 2 x 3 x capQ granules
+  // exchange: an error word shared by the streams (zeroed per batch), then
+  // per stream roundsCap x 3 x capQ granules (zeroed per launch)
   void* xblock;
   size_t xbytes;
   unsigned* xerr;
@@ -124,10 +128,19 @@ void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hip
 // order); d_carry[S].
 void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_carry, hipStream_t s,
                StageTimer* tm);
-// K scans per stream over ob.S streams.  Returns 0 on a successful launch.
+// K scans per stream over ob.S streams (the caller zeroes *ob.xerr once per
+// batch).  Returns 0 on a successful launch.
 int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int K, hipStream_t s,
                 StageTimer* tm, unsigned long long* prof);
 int odom_workgroups(int N, int cusAvailable);
+
+// One scan's pose-record fields, gathered on the device so a batch returns in
+// one copy; slot B of the array carries the exchange timeout word in `bad`.
+struct PackedRec {
+  float sum[6];
+  int ns, cnt[4], valid, flags, bad;
+};
+void launch_pack_recs(const BatchBufs& bb, const OdomBufs& ob, int B, PackedRec* out, hipStream_t s);
 // HBM index sizes for clouds of up to capCorner / capSurf points.
 void odom_index_caps(int capCorner, int capSurf, int* gTC, int* gTS);
 

@@ -886,24 +886,33 @@ __device__ __forceinline__ double r2d(double r) { return r * 180.0 / M_PI; }
 // The workgroups of a launch run the same serial chain on identical inputs
 // and split only the correspondence searches.  Results travel as 8-byte
 // {tag = round + 1, value} granules (MI355X L2s are per XCD: agent-scope
-// relaxed atomics, the data is its own flag), double-buffered by round parity
-// so a fast workgroup cannot overwrite a granule a slow one has yet to read.
-// The granules are zeroed before every launch.  A bounded spin records a
-// timeout in *err instead of hanging.
+// relaxed atomics, the data is its own flag), one slot per NN round of the
+// launch, zeroed before the launch.  Nothing assumes the launch's workgroups
+// are resident together: a granule that has not arrived within kStealTicks is
+// computed by the waiting wave itself (the search is deterministic: the same
+// bits as its owner's), and a workgroup that starts late replays the chain
+// from the rounds already published.  So a plain launch is safe next to any
+// other work on the device.
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
+constexpr unsigned long long kStealTicks = 4000;  // 40 us at the 100 MHz wall clock
 __device__ __forceinline__ void x_publish(unsigned long long* p, unsigned long long v) {
   __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ int x_consume(unsigned long long* p, unsigned long long tag, unsigned* err) {
-  for (unsigned spins = 0;; ++spins) {
+// Bounded wait for a granule; false when it did not arrive in time.  The
+// clock (an SMEM read) is consulted only every 32 polls.
+__device__ __forceinline__ bool x_try(const unsigned long long* p, unsigned long long tag, int* v) {
+  unsigned long long t0 = 0;
+  for (unsigned n = 0;; ++n) {
     const unsigned long long x = __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if ((x & 0xffffffff00000000ull) == tag) return (int)(unsigned)x;
-    if ((spins & 1023) == 1023 && __hip_atomic_load((gu32*)err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-      return -1;  // another wait already timed out: fail fast
-    if (spins > (1u << 20)) {
-      __hip_atomic_store((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return -1;
+    if ((x & 0xffffffff00000000ull) == tag) {
+      *v = (int)(unsigned)x;
+      return true;
+    }
+    if ((n & 31) == 0) {
+      const unsigned long long t = wall_clock64();
+      if (n == 0) t0 = t;
+      else if (t - t0 > kStealTicks) return false;
     }
     __builtin_amdgcn_s_sleep(1);
   }
@@ -975,29 +984,34 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
       // of the other workgroups of the launch arrive through the exchange.
       const int G = ob.G, per = (nQ + G - 1) / G;
       const int q0 = min(nQ, ob.wg * per), q1 = min(nQ, q0 + per);
-      const int round = L.n[N_ROUND];
-      unsigned long long* xg = ob.xg + (size_t)(round & 1) * 3 * ob.capQ;  // this stream's (odom_private)
+      int round = L.n[N_ROUND];
+      const bool xch = G > 1 && round < ob.roundsCap;
+      if (G > 1 && !xch && tid == 0) *ob.xerr = 1;  // more rounds than the slots (cannot happen: 10 per scan)
+      unsigned long long* xg = ob.xg + (size_t)round * 3 * ob.capQ;  // this stream's (odom_private)
       const unsigned long long tag = (unsigned long long)(round + 1) << 32;
       const bool w0 = S.prof && tid == 0;
-      for (int q = q0 + grp; q < q1; q += kNGrp) {
-        unsigned long long ta = w0 ? wall_clock64() : 0;
+      // findCorresponding{Surf,Corner}Features for query q by one wave
+      auto search = [&](int q, int& i1, int& i2, int& i3) {
         const float4 sel = to_start(qp[q], tc);
-        unsigned long long tb = w0 ? wall_clock64() : 0;
-        int i1 = stale ? nn_brute(snap, snapN, sel, c.nn_sq, g) : nn_i1(nn, sel, c.nn_sq, g, S.prof);
+        i1 = stale ? nn_brute(snap, snapN, sel, c.nn_sq, g) : nn_i1(nn, sel, c.nn_sq, g, S.prof);
         if (i1 >= lastN) i1 = -1;  // an index past a stale snapshot's cloud
-        unsigned long long tcn = w0 ? wall_clock64() : 0;
-        int i2 = -1, i3 = -1;
+        i2 = -1; i3 = -1;
         if (i1 >= 0 && (stale || !nn_lines(nn, i1, jend, sel, surf, c.nn_sq, g, &i2, &i3))) {
           if (S.prof && g == 0) atomicAdd(&S.prof[P_SCANLINE], 1ull);
           scanline_group(last, jend, i1, sel, surf, c.nn_sq, g, &i2, &i3);
         }
+      };
+      const int qa = xch ? q0 : 0, qb = xch ? q1 : nQ;  // no exchange: every query here
+      for (int q = qa + grp; q < qb; q += kNGrp) {
+        unsigned long long ta = w0 ? wall_clock64() : 0;
+        int i1, i2, i3;
+        search(q, i1, i2, i3);
         if (w0) {
-          const unsigned long long td = wall_clock64();
-          S.prof[27] += tb - ta; S.prof[28] += tcn - tb; S.prof[29] += td - tcn; S.prof[30] += 1;
+          S.prof[28] += wall_clock64() - ta; S.prof[30] += 1;
         }
         if (g == 0) {
           qi[q] = i1; qi[qs + q] = i2; qi[2 * qs + q] = i3;
-          if (G > 1) {
+          if (xch) {
             x_publish(xg + 3 * q + 0, tag | (unsigned)i1);
             x_publish(xg + 3 * q + 1, tag | (unsigned)i2);
             x_publish(xg + 3 * q + 2, tag | (unsigned)i3);
@@ -1005,11 +1019,33 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
         }
       }
       S.add(P_X_LOCAL);
-      if (G > 1) {
-        for (int e = tid; e < 3 * nQ; e += kOdomThreads) {
-          const int q = e / 3, k = e - 3 * q;
-          if (q >= q0 && q < q1) continue;
-          qi[k * qs + q] = x_consume(xg + e, tag, ob.xerr);
+      if (xch) {
+        // the other slices: lane l of a wave waits for granule l % 3 of query
+        // base + l / 3 (21 queries per pass); what does not arrive in time the
+        // wave computes itself
+        constexpr int kQPer = 21;
+        for (int base = grp * kQPer; base < nQ; base += kNGrp * kQPer) {
+          const int q = base + g / 3, k = g - 3 * (g / 3);
+          const bool want = g < 3 * kQPer && q < nQ && !(q >= q0 && q < q1);
+          bool got = !want;
+          if (want) {
+            int v;
+            got = x_try(xg + 3 * q + k, tag, &v);
+            if (got) qi[k * qs + q] = v;
+          }
+          unsigned long long miss = __ballot(!got);
+          while (miss) {
+            const int qm = base + (__ffsll((long long)miss) - 1) / 3;
+            int i1, i2, i3;
+            search(qm, i1, i2, i3);
+            if (g == 0) {
+              qi[qm] = i1; qi[qs + qm] = i2; qi[2 * qs + qm] = i3;
+              x_publish(xg + 3 * qm + 0, tag | (unsigned)i1);
+              x_publish(xg + 3 * qm + 1, tag | (unsigned)i2);
+              x_publish(xg + 3 * qm + 2, tag | (unsigned)i3);
+            }
+            miss &= ~(7ull << (3 * (qm - base)));
+          }
         }
       }
       __syncthreads();
@@ -1153,7 +1189,7 @@ __device__ __forceinline__ OdomBufs odom_private(OdomBufs ob) {
   ob.wg = blockIdx.x - s * ob.G;
   const size_t w = blockIdx.x;  // index into the [S x G x] arrays
   ob.st += s;
-  ob.xg += (size_t)s * 2 * 3 * ob.capQ;
+  ob.xg += (size_t)s * ob.roundsCap * 3 * ob.capQ;
   ob.cornerLast[0] += w * ob.capCorner;
   ob.cornerLast[1] += w * ob.capCorner;
   ob.surfLast[0] += w * ob.capSurf;
@@ -1169,6 +1205,10 @@ __device__ __forceinline__ OdomBufs odom_private(OdomBufs ob) {
 // [s*K, s*K + K) of the batch.
 __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs obShared, DevCfg c, int K,
                                                       unsigned long long* prof) {
+  // Claim the whole register file of the SIMD (2 waves x 256): no other
+  // kernel's waves share a SIMD with the latency-bound chain while the next
+  // chunk's extraction runs beside it.
+  asm volatile("v_mov_b32 v255, 0" ::: "v255");
   const OdomBufs ob = odom_private(obShared);
   const int b0 = (int)(blockIdx.x / ob.G) * K;
   const bool lead = ob.wg == 0;  // writes the stream's outputs and state
@@ -1211,7 +1251,9 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     ImuScan iq = {};
     if (bb.imu) iq = bb.imuScan[b];
     if (!init) {
-      // updateInitialGuess :1639-1664 (imuShiftFromStart* stays 0)
+      // updateInitialGuess :1639-1664 (imuShiftFromStart* stays 0; a no-op
+      // until the stream's first IMU message)
+      if (bb.imu) {
       if (tid == 0) {
         float* tc = st->transformCur;
         if (iq.angFromStart[0] != 0 || iq.angFromStart[1] != 0 || iq.angFromStart[2] != 0) {
@@ -1226,6 +1268,7 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
         }
       }
       __syncthreads();
+      }
       if (st->cornerLastNum >= 10 && st->surfLastNum >= 100) {
         if (st->resident) {
           for (int t = tid; t < F.nFlat; t += kOdomThreads) L.qflat[t] = F.flat[t];
@@ -1261,10 +1304,12 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     for (int i = 0; i < 6; ++i) tcur[i] = st->transformCur[i];
     const EndTrig et = end_trig(tcur);
     // updateImuRollPitchYawStartSinCos (:1761) and the imu*Last terms of TransformToEnd
-    const ImuEnd im{lego_cosf(iq.rollStart), lego_cosf(iq.pitchStart), lego_cosf(iq.yawStart),
-                    lego_sinf(iq.rollStart), lego_sinf(iq.pitchStart), lego_sinf(iq.yawStart),
-                    lego_cosf(iq.yawCur), lego_sinf(iq.yawCur), lego_cosf(iq.pitchCur),
-                    lego_sinf(iq.pitchCur), lego_cosf(iq.rollCur), lego_sinf(iq.rollCur)};
+    ImuEnd im{1.f, 1.f, 1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 1.f, 0.f, 1.f, 0.f};  // cos 0 / sin 0
+    if (bb.imu)
+      im = ImuEnd{lego_cosf(iq.rollStart), lego_cosf(iq.pitchStart), lego_cosf(iq.yawStart),
+                  lego_sinf(iq.rollStart), lego_sinf(iq.pitchStart), lego_sinf(iq.yawStart),
+                  lego_cosf(iq.yawCur), lego_sinf(iq.yawCur), lego_cosf(iq.pitchCur),
+                  lego_sinf(iq.pitchCur), lego_cosf(iq.rollCur), lego_sinf(iq.rollCur)};
     for (int t = tid; t < F.nLS; t += kOdomThreads) {
       const float4 p = init ? F.lsharp[t] : to_end(F.lsharp[t], tcur, et, im);
       gCn[t] = p;
@@ -1323,6 +1368,27 @@ void odom_index_caps(int capCorner, int capSurf, int* gTC, int* gTS) {
 
 // Workgroups of the odometry launch: LDS-resident sensors split each NN round
 // over one wave per query of the largest round (flat <= 24 N queries).
+__global__ void k_pack_recs(BatchBufs bb, OdomBufs ob, int B, PackedRec* out) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b > B) return;
+  PackedRec r = {};
+  if (b == B) {
+    r.bad = (int)*ob.xerr;
+  } else {
+    for (int i = 0; i < 6; ++i) r.sum[i] = ob.sumOut[b * 6 + i];
+    r.ns = bb.ns[b];
+    for (int i = 0; i < 4; ++i) r.cnt[i] = bb.f_cnt[b * 4 + i];
+    r.valid = ob.validOut[b];
+    r.flags = bb.fa_flags[b];
+    r.bad = bb.bad[b];
+  }
+  out[b] = r;
+}
+
+void launch_pack_recs(const BatchBufs& bb, const OdomBufs& ob, int B, PackedRec* out, hipStream_t s) {
+  k_pack_recs<<<(B + 1 + 63) / 64, 64, 0, s>>>(bb, ob, B, out);
+}
+
 int odom_workgroups(int N, int cusAvailable) {
   if (N * kFlatPerRing > kLdsQ) return 1;
   const int g = (N * kFlatPerRing + kOdomWaves - 1) / kOdomWaves;
@@ -1332,21 +1398,14 @@ int odom_workgroups(int N, int cusAvailable) {
 int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int K, hipStream_t s, StageTimer* tm,
                 unsigned long long* prof) {
   tm->mark("odom.lm", s);
-  // the exchange granules and the timeout word are zeroed before every launch
-  if (hipMemsetAsync(ob.xblock, 0, ob.xbytes, s) != hipSuccess) return -1;
-  const int blocks = ob.S * ob.G;
-  if (ob.G <= 1) {  // no exchange: the streams' workgroups need not be co-resident
-    k_odom<<<blocks, kOdomThreads, odom_lds_bytes(), s>>>(bb, ob, c, K, prof);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-  }
-  BatchBufs a0 = bb;
-  OdomBufs a1 = ob;
-  DevCfg a2 = c;
-  int a3 = K;
-  unsigned long long* a4 = prof;
-  void* args[] = {&a0, &a1, &a2, &a3, &a4};
-  return hipLaunchCooperativeKernel((const void*)k_odom, dim3(blocks), dim3(kOdomThreads), args,
-                                    (unsigned)odom_lds_bytes(), s) == hipSuccess ? 0 : -1;
+  // zero the exchange slots of the rounds this launch can use (10 per scan)
+  const size_t slot = (size_t)3 * ob.capQ * sizeof(unsigned long long);
+  const size_t bytes = ob.S == 1 ? std::min<size_t>(ob.roundsCap, (size_t)10 * K) * slot
+                                 : (size_t)ob.S * ob.roundsCap * slot;
+  if (ob.G > 1 && hipMemsetAsync(ob.xg, 0, bytes, s) != hipSuccess) return -1;
+  // A plain launch: the exchange needs no co-residency (see "exchange").
+  k_odom<<<ob.S * ob.G, kOdomThreads, odom_lds_bytes(), s>>>(bb, ob, c, K, prof);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 }  // namespace lego

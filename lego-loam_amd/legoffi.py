@@ -10,8 +10,10 @@ Libraries (all built in-tree by __graft_entry__.build()):
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
 import os
+import weakref
 from pathlib import Path
 
 import numpy as np
@@ -215,7 +217,7 @@ def oracle_lib() -> C.CDLL:
 
 HIP_EXPORTS = ["lego_sensor_preset", "lego_create", "lego_fleet_create", "lego_destroy", "lego_reset",
                "lego_ip_process", "lego_fa_process", "lego_odom_batch", "lego_odom_batch_imu",
-               "lego_imu_push", "lego_batch_fetch", "lego_pc2_decode", "lego_ip_process_pc2",
+               "lego_imu_push", "lego_odom_batch_submit", "lego_odom_batch_wait", "lego_batch_fetch", "lego_pc2_decode", "lego_ip_process_pc2",
                "lego_odom_batch_pc2", "lego_pc2_encode_xyzi", "lego_cloud_info_serialize",
                "lego_mo_set_map", "lego_mo_process", "lego_last_error", "lego_stage_times",
                "lego_odom_profile"]
@@ -239,6 +241,9 @@ def hip_lib() -> C.CDLL:
     lib.lego_odom_batch_imu.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
                                         C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
     lib.lego_imu_push.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
+    lib.lego_odom_batch_submit.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
+                                           C.c_int32, C.c_void_p, C.c_int32, C.c_void_p]
+    lib.lego_odom_batch_wait.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(C.c_int32)]
     lib.lego_pc2_decode.argtypes = [C.c_void_p, C.POINTER(Pc2Msg), C.c_void_p, C.c_int32, C.POINTER(C.c_int32)]
     lib.lego_ip_process_pc2.argtypes = [C.c_void_p, C.POINTER(Pc2Msg), C.c_uint32, C.POINTER(IpOut)]
     lib.lego_odom_batch_pc2.argtypes = [C.c_void_p, C.POINTER(Pc2Msg), C.c_int32, C.c_int32, C.c_void_p]
@@ -410,6 +415,18 @@ class Oracle:
                     if k.startswith("transform") else getattr(out, k)) for k, _ in MoOut._fields_}
 
 
+_live: "weakref.WeakSet[Lego]" = weakref.WeakSet()
+
+
+@atexit.register
+def _close_live_contexts():
+    """Destroys the contexts still open at interpreter exit, while the HIP
+    runtime (and torch's use of it) is still up: a context's destructor frees
+    device memory, pinned host buffers, events and streams."""
+    for g in list(_live):
+        g.close()
+
+
 class Lego:
     """The product pipeline (HIP) behind the C-ABI, one stream per context."""
 
@@ -428,6 +445,7 @@ class Lego:
                   "lego_create", self.lib)
         self._ip = IpOut()
         self._fa = FaOut()
+        _live.add(self)
 
     def close(self):
         if getattr(self, "h", None):
@@ -490,6 +508,21 @@ class Lego:
         mapOptimization queues (lego_imu_push)."""
         msgs = np.ascontiguousarray(msgs, dtype=IMU_DTYPE)
         check(self.lib.lego_imu_push(self.h, msgs.ctypes.data, len(msgs)), "lego_imu_push", self.lib)
+
+    def submit_device(self, pts_ptr: int, offsets_ptr: int, stamps: np.ndarray, k: int) -> None:
+        """lego_odom_batch_submit on device-resident inputs (returns at once)."""
+        stamps = np.ascontiguousarray(stamps, dtype=np.float64)
+        self._stamps_keep = stamps
+        check(self.lib.lego_odom_batch_submit(self.h, C.c_void_p(pts_ptr), C.c_void_p(offsets_ptr),
+                                              stamps.ctypes.data, k, 1, None, 0, None),
+              "lego_odom_batch_submit", self.lib)
+
+    def wait(self, recs) -> int:
+        """lego_odom_batch_wait: the oldest submitted batch's records."""
+        n = C.c_int32()
+        check(self.lib.lego_odom_batch_wait(self.h, recs, len(recs), C.byref(n)), "lego_odom_batch_wait",
+              self.lib)
+        return n.value
 
     def odom_batch_device(self, pts_ptr: int, offsets_ptr: int, stamps: np.ndarray, k: int, recs):
         check(self.lib.lego_odom_batch(self.h, C.c_void_p(pts_ptr), C.c_void_p(offsets_ptr),

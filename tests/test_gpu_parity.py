@@ -1,6 +1,8 @@
 """GPU parity: the HIP path through the C-ABI vs the CPU oracle on the same
 seeded synthetic scans.  Bit-exact for images, labels, the segmented cloud,
 cloud_info and feature clouds; poses within the north-star tolerance 1e-4."""
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -361,3 +363,82 @@ def test_fleet_equals_single_streams(L, workgroups):
     fl.close()
     for s in range(S):
         assert got[s] == ref[s], s
+
+
+def test_async_batches_equal_sync(L):
+    """lego_odom_batch_submit / _wait two deep (the second batch's extraction
+    overlapping the first one's odometry, the slots alternating) gives the
+    same records as synchronous lego_odom_batch calls; misuse is refused."""
+    cfg = L.sensor_cfg("VLP-16", L.hip_lib())
+    sc = L.synth_cfg("VLP-16", 11)
+    K, nb = 5, 4
+    scans = [L.synth_scan(sc, k) for k in range(K * nb)]
+
+    def pack(lo, hi):
+        pts = np.concatenate([p for p, _ in scans[lo:hi]])
+        off = np.zeros(hi - lo + 1, np.int64)
+        off[1:] = np.cumsum([len(p) for p, _ in scans[lo:hi]])
+        return pts, off, np.array([t for _, t in scans[lo:hi]])
+
+    a = L.Lego(cfg, max_points=40000, max_batch=K)
+    ref = [bytes(a.odom_batch(*pack(i * K, (i + 1) * K))) for i in range(nb)]
+    a.close()
+    b = L.Lego(cfg, max_points=40000, max_batch=K)
+    keep, got = [], []
+    recs = (L.PoseRec * K)()
+    for i in range(nb):
+        pts, off, st = pack(i * K, (i + 1) * K)
+        keep.append((pts, off, st))
+        assert b.lib.lego_odom_batch_submit(b.h, pts.ctypes.data, off.ctypes.data, st.ctypes.data, K, 0,
+                                            None, 0, None) == 0
+        if i >= 1:
+            if i == 1:  # a third batch in flight and a node call are refused
+                assert b.lib.lego_odom_batch_submit(b.h, pts.ctypes.data, off.ctypes.data, st.ctypes.data, K,
+                                                    0, None, 0, None) == L.LEGO_E_STATE
+                out = L.IpOut()
+                assert b.lib.lego_fa_process(b.h, C.byref(out), C.byref(L.FaOut())) == L.LEGO_E_STATE
+            b.wait(recs)
+            got.append(bytes(recs))
+    b.wait(recs)
+    got.append(bytes(recs))
+    assert b.lib.lego_odom_batch_wait(b.h, recs, K, None) == L.LEGO_E_STATE
+    b.close()
+    for i in range(nb):
+        for k in range(K):
+            assert ref[i][64 * k:64 * k + 60] == got[i][64 * k:64 * k + 60], (i, k)
+
+
+def test_reset_in_flight(L):
+    """lego_reset with a batch in flight: that batch finishes with the old
+    state, the next one starts fresh (== a new context)."""
+    cfg = L.sensor_cfg("VLP-16", L.hip_lib())
+    sc = L.synth_cfg("VLP-16", 12)
+    K = 4
+    scans = [L.synth_scan(sc, k) for k in range(2 * K)]
+    pts = np.concatenate([p for p, _ in scans])
+    off = np.zeros(2 * K + 1, np.int64)
+    off[1:] = np.cumsum([len(p) for p, _ in scans])
+    st = np.array([t for _, t in scans])
+    lo, hi = (pts[:off[K]], off[:K + 1], st[:K]), (pts[off[K]:], off[K:] - off[K], st[K:])
+    a = L.Lego(cfg, max_points=40000, max_batch=K)
+    r1 = bytes(a.odom_batch(*lo))
+    a.close()
+    a = L.Lego(cfg, max_points=40000, max_batch=K)
+    r2 = bytes(a.odom_batch(*hi))  # the second half from a fresh state
+    a.close()
+    b = L.Lego(cfg, max_points=40000, max_batch=K)
+    recs = (L.PoseRec * K)()
+    keep = [lo, hi]
+    for p, o, s_ in keep:
+        assert b.lib.lego_odom_batch_submit(b.h, p.ctypes.data, o.ctypes.data, s_.ctypes.data, K, 0,
+                                            None, 0, None) == 0
+        if p is lo[0]:
+            b.reset()
+    b.wait(recs)
+    g1 = bytes(recs)
+    b.wait(recs)
+    g2 = bytes(recs)
+    b.close()
+    for k in range(K):
+        assert r1[64 * k:64 * k + 60] == g1[64 * k:64 * k + 60], k
+        assert r2[64 * k:64 * k + 60] == g2[64 * k:64 * k + 60], k
