@@ -196,6 +196,38 @@ def mapping_bench(L, steps: int, cpu: bool):
     return res
 
 
+def dense_bench(L, nscans: int, batch: int, device: int):
+    """Auxiliary (not the headline metric): config C3, the HDL-64E-shaped
+    synthetic stream (64 x 2048) through the same pipeline
+    on one GPU, two batches in flight.  Host wall clock, like the headline."""
+    import torch
+
+    cfg = L.sensor_cfg("HDL-64E", L.hip_lib())
+    pts, off, stamps, maxn = make_stream(L, "HDL-64E", 2, nscans)
+    nb = nscans // batch
+    d_pts = torch.from_numpy(pts.view(np.uint8)).to(device)
+    d_off = [torch.from_numpy(off[i * batch:(i + 1) * batch + 1].astype(np.int64)).to(device) for i in range(nb)]
+    g = L.Lego(cfg, device=device, max_points=maxn + 16, max_batch=batch)
+    recs = (L.PoseRec * batch)()
+    sub = lambda j: g.submit_device(d_pts.data_ptr(), d_off[j].data_ptr(), stamps[j * batch:(j + 1) * batch],  # noqa: E731
+                                    batch)
+    sub(0)  # warm-up batch
+    g.wait(recs)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for j in range(1, nb):
+        sub(j)
+        if j > 1:
+            g.wait(recs)
+    g.wait(recs)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    g.close()
+    n = (nb - 1) * batch
+    return {"workload": f"C3: HDL-64E 64x2048 synthetic stream (seed 2), {batch} scans per call, two in flight",
+            "scans": n, "scans_per_s": n / dt, "ms_per_scan": dt / n * 1e3, "points_per_scan": int(maxn)}
+
+
 def fleet_bench(L, streams: int, k: int, steps: int, device: int):
     """Auxiliary (not the headline metric): `streams` independent VLP-16
     streams in one fleet context (lego_fleet_create) on one GPU, k scans per
@@ -221,17 +253,21 @@ def fleet_bench(L, streams: int, k: int, steps: int, device: int):
                      torch.from_numpy(off).to(device), st))
     fl = L.Lego(cfg, device=device, max_points=maxn + 16, max_batch=k, streams=streams)
     recs = (L.PoseRec * (streams * k))()
-    run = lambda w: fl.odom_batch_device(w[0].data_ptr(), w[1].data_ptr(), w[2], streams * k, recs)  # noqa: E731
-    run(wins[0])  # warm-up (initialises every stream)
+    sub = lambda w: fl.submit_device(w[0].data_ptr(), w[1].data_ptr(), w[2], streams * k)  # noqa: E731
+    sub(wins[0])  # warm-up (initialises every stream)
+    fl.wait(recs)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(steps):
-        run(wins[1 + i])
+    for i in range(steps):  # two calls in flight, as the headline loop
+        sub(wins[1 + i])
+        if i:
+            fl.wait(recs)
+    fl.wait(recs)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     fl.close()
     return {"workload": f"fleet: {streams} independent VLP-16 streams x {k} scans per call on one GPU "
-                        "(lego_fleet_create), full per-scan pipeline incl. LM odometry",
+                        "(lego_fleet_create, two calls in flight), full per-scan pipeline incl. LM odometry",
             "streams": streams, "scans_per_stream_per_call": k, "calls": steps,
             "scans_per_s": streams * k * steps / dt, "ms_per_call": dt / steps * 1e3}
 
@@ -250,6 +286,7 @@ def main():
     ap.add_argument("--odom-profile", action="store_true", help="in-kernel phase stamps (diagnostic)")
     ap.add_argument("--mapping-steps", type=int, default=5, help="C5 scan-to-map steps (aux; 0 = skip)")
     ap.add_argument("--fleet-streams", type=int, default=64, help="streams of the fleet aux line (0 = skip)")
+    ap.add_argument("--dense-scans", type=int, default=60, help="C3 HDL-64E scans of the aux line (0 = skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -405,6 +442,8 @@ def main():
             aux["scan_to_map_c5"] = mapping_bench(L, args.mapping_steps, not args.no_cpu)
         if args.fleet_streams > 0 and world == 1:
             aux["fleet_vlp16"] = fleet_bench(L, args.fleet_streams, 20, 3, local)
+        if args.dense_scans > 0 and world == 1:
+            aux["dense_hdl64_c3"] = dense_bench(L, args.dense_scans, 20, local)
         if cpu_all:
             aux["cpu_all_cores"] = cpu_all
         aux["host"] = host_info()

@@ -1389,9 +1389,16 @@ void launch_pack_recs(const BatchBufs& bb, const OdomBufs& ob, int B, PackedRec*
   k_pack_recs<<<(B + 1 + 63) / 64, 64, 0, s>>>(bb, ob, B, out);
 }
 
+// LDS-resident sensors: one wave per query of the largest NN round (the flat
+// features, 24 per ring) — 48 workgroups for VLP-16.  Larger sensors keep
+// their clouds and indexes in HBM, and each workgroup builds its own index
+// copy per scan: four queries per wave balance that redundant build against
+// the search split (HDL-64E: 48 workgroups; measured 1.4 k scans/s at 192,
+// 2.7 k at 48, 2.6 k at 24).  Capped at the CU count.
 int odom_workgroups(int N, int cusAvailable) {
-  if (N * kFlatPerRing > kLdsQ) return 1;
-  const int g = (N * kFlatPerRing + kOdomWaves - 1) / kOdomWaves;
+  const bool resident = N * kFlatPerRing <= kLdsQ && N * kSharpPerRing <= kLdsQ / 2;
+  const int perWg = kOdomWaves * (resident ? 1 : 4);
+  const int g = (N * kFlatPerRing + perWg - 1) / perWg;
   return g < cusAvailable ? g : cusAvailable;
 }
 
