@@ -310,6 +310,22 @@ int lego_mo_set_map(lego_ctx* ctx, const lego_point_xyzi* corner, int32_t n_corn
                     const lego_point_xyzi* surf, int32_t n_surf);
 int lego_mo_process(lego_ctx* ctx, const lego_fa_out* in, lego_mo_out* out);
 
+/* transformFusion (transformFusion.cpp:94-239): /integrated_to_init, the
+ * odometry pose composed with the latest mapping correction.  Host math, per
+ * message, in the context's fusion state. */
+typedef struct lego_fusion_out {
+  double stamp;
+  float transform_mapped[6];
+  double quat[4];  /* orientation x, y, z, w as published (:189-196) */
+  double pos[3];
+} lego_fusion_out;
+/* laserOdometryHandler (:174-205): one /laser_odom_to_init message (the
+ * odom_quat / odom_pos / stamp of a lego_fa_out). */
+int lego_fusion_odometry(lego_ctx* ctx, const lego_fa_out* odom, lego_fusion_out* out);
+/* odomAftMappedHandler (:207-227): the /aft_mapped_to_init message of a
+ * processed lego_mo_out (mapOptmization.cpp:654-679 publishTF). */
+int lego_fusion_aft_mapped(lego_ctx* ctx, const lego_mo_out* mo);
+
 /* Last device error string (static storage). */
 const char* lego_last_error(void);
 

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "lego_device.h"
+#include "lego_fusion_host.h"
 #include "lego_imu_host.h"
 #include "lego_kernels.h"
 #include "lego_mo.h"
@@ -118,6 +119,7 @@ struct lego_ctx {
   int64_t* h_offp = nullptr;    // pinned [maxBatch + 1]: device offsets read back for validation
   OdomState* h_resetSt = nullptr;   // pinned [S]: construction state (ctx_reset)
   FaCarry* h_resetCarry = nullptr;  // pinned [S]
+  Fusion fusion;  // transformFusion state
   FaImuQueue faImu;
   MoImuQueue moImu;
   std::vector<ImuSnap> h_imu;
@@ -199,6 +201,7 @@ static int ctx_reset(lego_ctx* x) {
   x->lastB = 0;
   x->faImu = FaImuQueue{};
   x->moImu = MoImuQueue{};
+  x->fusion = Fusion{};
   if (x->moAlloc) {
     HIPCHK(hipMemsetAsync(x->mo.st, 0, sizeof(MoState), x->stream));
     if (x->mo.kf.kcap) {
@@ -1263,6 +1266,26 @@ int lego_odom_batch_pc2(lego_ctx* x, const lego_pc2_msg* msgs, int32_t nscans, i
   std::vector<double> stamps(nscans);
   for (int k = 0; k < nscans; ++k) stamps[k] = msgs[k].stamp;
   return lego_odom_batch(x, x->d_pts, x->d_off, stamps.data(), nscans, 1, recs);
+}
+
+// ---------------------------------------------------------------- transformFusion
+int lego_fusion_odometry(lego_ctx* x, const lego_fa_out* odom, lego_fusion_out* out) {
+  if (!x || !odom || !out) return LEGO_E_ARG;
+  x->fusion.odometry(odom->odom_quat, odom->odom_pos);
+  std::memset(out, 0, sizeof(*out));
+  out->stamp = odom->stamp;
+  for (int i = 0; i < 6; ++i) out->transform_mapped[i] = x->fusion.transformMapped[i];
+  odom_quat(x->fusion.transformMapped, out->quat, out->pos);  // the same setRPY + axis shuffle (:187-196)
+  return LEGO_OK;
+}
+
+int lego_fusion_aft_mapped(lego_ctx* x, const lego_mo_out* mo) {
+  if (!x || !mo) return LEGO_E_ARG;
+  if (!mo->processed) return LEGO_OK;  // nothing was published
+  double q[4], pos[3];
+  odom_quat(mo->transform_aft_mapped, q, pos);  // publishTF (mapOptmization.cpp:656-665)
+  x->fusion.aft_mapped(q, pos, mo->transform_bef_mapped);
+  return LEGO_OK;
 }
 
 int lego_odom_profile(lego_ctx* x, int32_t enable, uint64_t* out32) {

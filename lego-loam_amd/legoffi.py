@@ -100,6 +100,11 @@ class MoOut(C.Structure):
                 ("n_surf_scan_ds", C.c_int32), ("n_rows_last", C.c_int32)]
 
 
+class FusionOut(C.Structure):  # lego_fusion_out (/integrated_to_init)
+    _fields_ = [("stamp", C.c_double), ("transform_mapped", C.c_float * 6), ("quat", C.c_double * 4),
+                ("pos", C.c_double * 3)]
+
+
 class PoseRec(C.Structure):
     _fields_ = [("stamp", C.c_double), ("transform_sum", C.c_float * 6),
                 ("n_segmented", C.c_int32), ("n_sharp", C.c_int32), ("n_less_sharp", C.c_int32),
@@ -204,6 +209,8 @@ def oracle_lib() -> C.CDLL:
     lib.lego_oracle_mo_set_map.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32]
     lib.lego_oracle_mo_process.argtypes = [C.c_void_p, C.POINTER(FaOut), C.POINTER(MoOut)]
     lib.lego_oracle_imu_push.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
+    lib.lego_oracle_fusion_odometry.argtypes = [C.c_void_p, C.POINTER(FaOut), C.POINTER(FusionOut)]
+    lib.lego_oracle_fusion_aft_mapped.argtypes = [C.c_void_p, C.POINTER(MoOut)]
     lib.lego_oracle_voxel_grid.argtypes = [C.c_void_p, C.c_int32, C.c_float, C.c_int32,
                                            C.c_void_p, C.POINTER(C.c_int32)]
     for fn in ("atan2f",):
@@ -219,6 +226,7 @@ HIP_EXPORTS = ["lego_sensor_preset", "lego_create", "lego_fleet_create", "lego_d
                "lego_ip_process", "lego_fa_process", "lego_odom_batch", "lego_odom_batch_imu",
                "lego_imu_push", "lego_odom_batch_submit", "lego_odom_batch_wait", "lego_batch_fetch", "lego_pc2_decode", "lego_ip_process_pc2",
                "lego_odom_batch_pc2", "lego_pc2_encode_xyzi", "lego_cloud_info_serialize",
+               "lego_fusion_odometry", "lego_fusion_aft_mapped",
                "lego_mo_set_map", "lego_mo_process", "lego_last_error", "lego_stage_times",
                "lego_odom_profile"]
 
@@ -241,6 +249,8 @@ def hip_lib() -> C.CDLL:
     lib.lego_odom_batch_imu.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
                                         C.c_int32, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
     lib.lego_imu_push.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
+    lib.lego_fusion_odometry.argtypes = [C.c_void_p, C.POINTER(FaOut), C.POINTER(FusionOut)]
+    lib.lego_fusion_aft_mapped.argtypes = [C.c_void_p, C.POINTER(MoOut)]
     lib.lego_odom_batch_submit.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
                                            C.c_int32, C.c_void_p, C.c_int32, C.c_void_p]
     lib.lego_odom_batch_wait.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(C.c_int32)]
@@ -411,8 +421,19 @@ class Oracle:
     def mo(self) -> dict:
         out = MoOut()
         check(self.lib.lego_oracle_mo_process(self.h, C.byref(self._fa), C.byref(out)), "oracle_mo")
+        self._mo = out
         return {k: (np.array(list(getattr(out, k)), dtype=np.float32)
                     if k.startswith("transform") else getattr(out, k)) for k, _ in MoOut._fields_}
+
+    def fusion(self) -> np.ndarray:
+        """transformFusion: the last mapping output (if any) then the last
+        odometry message -> /integrated_to_init transform_mapped."""
+        if getattr(self, "_mo", None) is not None:
+            check(self.lib.lego_oracle_fusion_aft_mapped(self.h, C.byref(self._mo)), "oracle_fusion_aft")
+            self._mo = None
+        out = FusionOut()
+        check(self.lib.lego_oracle_fusion_odometry(self.h, C.byref(self._fa), C.byref(out)), "oracle_fusion")
+        return np.array(list(out.transform_mapped), np.float32)
 
 
 _live: "weakref.WeakSet[Lego]" = weakref.WeakSet()
@@ -480,8 +501,20 @@ class Lego:
         """Scan-to-map on the last fa() output (mapOptimization::run)."""
         out = MoOut()
         check(self.lib.lego_mo_process(self.h, C.byref(self._fa), C.byref(out)), "lego_mo_process", self.lib)
+        self._mo = out
         return {k: (np.array(list(getattr(out, k)), dtype=np.float32)
                     if k.startswith("transform") else getattr(out, k)) for k, _ in MoOut._fields_}
+
+    def fusion(self) -> np.ndarray:
+        """transformFusion (lego_fusion_aft_mapped with the last mapping
+        output, then lego_fusion_odometry with the last odometry)."""
+        if getattr(self, "_mo", None) is not None:
+            check(self.lib.lego_fusion_aft_mapped(self.h, C.byref(self._mo)), "lego_fusion_aft_mapped", self.lib)
+            self._mo = None
+        out = FusionOut()
+        check(self.lib.lego_fusion_odometry(self.h, C.byref(self._fa), C.byref(out)), "lego_fusion_odometry",
+              self.lib)
+        return np.array(list(out.transform_mapped), np.float32)
 
     def odom_batch(self, pts: np.ndarray, offsets: np.ndarray, stamps: np.ndarray,
                    imu: np.ndarray | None = None, imu_before: np.ndarray | None = None) -> np.ndarray:

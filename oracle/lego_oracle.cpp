@@ -1314,6 +1314,7 @@ struct lego_oracle {
   std::unique_ptr<oracle::ImageProjection> ip;
   std::unique_ptr<oracle::FeatureAssociation> fa;
   std::unique_ptr<oracle::MapOptimization> mo;
+  oracle::TransformFusionNode fusion;
   double ip_stamp = 0;
 };
 
@@ -1398,6 +1399,25 @@ extern "C" int lego_oracle_fa_process(lego_oracle* o, const lego_ip_out* in, leg
     out->surf_last = fa.outSurfLast.data(); out->n_surf_last = (int32_t)fa.outSurfLast.size();
     out->outlier_last = fa.outOutlierLast.data(); out->n_outlier_last = (int32_t)fa.outOutlierLast.size();
   }
+  return LEGO_OK;
+}
+
+extern "C" int lego_oracle_fusion_odometry(lego_oracle* o, const lego_fa_out* odom, lego_fusion_out* out) {
+  if (!o || !odom || !out) return LEGO_E_ARG;
+  o->fusion.laserOdometryHandler(odom->odom_quat, odom->odom_pos);
+  std::memset(out, 0, sizeof(*out));
+  out->stamp = odom->stamp;
+  for (int i = 0; i < 6; ++i) out->transform_mapped[i] = o->fusion.transformMapped[i];
+  oracle::odom_quaternion(o->fusion.transformMapped, out->quat, out->pos);  // :187-196
+  return LEGO_OK;
+}
+
+extern "C" int lego_oracle_fusion_aft_mapped(lego_oracle* o, const lego_mo_out* mo) {
+  if (!o || !mo) return LEGO_E_ARG;
+  if (!mo->processed) return LEGO_OK;
+  double q[4], pos[3];
+  oracle::odom_quaternion(mo->transform_aft_mapped, q, pos);  // publishTF, mapOptmization.cpp:656-665
+  o->fusion.odomAftMappedHandler(q, pos, mo->transform_bef_mapped);
   return LEGO_OK;
 }
 

@@ -242,3 +242,27 @@ def test_product_reproduces_imu_fixture_batched(L):
         c = [r.n_segmented, r.n_sharp, r.n_less_sharp, r.n_flat, r.n_less_flat, r.odom_valid]
         np.testing.assert_array_equal(c, g["counts"][k][:6], err_msg=str(k))
         assert np.abs(np.array(list(r.transform_sum), np.float64) - g["transform_sum"][k]).max() <= 1e-4, k
+
+
+@pytest.mark.gpu
+def test_product_fusion_matches_oracle(L):
+    """transformFusion after every scan of the keyframe-mapping stream: the
+    product's /integrated_to_init equals the oracle's (mapping corrections
+    arriving every 0.3 s)."""
+    g = load("vlp16_seed6_keyframe_map24")
+    sc = L.synth_cfg("VLP-16", int(g["seed"]))
+    ora = L.Oracle(L.sensor_cfg("VLP-16"))
+    gpu = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=40000)
+    exact = 0
+    for k in range(len(g["info"])):
+        pts, stamp = L.synth_scan(sc, k)
+        for e in (ora, gpu):
+            e.ip(pts, stamp)
+            e.fa()
+            e.mo()
+        a, b = ora.fusion(), gpu.fusion()
+        assert np.abs(a.astype(np.float64) - b).max() <= 1e-4, (k, a, b)
+        exact += int(np.array_equal(a.view(np.uint32), b.view(np.uint32)))
+    gpu.close()
+    print(f"fusion: bit-exact {exact}/{len(g['info'])}")
+    assert exact == len(g["info"])

@@ -266,3 +266,17 @@ def test_level_stationary_imu(L):
         else:
             assert np.array_equal(mo_a["transform_aft_mapped"], mo_b["transform_aft_mapped"]), k
     assert blended
+
+
+def test_fusion_without_mapping_is_odometry(L):
+    """KAT (transformFusion.cpp:94-205): before any /aft_mapped_to_init the
+    correction is the identity (aft = bef = 0), so /integrated_to_init
+    reproduces /laser_odom_to_init up to float rounding of the composition."""
+    sc = L.synth_cfg("VLP-16", 3)
+    ora = L.Oracle(L.sensor_cfg("VLP-16"))
+    for k in range(6):
+        pts, st = L.synth_scan(sc, k)
+        ora.ip(pts, st)
+        fa = ora.fa()
+        m = ora.fusion()
+        assert np.abs(m.astype(np.float64) - fa["transform_sum"]).max() < 2e-6, (k, m, fa["transform_sum"])
