@@ -1281,15 +1281,6 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
           lm_loop<false>(false, F, L, ob, c, S);
         }
       }
-      // integrateTransformation :1697-1725
-      S.start();
-      if (tid < 64) {
-        const float bl[3] = {iq.pitchStart, iq.yawStart, iq.rollStart};
-        const float al[3] = {iq.pitchCur, iq.yawCur, iq.rollCur};  // imu*Last = imu*Cur (:1641-1643)
-        integrate_wave(st->transformSum, st->transformCur, bl, al);
-      }
-      __syncthreads();
-      S.add(P_INTEG);
     }
     S.start();
     // hand-off: checkSystemInitialization (:1605-1637, no TransformToEnd) or
@@ -1310,17 +1301,28 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
                   lego_sinf(iq.rollStart), lego_sinf(iq.pitchStart), lego_sinf(iq.yawStart),
                   lego_cosf(iq.yawCur), lego_sinf(iq.yawCur), lego_cosf(iq.pitchCur),
                   lego_sinf(iq.pitchCur), lego_cosf(iq.rollCur), lego_sinf(iq.rollCur)};
-    for (int t = tid; t < F.nLS; t += kOdomThreads) {
-      const float4 p = init ? F.lsharp[t] : to_end(F.lsharp[t], tcur, et, im);
-      gCn[t] = p;
-      if (lead) cEnd[t] = p;
-      if (fits) L.lastC[t] = p;
+    // integrateTransformation (:1697-1725) on wave 0 while waves 1-7 run
+    // TransformToEnd: both read the final transformCur, only the former
+    // writes (transformSum)
+    const int t0 = init ? tid : tid - 64, tstep = init ? kOdomThreads : kOdomThreads - 64;
+    if (!init && tid < 64) {
+      const float bl[3] = {iq.pitchStart, iq.yawStart, iq.rollStart};
+      const float al[3] = {iq.pitchCur, iq.yawCur, iq.rollCur};  // imu*Last = imu*Cur (:1641-1643)
+      integrate_wave(st->transformSum, st->transformCur, bl, al);
     }
-    for (int t = tid; t < F.nLF; t += kOdomThreads) {
-      const float4 p = init ? F.lflat[t] : to_end(F.lflat[t], tcur, et, im);
-      gSn[t] = p;
-      if (lead) sEnd[t] = p;
-      if (fits) L.lastS[t] = p;
+    if (t0 >= 0) {
+      for (int t = t0; t < F.nLS; t += tstep) {
+        const float4 p = init ? F.lsharp[t] : to_end(F.lsharp[t], tcur, et, im);
+        gCn[t] = p;
+        if (lead) cEnd[t] = p;
+        if (fits) L.lastC[t] = p;
+      }
+      for (int t = t0; t < F.nLF; t += tstep) {
+        const float4 p = init ? F.lflat[t] : to_end(F.lflat[t], tcur, et, im);
+        gSn[t] = p;
+        if (lead) sEnd[t] = p;
+        if (fits) L.lastS[t] = p;
+      }
     }
     __syncthreads();
     S.add(P_TOEND);
