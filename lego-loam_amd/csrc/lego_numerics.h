@@ -616,6 +616,26 @@ LEGO_HD bool cv_inv_lu(const float (&S)[N][N], float (&D)[N][N]) {
   return true;
 }
 
+// True when every eigenvalue of the symmetric AtA provably exceeds thr by a
+// margin that dwarfs the float Jacobi's error (1e-4 of ||AtA||_F, ~10^3 ulp):
+// then cv::eigen's smallest eigenvalue is >= thr as well, the degeneracy test
+// of :1336-1347 / :1437-1448 finds nothing, and the 3x3 Jacobi can be skipped.
+// LDL^T of AtA - t I in double: positive definite iff all pivots are > 0
+// (NaN fails every comparison and takes the Jacobi path).
+LEGO_HD bool eig_min_above(const float (&A)[3][3], double thr) {
+  const double a00 = A[0][0], a01 = A[0][1], a02 = A[0][2], a11 = A[1][1], a12 = A[1][2], a22 = A[2][2];
+  const double fro = __builtin_sqrt(a00 * a00 + a11 * a11 + a22 * a22 + 2 * (a01 * a01 + a02 * a02 + a12 * a12));
+  const double t = thr + 1e-4 * fro;
+  const double d0 = a00 - t;
+  if (!(d0 > 0)) return false;
+  const double l10 = a01 / d0, l20 = a02 / d0;
+  const double d1 = (a11 - t) - l10 * a01;
+  if (!(d1 > 0)) return false;
+  const double l21 = (a12 - l20 * a01) / d1;
+  const double d2 = (a22 - t) - l20 * a02 - l21 * l21 * d1;
+  return d2 > 0;
+}
+
 // matP = matV.inv() * matV2 (cv gemm: double accumulation, float store).
 template <int N>
 LEGO_HD void cv_matmul(const float (&A)[N][N], const float (&B)[N][N], float (&C)[N][N]) {

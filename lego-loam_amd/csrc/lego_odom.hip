@@ -55,12 +55,11 @@ __device__ __forceinline__ Trig3 trig3(float rx, float ry, float rz) {
   return {lego_sinf(rx), lego_cosf(rx), lego_sinf(ry), lego_cosf(ry), lego_sinf(rz), lego_cosf(rz)};
 }
 
-__device__ __forceinline__ float4 to_start(float4 pi, const float* tc) {  // :860-883
-  const float s = 10 * (pi.w - (float)(int)pi.w);
-  const float rx = s * tc[0], ry = s * tc[1], rz = s * tc[2];
+__device__ __forceinline__ float start_s(float4 pi) { return 10 * (pi.w - (float)(int)pi.w); }
+// TransformToStart given the point's s and the six sines / cosines of s * tc[0..2]
+__device__ __forceinline__ float4 to_start_t(float4 pi, float s, const float* tc, float cx, float sx, float cy,
+                                             float sy, float cz, float sz) {
   const float tx = s * tc[3], ty = s * tc[4], tz = s * tc[5];
-  const float cz = lego_cosf(rz), sz = lego_sinf(rz), cx = lego_cosf(rx), sx = lego_sinf(rx);
-  const float cy = lego_cosf(ry), sy = lego_sinf(ry);
   const float x1 = cz * (pi.x - tx) + sz * (pi.y - ty);
   const float y1 = -sz * (pi.x - tx) + cz * (pi.y - ty);
   const float z1 = (pi.z - tz);
@@ -68,6 +67,40 @@ __device__ __forceinline__ float4 to_start(float4 pi, const float* tc) {  // :86
   const float y2 = cx * y1 + sx * z1;
   const float z2 = -sx * y1 + cx * z1;
   return make_float4(cy * x2 - sy * z2, y2, sy * x2 + cy * z2, pi.w);
+}
+__device__ __forceinline__ float4 to_start(float4 pi, const float* tc) {  // :860-883
+  const float s = start_s(pi);
+  const float rx = s * tc[0], ry = s * tc[1], rz = s * tc[2];
+  const float cz = lego_cosf(rz), sz = lego_sinf(rz), cx = lego_cosf(rx), sx = lego_sinf(rx);
+  const float cy = lego_cosf(ry), sy = lego_sinf(ry);
+  return to_start_t(pi, s, tc, cx, sx, cy, sy, cz, sz);
+}
+// One LM step moves only three of transformCur's components (surf: rx, rz,
+// ty; corner: ry, tx, tz), so the sines / cosines of the other angles are the
+// same in every iteration of the step.  A lane keeps them for its first query,
+// keyed by the bits of the angle they were computed from.
+struct FixTrig {
+  float sa, ca, sb, cb;
+  unsigned ka, kb;
+  bool have;
+};
+__device__ __forceinline__ float4 to_start_fix(float4 pi, const float* tc, bool surf, FixTrig& f) {
+  const float s = start_s(pi);
+  if (surf) {  // ry fixed
+    if (!f.have || __float_as_uint(tc[1]) != f.ka) {
+      const float ry = s * tc[1];
+      f.sa = lego_sinf(ry); f.ca = lego_cosf(ry); f.ka = __float_as_uint(tc[1]); f.have = true;
+    }
+    const float rx = s * tc[0], rz = s * tc[2];
+    return to_start_t(pi, s, tc, lego_cosf(rx), lego_sinf(rx), f.ca, f.sa, lego_cosf(rz), lego_sinf(rz));
+  }
+  if (!f.have || __float_as_uint(tc[0]) != f.ka || __float_as_uint(tc[2]) != f.kb) {  // rx, rz fixed
+    const float rx = s * tc[0], rz = s * tc[2];
+    f.sa = lego_sinf(rx); f.ca = lego_cosf(rx); f.ka = __float_as_uint(tc[0]);
+    f.sb = lego_sinf(rz); f.cb = lego_cosf(rz); f.kb = __float_as_uint(tc[2]); f.have = true;
+  }
+  const float ry = s * tc[1];
+  return to_start_t(pi, s, tc, f.ca, f.sa, lego_cosf(ry), lego_sinf(ry), f.cb, f.sb);
 }
 
 // TransformToEnd :885-953 with the IMU terms of an IMU-less run
@@ -851,7 +884,9 @@ __device__ __forceinline__ void solve_step(float (&AtA)[3][3], float (&AtB)[3], 
 #pragma unroll
     for (int b = 0; b < 3; ++b) Aq[a][b] = AtA[a][b];
   cv_solve_qr<3, 3>(Aq, AtB, X);
-  if (iter == 0) {
+  if (iter == 0 && eig_min_above(AtA, 10.0)) {
+    isDeg = 0;  // P is read only while isDeg is set, and the next iteration 0 rewrites both
+  } else if (iter == 0) {
     float E[3], V[3][3], V2[3][3], Vi[3][3];
     cv_eigen_sym3(AtA, E, V);
 #pragma unroll
@@ -958,6 +993,8 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
   for (int i = 0; i < 6; ++i) tc[i] = st->transformCur[i];
 #pragma unroll
   for (int i = 0; i < 9; ++i) Pm[i / 3][i % 3] = st->matP[i];
+  FixTrig fix;
+  fix.have = false;
   for (int it = 0; it < 25; it++) {
     S.start();
     S.count(surf ? P_ITERS_S : P_ITERS_C);
@@ -1054,7 +1091,7 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
     }
     for (int q = tid; q < nQ; q += kOdomThreads) {
       const float4 po = qp[q];
-      const float4 sel = to_start(po, tc);
+      const float4 sel = q == tid ? to_start_fix(po, tc, surf, fix) : to_start(po, tc);
       const int i1 = qi[q], i2 = qi[qs + q], i3 = qi[2 * qs + q];
       float4 cf;
       bool ok = false;

@@ -42,6 +42,16 @@ def test_eigen3_register_form_matches_generic(tmp_path):
     assert r.returncode == 0, r.stdout
 
 
+def test_eig_min_shortcut_is_sound(tmp_path):
+    """The odometry skips the iteration-0 Jacobi when an LDL^T test proves
+    every eigenvalue of AtA exceeds 10 by a margin; the Jacobi restatement
+    must then agree that nothing is degenerate."""
+    exe = _build(tmp_path, "eigmin_check", REPO / "tests/native/eigmin_check.cpp")
+    r = subprocess.run([str(exe), "300000"], capture_output=True, text=True, timeout=600)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout
+
+
 def test_segmentation_alpha_constants(L):
     """sin/cos of segmentAlphaX/Y (imageProjection.cpp:421) — bit patterns
     recorded in SURVEY.md §9.3 for VLP-16."""
