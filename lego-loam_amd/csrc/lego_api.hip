@@ -386,10 +386,8 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
     odom_index_caps(ob.capCorner, ob.capSurf, &gTC, &gTS);
     ob.gTC = gTC;
     ob.gTS = gTS;
-    ob.cntCap = gTC + gTS;
-    A(ob.nC.gEnd, G * gTC); A(ob.nC.gOrd, G * ob.capCorner);
-    A(ob.nS.gEnd, G * gTS); A(ob.nS.gOrd, G * ob.capSurf);
-    A(ob.cnt, G * ob.cntCap);
+    A(ob.nC.gPts, G * ob.capCorner);
+    A(ob.nS.gPts, G * ob.capSurf);
     ob.capQ = (int)(N * kFlatPerRing);
     A(ob.qi, G * 3 * ob.capQ);
     // exchange block: 16-byte error word, then per stream one slot of 3 x capQ
@@ -527,9 +525,8 @@ static OdomBufs ob_slice(const OdomBufs& a, const DevCfg& c, int c0, int s0, int
     o.cornerLast[i] += w * a.capCorner;
     o.surfLast[i] += w * a.capSurf;
   }
-  o.nC.gEnd += w * a.gTC; o.nC.gOrd += w * a.capCorner;
-  o.nS.gEnd += w * a.gTS; o.nS.gOrd += w * a.capSurf;
-  o.cnt += w * a.cntCap;
+  o.nC.gPts += w * a.capCorner;
+  o.nS.gPts += w * a.capSurf;
   o.qi += w * 3 * a.capQ;
   o.xg += (size_t)s0 * a.roundsCap * 3 * a.capQ;
   o.sumOut += k * 6; o.curOut += k * 6; o.validOut += k; o.pubOut += k;

@@ -68,8 +68,8 @@ class StageTimer {
 // HBM form of the two NN indexes over one last cloud (sensors whose working
 // set does not fit LDS); see lego_odom.hip.
 struct NNIndexBufs {
-  uint32_t* gEnd;  // [gT]        fine-grid bucket ends
-  uint32_t* gOrd;  // [cap]       point order
+  float4* gPts;  // [cap] the cloud in fine-grid bucket order, .w = the point's index (int bits);
+                 // the bucket ends live in LDS (lego_odom.hip, hbm_grid_ends)
 };
 
 // Odometry state kept on the device for one stream (featureAssociation.cpp
@@ -98,9 +98,8 @@ struct OdomBufs {
   float4* cornerLast[2];  // [G x capCorner] double-buffered: current / stale snapshot
   float4* surfLast[2];    // [G x capSurf]
   NNIndexBufs nC, nS;     // [G x] HBM indexes (sensors too large for LDS)
-  uint32_t* cnt;          // [G x cntCap] index-build counters
   int* qi;                // [G x 3 * capQ] HBM correspondences
-  int gTC, gTS, cntCap;
+  int gTC, gTS;           // bucket caps of the HBM-resident grids
   int capCorner, capSurf, capQ;
   int G;                  // workgroups per stream
   int S;                  // streams

@@ -365,7 +365,8 @@ struct NNView {
   const float4* pts;
   int n;
   const Idx* gEnd;
-  const Idx* gOrd;
+  const Idx* gOrd;     // LDS grids: point order
+  const float4* gPts;  // HBM grids: the points themselves in bucket order (.w = index bits)
   int T, NK;
   const int* sufFirst;  // [NK + 1] first index whose key >= k (INT_MAX if none)
   const int* preLast;   // [NK]     last index whose key <= k (-1 if none)
@@ -375,6 +376,7 @@ struct NNView {
 template <class Idx>
 struct NNStore {
   Idx *gEnd, *gOrd;
+  float4* gPts;
   int *sufFirst, *preLast, *irregular;
   int Tcap;
 };
@@ -435,30 +437,44 @@ __device__ __forceinline__ void nn_build2(const float4* ptsS, int nS, const NNSt
   for (int k = tid; k < 2 * NK; k += kOdomThreads) { kfirst[k] = INT_MAX; klast[k] = -1; }
   if (tid == 0) { *S.irregular = 0; *Cs.irregular = 0; }
   __syncthreads();
-  for (int i0 = tid - lane; i0 < n; i0 += kOdomThreads) {  // wave-uniform loop
-    const int i = i0 + lane;
-    int kk = -1;
-    if (i < n) {
-      const bool corner = i >= nS;
-      const float4 p = corner ? ptsC[i - nS] : ptsS[i];
-      const int T = corner ? TC : TS;
-      atomicAdd(&cnt[(corner ? TS : 0) + fine_bucket(cell_of(p.x), cell_of(p.y), cell_of(p.z), T)], 1u);
-      const int k = (int)p.w;
-      if (k < 0 || k >= NK) *(corner ? Cs.irregular : S.irregular) = 1;
-      else kk = k + (corner ? NK : 0);
+  // kBuildU points per lane in flight (HBM clouds: one load latency per pass
+  // of kBuildU, not per point)
+  constexpr int kBuildU = 4;
+  for (int j0 = tid - lane; j0 < n; j0 += kBuildU * kOdomThreads) {  // wave-uniform loop
+    float4 pu[kBuildU];
+#pragma unroll
+    for (int u = 0; u < kBuildU; ++u) {
+      const int i = j0 + u * kOdomThreads + lane;
+      if (i < n) pu[u] = i >= nS ? ptsC[i - nS] : ptsS[i];
     }
-    // per-key first/last: one atomic per distinct (cloud, key) of the wave
-    unsigned long long todo = __ballot(kk >= 0);
-    while (todo) {
-      const int leader = __ffsll((long long)todo) - 1;
-      const int key = __builtin_amdgcn_readlane(kk, leader);
-      const unsigned long long m = __ballot(kk == key);
-      if (lane == leader) {
-        const int base = key >= NK ? nS : 0;
-        atomicMin(&kfirst[key], i0 + leader - base);
-        atomicMax(&klast[key], i0 + 63 - __clzll((long long)m) - base);
+#pragma unroll
+    for (int u = 0; u < kBuildU; ++u) {
+      const int i0 = j0 + u * kOdomThreads;
+      if (i0 >= n) break;
+      const int i = i0 + lane;
+      int kk = -1;
+      if (i < n) {
+        const bool corner = i >= nS;
+        const float4 p = pu[u];
+        const int T = corner ? TC : TS;
+        atomicAdd(&cnt[(corner ? TS : 0) + fine_bucket(cell_of(p.x), cell_of(p.y), cell_of(p.z), T)], 1u);
+        const int k = (int)p.w;
+        if (k < 0 || k >= NK) *(corner ? Cs.irregular : S.irregular) = 1;
+        else kk = k + (corner ? NK : 0);
       }
-      todo &= ~m;
+      // per-key first/last: one atomic per distinct (cloud, key) of the wave
+      unsigned long long todo = __ballot(kk >= 0);
+      while (todo) {
+        const int leader = __ffsll((long long)todo) - 1;
+        const int key = __builtin_amdgcn_readlane(kk, leader);
+        const unsigned long long m = __ballot(kk == key);
+        if (lane == leader) {
+          const int base = key >= NK ? nS : 0;
+          atomicMin(&kfirst[key], i0 + leader - base);
+          atomicMax(&klast[key], i0 + 63 - __clzll((long long)m) - base);
+        }
+        todo &= ~m;
+      }
     }
   }
   __syncthreads();
@@ -473,13 +489,30 @@ __device__ __forceinline__ void nn_build2(const float4* ptsS, int nS, const NNSt
   }
   if (tid == 0) { S.sufFirst[NK] = INT_MAX; Cs.sufFirst[NK] = INT_MAX; }
   block_exscan(cnt, TS + TC, wtot);  // corner starts come out offset by nS
-  for (int i = tid; i < n; i += kOdomThreads) {
-    const bool corner = i >= nS;
-    const float4 p = corner ? ptsC[i - nS] : ptsS[i];
-    const int T = corner ? TC : TS;
-    const unsigned pos = atomicAdd(&cnt[(corner ? TS : 0) + fine_bucket(cell_of(p.x), cell_of(p.y), cell_of(p.z), T)], 1u);
-    if (corner) Cs.gOrd[pos - nS] = (Idx)(i - nS);
-    else S.gOrd[pos] = (Idx)i;
+  for (int j = tid; j < n; j += kBuildU * kOdomThreads) {
+    float4 pu[kBuildU];
+#pragma unroll
+    for (int u = 0; u < kBuildU; ++u) {
+      const int i = j + u * kOdomThreads;
+      if (i < n) pu[u] = i >= nS ? ptsC[i - nS] : ptsS[i];
+    }
+#pragma unroll
+    for (int u = 0; u < kBuildU; ++u) {
+      const int i = j + u * kOdomThreads;
+      if (i >= n) break;
+      const bool corner = i >= nS;
+      const float4 p = pu[u];
+      const int T = corner ? TC : TS;
+      const unsigned pos =
+          atomicAdd(&cnt[(corner ? TS : 0) + fine_bucket(cell_of(p.x), cell_of(p.y), cell_of(p.z), T)], 1u);
+      if constexpr (std::is_same<Idx, uint32_t>::value) {  // HBM grids: the point itself, one load per visit
+        if (corner) Cs.gPts[pos - nS] = make_float4(p.x, p.y, p.z, __int_as_float(i - nS));
+        else S.gPts[pos] = make_float4(p.x, p.y, p.z, __int_as_float(i));
+      } else {
+        if (corner) Cs.gOrd[pos - nS] = (Idx)(i - nS);
+        else S.gOrd[pos] = (Idx)i;
+      }
+    }
   }
   __syncthreads();
   for (int b = tid; b < TS + TC; b += kOdomThreads) {
@@ -579,10 +612,18 @@ __device__ __forceinline__ int nn_i1(const NNView<Idx>& v, float4 q, float bound
     const int cc = g % 27, half = g / 27;
     int lo, hi;
     bucket_range(v.gEnd, fine_bucket(cx + cc % 3 - 1, cy + (cc / 3) % 3 - 1, cz + cc / 9 - 1, v.T), lo, hi);
+    if constexpr (std::is_same<Idx, uint32_t>::value) {
 #pragma unroll 2
-    for (int t = lo + half; t < hi; t += 2) {
-      const int j = (int)v.gOrd[t];
-      lex_min(bd, bi, flann_d2(q, v.pts[j]), j);
+      for (int t = lo + half; t < hi; t += 2) {
+        const float4 p = v.gPts[t];
+        lex_min(bd, bi, flann_d2(q, p), __float_as_int(p.w));
+      }
+    } else {
+#pragma unroll 2
+      for (int t = lo + half; t < hi; t += 2) {
+        const int j = (int)v.gOrd[t];
+        lex_min(bd, bi, flann_d2(q, v.pts[j]), j);
+      }
     }
   }
   group_lex_min(bd, bi);
@@ -778,17 +819,25 @@ __device__ __forceinline__ bool sensor_resident(const DevCfg& c) {
 // Views of the current indexes (valid when the snapshot is current).
 __device__ __forceinline__ NNView<uint16_t> view_lds(bool surf, const OdomLds& L, const OdomState* st, const DevCfg& c) {
   if (surf)
-    return NNView<uint16_t>{L.lastS, st->surfLastNum, L.gEndS, L.gOrdS, fine_T(st->surfLastNum, kLdsGridS),
+    return NNView<uint16_t>{L.lastS, st->surfLastNum, L.gEndS, L.gOrdS, nullptr, fine_T(st->surfLastNum, kLdsGridS),
                             c.N, L.sufS, L.preS, L.n[N_IRR_S]};
-  return NNView<uint16_t>{L.lastC, st->cornerLastNum, L.gEndC, L.gOrdC, fine_T(st->cornerLastNum, kLdsGridC),
+  return NNView<uint16_t>{L.lastC, st->cornerLastNum, L.gEndC, L.gOrdC, nullptr, fine_T(st->cornerLastNum, kLdsGridC),
                           c.N, L.sufC, L.preC, L.n[N_IRR_C]};
 }
+// HBM-resident clouds: the LDS that holds the clouds, queries and counters of
+// the resident layout (lastS .. cnt, contiguous) is free, and takes both
+// grids' bucket arrays (the counting sort's counters, which end the build as
+// the bucket ends); the point-order arrays stay in HBM.
+constexpr int kHbmLdsCnt = (kLdsSurf * 16 + kLdsCorner * 16 + kLdsQ * 16 + (kLdsQ / 2) * 16 + kLdsCnt * 4) / 4;
+__device__ __forceinline__ unsigned* hbm_grid_ends(const OdomLds& L) { return (unsigned*)L.lastS; }
 __device__ __forceinline__ NNView<uint32_t> view_hbm(bool surf, const OdomLds& L, const OdomBufs& ob,
                                                      const OdomState* st, const DevCfg& c) {
+  unsigned* ends = hbm_grid_ends(L);
+  const int TS = fine_T(st->surfLastNum, ob.gTS);
   if (surf)
-    return NNView<uint32_t>{buf2(ob.surfLast, st->curBuf), st->surfLastNum, ob.nS.gEnd, ob.nS.gOrd,
-                            fine_T(st->surfLastNum, ob.gTS), c.N, L.sufS, L.preS, L.n[N_IRR_S]};
-  return NNView<uint32_t>{buf2(ob.cornerLast, st->curBuf), st->cornerLastNum, ob.nC.gEnd, ob.nC.gOrd,
+    return NNView<uint32_t>{buf2(ob.surfLast, st->curBuf), st->surfLastNum, ends, nullptr, ob.nS.gPts, TS, c.N,
+                            L.sufS, L.preS, L.n[N_IRR_S]};
+  return NNView<uint32_t>{buf2(ob.cornerLast, st->curBuf), st->cornerLastNum, ends + TS, nullptr, ob.nC.gPts,
                           fine_T(st->cornerLastNum, ob.gTC), c.N, L.sufC, L.preC, L.n[N_IRR_C]};
 }
 
@@ -797,15 +846,19 @@ __device__ __forceinline__ void build_indexes(const OdomLds& L, const OdomBufs& 
                                               const DevCfg& c, unsigned long long* prof = nullptr) {
   const unsigned long long t0 = (prof && threadIdx.x == 0) ? wall_clock64() : 0;
   if (st->resident) {
-    NNStore<uint16_t> sS{L.gEndS, L.gOrdS, L.sufS, L.preS, &L.n[N_IRR_S], kLdsGridS};
-    NNStore<uint16_t> sC{L.gEndC, L.gOrdC, L.sufC, L.preC, &L.n[N_IRR_C], kLdsGridC};
+    NNStore<uint16_t> sS{L.gEndS, L.gOrdS, nullptr, L.sufS, L.preS, &L.n[N_IRR_S], kLdsGridS};
+    NNStore<uint16_t> sC{L.gEndC, L.gOrdC, nullptr, L.sufC, L.preC, &L.n[N_IRR_C], kLdsGridC};
     nn_build2<uint16_t>(L.lastS, st->surfLastNum, sS, L.lastC, st->cornerLastNum, sC, c.N, L.cnt, L.wtot,
                         L.kfirst, L.klast);
   } else {
-    NNStore<uint32_t> sS{ob.nS.gEnd, ob.nS.gOrd, L.sufS, L.preS, &L.n[N_IRR_S], ob.gTS};
-    NNStore<uint32_t> sC{ob.nC.gEnd, ob.nC.gOrd, L.sufC, L.preC, &L.n[N_IRR_C], ob.gTC};
+    // counters in LDS; the bucket ends are the counters themselves (the
+    // build's final pass rewrites each in place, corner ends less nS)
+    unsigned* cnt = hbm_grid_ends(L);
+    const int TS = fine_T(st->surfLastNum, ob.gTS);
+    NNStore<uint32_t> sS{cnt, nullptr, ob.nS.gPts, L.sufS, L.preS, &L.n[N_IRR_S], ob.gTS};
+    NNStore<uint32_t> sC{cnt + TS, nullptr, ob.nC.gPts, L.sufC, L.preC, &L.n[N_IRR_C], ob.gTC};
     nn_build2<uint32_t>(buf2(ob.surfLast, st->curBuf), st->surfLastNum, sS, buf2(ob.cornerLast, st->curBuf),
-                        st->cornerLastNum, sC, c.N, ob.cnt, L.wtot, L.kfirst, L.klast);
+                        st->cornerLastNum, sC, c.N, cnt, L.wtot, L.kfirst, L.klast);
   }
   if (prof && threadIdx.x == 0) prof[P_B_SURF] += wall_clock64() - t0;
 }
@@ -1231,9 +1284,8 @@ __device__ __forceinline__ OdomBufs odom_private(OdomBufs ob) {
   ob.cornerLast[1] += w * ob.capCorner;
   ob.surfLast[0] += w * ob.capSurf;
   ob.surfLast[1] += w * ob.capSurf;
-  ob.nC.gEnd += w * ob.gTC; ob.nC.gOrd += w * ob.capCorner;
-  ob.nS.gEnd += w * ob.gTS; ob.nS.gOrd += w * ob.capSurf;
-  ob.cnt += w * ob.cntCap;
+  ob.nC.gPts += w * ob.capCorner;
+  ob.nS.gPts += w * ob.capSurf;
   ob.qi += w * 3 * ob.capQ;
   return ob;
 }
@@ -1396,12 +1448,16 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
   if (lead && tid < (int)(sizeof(OdomState) / 4)) ((int*)ob.st)[tid] = ((const int*)st)[tid];
 }
 
+// Bucket caps of the HBM-resident grids: both bucket arrays live in LDS
+// (kHbmLdsCnt counters), so at most 16 k surf + 8 k corner buckets.
+constexpr int kHbmTS = 16384, kHbmTC = 8192;
+static_assert(kHbmTS + kHbmTC <= kHbmLdsCnt, "HBM-path grid ends fit the free LDS");
 void odom_index_caps(int capCorner, int capSurf, int* gTC, int* gTS) {
   int t = 64;
-  while (t < capCorner / 2) t <<= 1;
+  while (t < capCorner / 2 && t < kHbmTC) t <<= 1;
   *gTC = t;
   t = 64;
-  while (t < capSurf / 2) t <<= 1;
+  while (t < capSurf / 2 && t < kHbmTS) t <<= 1;
   *gTS = t;
 }
 
