@@ -766,7 +766,7 @@ struct OdomLds {
   uint16_t *gEndS, *gOrdS, *gEndC, *gOrdC;  // fine grids
   int *sufS, *preS, *sufC, *preC;           // [kKeyTab] per-key first / last
   int *kfirst, *klast;                      // [2 * kMaxRings] build scratch
-  double* red;       // [2][kOdomWaves * 10] reduction partials (iteration parity)
+  double* red;       // [2][kOdomWaves * 4 * 10] reduction row partials (iteration parity)
   SolveWs* sw;
   int* wtot;         // [kOdomWaves]
   int* n;            // [16] flags
@@ -774,15 +774,17 @@ struct OdomLds {
 };
 enum { N_BREAK = 0, N_IRR_S = 1, N_IRR_C = 2, N_ROUND = 3 };
 
-__host__ __device__ inline size_t odom_lds_bytes() {
+__host__ __device__ constexpr size_t odom_lds_bytes() {
   size_t s = 0;
   s += (size_t)kLdsSurf * 16 + (size_t)kLdsCorner * 16 + (size_t)kLdsCnt * 4 + (size_t)3 * kLdsQ * 4;
   s += (size_t)kLdsQ * 16 + (size_t)(kLdsQ / 2) * 16;
   s += (size_t)(kLdsGridS + kLdsSurf + kLdsGridC + kLdsCorner) * 2;
   s += (size_t)4 * kKeyTab * 4 + (size_t)4 * kMaxRings * 4;
-  s += (size_t)2 * kOdomWaves * 10 * 8 + 256 + (size_t)kOdomWaves * 4 + 16 * 4 + 128;
+  s += (size_t)2 * kOdomWaves * 4 * 10 * 8 + 256 + (size_t)kOdomWaves * 4 + 16 * 4 + 128;
   return s;
 }
+
+static_assert(odom_lds_bytes() <= 160 * 1024, "odometry LDS fits one CU");
 
 __device__ __forceinline__ OdomLds odom_carve(unsigned char* base) {
   OdomLds L;
@@ -793,7 +795,7 @@ __device__ __forceinline__ OdomLds odom_carve(unsigned char* base) {
   L.qsharp = (float4*)(base + o); o += (size_t)(kLdsQ / 2) * 16;
   L.cnt = (unsigned*)(base + o); o += (size_t)kLdsCnt * 4;
   L.qi = (int*)(base + o); o += (size_t)3 * kLdsQ * 4;
-  L.red = (double*)(base + o); o += (size_t)2 * kOdomWaves * 10 * 8;
+  L.red = (double*)(base + o); o += (size_t)2 * kOdomWaves * 4 * 10 * 8;
   L.sw = (SolveWs*)(base + o); o += 256;
   L.gEndS = (uint16_t*)(base + o); o += (size_t)kLdsGridS * 2;
   L.gOrdS = (uint16_t*)(base + o); o += (size_t)kLdsSurf * 2;
@@ -879,45 +881,53 @@ __device__ __forceinline__ double rdlane_f64(double v, int l) {
   const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
-__device__ __forceinline__ double wave_sum_f64(double v) {
+
+// Row sums (16 lanes) of a double through DPP lane moves: quad swaps, then
+// half-row and row mirrors leave every lane of a row its row's sum.
+__device__ __forceinline__ double row_sum_f64(double v) {
   v += dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]
   v += dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]
   v += dpp_f64<0x141>(v);  // row_half_mirror
   v += dpp_f64<0x140>(v);  // row_mirror
-  return (rdlane_f64(v, 0) + rdlane_f64(v, 16)) + (rdlane_f64(v, 32) + rdlane_f64(v, 48));
+  return v;
 }
 
 // 9 doubles (AtA upper triangle 6 + AtB 3) + the row count over the block.
-// Every wave gets the totals (waves summed in order, identically in each), so
-// the solve that follows runs redundantly in every wave without a second
-// barrier.  The partials are double-buffered by iteration parity: a wave can
-// run at most one iteration ahead of the slowest reader.  Waves without
-// queries contribute zeros and skip the lane reduction.
+// The waves that hold queries (nw) reduce each quantity to four row sums and
+// their row leaders put them in LDS; after the barrier lane 4k + r of every
+// wave sums row r of quantity k over the waves in order, a quad DPP adds the
+// four rows, and readlanes hand every wave the same totals, so the solve
+// that follows runs redundantly in every wave without a second barrier.
+// Deterministic (a fixed tree).  The partials are double-buffered by
+// iteration parity: a wave can run at most one iteration ahead of the
+// slowest reader.
 __device__ __forceinline__ void block_sum9(double v[9], int m, int nQ, int parity, const OdomLds& L, double out[9],
                                            int* mt) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  double* red = L.red + parity * kOdomWaves * 10;
-  double r[10];
-  if (wave * 64 < nQ) {
+  const int nw = min(kOdomWaves, (nQ + 63) >> 6);
+  double* red = L.red + parity * kOdomWaves * 4 * 10;
+  if (wave < nw) {
+    double r[10];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) r[k] = wave_sum_f64(v[k]);
-    r[9] = wave_sum_f64((double)m);
-  } else {
+    for (int k = 0; k < 9; ++k) r[k] = row_sum_f64(v[k]);
+    r[9] = row_sum_f64((double)m);
+    if ((lane & 15) == 0) {
+      double* dst = red + (wave * 4 + (lane >> 4)) * 10;
 #pragma unroll
-    for (int k = 0; k < 10; ++k) r[k] = 0.0;
-  }
-  if (lane == 0) {
-#pragma unroll
-    for (int k = 0; k < 10; ++k) red[wave * 10 + k] = r[k];
+      for (int k = 0; k < 10; ++k) dst[k] = r[k];
+    }
   }
   __syncthreads();
-  // lanes 0..9 of every wave each sum one quantity over the waves
-  double sum = 0;
-  if (lane < 10)
-    for (int w = 0; w < kOdomWaves; ++w) sum += red[w * 10 + lane];
+  double s = 0;
+  if (lane < 40) {
+    const int row = lane & 3, k = lane >> 2;
+    for (int w = 0; w < nw; ++w) s += red[(w * 4 + row) * 10 + k];
+  }
+  s += dpp_f64<0xB1>(s);
+  s += dpp_f64<0x4E>(s);
 #pragma unroll
-  for (int k = 0; k < 9; ++k) out[k] = rdlane_f64(sum, k);
-  *mt = (int)rdlane_f64(sum, 9);
+  for (int k = 0; k < 9; ++k) out[k] = rdlane_f64(s, 4 * k);
+  *mt = (int)rdlane_f64(s, 36);
 }
 
 struct ScanFeat {
