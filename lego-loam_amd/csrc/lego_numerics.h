@@ -252,6 +252,41 @@ LEGO_HD float lego_cosf(float y) {
   return (y - y) / (y - y);
 }
 
+// sinf and cosf of one argument (glibc's sincosf structure): the range
+// reduction, sign and table are shared and each result is the very
+// expression lego_sinf / lego_cosf evaluate, so both are bit-identical to them.
+LEGO_HD void lego_sincosf(float y, float* sp, float* cp) {
+  double x = y;
+  int n;
+  const float pio4 = 0x1.921FB6p-1f;
+  if (abstop12(y) < abstop12(pio4)) {
+    const double x2 = x * x;
+    if (abstop12(y) < abstop12(0x1p-12f)) {
+      *sp = y;
+      *cp = 1.0f;
+      return;
+    }
+    *sp = sinf_poly(x, x2, sincos_tab(0), 0);
+    *cp = sinf_poly(x, x2, sincos_tab(0), 1);
+  } else if (abstop12(y) < abstop12(120.0f)) {
+    x = reduce_fast(x, sincos_tab(0), &n);
+    const double s = sincos_sign(n & 3);
+    const SinCosTab p = sincos_tab((n & 2) ? 1 : 0);
+    *sp = sinf_poly(x * s, x * x, p, n);
+    *cp = sinf_poly(x * s, x * x, p, n ^ 1);
+  } else if (abstop12(y) < abstop12(__builtin_inff())) {
+    const uint32_t xi = f2u(y);
+    const int sign = xi >> 31;
+    x = reduce_large(xi, &n);
+    const double s = sincos_sign((n + sign) & 3);
+    const SinCosTab p = sincos_tab(((n + sign) & 2) ? 1 : 0);
+    *sp = sinf_poly(x * s, x * x, p, n);
+    *cp = sinf_poly(x * s, x * x, p, n ^ 1);
+  } else {
+    *sp = *cp = (y - y) / (y - y);
+  }
+}
+
 // ---------------------------------------------------------------- asinf
 LEGO_HD float lego_asinf(float x) {
   const float one = 1.0f;

@@ -70,9 +70,10 @@ __device__ __forceinline__ float4 to_start_t(float4 pi, float s, const float* tc
 }
 __device__ __forceinline__ float4 to_start(float4 pi, const float* tc) {  // :860-883
   const float s = start_s(pi);
-  const float rx = s * tc[0], ry = s * tc[1], rz = s * tc[2];
-  const float cz = lego_cosf(rz), sz = lego_sinf(rz), cx = lego_cosf(rx), sx = lego_sinf(rx);
-  const float cy = lego_cosf(ry), sy = lego_sinf(ry);
+  float cx, sx, cy, sy, cz, sz;
+  lego_sincosf(s * tc[0], &sx, &cx);
+  lego_sincosf(s * tc[1], &sy, &cy);
+  lego_sincosf(s * tc[2], &sz, &cz);
   return to_start_t(pi, s, tc, cx, sx, cy, sy, cz, sz);
 }
 // One LM step moves only three of transformCur's components (surf: rx, rz,
@@ -88,19 +89,25 @@ __device__ __forceinline__ float4 to_start_fix(float4 pi, const float* tc, bool 
   const float s = start_s(pi);
   if (surf) {  // ry fixed
     if (!f.have || __float_as_uint(tc[1]) != f.ka) {
-      const float ry = s * tc[1];
-      f.sa = lego_sinf(ry); f.ca = lego_cosf(ry); f.ka = __float_as_uint(tc[1]); f.have = true;
+      lego_sincosf(s * tc[1], &f.sa, &f.ca);
+      f.ka = __float_as_uint(tc[1]);
+      f.have = true;
     }
-    const float rx = s * tc[0], rz = s * tc[2];
-    return to_start_t(pi, s, tc, lego_cosf(rx), lego_sinf(rx), f.ca, f.sa, lego_cosf(rz), lego_sinf(rz));
+    float cx, sx, cz, sz;
+    lego_sincosf(s * tc[0], &sx, &cx);
+    lego_sincosf(s * tc[2], &sz, &cz);
+    return to_start_t(pi, s, tc, cx, sx, f.ca, f.sa, cz, sz);
   }
   if (!f.have || __float_as_uint(tc[0]) != f.ka || __float_as_uint(tc[2]) != f.kb) {  // rx, rz fixed
-    const float rx = s * tc[0], rz = s * tc[2];
-    f.sa = lego_sinf(rx); f.ca = lego_cosf(rx); f.ka = __float_as_uint(tc[0]);
-    f.sb = lego_sinf(rz); f.cb = lego_cosf(rz); f.kb = __float_as_uint(tc[2]); f.have = true;
+    lego_sincosf(s * tc[0], &f.sa, &f.ca);
+    f.ka = __float_as_uint(tc[0]);
+    lego_sincosf(s * tc[2], &f.sb, &f.cb);
+    f.kb = __float_as_uint(tc[2]);
+    f.have = true;
   }
-  const float ry = s * tc[1];
-  return to_start_t(pi, s, tc, f.ca, f.sa, lego_cosf(ry), lego_sinf(ry), f.cb, f.sb);
+  float cy, sy;
+  lego_sincosf(s * tc[1], &sy, &cy);
+  return to_start_t(pi, s, tc, f.ca, f.sa, cy, sy, f.cb, f.sb);
 }
 
 // TransformToEnd :885-953 with the IMU terms of an IMU-less run
@@ -119,10 +126,11 @@ __device__ __forceinline__ EndTrig end_trig(const float* tc) {
 }
 __device__ __forceinline__ float4 to_end(float4 pi, const float* tc, const EndTrig& et, const ImuEnd& im) {
   const float s = 10 * (pi.w - (float)(int)pi.w);
-  float rx = s * tc[0], ry = s * tc[1], rz = s * tc[2];
   float tx = s * tc[3], ty = s * tc[4], tz = s * tc[5];
-  float cz = lego_cosf(rz), sz = lego_sinf(rz), cx = lego_cosf(rx), sx = lego_sinf(rx);
-  float cy = lego_cosf(ry), sy = lego_sinf(ry);
+  float cx, sx, cy, sy, cz, sz;
+  lego_sincosf(s * tc[0], &sx, &cx);
+  lego_sincosf(s * tc[1], &sy, &cy);
+  lego_sincosf(s * tc[2], &sz, &cz);
   const float x1 = cz * (pi.x - tx) + sz * (pi.y - ty);
   const float y1 = -sz * (pi.x - tx) + cz * (pi.y - ty);
   const float z1 = (pi.z - tz);
@@ -1065,10 +1073,11 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
     if (nnIter) S.count(P_NNR);
     // sin / cos of the three angles: lanes 0-2 and 3-5 of each wave, then broadcast
     float trig;
-    {
+    {  // lanes 0-2 the sines, 3-5 the cosines: one fused evaluation, no divergence
       const int l = tid & 63;
-      const float a = tc[l % 3];
-      trig = l < 3 ? lego_sinf(a) : lego_cosf(a);
+      float sv, cv;
+      lego_sincosf(tc[l % 3], &sv, &cv);
+      trig = l < 3 ? sv : cv;
     }
     const float srx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(trig), 0));
     const float sry = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(trig), 1));

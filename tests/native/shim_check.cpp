@@ -1,7 +1,7 @@
 // Pins lego-loam_amd/csrc/lego_numerics.h (the libm restatement shared by the
 // oracle and the gfx950 kernels) against THIS host's glibc, bit for bit.
 //   shim_check <stride> <pairs>
-// sinf/cosf/atanf/asinf over every `stride`-th float bit pattern (stride 1 =
+// sinf/cosf (and the fused lego_sincosf)/atanf/asinf over every `stride`-th float bit pattern (stride 1 =
 // exhaustive), atan2f over `pairs` random bit-pattern pairs plus `pairs`
 // uniform pairs in [-100,100]^2.  Prints mismatch counts; exit 1 on any.
 #include <cmath>
@@ -28,6 +28,10 @@ int main(int argc, char** argv) {
       ++n_;
       if (!same(sinf(x), lego_sinf(x))) s_++;
       if (!same(cosf(x), lego_cosf(x))) c_++;
+      float fs, fc;  // the fused form must equal both (and so glibc)
+      lego_sincosf(x, &fs, &fc);
+      if (!same(fs, lego_sinf(x))) s_++;
+      if (!same(fc, lego_cosf(x))) c_++;
       if (!same(asinf(x), lego_asinf(x))) a_++;
       if (!same(atanf(x), lego_atanf(x))) t_++;
     }
