@@ -792,7 +792,7 @@ __host__ __device__ constexpr size_t odom_lds_bytes() {
   return s;
 }
 
-static_assert(odom_lds_bytes() <= 160 * 1024, "odometry LDS fits one CU");
+static_assert(odom_lds_bytes() + 32 * 8 <= 160 * 1024, "odometry LDS (+ the stamp accumulators) fits one CU");
 
 __device__ __forceinline__ OdomLds odom_carve(unsigned char* base) {
   OdomLds L;
@@ -1321,6 +1321,14 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
   const int b0 = (int)(blockIdx.x / ob.G) * K;
   const bool lead = ob.wg == 0;  // writes the stream's outputs and state
   if (blockIdx.x != 0) prof = nullptr;
+  // stamps accumulate in LDS (a global read-modify-write per stamp would put
+  // an L2 round trip on the chain it measures); added to prof at the end
+  __shared__ unsigned long long sprof[P_NPROF];
+  unsigned long long* const gprof = prof;
+  if (gprof) {
+    if (threadIdx.x < P_NPROF) sprof[threadIdx.x] = 0;
+    prof = sprof;
+  }
   Stamp S{prof, 0};
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   const OdomLds L = odom_carve(lds_raw);
@@ -1465,6 +1473,7 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
   }
   __syncthreads();
   if (lead && tid < (int)(sizeof(OdomState) / 4)) ((int*)ob.st)[tid] = ((const int*)st)[tid];
+  if (gprof && tid < P_NPROF) gprof[tid] += sprof[tid];
 }
 
 // Bucket caps of the HBM-resident grids: both bucket arrays live in LDS
