@@ -430,10 +430,11 @@ def main():
                   f" scan-line indexed {prof[20] / nsc:.1f}, scan-line literal {prof[13] / nsc:.1f}",
                   file=sys.stderr)
             for i, nm in ((21, "rows (excl. reduce)"), (22, "solve_qr+eig it0"), (23, "solve_qr it>0"),
-                          (24, "nn local work"), (25, "build surf"), (26, "build corner")):
+                          (24, "nn local work"), (25, "build (all)"), (26, "build: count pass"),
+                          (27, "build: key tables+scan"), (29, "build: scatter pass"), (31, "build: bucket ends")):
                 print(f"  odom.{nm:20s} {prof[i] / 100.0 / nsc:9.2f} us/scan", file=sys.stderr)
             nq0 = max(prof[30], 1)
-            for i, nm in ((27, "wave0 q: to_start"), (28, "wave0 q: nn i1"), (29, "wave0 q: scan-line")):
+            for i, nm in ((28, "wave0 q: nn i1"),):
                 print(f"  odom.{nm:20s} {prof[i] / 100.0 / nq0:9.2f} us/query ({prof[30] / nsc:.1f} q/scan)",
                       file=sys.stderr)
         if args.stages:

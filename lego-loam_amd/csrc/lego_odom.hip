@@ -350,7 +350,8 @@ enum { P_SURF_NN = 0, P_SURF = 1, P_CORN_NN = 2, P_CORN = 3, P_SOLVE = 4, P_INTE
        P_TOEND = 6, P_BUILD = 7, P_RESID = 8, P_ITERS_S = 9, P_ITERS_C = 10, P_NNR = 11,
        P_QUERY = 12, P_SCANLINE = 13, P_NN_SHELL1 = 14, P_NN_BRUTE = 15,
        P_G0_TOSTART = 16, P_G0_NN = 17, P_G0_SCAN = 18, P_G0_Q = 19, P_AZLINE = 20,
-       P_T_ROWS = 21, P_T_SOLVE0 = 22, P_T_SOLVE = 23, P_X_LOCAL = 24, P_B_SURF = 25, P_B_CORN = 26,
+       P_T_ROWS = 21, P_T_SOLVE0 = 22, P_T_SOLVE = 23, P_X_LOCAL = 24, P_B_SURF = 25,
+       P_B_PASS1 = 26, P_B_SCAN = 27, P_B_SCATTER = 29, P_B_ENDS = 31,  // index-build sub-phases
        P_NPROF = 32 };
 struct Stamp {
   unsigned long long* prof;
@@ -434,75 +435,93 @@ __device__ __forceinline__ void block_exscan(unsigned* a, int n, int* wtot) {
 // Builds both clouds' fine grids and key tables in shared passes (all
 // threads; half the barriers of two builds): ptsS[0..nS) then ptsC[0..nC) as
 // one index range, surf buckets [0, TS) then corner buckets [TS, TS + TC) in
-// one counter array (>= TS + TC entries), kfirst / klast [2 * NK].
+// one counter array (>= TS + TC entries), kfirst / klast [2 * NK].  Three
+// phases: build_zero, build_count (per wave chunk of 64 consecutive indices;
+// the hand-off runs it on the points TransformToEnd has just produced, so the
+// clouds are not read back for it) and build_finish.
 template <class Idx>
-__device__ __forceinline__ void nn_build2(const float4* ptsS, int nS, const NNStore<Idx>& S, const float4* ptsC,
-                                          int nC, const NNStore<Idx>& Cs, int NK, unsigned* cnt, int* wtot,
-                                          int* kfirst, int* klast) {
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int TS = fine_T(nS, S.Tcap), TC = fine_T(nC, Cs.Tcap), n = nS + nC;
-  for (int b = tid; b < TS + TC; b += kOdomThreads) cnt[b] = 0;
-  for (int k = tid; k < 2 * NK; k += kOdomThreads) { kfirst[k] = INT_MAX; klast[k] = -1; }
-  if (tid == 0) { *S.irregular = 0; *Cs.irregular = 0; }
-  __syncthreads();
-  // kBuildU points per lane in flight (HBM clouds: one load latency per pass
-  // of kBuildU, not per point)
-  constexpr int kBuildU = 4;
-  for (int j0 = tid - lane; j0 < n; j0 += kBuildU * kOdomThreads) {  // wave-uniform loop
-    float4 pu[kBuildU];
-#pragma unroll
-    for (int u = 0; u < kBuildU; ++u) {
-      const int i = j0 + u * kOdomThreads + lane;
-      if (i < n) pu[u] = i >= nS ? ptsC[i - nS] : ptsS[i];
-    }
-#pragma unroll
-    for (int u = 0; u < kBuildU; ++u) {
-      const int i0 = j0 + u * kOdomThreads;
-      if (i0 >= n) break;
-      const int i = i0 + lane;
-      int kk = -1;
-      if (i < n) {
-        const bool corner = i >= nS;
-        const float4 p = pu[u];
-        const int T = corner ? TC : TS;
-        atomicAdd(&cnt[(corner ? TS : 0) + fine_bucket(cell_of(p.x), cell_of(p.y), cell_of(p.z), T)], 1u);
-        const int k = (int)p.w;
-        if (k < 0 || k >= NK) *(corner ? Cs.irregular : S.irregular) = 1;
-        else kk = k + (corner ? NK : 0);
-      }
-      // per-key first/last: one atomic per distinct (cloud, key) of the wave
-      unsigned long long todo = __ballot(kk >= 0);
-      while (todo) {
-        const int leader = __ffsll((long long)todo) - 1;
-        const int key = __builtin_amdgcn_readlane(kk, leader);
-        const unsigned long long m = __ballot(kk == key);
-        if (lane == leader) {
-          const int base = key >= NK ? nS : 0;
-          atomicMin(&kfirst[key], i0 + leader - base);
-          atomicMax(&klast[key], i0 + 63 - __clzll((long long)m) - base);
-        }
-        todo &= ~m;
-      }
-    }
+struct BuildArgs {
+  const float4 *ptsS, *ptsC;
+  int nS, nC, TS, TC, NK;
+  NNStore<Idx> S, Cs;
+  unsigned* cnt;
+  int *wtot, *kfirst, *klast;
+};
+template <class Idx>
+__device__ __forceinline__ BuildArgs<Idx> build_args(const float4* ptsS, int nS, const NNStore<Idx>& S,
+                                                     const float4* ptsC, int nC, const NNStore<Idx>& Cs, int NK,
+                                                     unsigned* cnt, int* wtot, int* kfirst, int* klast) {
+  return BuildArgs<Idx>{ptsS, ptsC, nS, nC, fine_T(nS, S.Tcap), fine_T(nC, Cs.Tcap), NK, S, Cs,
+                        cnt, wtot, kfirst, klast};
+}
+// zeroes the counters and key tables (all threads; the caller's barrier follows)
+template <class Idx>
+__device__ __forceinline__ void build_zero(const BuildArgs<Idx>& B) {
+  const int tid = threadIdx.x;
+  for (int b = tid; b < B.TS + B.TC; b += kOdomThreads) B.cnt[b] = 0;
+  for (int k = tid; k < 2 * B.NK; k += kOdomThreads) { B.kfirst[k] = INT_MAX; B.klast[k] = -1; }
+  if (tid == 0) { *B.S.irregular = 0; *B.Cs.irregular = 0; }
+}
+// counts the wave's chunk [i0, i0 + 64) of the combined index range; lane
+// i0 + lane holds point p (ignored past nS + nC).  Wave-uniform call.
+template <class Idx>
+__device__ __forceinline__ void build_count(const BuildArgs<Idx>& B, int i0, float4 p) {
+  const int lane = threadIdx.x & 63, i = i0 + lane, n = B.nS + B.nC;
+  int kk = -1;
+  if (i < n) {
+    const bool corner = i >= B.nS;
+    const int T = corner ? B.TC : B.TS;
+    atomicAdd(&B.cnt[(corner ? B.TS : 0) + fine_bucket(cell_of(p.x), cell_of(p.y), cell_of(p.z), T)], 1u);
+    const int k = (int)p.w;
+    if (k < 0 || k >= B.NK) *(corner ? B.Cs.irregular : B.S.irregular) = 1;
+    else kk = k + (corner ? B.NK : 0);
   }
-  __syncthreads();
+  // per-key first/last: one atomic per distinct (cloud, key) of the wave
+  unsigned long long todo = __ballot(kk >= 0);
+  while (todo) {
+    const int leader = __ffsll((long long)todo) - 1;
+    const int key = __builtin_amdgcn_readlane(kk, leader);
+    const unsigned long long m = __ballot(kk == key);
+    if (lane == leader) {
+      const int base = key >= B.NK ? B.nS : 0;
+      atomicMin(&B.kfirst[key], i0 + leader - base);
+      atomicMax(&B.klast[key], i0 + 63 - __clzll((long long)m) - base);
+    }
+    todo &= ~m;
+  }
+}
+// key tables, bucket starts, scatter, bucket ends (all threads, after a
+// barrier that follows the last build_count)
+template <class Idx>
+__device__ __forceinline__ void build_finish(const BuildArgs<Idx>& B, unsigned long long* prof) {
+  const int tid = threadIdx.x;
+  const int nS = B.nS, TS = B.TS, TC = B.TC, NK = B.NK, n = B.nS + B.nC;
+  const NNStore<Idx>& S = B.S;
+  const NNStore<Idx>& Cs = B.Cs;
+  unsigned* cnt = B.cnt;
+  unsigned long long tp = (prof && tid == 0) ? wall_clock64() : 0;
+  auto stamp = [&](int k) {
+    if (prof && tid == 0) { const unsigned long long t = wall_clock64(); prof[k] += t - tp; tp = t; }
+  };
   // suffix-min of first / prefix-max of last, one thread per (cloud, key)
   for (int t = tid; t < 2 * NK; t += kOdomThreads) {
     const int c0 = t >= NK ? NK : 0, k = t - c0;
     int m = INT_MAX, M = -1;
-    for (int j = k; j < NK; ++j) m = min(m, kfirst[c0 + j]);
-    for (int j = 0; j <= k; ++j) M = max(M, klast[c0 + j]);
+    for (int j = k; j < NK; ++j) m = min(m, B.kfirst[c0 + j]);
+    for (int j = 0; j <= k; ++j) M = max(M, B.klast[c0 + j]);
     (c0 ? Cs : S).sufFirst[k] = m;
     (c0 ? Cs : S).preLast[k] = M;
   }
   if (tid == 0) { S.sufFirst[NK] = INT_MAX; Cs.sufFirst[NK] = INT_MAX; }
-  block_exscan(cnt, TS + TC, wtot);  // corner starts come out offset by nS
+  block_exscan(cnt, TS + TC, B.wtot);  // corner starts come out offset by nS
+  stamp(P_B_SCAN);
+  constexpr int kBuildU = 4;  // points per lane in flight
   for (int j = tid; j < n; j += kBuildU * kOdomThreads) {
     float4 pu[kBuildU];
 #pragma unroll
     for (int u = 0; u < kBuildU; ++u) {
       const int i = j + u * kOdomThreads;
-      if (i < n) pu[u] = i >= nS ? ptsC[i - nS] : ptsS[i];
+      if (i < n) pu[u] = i >= nS ? B.ptsC[i - nS] : B.ptsS[i];
     }
 #pragma unroll
     for (int u = 0; u < kBuildU; ++u) {
@@ -523,11 +542,38 @@ __device__ __forceinline__ void nn_build2(const float4* ptsS, int nS, const NNSt
     }
   }
   __syncthreads();
+  stamp(P_B_SCATTER);
   for (int b = tid; b < TS + TC; b += kOdomThreads) {
     if (b < TS) S.gEnd[b] = (Idx)cnt[b];
     else Cs.gEnd[b - TS] = (Idx)(cnt[b] - nS);
   }
   __syncthreads();
+  stamp(P_B_ENDS);
+}
+template <class Idx>
+__device__ __forceinline__ void nn_build2(const BuildArgs<Idx>& B, unsigned long long* prof = nullptr) {
+  const int tid = threadIdx.x, lane = tid & 63, n = B.nS + B.nC;
+  const unsigned long long tp = (prof && tid == 0) ? wall_clock64() : 0;
+  build_zero(B);
+  __syncthreads();
+  constexpr int kBuildU = 4;  // points per lane in flight
+  for (int j0 = tid - lane; j0 < n; j0 += kBuildU * kOdomThreads) {  // wave-uniform loop
+    float4 pu[kBuildU];
+#pragma unroll
+    for (int u = 0; u < kBuildU; ++u) {
+      const int i = j0 + u * kOdomThreads + lane;
+      if (i < n) pu[u] = i >= B.nS ? B.ptsC[i - B.nS] : B.ptsS[i];
+    }
+#pragma unroll
+    for (int u = 0; u < kBuildU; ++u) {
+      const int i0 = j0 + u * kOdomThreads;
+      if (i0 >= n) break;
+      build_count(B, i0, pu[u]);
+    }
+  }
+  __syncthreads();
+  if (prof && tid == 0) prof[P_B_PASS1] += wall_clock64() - tp;
+  build_finish(B, prof);
 }
 
 template <class Idx>
@@ -851,25 +897,33 @@ __device__ __forceinline__ NNView<uint32_t> view_hbm(bool surf, const OdomLds& L
                           fine_T(st->cornerLastNum, ob.gTC), c.N, L.sufC, L.preC, L.n[N_IRR_C]};
 }
 
+// The build arguments of both clouds' indexes over the current last clouds
+// (st->curBuf, st->*LastNum) in the layout `resident` selects.
+__device__ __forceinline__ BuildArgs<uint16_t> lds_build_args(const OdomLds& L, const OdomState* st,
+                                                              const DevCfg& c) {
+  NNStore<uint16_t> sS{L.gEndS, L.gOrdS, nullptr, L.sufS, L.preS, &L.n[N_IRR_S], kLdsGridS};
+  NNStore<uint16_t> sC{L.gEndC, L.gOrdC, nullptr, L.sufC, L.preC, &L.n[N_IRR_C], kLdsGridC};
+  return build_args<uint16_t>(L.lastS, st->surfLastNum, sS, L.lastC, st->cornerLastNum, sC, c.N, L.cnt, L.wtot,
+                              L.kfirst, L.klast);
+}
+__device__ __forceinline__ BuildArgs<uint32_t> hbm_build_args(const OdomLds& L, const OdomBufs& ob,
+                                                              const OdomState* st, const DevCfg& c) {
+  // counters in LDS; the bucket ends are the counters themselves (the
+  // build's final pass rewrites each in place, corner ends less nS)
+  unsigned* cnt = hbm_grid_ends(L);
+  const int TS = fine_T(st->surfLastNum, ob.gTS);
+  NNStore<uint32_t> sS{cnt, nullptr, ob.nS.gPts, L.sufS, L.preS, &L.n[N_IRR_S], ob.gTS};
+  NNStore<uint32_t> sC{cnt + TS, nullptr, ob.nC.gPts, L.sufC, L.preC, &L.n[N_IRR_C], ob.gTC};
+  return build_args<uint32_t>(buf2(ob.surfLast, st->curBuf), st->surfLastNum, sS, buf2(ob.cornerLast, st->curBuf),
+                              st->cornerLastNum, sC, c.N, cnt, L.wtot, L.kfirst, L.klast);
+}
+
 // Rebuilds both clouds' indexes (all threads) over the current last clouds.
 __device__ __forceinline__ void build_indexes(const OdomLds& L, const OdomBufs& ob, const OdomState* st,
                                               const DevCfg& c, unsigned long long* prof = nullptr) {
   const unsigned long long t0 = (prof && threadIdx.x == 0) ? wall_clock64() : 0;
-  if (st->resident) {
-    NNStore<uint16_t> sS{L.gEndS, L.gOrdS, nullptr, L.sufS, L.preS, &L.n[N_IRR_S], kLdsGridS};
-    NNStore<uint16_t> sC{L.gEndC, L.gOrdC, nullptr, L.sufC, L.preC, &L.n[N_IRR_C], kLdsGridC};
-    nn_build2<uint16_t>(L.lastS, st->surfLastNum, sS, L.lastC, st->cornerLastNum, sC, c.N, L.cnt, L.wtot,
-                        L.kfirst, L.klast);
-  } else {
-    // counters in LDS; the bucket ends are the counters themselves (the
-    // build's final pass rewrites each in place, corner ends less nS)
-    unsigned* cnt = hbm_grid_ends(L);
-    const int TS = fine_T(st->surfLastNum, ob.gTS);
-    NNStore<uint32_t> sS{cnt, nullptr, ob.nS.gPts, L.sufS, L.preS, &L.n[N_IRR_S], ob.gTS};
-    NNStore<uint32_t> sC{cnt + TS, nullptr, ob.nC.gPts, L.sufC, L.preC, &L.n[N_IRR_C], ob.gTC};
-    nn_build2<uint32_t>(buf2(ob.surfLast, st->curBuf), st->surfLastNum, sS, buf2(ob.cornerLast, st->curBuf),
-                        st->cornerLastNum, sC, c.N, cnt, L.wtot, L.kfirst, L.klast);
-  }
+  if (st->resident) nn_build2(lds_build_args(L, st, c), prof);
+  else nn_build2(hbm_build_args(L, ob, st, c), prof);
   if (prof && threadIdx.x == 0) prof[P_B_SURF] += wall_clock64() - t0;
 }
 
@@ -1421,28 +1475,57 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     // TransformToEnd: both read the final transformCur, only the former
     // writes (transformSum)
     const int t0 = init ? tid : tid - 64, tstep = init ? kOdomThreads : kOdomThreads - 64;
+    const bool rebuild = init || (F.nLS > 10 && F.nLF > 100);
+    // the new clouds' build arguments in the layout they will use
+    NNStore<uint16_t> nsS{L.gEndS, L.gOrdS, nullptr, L.sufS, L.preS, &L.n[N_IRR_S], kLdsGridS};
+    NNStore<uint16_t> nsC{L.gEndC, L.gOrdC, nullptr, L.sufC, L.preC, &L.n[N_IRR_C], kLdsGridC};
+    const BuildArgs<uint16_t> BL = build_args<uint16_t>(L.lastS, F.nLF, nsS, L.lastC, F.nLS, nsC, c.N, L.cnt,
+                                                        L.wtot, L.kfirst, L.klast);
+    unsigned* hcnt = hbm_grid_ends(L);
+    const int hTS = fine_T(F.nLF, ob.gTS);
+    NNStore<uint32_t> hsS{hcnt, nullptr, ob.nS.gPts, L.sufS, L.preS, &L.n[N_IRR_S], ob.gTS};
+    NNStore<uint32_t> hsC{hcnt + hTS, nullptr, ob.nC.gPts, L.sufC, L.preC, &L.n[N_IRR_C], ob.gTC};
+    const BuildArgs<uint32_t> BH = build_args<uint32_t>(gSn, F.nLF, hsS, gCn, F.nLS, hsC, c.N, hcnt, L.wtot,
+                                                        L.kfirst, L.klast);
+    if (rebuild) {  // the counters must be zero before the first chunk is counted
+      if (fits) build_zero(BL);
+      else build_zero(BH);
+    }
+    __syncthreads();
     if (!init && tid < 64) {
       const float bl[3] = {iq.pitchStart, iq.yawStart, iq.rollStart};
       const float al[3] = {iq.pitchCur, iq.yawCur, iq.rollCur};  // imu*Last = imu*Cur (:1641-1643)
       integrate_wave(st->transformSum, st->transformCur, bl, al);
     }
-    if (t0 >= 0) {
-      for (int t = t0; t < F.nLS; t += tstep) {
-        const float4 p = init ? F.lsharp[t] : to_end(F.lsharp[t], tcur, et, im);
-        gCn[t] = p;
-        if (lead) cEnd[t] = p;
-        if (fits) L.lastC[t] = p;
+    // TransformToEnd of less-flat then less-sharp as one index range in
+    // wave-uniform chunks, each chunk counted into the next index as it is
+    // produced (build_count: no read-back of the clouds for the counting pass)
+    auto hand_off = [&](const auto& B) {
+      if (t0 >= 0) {
+        const int nS = F.nLF, n = F.nLF + F.nLS, lane = tid & 63;
+        for (int i0 = t0 - lane; i0 < n; i0 += tstep) {  // wave-uniform
+          const int i = i0 + lane;
+          float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (i < nS) {
+            p = init ? F.lflat[i] : to_end(F.lflat[i], tcur, et, im);
+            gSn[i] = p;
+            if (lead) sEnd[i] = p;
+            if (fits) L.lastS[i] = p;
+          } else if (i < n) {
+            const int j = i - nS;
+            p = init ? F.lsharp[j] : to_end(F.lsharp[j], tcur, et, im);
+            gCn[j] = p;
+            if (lead) cEnd[j] = p;
+            if (fits) L.lastC[j] = p;
+          }
+          if (rebuild) build_count(B, i0, p);
+        }
       }
-      for (int t = t0; t < F.nLF; t += tstep) {
-        const float4 p = init ? F.lflat[t] : to_end(F.lflat[t], tcur, et, im);
-        gSn[t] = p;
-        if (lead) sEnd[t] = p;
-        if (fits) L.lastS[t] = p;
-      }
-    }
+    };
+    if (fits) hand_off(BL);
+    else hand_off(BH);
     __syncthreads();
     S.add(P_TOEND);
-    const bool rebuild = init || (F.nLS > 10 && F.nLF > 100);
     if (tid == 0) {
       st->cornerLastNum = F.nLS;
       st->surfLastNum = F.nLF;
@@ -1468,7 +1551,10 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     __syncthreads();
     unsigned long long tb = 0;
     if (prof && tid == 0) tb = wall_clock64();
-    if (rebuild) build_indexes(L, ob, st, c, prof);
+    if (rebuild) {
+      if (fits) build_finish(BL, prof);
+      else build_finish(BH, prof);
+    }
     if (prof && tid == 0) prof[P_BUILD] += wall_clock64() - tb;
   }
   __syncthreads();
