@@ -290,7 +290,7 @@ def main():
     ap.add_argument("--odom-profile", action="store_true", help="in-kernel phase stamps (diagnostic)")
     ap.add_argument("--mapping-steps", type=int, default=15, help="C5 scan-to-map steps (aux; 0 = skip)")
     ap.add_argument("--fleet-streams", type=int, default=64, help="streams of the fleet aux line (0 = skip)")
-    ap.add_argument("--dense-scans", type=int, default=60, help="C3 HDL-64E scans of the aux line (0 = skip)")
+    ap.add_argument("--dense-scans", type=int, default=200, help="C3 HDL-64E scans of the aux line (0 = skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
