@@ -1,0 +1,52 @@
+#include "../../lego-loam_amd/csrc/lego_odom.hip"
+using namespace lego;
+template <int MODE>
+__global__ void __launch_bounds__(512) ks(double* o, long long* t, int iters) {
+  float tc[6] = {0.01f, 0.02f, -0.015f, 0.1f, 0.05f, 0.2f};
+  float Pm[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+  int isDeg = 0;
+  double tot[9] = {310.5, 12.25, -3.5, 220.75, 4.5, 150.125, 1.5, -0.75, 0.25};
+  int brkc = 0;
+  long long t0 = wall_clock64();
+  for (int it = 0; it < iters; ++it) {
+    float AtA[3][3] = {{(float)tot[0], (float)tot[1], (float)tot[2]},
+                       {(float)tot[1], (float)tot[3], (float)tot[4]},
+                       {(float)tot[2], (float)tot[4], (float)tot[5]}};
+    float AtB[3] = {(float)tot[6], (float)tot[7], (float)tot[8]};
+    float X[3];
+    if (MODE == 2) {
+      float Aq[3][3];
+      for (int a = 0; a < 3; ++a) for (int b = 0; b < 3; ++b) Aq[a][b] = AtA[a][b];
+      cv_solve_qr<3, 3>(Aq, AtB, X);
+    } else {
+      solve_step(AtA, AtB, 1, Pm, isDeg, X);
+    }
+    tc[1] += X[0]; tc[3] += X[1]; tc[5] += X[2];
+    for (int i = 0; i < 6; i++) if (__builtin_isnan(tc[i])) tc[i] = 0;
+    if (MODE == 0) {
+      const double r0 = r2d(X[0]), t1 = (double)(X[1] * 100), t2 = (double)(X[2] * 100);
+      const double dR = (double)(float)__builtin_sqrt(r0 * r0);
+      const double dT = (double)(float)__builtin_sqrt(t1 * t1 + t2 * t2);
+      brkc += dR < 0.1 && dT < 0.1;
+    }
+    tot[6] += tc[1] * 1e-3;  // dependent: the next solve needs this one's result
+  }
+  long long t1 = wall_clock64();
+  if (threadIdx.x == 0) { *t = t1 - t0; *o = tc[1] + tc[3] + brkc; }
+}
+int main() {
+  double* o; long long* t;
+  (void)hipMalloc(&o, 8); (void)hipMalloc(&t, 8);
+  const char* nm[3] = {"solve+update+conv", "solve+update", "QR only"};
+  for (int mode = 0; mode < 3; ++mode) {
+    long long ht = 0;
+    for (int rep = 0; rep < 2; ++rep) {
+      if (mode == 0) ks<0><<<1, 512>>>(o, t, 5000);
+      if (mode == 1) ks<1><<<1, 512>>>(o, t, 5000);
+      if (mode == 2) ks<2><<<1, 512>>>(o, t, 5000);
+      (void)hipDeviceSynchronize();
+      (void)hipMemcpy(&ht, t, 8, hipMemcpyDeviceToHost);
+    }
+    printf("%-20s: %.3f us per iteration\n", nm[mode], ht / 100.0 / 5000);
+  }
+}
