@@ -610,47 +610,46 @@ template <int kCtrl>
 __device__ __forceinline__ int dpp_i32(int v) {
   return __builtin_amdgcn_mov_dpp(v, kCtrl, 0xf, 0xf, false);
 }
-template <int kCtrl>
-__device__ __forceinline__ void lex_step(float& d, int& i) {
-  lex_min(d, i, dpp_f32<kCtrl>(d), dpp_i32<kCtrl>(i));
+// Wave minima through DPP lane moves: quad swaps, half-row and row mirrors
+// leave every lane its row's minimum, four readlanes combine the rows.
+__device__ __forceinline__ float wave_min_f32(float v) {
+  v = fminf(v, dpp_f32<0xB1>(v));
+  v = fminf(v, dpp_f32<0x4E>(v));
+  v = fminf(v, dpp_f32<0x141>(v));
+  v = fminf(v, dpp_f32<0x140>(v));
+  const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float c = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float e = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return fminf(fminf(a, b), fminf(c, e));
 }
+__device__ __forceinline__ int wave_min_i32(int v) {
+  v = min(v, dpp_i32<0xB1>(v));
+  v = min(v, dpp_i32<0x4E>(v));
+  v = min(v, dpp_i32<0x141>(v));
+  v = min(v, dpp_i32<0x140>(v));
+  return min(min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+             min(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+// Lexicographic (distance, second key) minimum over the wave in two plain
+// minima: the smallest distance (distances are finite and >= 0), then the
+// smallest second key among the lanes that hold it.  The order is a total
+// one, so this equals any pairwise lexicographic reduction.
 __device__ __forceinline__ void group_lex_min(float& d, int& i) {
   static_assert(kGL == 64, "DPP reductions span one wave");
-  lex_step<0xB1>(d, i);
-  lex_step<0x4E>(d, i);
-  lex_step<0x141>(d, i);
-  lex_step<0x140>(d, i);
-  float bd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), 0));
-  int bi = __builtin_amdgcn_readlane(i, 0);
-#pragma unroll
-  for (int r = 16; r < 64; r += 16)
-    lex_min(bd, bi, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), r)), __builtin_amdgcn_readlane(i, r));
-  d = bd;
-  i = bi;
+  const float dm = wave_min_f32(d);
+  i = wave_min_i32(d == dm ? i : INT_MAX);
+  d = dm;
 }
-// (distance, visit rank) minimum carrying the index
-template <int kCtrl>
-__device__ __forceinline__ void lex3_step(float& d, int& r, int& j) {
-  const float d2 = dpp_f32<kCtrl>(d);
-  const int r2 = dpp_i32<kCtrl>(r), j2 = dpp_i32<kCtrl>(j);
-  if (d2 < d || (d2 == d && r2 < r)) { d = d2; r = r2; j = j2; }
-}
+// (distance, visit rank) minimum carrying the index of the lane that holds it
+// (ranks are distinct among candidates; without one every lane holds j = -1)
 __device__ __forceinline__ void group_lex_min3(float& d, int& r, int& j) {
-  lex3_step<0xB1>(d, r, j);
-  lex3_step<0x4E>(d, r, j);
-  lex3_step<0x141>(d, r, j);
-  lex3_step<0x140>(d, r, j);
-  float bd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), 0));
-  int br = __builtin_amdgcn_readlane(r, 0), bj = __builtin_amdgcn_readlane(j, 0);
-#pragma unroll
-  for (int q = 16; q < 64; q += 16) {
-    const float d2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), q));
-    const int r2 = __builtin_amdgcn_readlane(r, q), j2 = __builtin_amdgcn_readlane(j, q);
-    if (d2 < bd || (d2 == bd && r2 < br)) { bd = d2; br = r2; bj = j2; }
-  }
-  d = bd;
-  r = br;
-  j = bj;
+  const float dm = wave_min_f32(d);
+  const int rm = wave_min_i32(d == dm ? r : INT_MAX);
+  const int owner = __ffsll((long long)__ballot(d == dm && r == rm)) - 1;
+  j = __builtin_amdgcn_readlane(j, owner);
+  d = dm;
+  r = rm;
 }
 
 // Exact nearest neighbour with d2 < bound, by the calling wave: the fine
