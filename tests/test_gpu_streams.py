@@ -1,0 +1,97 @@
+"""GPU parity over whole streams at BASELINE.json's configurations, through the
+device-resident batch entry the bench times (lego_odom_batch_submit / _wait,
+two batches in flight) and the host-buffer batch entry:
+
+* C2: the 600-scan VLP-16 stream (seed 1) the headline is measured on, in the
+  bench's 100-scan batches;
+* C3: 40 scans of the HDL-64E stream (seed 2): the HBM-resident odometry
+  (grid ends in LDS, points in bucket order, counting fused into
+  TransformToEnd);
+* VLS-128 (C5's sensor, seed 3): 12 scans, 128 rings.
+
+Every scan's pose record is checked against the oracle run over the same
+stream: transformSum within the north-star 1e-4, feature counts and the
+odometry-valid flag exact; the fraction of bit-exact poses is printed."""
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+POSE_TOL = 1e-4  # BASELINE.json north_star: "within 1e-4 on the 6-DoF pose"
+
+
+def _stream(L, sensor, seed, n):
+    sc = L.synth_cfg(sensor, seed)
+    scans = [L.synth_scan(sc, k) for k in range(n)]
+    pts = np.concatenate([s[0] for s in scans])
+    off = np.zeros(n + 1, np.int64)
+    off[1:] = np.cumsum([len(s[0]) for s in scans])
+    stamps = np.array([s[1] for s in scans])
+    return scans, pts, off, stamps
+
+
+def _oracle_recs(L, sensor, scans):
+    ora = L.Oracle(L.sensor_cfg(sensor))
+    out = []
+    for p, s in scans:
+        ora.ip(p, s)
+        f = ora.fa()
+        out.append((f["transform_sum"].astype(np.float64), len(f["sharp"]), len(f["less_sharp"]),
+                    len(f["flat"]), len(f["less_flat"]), f["odom_valid"]))
+    return out
+
+
+def _check(recs, ref, label):
+    worst, exact = 0.0, 0
+    for k, (r, o) in enumerate(zip(recs, ref)):
+        ts = np.array(list(r.transform_sum), np.float64)
+        assert (r.n_sharp, r.n_less_sharp, r.n_flat, r.n_less_flat, r.odom_valid) == o[1:], (label, k)
+        d = float(np.max(np.abs(ts - o[0])))
+        assert d <= POSE_TOL, (label, k, ts, o[0])
+        worst = max(worst, d)
+        exact += int(np.array_equal(ts.astype(np.float32), o[0].astype(np.float32)))
+    print(f"{label}: {len(recs)} scans, worst |dpose| {worst:.3g}, bit-exact {exact}/{len(recs)}")
+
+
+def test_c2_full_stream_device_batches(L):
+    """The headline workload: 600 VLP-16 scans, device-resident inputs, 100-scan
+    batches submitted two deep (bench.py's path)."""
+    import torch
+
+    n, B = 600, 100
+    scans, pts, off, stamps = _stream(L, "VLP-16", 1, n)
+    t0 = time.time()
+    ref = _oracle_recs(L, "VLP-16", scans)
+    t_ora = time.time() - t0
+    d_pts = torch.from_numpy(pts.view(np.uint8)).to("cuda:0")
+    # each batch's offsets index the whole resident stream (as bench.py passes them)
+    d_off = [torch.from_numpy(off[i * B:(i + 1) * B + 1].copy()).to("cuda:0") for i in range(n // B)]
+    g = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=int(np.max(np.diff(off))) + 16, max_batch=B)
+    recs = []
+    out = [(L.PoseRec * B)() for _ in range(n // B)]
+    for i in range(n // B):
+        g.submit_device(d_pts.data_ptr(), d_off[i].data_ptr(), stamps[i * B:(i + 1) * B], B)
+        if i >= 1:
+            assert g.wait(out[i - 1]) == B
+    assert g.wait(out[n // B - 1]) == B
+    for o in out:
+        recs.extend(o)
+    g.close()
+    print(f"oracle: {n / t_ora:.0f} scans/s on one core")
+    _check(recs, ref, "C2 VLP-16 seed 1")
+
+
+@pytest.mark.parametrize("sensor,seed,n,B", [("HDL-64E", 2, 40, 20), ("VLS-128", 3, 12, 6)])
+def test_dense_stream_host_batches(L, sensor, seed, n, B):
+    """HBM-resident odometry over host-buffer batches (lego_odom_batch)."""
+    scans, pts, off, stamps = _stream(L, sensor, seed, n)
+    ref = _oracle_recs(L, sensor, scans)
+    g = L.Lego(L.sensor_cfg(sensor, L.hip_lib()), max_points=int(np.max(np.diff(off))) + 16, max_batch=B)
+    recs = []
+    for i in range(n // B):
+        a, b = off[i * B], off[(i + 1) * B]
+        recs.extend(g.odom_batch(pts[a:b], off[i * B:(i + 1) * B + 1] - a, stamps[i * B:(i + 1) * B]))
+    g.close()
+    _check(recs, ref, f"{sensor} seed {seed}")
