@@ -200,6 +200,45 @@ def mapping_bench(L, steps: int, cpu: bool):
     return res
 
 
+def loop_bench(L, nscans: int, calls: int, cpu: bool):
+    """Auxiliary (not the headline metric): performLoopClosure
+    (lego_mo_loop_closure) after a synthetic VLP-16 drive in a 3.8 m circle
+    (15 deg/s, 1 m/s) long enough to revisit 30 s old keyframes, mapping on
+    the keyframe-built map.  GPU: host wall clock per call (detection, the
+    history cloud's gather / VoxelGrid / index, the ICP and the fitness),
+    median of `calls`; CPU: the oracle's same call."""
+    sc = L.synth_cfg("VLP-16", 6, yaw_rate_dps=15.0, speed_mps=1.0)
+    cap = L.synth_lib().lego_synth_max_points(L.C.byref(sc))
+    scans = [L.synth_scan(sc, k) for k in range(nscans)]
+    gpu = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=cap)
+    for pts, stamp in scans:
+        gpu.ip(pts, stamp)
+        gpu.fa()
+        gpu.mo()
+    g = gpu.loop_closure()  # warm-up (allocates the loop buffers)
+    dts = []
+    for _ in range(calls):
+        t0 = time.perf_counter()
+        g = gpu.loop_closure()
+        dts.append((time.perf_counter() - t0) * 1e3)
+    gpu.close()
+    res = {"workload": f"loop closure after {nscans} VLP-16 scans in a 3.8 m circle (keyframe map)",
+           "gpu_ms_per_call": statistics.median(dts), "detected": g["detected"], "accepted": g["accepted"],
+           "iterations": g["iterations"], "n_source": g["n_source"], "n_target": g["n_target"],
+           "fitness": g["fitness"]}
+    if cpu:
+        ora = L.Oracle(L.sensor_cfg("VLP-16"))
+        for pts, stamp in scans:
+            ora.ip(pts, stamp)
+            ora.fa()
+            ora.mo()
+        t0 = time.perf_counter()
+        ora.loop_closure()
+        res["cpu_ms_per_call"] = (time.perf_counter() - t0) * 1e3
+        res["cpu_sample"] = "1 call of the oracle (1 thread; kd-tree ICP as PCL)"
+    return res
+
+
 def dense_bench(L, nscans: int, batch: int, device: int):
     """Auxiliary (not the headline metric): config C3, the HDL-64E-shaped
     synthetic stream (64 x 2048) through the same pipeline
@@ -290,6 +329,7 @@ def main():
     ap.add_argument("--odom-profile", action="store_true", help="in-kernel phase stamps (diagnostic)")
     ap.add_argument("--mapping-steps", type=int, default=15, help="C5 scan-to-map steps (aux; 0 = skip)")
     ap.add_argument("--fleet-streams", type=int, default=64, help="streams of the fleet aux line (0 = skip)")
+    ap.add_argument("--loop-scans", type=int, default=340, help="loop-closure aux stream length (0 = skip)")
     ap.add_argument("--dense-scans", type=int, default=200, help="C3 HDL-64E scans of the aux line (0 = skip)")
     args = ap.parse_args()
 
@@ -449,6 +489,8 @@ def main():
             aux["fleet_vlp16"] = fleet_bench(L, args.fleet_streams, 20, 3, local)
         if args.dense_scans > 0 and world == 1:
             aux["dense_hdl64_c3"] = dense_bench(L, args.dense_scans, 20, local)
+        if args.loop_scans > 0 and world == 1:
+            aux["loop_closure"] = loop_bench(L, args.loop_scans, 5, not args.no_cpu)
         if cpu_all:
             aux["cpu_all_cores"] = cpu_all
         aux["host"] = host_info()

@@ -155,6 +155,31 @@ typedef struct lego_mo_out {
   int32_t n_rows_last;        /* laserCloudOri size at the last iteration */
 } lego_mo_out;
 
+/* One performLoopClosure (mapOptmization.cpp:875-945; loopClosureThread runs
+ * it at 1 Hz when loopClosureEnableFlag is set, utility.h:104): the history
+ * keyframe search (detectLoopClosure :814-872), the ICP of the latest
+ * keyframe against the +-25 keyframes around the closest old one, and the
+ * loop constraint the reference adds to iSAM2 (:919-939).  GTSAM is not part
+ * of this library: the constraint is returned for the caller's pose graph. */
+typedef struct lego_loop_out {
+  int32_t detected;        /* a keyframe > 30 s old within 7 m of the robot */
+  int32_t converged;       /* icp.hasConverged() */
+  int32_t accepted;        /* converged && fitness <= historyKeyframeFitnessScore: the factor is added */
+  int32_t latest_id;       /* latestFrameIDLoopCloure */
+  int32_t closest_id;      /* closestHistoryFrameID */
+  int32_t iterations;      /* ICP iterations run */
+  int32_t n_source;        /* latestSurfKeyFrameCloud (intensity >= 0) */
+  int32_t n_target;        /* nearHistorySurfKeyFrameCloudDS */
+  double fitness;          /* icp.getFitnessScore() = the constraint's noise variance */
+  float icp_transform[16]; /* getFinalTransformation(), row-major (camera frame) */
+  double from_rotation[9]; /* gtsam poseFrom (corrected latest keyframe), row-major */
+  double from_translation[3];
+  double to_rotation[9];   /* poseTo (the history keyframe) */
+  double to_translation[3];
+  double between_rotation[9];  /* poseFrom.between(poseTo): the BetweenFactor's measurement */
+  double between_translation[3];
+} lego_loop_out;
+
 /* /imu_raw message (sensor_msgs/Imu; utility.h:54): the fields the
  * reference's imuHandlers read (featureAssociation.cpp:431-458,
  * mapOptmization.cpp:643-652). */
@@ -309,6 +334,9 @@ int lego_cloud_info_serialize(const lego_cloud_info* info, int32_t n_scan, int32
 int lego_mo_set_map(lego_ctx* ctx, const lego_point_xyzi* corner, int32_t n_corner,
                     const lego_point_xyzi* surf, int32_t n_surf);
 int lego_mo_process(lego_ctx* ctx, const lego_fa_out* in, lego_mo_out* out);
+/* performLoopClosure over the keyframes the mapping calls have saved (needs
+ * the keyframe-built map, i.e. no lego_mo_set_map); LEGO_E_ARG otherwise. */
+int lego_mo_loop_closure(lego_ctx* ctx, lego_loop_out* out);
 
 /* transformFusion (transformFusion.cpp:94-239): /integrated_to_init, the
  * odometry pose composed with the latest mapping correction.  Host math, per

@@ -128,6 +128,8 @@ struct lego_ctx {
   MoDev mo{};
   bool moAlloc = false, moFixed = false;
   double moTimeLast = -1;
+  double moTimeOdom = 0;  // timeLaserOdometry: the last hand-off's stamp (laserOdometryHandler :630)
+  LcDev lc{};             // loop closure buffers (first lego_mo_loop_closure)
   std::vector<std::string> tnames;
   std::vector<float> tms;
 
@@ -211,6 +213,7 @@ static int ctx_reset(lego_ctx* x) {
     HIPCHK(hipStreamSynchronize(x->stream));
   }
   x->moTimeLast = -1;
+  x->moTimeOdom = 0;
   return LEGO_OK;
 }
 
@@ -1051,7 +1054,7 @@ static int mo_alloc_keyframes(lego_ctx* x) {
   const int kcap = 16384, acap = 16 << 20;
 #define MA(ptr, n) \
   if (x->alloc(&(ptr), (size_t)(n)) != hipSuccess) { set_err("hipMalloc failed for %s", #ptr); return LEGO_E_DEVICE; }
-  MA(kf.pos3, kcap); MA(kf.pose6, kcap * 6); MA(kf.seg, kcap * 6); MA(kf.arena, acap);
+  MA(kf.pos3, kcap); MA(kf.pose6, kcap * 6); MA(kf.time, kcap); MA(kf.seg, kcap * 6); MA(kf.arena, acap);
   MA(kf.exID, kcap); MA(kf.plan, kcap * 4); MA(kf.sur, kcap); MA(kf.surDS, kcap); MA(kf.sortKeys, kcap);
   MA(kf.meta, kKfMeta); MA(kf.robot, 8);
   MA(m.cornerFromMap, fromCap); MA(m.surfFromMap, fromCap);
@@ -1091,6 +1094,71 @@ int lego_mo_set_map(lego_ctx* x, const lego_point_xyzi* corner, int32_t n_corner
   return LEGO_OK;
 }
 
+int lego_mo_loop_closure(lego_ctx* x, lego_loop_out* out) {
+  if (x && x->nStreams != 1) {
+    set_err("loop closure needs a single-stream context");
+    return LEGO_E_ARG;
+  }
+  if (!x || !out) return LEGO_E_ARG;
+  std::memset(out, 0, sizeof(*out));
+  out->latest_id = out->closest_id = -1;
+  if (x->moFixed) {
+    set_err("loop closure runs over the keyframe store (no fixed map installed)");
+    return LEGO_E_ARG;
+  }
+  MoDev& m = x->mo;
+  if (!m.kf.kcap) return LEGO_OK;  // no mapping step yet: cloudKeyPoses3D is empty
+  HIPCHK(hipSetDevice(x->device));
+  LcDev& lc = x->lc;
+  if (!lc.cap) {
+    const int cap = m.fromMapCap;
+    int T = 64;
+    while (T < cap) T <<= 1;
+#define MA(ptr, n) \
+  if (x->alloc(&(ptr), (size_t)(n)) != hipSuccess) { set_err("hipMalloc failed for %s", #ptr); return LEGO_E_DEVICE; }
+    MA(lc.st, 1); MA(lc.srcRaw, cap); MA(lc.src, cap); MA(lc.cur, cap); MA(lc.tgtRaw, cap); MA(lc.tgt, cap);
+    MA(lc.cIdx, cap); MA(lc.cD, cap); MA(lc.ix.begin, T); MA(lc.ix.end, T); MA(lc.ix.sorted, cap);
+#undef MA
+    lc.ix.cap = cap;
+    lc.cap = cap;
+  }
+  LcState hs;
+  const int rs = mo_loop_closure_device(m, lc, x->moTimeOdom, &hs, x->stream);
+  if (rs == -2) {
+    set_err("loop closure: clouds larger than the loop buffers");
+    return LEGO_E_CAPACITY;
+  }
+  if (rs != 0) {
+    set_err("loop closure launch failed");
+    return LEGO_E_DEVICE;
+  }
+  if (!hs.detected) return LEGO_OK;
+  out->detected = 1;
+  out->latest_id = hs.latest;
+  out->closest_id = hs.closest;
+  out->n_source = hs.nSrc;
+  out->n_target = hs.nTgt;
+  out->iterations = hs.iterations;
+  out->converged = hs.converged;
+  out->fitness = hs.fitness;
+  std::memcpy(out->icp_transform, hs.fin, sizeof(hs.fin));
+  out->accepted = hs.converged && !(hs.fitness > 0.3);  // historyKeyframeFitnessScore, utility.h:134
+  if (out->accepted) {
+    float p6[2][6];
+    HIPCHK(hipMemcpy(p6[0], m.kf.pose6 + 6 * hs.latest, sizeof(p6[0]), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(p6[1], m.kf.pose6 + 6 * hs.closest, sizeof(p6[1]), hipMemcpyDeviceToHost));
+    LoopFactor f;
+    loop_factor(hs.fin, p6[0], p6[1], &f);
+    std::memcpy(out->from_rotation, f.fromR, sizeof(f.fromR));
+    std::memcpy(out->from_translation, f.fromT, sizeof(f.fromT));
+    std::memcpy(out->to_rotation, f.toR, sizeof(f.toR));
+    std::memcpy(out->to_translation, f.toT, sizeof(f.toT));
+    std::memcpy(out->between_rotation, f.betweenR, sizeof(f.betweenR));
+    std::memcpy(out->between_translation, f.betweenT, sizeof(f.betweenT));
+  }
+  return LEGO_OK;
+}
+
 int lego_mo_process(lego_ctx* x, const lego_fa_out* in, lego_mo_out* out) {
   if (x && x->nStreams != 1) {
     set_err("mapping needs a single-stream context");
@@ -1100,6 +1168,7 @@ int lego_mo_process(lego_ctx* x, const lego_fa_out* in, lego_mo_out* out) {
   std::memset(out, 0, sizeof(*out));
   // run() gates (mapOptmization.cpp:1487-1499): a new hand-off, then the interval
   if (!in->publish_to_mapping || !in->odom_valid) return LEGO_OK;
+  x->moTimeOdom = in->stamp;
   if (!(in->stamp - x->moTimeLast >= x->cfg.mapping_process_interval)) return LEGO_OK;
   if (!x->moFixed) {
     const int st = mo_alloc_keyframes(x);
@@ -1128,6 +1197,7 @@ int lego_mo_process(lego_ctx* x, const lego_fa_out* in, lego_mo_out* out) {
   a.nCorner = in->n_corner_last;
   a.nSurf = in->n_surf_last;
   a.nOutlier = in->n_outlier_last;
+  a.stamp = in->stamp;
   int moFront = x->moImu.front;
   a.imuOn = x->moImu.at(in->stamp, x->cfg.scan_period, &a.imuRoll, &a.imuPitch, &moFront) ? 1 : 0;
   if (!a.imuOn) a.imuRoll = a.imuPitch = 0.f;

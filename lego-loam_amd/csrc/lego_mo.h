@@ -5,6 +5,8 @@
 
 #include <cstddef>
 
+#include "lego_icp.h"
+
 namespace lego {
 
 // mapOptimization member state that persists across mapping steps
@@ -54,6 +56,7 @@ struct MoIndex {
 struct MoKeyframes {
   float4* pos3;      // [kcap] x, y, z, intensity = key index (cloudKeyPoses3D)
   float* pose6;      // [kcap * 6] x, y, z, roll, pitch, yaw (cloudKeyPoses6D)
+  double* time;      // [kcap] cloudKeyPoses6D[i].time
   int* seg;          // [kcap * 6] arena offset / count of corner, surf, outlier DS clouds
   float4* arena;     // [acap] keyframe clouds
   int* exID;         // [kcap] surroundingExistingKeyPosesID
@@ -94,12 +97,40 @@ struct MoStepArgs {
   int nCorner, nSurf, nOutlier;
   int imuOn;              // transformUpdate's IMU blend (:465-490), roll / pitch from the host queue
   float imuRoll, imuPitch;
+  double stamp;           // timeLaserOdometry (the keyframe's time)
+};
+
+// Loop closure (lego_loop.hip): the detection result and gather plan, the
+// ICP state.  Device-resident; the host reads it back.
+constexpr int kLcPlan = 2 + 2 * 51;  // latest corner + surf, then +-25 keyframes x 2 clouds
+struct LcState {
+  int K, latest, closest, detected;
+  int nPlan, nPlanSrc, nSrcRaw, nTgtRaw;
+  int plan[kLcPlan][4];  // key, arena offset, count, output offset
+  int nSrc, nTgt;
+  int iterations, converged, done, nFit;
+  float T[4][4], fin[4][4];
+  IcpCriteria crit;
+  double fitness;
+};
+struct LcDev {
+  LcState* st;
+  float4 *srcRaw, *src, *cur, *tgtRaw, *tgt;
+  int* cIdx;
+  float* cD;
+  MoIndex ix;
+  int cap;
 };
 
 size_t voxel_scratch_tmp_bytes(int cap);
 int voxel_grid_device(const float4* in, int n, const int* nDev, float leaf, float4* out, int* nOut,
                       const VgScratch& v, hipStream_t s);
 int mo_set_map_device(MoDev& m, int nCornerMap, int nSurfMap, hipStream_t s);
+int index_build_device(const float4* pts, int n, const int* nDev, MoIndex& ix, const VgScratch& v, hipStream_t s);
+// One performLoopClosure over the keyframe store (tnow = timeLaserOdometry).
+// Returns 0 (hostState holds the result), -1 on a launch failure, -2 when the
+// clouds exceed the loop buffers.
+int mo_loop_closure_device(MoDev& m, LcDev& lc, double tnow, LcState* hostState, hipStream_t s);
 // One mapping step.  fixedMap: the installed map; otherwise the keyframe map.
 // Returns 0, -1 on a launch failure, -2 when the keyframe store is full.
 int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, hipStream_t s);

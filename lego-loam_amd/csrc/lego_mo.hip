@@ -768,7 +768,7 @@ __global__ void k_kf_gather(MoKeyframes kf, float4* cornerFromMap, float4* surfF
 
 // saveKeyFramesAndFactor (:1353-1454) with iSAM2's chain estimate: keyframe
 // decision, pose append, arena slots for this step's filtered clouds.
-__global__ void k_kf_save(MoKeyframes kf, MoState* st, const MoCounts* cnt) {
+__global__ void k_kf_save(MoKeyframes kf, MoState* st, const MoCounts* cnt, double stamp) {
   if (threadIdx.x != 0) return;
   float* prev = kf.robot;
   float* cur = kf.robot + 3;
@@ -792,6 +792,7 @@ __global__ void k_kf_save(MoKeyframes kf, MoState* st, const MoCounts* cnt) {
   kf.pos3[K] = make_float4(e[3], e[4], e[5], (float)K);
   float* p6 = kf.pose6 + 6 * K;
   p6[0] = e[3]; p6[1] = e[4]; p6[2] = e[5]; p6[3] = e[0]; p6[4] = e[1]; p6[5] = e[2];
+  kf.time[K] = stamp;  // thisPose6D.time = timeLaserOdometry (:1424)
   if (K + 1 > 1)
     for (int i = 0; i < 6; ++i) st->transformTobeMapped[i] = aft[i];
   int* sg = kf.seg + 6 * K;
@@ -860,7 +861,7 @@ int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, h
   }
   k_mo_finish<<<1, 64, 0, s>>>(m.st, a.imuOn, a.imuRoll, a.imuPitch);
   if (!fixedMap) {  // saveKeyFramesAndFactor :1353-1454
-    k_kf_save<<<1, 64, 0, s>>>(m.kf, m.st, m.cnt);
+    k_kf_save<<<1, 64, 0, s>>>(m.kf, m.st, m.cnt, a.stamp);
     k_kf_copy<<<grid_for(qcap), 256, 0, s>>>(m.kf, m.cornerDS, m.surfDS, m.outlierDS);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -100,6 +100,21 @@ class MoOut(C.Structure):
                 ("n_surf_scan_ds", C.c_int32), ("n_rows_last", C.c_int32)]
 
 
+class LoopOut(C.Structure):  # lego_loop_out (performLoopClosure)
+    _fields_ = [("detected", C.c_int32), ("converged", C.c_int32), ("accepted", C.c_int32),
+                ("latest_id", C.c_int32), ("closest_id", C.c_int32), ("iterations", C.c_int32),
+                ("n_source", C.c_int32), ("n_target", C.c_int32), ("fitness", C.c_double),
+                ("icp_transform", C.c_float * 16), ("from_rotation", C.c_double * 9),
+                ("from_translation", C.c_double * 3), ("to_rotation", C.c_double * 9),
+                ("to_translation", C.c_double * 3), ("between_rotation", C.c_double * 9),
+                ("between_translation", C.c_double * 3)]
+
+
+def loop_to_dict(o: LoopOut) -> dict:
+    return {k: (np.array(list(getattr(o, k))) if isinstance(getattr(o, k), C.Array) else getattr(o, k))
+            for k, _ in LoopOut._fields_}
+
+
 class FusionOut(C.Structure):  # lego_fusion_out (/integrated_to_init)
     _fields_ = [("stamp", C.c_double), ("transform_mapped", C.c_float * 6), ("quat", C.c_double * 4),
                 ("pos", C.c_double * 3)]
@@ -208,6 +223,7 @@ def oracle_lib() -> C.CDLL:
     lib.lego_oracle_fa_process.argtypes = [C.c_void_p, C.POINTER(IpOut), C.POINTER(FaOut)]
     lib.lego_oracle_mo_set_map.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32]
     lib.lego_oracle_mo_process.argtypes = [C.c_void_p, C.POINTER(FaOut), C.POINTER(MoOut)]
+    lib.lego_oracle_mo_loop_closure.argtypes = [C.c_void_p, C.POINTER(LoopOut)]
     lib.lego_oracle_imu_push.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
     lib.lego_oracle_fusion_odometry.argtypes = [C.c_void_p, C.POINTER(FaOut), C.POINTER(FusionOut)]
     lib.lego_oracle_fusion_aft_mapped.argtypes = [C.c_void_p, C.POINTER(MoOut)]
@@ -227,7 +243,7 @@ HIP_EXPORTS = ["lego_sensor_preset", "lego_create", "lego_fleet_create", "lego_d
                "lego_imu_push", "lego_odom_batch_submit", "lego_odom_batch_wait", "lego_batch_fetch", "lego_pc2_decode", "lego_ip_process_pc2",
                "lego_odom_batch_pc2", "lego_pc2_encode_xyzi", "lego_cloud_info_serialize",
                "lego_fusion_odometry", "lego_fusion_aft_mapped",
-               "lego_mo_set_map", "lego_mo_process", "lego_last_error", "lego_stage_times",
+               "lego_mo_set_map", "lego_mo_process", "lego_mo_loop_closure", "lego_last_error", "lego_stage_times",
                "lego_odom_profile"]
 
 
@@ -263,6 +279,7 @@ def hip_lib() -> C.CDLL:
     lib.lego_batch_fetch.argtypes = [C.c_void_p, C.c_int32, C.POINTER(IpOut), C.POINTER(FaOut)]
     lib.lego_mo_set_map.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32]
     lib.lego_mo_process.argtypes = [C.c_void_p, C.POINTER(FaOut), C.POINTER(MoOut)]
+    lib.lego_mo_loop_closure.argtypes = [C.c_void_p, C.POINTER(LoopOut)]
     lib.lego_last_error.restype = C.c_char_p
     lib.lego_odom_profile.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
     lib.lego_stage_times.argtypes = [C.c_void_p, C.POINTER(C.c_char_p), f32p, C.c_int32,
@@ -418,6 +435,11 @@ class Oracle:
         check(self.lib.lego_oracle_mo_set_map(self.h, corner.ctypes.data, len(corner),
                                               surf.ctypes.data, len(surf)), "oracle_mo_set_map")
 
+    def loop_closure(self) -> dict:
+        out = LoopOut()
+        check(self.lib.lego_oracle_mo_loop_closure(self.h, C.byref(out)), "oracle_mo_loop_closure")
+        return loop_to_dict(out)
+
     def mo(self) -> dict:
         out = MoOut()
         check(self.lib.lego_oracle_mo_process(self.h, C.byref(self._fa), C.byref(out)), "oracle_mo")
@@ -504,6 +526,12 @@ class Lego:
         self._mo = out
         return {k: (np.array(list(getattr(out, k)), dtype=np.float32)
                     if k.startswith("transform") else getattr(out, k)) for k, _ in MoOut._fields_}
+
+    def loop_closure(self) -> dict:
+        """performLoopClosure on the device (lego_mo_loop_closure)."""
+        out = LoopOut()
+        check(self.lib.lego_mo_loop_closure(self.h, C.byref(out)), "lego_mo_loop_closure", self.lib)
+        return loop_to_dict(out)
 
     def fusion(self) -> np.ndarray:
         """transformFusion (lego_fusion_aft_mapped with the last mapping

@@ -9,7 +9,7 @@ R="${GRAFT_REPO_ROOT:-$(pwd)}"
 O="$R/gpurun_out/${TAG:-run}"
 mkdir -p "$O"
 cd /tmp
-B="$R/bench.py --no-cpu --mapping-steps 0 --fleet-streams 0 --dense-scans 0"
+B="$R/bench.py --no-cpu --mapping-steps 0 --fleet-streams 0 --dense-scans 0 --loop-scans 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_stats" -o run \
   -- python3 $B > "$O/prof_stats.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch" -o run \

@@ -16,6 +16,8 @@ int main(void) {
   O(lego_fa_out, n_outlier_last);
   S(lego_mo_out); O(lego_mo_out, transform_bef_mapped); O(lego_mo_out, n_rows_last);
   S(lego_pose_rec); O(lego_pose_rec, n_segmented); O(lego_pose_rec, flags);
+  S(lego_loop_out); O(lego_loop_out, fitness); O(lego_loop_out, icp_transform); O(lego_loop_out, from_rotation);
+  O(lego_loop_out, between_translation);
   S(lego_synth_cfg); O(lego_synth_cfg, seed);
   return 0;
 }

@@ -1,0 +1,54 @@
+"""GPU loop closure (lego_mo_loop_closure, mapOptmization.cpp:875-945) vs the
+oracle's restatement on the same stream: a synthetic VLP-16 drive in a tight
+circle (15 deg/s, 1 m/s: radius 3.8 m) so that after 30 s the robot is back
+among keyframes older than the history time window.  Mapping runs on the
+keyframe-built map (no fixed map), as loop closure requires.
+
+Bar: detection, keyframe ids and cloud sizes exact; convergence, acceptance
+and the ICP iteration count equal; the final transformation, the fitness and
+the constraint within 1e-4 (the ICP's reductions run in a different order on
+the device)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+def test_loop_closure_matches_oracle(L):
+    sc = L.synth_cfg("VLP-16", 6, yaw_rate_dps=15.0, speed_mps=1.0)
+    cap = L.synth_lib().lego_synth_max_points(L.C.byref(sc))
+    gpu = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=cap)
+    ora = L.Oracle(L.sensor_cfg("VLP-16"))
+    checked = accepted = 0
+    for k in range(340):
+        pts, stamp = L.synth_scan(sc, k)
+        gpu.ip(pts, stamp)
+        ora.ip(pts, stamp)
+        gpu.fa()
+        ora.fa()
+        gm, om = gpu.mo(), ora.mo()
+        assert gm["processed"] == om["processed"]
+        if k not in (289, 309, 324, 339):
+            continue
+        g, o = gpu.loop_closure(), ora.loop_closure()
+        for key in ("detected", "latest_id", "closest_id", "n_source", "n_target", "converged", "accepted",
+                    "iterations"):
+            assert g[key] == o[key], (k, key, g[key], o[key])
+        checked += 1
+        if not o["detected"]:
+            assert k == 289  # no keyframe is 30 s old yet
+            continue
+        assert abs(g["fitness"] - o["fitness"]) <= TOL * max(1.0, abs(o["fitness"])), (k, g["fitness"], o["fitness"])
+        assert np.max(np.abs(g["icp_transform"] - o["icp_transform"])) <= TOL, k
+        if o["accepted"]:
+            accepted += 1
+            for key in ("from_rotation", "from_translation", "to_rotation", "to_translation", "between_rotation",
+                        "between_translation"):
+                assert np.max(np.abs(g[key] - o[key])) <= TOL, (k, key)
+        print(f"scan {k}: keyframes {o['latest_id']} -> {o['closest_id']}, {o['iterations']} ICP iterations, "
+              f"fitness {o['fitness']:.4g} (gpu {g['fitness']:.4g}), "
+              f"max |dT| {np.max(np.abs(g['icp_transform'] - o['icp_transform'])):.2g}")
+    assert checked == 4 and accepted >= 2
+    gpu.close()

@@ -52,6 +52,16 @@ def test_eig_min_shortcut_is_sound(tmp_path):
     assert r.returncode == 0, r.stdout
 
 
+def test_jacobi_svd3_and_umeyama(tmp_path):
+    """The loop closure's Eigen JacobiSVD / umeyama / PCL convergence-criteria
+    restatement (lego_icp.h): reconstruction, orthonormality, ordering, exact
+    rigid-motion recovery, criteria branches."""
+    exe = _build(tmp_path, "svd3_check", REPO / "tests/native/svd3_check.cpp")
+    r = subprocess.run([str(exe), "200000"], capture_output=True, text=True, timeout=600)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout
+
+
 def test_segmentation_alpha_constants(L):
     """sin/cos of segmentAlphaX/Y (imageProjection.cpp:421) — bit patterns
     recorded in SURVEY.md §9.3 for VLP-16."""

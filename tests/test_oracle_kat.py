@@ -280,3 +280,32 @@ def test_fusion_without_mapping_is_odometry(L):
         fa = ora.fa()
         m = ora.fusion()
         assert np.abs(m.astype(np.float64) - fa["transform_sum"]).max() < 2e-6, (k, m, fa["transform_sum"])
+
+
+def test_oracle_loop_closure_on_a_circle(L):
+    """performLoopClosure (mapOptmization.cpp:875-945) restated: on a drive in
+    a 3.8 m circle no history keyframe qualifies before 30 s; afterwards the
+    closest old keyframe is found, the ICP converges to a near-identity
+    correction (the synthetic odometry drifts little) with a fitness below
+    historyKeyframeFitnessScore, and the constraint is a proper rigid motion."""
+    import numpy as np
+
+    sc = L.synth_cfg("VLP-16", 6, yaw_rate_dps=15.0, speed_mps=1.0)
+    ora = L.Oracle(L.sensor_cfg("VLP-16"))
+    for k in range(340):
+        ora.ip(*L.synth_scan(sc, k))
+        ora.fa()
+        ora.mo()
+        if k == 289:
+            early = ora.loop_closure()
+            assert early["detected"] == 0 and early["closest_id"] == -1
+    o = ora.loop_closure()
+    assert o["detected"] == 1 and o["converged"] == 1 and o["accepted"] == 1
+    assert 0 <= o["closest_id"] < o["latest_id"] and o["n_source"] > 100 and o["n_target"] > 1000
+    assert 1 <= o["iterations"] < 100 and 0 < o["fitness"] < 0.3
+    T = o["icp_transform"].reshape(4, 4)
+    assert np.allclose(T[3], [0, 0, 0, 1]) and np.max(np.abs(T[:3, :3] - np.eye(3))) < 0.05
+    assert np.max(np.abs(T[:3, 3])) < 0.5
+    for key in ("from_rotation", "to_rotation", "between_rotation"):
+        R = o[key].reshape(3, 3)
+        assert np.allclose(R @ R.T, np.eye(3), atol=1e-6) and abs(np.linalg.det(R) - 1) < 1e-6, key
