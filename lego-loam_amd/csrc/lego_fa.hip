@@ -233,28 +233,34 @@ __host__ __device__ inline int next_pow2(int x) {
   return m;
 }
 
+// The six sectors' sort buffers (each padded to a power of two, packed: at
+// most 2 W entries) share their region with the VoxelGrid keys, which are
+// used only after the picking.
+__host__ __device__ inline size_t extract_sort_region(int H) {
+  const size_t W = (size_t)H + 32;
+  const size_t vox = (size_t)next_pow2((int)W) * 8, sec = 2 * W * 8;
+  return vox > sec ? vox : sec;
+}
 __host__ __device__ inline size_t extract_lds_bytes(int H) {
   const size_t W = (size_t)H + 32;
-  const size_t vox = (size_t)next_pow2((int)W);
   size_t s = 0;
-  s += W * 4;                 // curv
-  s += W * 4;                 // lf
-  s += 2 * kSortCap * 8;      // srt + orig
-  s += vox * 8;               // vox
-  s += 64 * 4 + 64 * 4;       // misc + red
-  s += W * 2;                 // col
-  s += W * 3;                 // picked, label, gfl
+  s += W * 4;                     // curv
+  s += W * 4;                     // lf
+  s += extract_sort_region(H);    // sector sorts / vox
+  s += 64 * 4 + 64 * 4;           // misc + red
+  s += W * 2;                     // col
+  s += W * 3;                     // picked, label, gfl
   return (s + 15) & ~(size_t)15;
 }
 
 __device__ __forceinline__ ExtractLds carve(unsigned char* base, int H) {
   const size_t W = (size_t)H + 32;
-  const size_t vox = (size_t)next_pow2((int)W);
   ExtractLds L;
   size_t o = 0;
-  L.vox = (unsigned long long*)(base + o); o += vox * 8;
-  L.srt = (SmoothEntry*)(base + o); o += kSortCap * 8;
-  L.orig = (SmoothEntry*)(base + o); o += kSortCap * 8;
+  L.vox = (unsigned long long*)(base + o);
+  L.srt = (SmoothEntry*)(base + o);
+  L.orig = nullptr;
+  o += extract_sort_region(H);
   L.curv = (float*)(base + o); o += W * 4;
   L.lf = (int*)(base + o); o += W * 4;
   L.misc = (int*)(base + o); o += 64 * 4;
@@ -267,7 +273,7 @@ __device__ __forceinline__ ExtractLds carve(unsigned char* base, int H) {
 }
 
 enum { M_TIE = 0, M_LF = 1, M_OVF = 2, M_NSH = 3, M_NLS = 4, M_NFL = 5, M_D0 = 6, M_D1 = 7,
-       M_MB0 = 8, M_MB1 = 9, M_MB2 = 10, M_WOFF = 16 };
+       M_MB0 = 8, M_MB1 = 9, M_MB2 = 10, M_PH = 11, M_WOFF = 16 };
 
 // Bitonic sort of m (power of two) entries in LDS by value, all threads.
 __device__ __forceinline__ void bitonic_entries(SmoothEntry* a, int m) {
@@ -281,6 +287,27 @@ __device__ __forceinline__ void bitonic_entries(SmoothEntry* a, int m) {
         if ((x.value > y.value) == up) { a[i] = y; a[l] = x; }
       }
       __syncthreads();
+    }
+  }
+}
+// The same network by one wave on its own LDS buffer (no block barrier).
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ void wave_bitonic_entries(SmoothEntry* a, int m) {
+  const int lane = threadIdx.x & 63;
+  for (int k = 2; k <= m; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int t = lane; t < m / 2; t += 64) {
+        const int i = (t / j) * 2 * j + (t % j);
+        const int l = i + j;
+        const bool up = (i & k) == 0;
+        const SmoothEntry x = a[i], y = a[l];
+        if ((x.value > y.value) == up) { a[i] = y; a[l] = x; }
+      }
+      wave_sync_lds();
     }
   }
 }
@@ -386,117 +413,155 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
     ph = carry->phantom_ind;
     if (tid == 0 && R.lo == 0 && R.Wn > 0 && carry->picked0) L.picked[0] = 1;
   }
+  if (tid == 0) L.misc[M_PH] = ph;  // the phantom entry's index unless a sector sort replaces it
   __syncthreads();
-  int newph = ph;
   int flags = 0;
-  for (int j = 0; j < 6; j++) {
-    const int sp = (s * (6 - j) + e * j) / 6;
-    const int ep = (s * (5 - j) + e * (j + 1)) / 6 - 1;
+  // sector j: [sp, ep] (ep scanned, excluded from the sort, :699-702), sorted
+  // by value in its own buffer at off(j) = sum of the earlier padded sizes
+  auto sector = [&](int j, int* sp, int* ep, int* off) {
+    int o = 0;
+    for (int i = 0; i < j; ++i) {
+      const int a0 = (s * (6 - i) + e * i) / 6, b0 = (s * (5 - i) + e * (i + 1)) / 6 - 1;
+      if (a0 < b0) o += next_pow2(b0 - a0);
+    }
+    *sp = (s * (6 - j) + e * j) / 6;
+    *ep = (s * (5 - j) + e * (j + 1)) / 6 - 1;
+    *off = o;
+  };
+  // ---- the six sector sorts at once, one wave per sector (they do not depend
+  // on the picking; only the picking runs in sector order)
+  const int nw = blockDim.x >> 6;
+  for (int j = wave; j < 6; j += nw) {
+    int sp, ep, off;
+    sector(j, &sp, &ep, &off);
     if (sp >= ep) continue;
-    const int n = ep - sp;
-    const int m = next_pow2(n);
+    const int n = ep - sp, m = next_pow2(n);
+    SmoothEntry* a = L.srt + off;
     const bool phantom_here = (ring == 0 && sp <= 4 && 4 < ep);
-    for (int t = tid; t < m; t += blockDim.x) {
+    for (int t = lane; t < m; t += 64) {
       SmoothEntry en;
       if (t < n) {
         const int pos = sp + t;
-        if (phantom_here && pos == 4) en = {0.0f, ph};
-        else en = {L.curv[pos - R.lo], pos};
-        L.orig[t] = en;
+        en = (phantom_here && pos == 4) ? SmoothEntry{0.0f, ph} : SmoothEntry{L.curv[pos - R.lo], pos};
       } else {
         en = {__builtin_inff(), INT_MAX};
       }
-      L.srt[t] = en;
+      a[t] = en;
     }
-    __syncthreads();
-    bitonic_entries(L.srt, m);
-    for (int t = tid; t < n - 1; t += blockDim.x)
-      if (L.srt[t].value == L.srt[t + 1].value) L.misc[M_TIE] = 1;
-    __syncthreads();
-    if (L.misc[M_TIE]) {
+    wave_sync_lds();
+    wave_bitonic_entries(a, m);
+    bool tie = false;
+    for (int t = lane; t < n - 1; t += 64) tie |= a[t].value == a[t + 1].value;
+    if (__ballot(tie)) {
       // equal curvatures: their relative order is std::sort's
-      if (tid == 0) {
-        for (int t = 0; t < n; ++t) L.srt[t] = L.orig[t];
-        std_sort_by_value(L.srt, n);
-        L.misc[M_TIE] = 0;
+      if (lane == 0) {
+        for (int t = 0; t < n; ++t) {
+          const int pos = sp + t;
+          a[t] = (phantom_here && pos == 4) ? SmoothEntry{0.0f, ph} : SmoothEntry{L.curv[pos - R.lo], pos};
+        }
+        std_sort_by_value(a, n);
       }
-      __syncthreads();
+      wave_sync_lds();
     }
-    if (phantom_here) newph = L.srt[4 - sp].ind;
-    // ---- edge scan (wave 0), k = ep .. sp
-    if (wave == 0) {
-      int cnt = 0;
-      int nsh = L.misc[M_NSH], nls = L.misc[M_NLS];
-      bool done = false;
-      for (int base = ep; base >= sp && !done; base -= 64) {
-        const int k = base - lane;
-        bool act = k >= sp;
-        const int ind = act ? entry_ind(L.srt, sp, ep, k) : -1;
-        if (act && !in_win(R, ind)) { act = false; flags |= 1; }
-        while (true) {
-          bool el = false;
-          if (act) {
-            const int w = ind - R.lo;
-            el = picked[w] == 0 && L.curv[w] > c.edge_thr && L.gfl[w] == 0;
+    if (phantom_here && lane == 0) L.misc[M_PH] = a[4 - sp].ind;
+  }
+  __syncthreads();
+  const int newph = L.misc[M_PH];
+  // ---- picking, sector by sector (wave 0): edge scan k = ep .. sp, then
+  // flat scan k = sp .. ep (:699-769)
+  if (wave == 0) {
+    int nsh = 0, nls = 0, nfl = 0;
+    for (int j = 0; j < 6; j++) {
+      int sp, ep, off;
+      sector(j, &sp, &ep, &off);
+      if (sp >= ep) continue;
+      const SmoothEntry* srt = L.srt + off;
+      {
+        int cnt = 0;
+        bool done = false;
+        for (int base = ep; base >= sp && !done; base -= 64) {
+          const int k = base - lane;
+          bool act = k >= sp;
+          const int ind = act ? entry_ind(srt, sp, ep, k) : -1;
+          if (act && !in_win(R, ind)) { act = false; flags |= 1; }
+          while (true) {
+            bool el = false;
+            if (act) {
+              const int w = ind - R.lo;
+              el = picked[w] == 0 && L.curv[w] > c.edge_thr && L.gfl[w] == 0;
+            }
+            const unsigned long long msk = __ballot(el);
+            if (msk == 0) break;
+            const int l = __ffsll((long long)msk) - 1;
+            cnt++;
+            if (cnt > 20) { done = true; break; }
+            if (lane == l) {
+              const int w = ind - R.lo;
+              label[w] = cnt <= 2 ? 2 : 1;
+              const float4 pt = bb.dsk[R.base + ind];
+              if (cnt <= 2) R.osh[nsh] = pt;
+              R.ols[nls] = pt;
+              suppress(R, picked, L.col, ind);
+            }
+            if (cnt <= 2) nsh++;
+            nls++;
+            act = act && lane > l;
           }
-          const unsigned long long msk = __ballot(el);
-          if (msk == 0) break;
-          const int l = __ffsll((long long)msk) - 1;
-          cnt++;
-          if (cnt > 20) { done = true; break; }
-          if (lane == l) {
-            const int w = ind - R.lo;
-            label[w] = cnt <= 2 ? 2 : 1;
-            const float4 pt = bb.dsk[R.base + ind];
-            if (cnt <= 2) R.osh[nsh] = pt;
-            R.ols[nls] = pt;
-            suppress(R, picked, L.col, ind);
-          }
-          if (cnt <= 2) nsh++;
-          nls++;
-          act = act && lane > l;
         }
       }
-      if (lane == 0) { L.misc[M_NSH] = nsh; L.misc[M_NLS] = nls; }
-    }
-    __syncthreads();
-    // ---- flat scan (wave 0), k = sp .. ep
-    if (wave == 0) {
-      int cnt = 0;
-      int nfl = L.misc[M_NFL];
-      bool done = false;
-      for (int base = sp; base <= ep && !done; base += 64) {
-        const int k = base + lane;
-        bool act = k <= ep;
-        const int ind = act ? entry_ind(L.srt, sp, ep, k) : -1;
-        if (act && !in_win(R, ind)) { act = false; flags |= 1; }
-        while (true) {
-          bool el = false;
-          if (act) {
-            const int w = ind - R.lo;
-            el = picked[w] == 0 && L.curv[w] < c.surf_thr && L.gfl[w] == 1;
+      {
+        int cnt = 0;
+        bool done = false;
+        for (int base = sp; base <= ep && !done; base += 64) {
+          const int k = base + lane;
+          bool act = k <= ep;
+          const int ind = act ? entry_ind(srt, sp, ep, k) : -1;
+          if (act && !in_win(R, ind)) { act = false; flags |= 1; }
+          while (true) {
+            bool el = false;
+            if (act) {
+              const int w = ind - R.lo;
+              el = picked[w] == 0 && L.curv[w] < c.surf_thr && L.gfl[w] == 1;
+            }
+            const unsigned long long msk = __ballot(el);
+            if (msk == 0) break;
+            const int l = __ffsll((long long)msk) - 1;
+            if (lane == l) {
+              label[ind - R.lo] = -1;
+              R.ofl[nfl] = bb.dsk[R.base + ind];
+            }
+            nfl++;
+            cnt++;
+            if (cnt >= 4) { done = true; break; }
+            if (lane == l) suppress(R, picked, L.col, ind);
+            act = act && lane > l;
           }
-          const unsigned long long msk = __ballot(el);
-          if (msk == 0) break;
-          const int l = __ffsll((long long)msk) - 1;
-          if (lane == l) {
-            label[ind - R.lo] = -1;
-            R.ofl[nfl] = bb.dsk[R.base + ind];
-          }
-          nfl++;
-          cnt++;
-          if (cnt >= 4) { done = true; break; }
-          if (lane == l) suppress(R, picked, L.col, ind);
-          act = act && lane > l;
         }
       }
-      if (lane == 0) L.misc[M_NFL] = nfl;
     }
-    __syncthreads();
-    // ---- less-flat set: positions k in [sp, ep] with label <= 0, in order (:771-775)
-    for (int k0 = sp; k0 <= ep; k0 += blockDim.x) {
+    if (lane == 0) { L.misc[M_NSH] = nsh; L.misc[M_NLS] = nls; L.misc[M_NFL] = nfl; }
+  }
+  __syncthreads();
+  // ---- less-flat set: per sector the positions k in [sp, ep] with label <= 0,
+  // in order (:771-775); the sectors are consecutive ranges, so one ordered
+  // pass over [s, e - 1] restricted to the sectors that ran
+  {
+    int sp0, ep0, o0;
+    sector(0, &sp0, &ep0, &o0);
+    int sp5, ep5, o5;
+    sector(5, &sp5, &ep5, &o5);
+    for (int k0 = sp0; k0 <= ep5; k0 += blockDim.x) {
       const int k = k0 + tid;
-      const bool f = k <= ep && label[k - R.lo] <= 0;
+      bool f = false;
+      if (k <= ep5 && label[k - R.lo] <= 0) {
+        int j = 0;
+        int sp, ep, off;
+        for (; j < 6; ++j) {
+          sector(j, &sp, &ep, &off);
+          if (k <= ep) break;
+        }
+        f = j < 6 && k >= sp && sp < ep;
+      }
       int tot;
       const int r = block_rank(f, L.misc + M_WOFF, &tot);
       if (f) L.lf[L.misc[M_LF] + r] = k;
