@@ -448,7 +448,7 @@ def main():
                 traffic = None
         cpu = None
         cpu_all = None
-        if not args.no_cpu:
+        if not args.no_cpu and world == 1:  # the CPU baseline is an N = 1 line
             v, n, passes = cpu_baseline(L, args.sensor, seed, args.stream_len, args.cpu_budget)
             cpu = {"value": v, "unit": "scans/s", "cores": 1, "kind": "port",
                    "sample": f"{n} scans ({passes} pass(es) over the {args.stream_len}-scan "
@@ -483,7 +483,7 @@ def main():
                 print(f"  {k:14s} {v / args.steps:9.3f} ms/step  {100 * v / max(tot, 1e-9):5.1f}%",
                       file=sys.stderr)
         aux = {}
-        if args.mapping_steps > 0:
+        if args.mapping_steps > 0 and world == 1:
             aux["scan_to_map_c5"] = mapping_bench(L, args.mapping_steps, not args.no_cpu)
         if args.fleet_streams > 0 and world == 1:
             aux["fleet_vlp16"] = fleet_bench(L, args.fleet_streams, 20, 3, local)
