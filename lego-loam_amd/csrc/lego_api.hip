@@ -375,10 +375,11 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
     ob.G = odom_workgroups((int)N, cus);
     // a fleet's streams share the device: S x G workgroups, all resident
     if (n_streams > 1) ob.G = std::max(1, std::min(ob.G, cus / n_streams));
-    // diagnostic override (profiling / scaling studies); never above the default
+    // diagnostic override (profiling / scaling studies); at most one
+    // workgroup per CU over the fleet's streams
     if (const char* e = std::getenv("LEGO_ODOM_WORKGROUPS")) {
       const int g = std::atoi(e);
-      if (g >= 1 && g < ob.G) ob.G = g;
+      if (g >= 1 && (long)g * (long)n_streams <= (long)cus) ob.G = g;
     }
     const size_t G = S * ob.G;  // private copies over all streams' workgroups
     for (int k = 0; k < 2; ++k) {
