@@ -78,17 +78,36 @@ def cpu_baseline(L, sensor, seed, nscans, budget_s):
     done = 0
     t0 = time.perf_counter()
     passes = 0
+    ref = []  # the first pass's transformSum per scan (the pose reference of the bench line)
     while True:
         ora = L.Oracle(cfg)
         for pts, st in scans:
             ora.ip(pts, st)
-            ora.fa()
+            f = ora.fa()
+            if passes == 0:
+                ref.append(f["transform_sum"])
             done += 1
         passes += 1
         if time.perf_counter() - t0 >= budget_s:
             break
     dt = time.perf_counter() - t0
-    return done / dt, done, passes
+    return done / dt, done, passes, ref
+
+
+def pose_delta_vs_oracle(gpu_recs: dict, ref: list, B: int):
+    """The metric's "pose delta vs ref": every timed scan's transformSum from
+    the GPU records against the oracle's run over the same stream (bit-exact
+    count and max |delta|; the north-star tolerance is 1e-4)."""
+    worst, exact, n = 0.0, 0, 0
+    for j, rc in gpu_recs.items():
+        for k in range(B):
+            o = np.asarray(ref[j * B + k], np.float32)
+            g = np.array(list(rc[k].transform_sum), np.float32)
+            worst = max(worst, float(np.max(np.abs(g.astype(np.float64) - o.astype(np.float64)))))
+            exact += int(np.array_equal(g.view(np.uint32), o.view(np.uint32)))
+            n += 1
+    return {"scans": n, "max_abs": worst, "bit_exact": exact, "tolerance": 1e-4,
+            "reference": "oracle (CPU restatement, oracle/) over the same stream"}
 
 
 def cpu_all_cores(L, sensor, threads, nscans, budget_s):
@@ -407,9 +426,12 @@ def main():
     t0 = time.perf_counter()
     alg_bytes = 0.0
 
+    gpu_recs = {}  # batch index within the stream -> its pose records (each pass starts from reset)
+
     def account(done):
         nonlocal alg_bytes, gathered
-        for _, st, rc in done:
+        for i, st, rc in done:
+            gpu_recs[i % nb] = rc
             for k, v in st.items():
                 stage_acc[k] = stage_acc.get(k, 0.0) + v
             alg_bytes += odom_alg_bytes(rc)
@@ -448,8 +470,10 @@ def main():
                 traffic = None
         cpu = None
         cpu_all = None
+        pose_delta = None
         if not args.no_cpu and world == 1:  # the CPU baseline is an N = 1 line
-            v, n, passes = cpu_baseline(L, args.sensor, seed, args.stream_len, args.cpu_budget)
+            v, n, passes, ref = cpu_baseline(L, args.sensor, seed, args.stream_len, args.cpu_budget)
+            pose_delta = pose_delta_vs_oracle(gpu_recs, ref, B)
             cpu = {"value": v, "unit": "scans/s", "cores": 1, "kind": "port",
                    "sample": f"{n} scans ({passes} pass(es) over the {args.stream_len}-scan "
                              f"{args.sensor} stream, seed {seed}) through oracle ip+fa incl. LM, 1 thread"}
@@ -516,6 +540,7 @@ def main():
                          "kernel": "k_odom", "launch_ms": odom_ms / n_odom, "launches_per_step": n_odom,
                          "kernel_ms_per_step": odom_ms},
             "cpu_baseline": cpu,
+            "pose_delta_vs_oracle": pose_delta,
             "stages_ms_per_step": {k: v / args.steps for k, v in stage_acc.items()},
             "aux": aux,
         }

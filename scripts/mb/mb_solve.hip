@@ -2,6 +2,8 @@
 using namespace lego;
 template <int MODE>
 __global__ void __launch_bounds__(512) ks(double* o, long long* t, int iters) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  const OdomLds L = odom_carve(lds_raw);
   float tc[6] = {0.01f, 0.02f, -0.015f, 0.1f, 0.05f, 0.2f};
   float Pm[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
   int isDeg = 0;
@@ -9,6 +11,13 @@ __global__ void __launch_bounds__(512) ks(double* o, long long* t, int iters) {
   int brkc = 0;
   long long t0 = wall_clock64();
   for (int it = 0; it < iters; ++it) {
+    if (MODE == 3) {
+      double v[9], tt[9];
+      for (int k = 0; k < 9; ++k) v[k] = (double)(threadIdx.x & 63) * 1e-3 + tot[k] * 1e-9;
+      int M;
+      block_sum9(v, 1, 192, it & 1, L, tt, &M);
+      for (int k = 0; k < 9; ++k) tot[k] += tt[k] * 1e-12;
+    }
     float AtA[3][3] = {{(float)tot[0], (float)tot[1], (float)tot[2]},
                        {(float)tot[1], (float)tot[3], (float)tot[4]},
                        {(float)tot[2], (float)tot[4], (float)tot[5]}};
@@ -23,7 +32,7 @@ __global__ void __launch_bounds__(512) ks(double* o, long long* t, int iters) {
     }
     tc[1] += X[0]; tc[3] += X[1]; tc[5] += X[2];
     for (int i = 0; i < 6; i++) if (__builtin_isnan(tc[i])) tc[i] = 0;
-    if (MODE == 0) {
+    if (MODE == 0 || MODE == 3) {
       const double r0 = r2d(X[0]), t1 = (double)(X[1] * 100), t2 = (double)(X[2] * 100);
       const double dR = (double)(float)__builtin_sqrt(r0 * r0);
       const double dT = (double)(float)__builtin_sqrt(t1 * t1 + t2 * t2);
@@ -37,13 +46,20 @@ __global__ void __launch_bounds__(512) ks(double* o, long long* t, int iters) {
 int main() {
   double* o; long long* t;
   (void)hipMalloc(&o, 8); (void)hipMalloc(&t, 8);
-  const char* nm[3] = {"solve+update+conv", "solve+update", "QR only"};
-  for (int mode = 0; mode < 3; ++mode) {
+  const char* nm[4] = {"solve+update+conv", "solve+update", "QR only", "reduce+solve+update+conv"};
+  for (int k = 0; k < 4; ++k) (void)0;
+  (void)hipFuncSetAttribute((const void*)ks<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)odom_lds_bytes());
+  (void)hipFuncSetAttribute((const void*)ks<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)odom_lds_bytes());
+  (void)hipFuncSetAttribute((const void*)ks<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)odom_lds_bytes());
+  (void)hipFuncSetAttribute((const void*)ks<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)odom_lds_bytes());
+  for (int mode = 0; mode < 4; ++mode) {
     long long ht = 0;
     for (int rep = 0; rep < 2; ++rep) {
-      if (mode == 0) ks<0><<<1, 512>>>(o, t, 5000);
-      if (mode == 1) ks<1><<<1, 512>>>(o, t, 5000);
-      if (mode == 2) ks<2><<<1, 512>>>(o, t, 5000);
+      const size_t lb = odom_lds_bytes();
+      if (mode == 0) ks<0><<<1, 512, lb>>>(o, t, 5000);
+      if (mode == 1) ks<1><<<1, 512, lb>>>(o, t, 5000);
+      if (mode == 2) ks<2><<<1, 512, lb>>>(o, t, 5000);
+      if (mode == 3) ks<3><<<1, 512, lb>>>(o, t, 5000);
       (void)hipDeviceSynchronize();
       (void)hipMemcpy(&ht, t, 8, hipMemcpyDeviceToHost);
     }
