@@ -22,6 +22,8 @@ PKG_DIR = Path(__file__).resolve().parent
 REPO = PKG_DIR.parent
 BUILD = PKG_DIR / "build"
 HIP_LIB = BUILD / "liblego_hip.so"
+if os.environ.get("LEGO_HIP_LIB_AB"):  # A/B timing of two builds on one box (scripts/ab.sh); diagnostic
+    HIP_LIB = Path(os.environ["LEGO_HIP_LIB_AB"]).resolve()
 SYNTH_LIB = BUILD / "liblego_synth.so"
 ORACLE_LIB = REPO / "oracle" / "build" / "liblego_oracle.so"
 
