@@ -219,7 +219,8 @@ struct ExtractLds {
   uint8_t* picked;
   int8_t* label;
   uint8_t* gfl;
-  int* lf;
+  uint16_t* lf;
+  uint16_t* perm;
   SmoothEntry* srt;
   SmoothEntry* orig;
   unsigned long long* vox;
@@ -233,20 +234,25 @@ __host__ __device__ inline int next_pow2(int x) {
   return m;
 }
 
-// The six sectors' sort buffers (each padded to a power of two, packed: at
-// most 2 W entries) share their region with the VoxelGrid keys, which are
-// used only after the picking.
+// LDS of one (scan, ring) workgroup, sized so that four fit a CU for
+// VLP-16-class rings (occupancy: the picking is a serial, latency-bound walk).
+// The sectors are sorted in per-wave scratch buffers (one sector per wave at a
+// time) and kept as index permutations (uint16, the ring window's positions);
+// the scratch region is reused by the VoxelGrid keys after the picking.
+__host__ __device__ inline int extract_sector_cap(int H) { return next_pow2((H + 32) / 6 + 2); }
 __host__ __device__ inline size_t extract_sort_region(int H) {
   const size_t W = (size_t)H + 32;
-  const size_t vox = (size_t)next_pow2((int)W) * 8, sec = 2 * W * 8;
+  const size_t vox = (size_t)next_pow2((int)W) * 8;
+  const size_t sec = (size_t)(kExtractThreads / 64) * extract_sector_cap(H) * 8;
   return vox > sec ? vox : sec;
 }
 __host__ __device__ inline size_t extract_lds_bytes(int H) {
   const size_t W = (size_t)H + 32;
   size_t s = 0;
   s += W * 4;                     // curv
-  s += W * 4;                     // lf
-  s += extract_sort_region(H);    // sector sorts / vox
+  s += W * 2;                     // lf
+  s += W * 2;                     // perm (the sectors' sorted positions)
+  s += extract_sort_region(H);    // sort scratch / vox
   s += 64 * 4 + 64 * 4;           // misc + red
   s += W * 2;                     // col
   s += W * 3;                     // picked, label, gfl
@@ -262,7 +268,8 @@ __device__ __forceinline__ ExtractLds carve(unsigned char* base, int H) {
   L.orig = nullptr;
   o += extract_sort_region(H);
   L.curv = (float*)(base + o); o += W * 4;
-  L.lf = (int*)(base + o); o += W * 4;
+  L.lf = (uint16_t*)(base + o); o += W * 2;
+  L.perm = (uint16_t*)(base + o); o += W * 2;
   L.misc = (int*)(base + o); o += 64 * 4;
   L.red = (float*)(base + o); o += 64 * 4;
   L.col = (uint16_t*)(base + o); o += W * 2;
@@ -372,8 +379,12 @@ __device__ __forceinline__ void suppress(const RingCtx& R, volatile uint8_t* pic
   }
 }
 
-__device__ __forceinline__ int entry_ind(const SmoothEntry* srt, int sp, int ep, int k) {
-  return (k == ep) ? ep : srt[k - sp].ind;
+// the reference's cloudSmoothness[k].ind after the sector sort (ep itself is
+// not sorted, :699): perm holds window positions, 0xFFFF the phantom entry
+__device__ __forceinline__ int entry_ind(const uint16_t* perm, int sp, int ep, int k, int lo, int ph) {
+  if (k == ep) return ep;
+  const int v = perm[k - sp];
+  return v == 0xFFFF ? ph : v + lo;
 }
 
 __device__ __forceinline__ bool in_win(const RingCtx& R, int ind) {
@@ -428,21 +439,25 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
     *ep = (s * (5 - j) + e * (j + 1)) / 6 - 1;
     *off = o;
   };
-  // ---- the six sector sorts at once, one wave per sector (they do not depend
-  // on the picking; only the picking runs in sector order)
+  // ---- the six sector sorts, one wave per sector at a time (they do not
+  // depend on the picking; only the picking runs in sector order).  Each is
+  // sorted in its wave's scratch and kept as window positions in perm (the
+  // phantom entry of ring 0, whose index is the carried one, as 0xFFFF).
   const int nw = blockDim.x >> 6;
+  constexpr int kPhantom = -2;
+  const int secCap = extract_sector_cap(c.H);
   for (int j = wave; j < 6; j += nw) {
     int sp, ep, off;
     sector(j, &sp, &ep, &off);
     if (sp >= ep) continue;
     const int n = ep - sp, m = next_pow2(n);
-    SmoothEntry* a = L.srt + off;
+    SmoothEntry* a = L.srt + wave * secCap;
     const bool phantom_here = (ring == 0 && sp <= 4 && 4 < ep);
     for (int t = lane; t < m; t += 64) {
       SmoothEntry en;
       if (t < n) {
         const int pos = sp + t;
-        en = (phantom_here && pos == 4) ? SmoothEntry{0.0f, ph} : SmoothEntry{L.curv[pos - R.lo], pos};
+        en = (phantom_here && pos == 4) ? SmoothEntry{0.0f, kPhantom} : SmoothEntry{L.curv[pos - R.lo], pos};
       } else {
         en = {__builtin_inff(), INT_MAX};
       }
@@ -457,13 +472,22 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
       if (lane == 0) {
         for (int t = 0; t < n; ++t) {
           const int pos = sp + t;
-          a[t] = (phantom_here && pos == 4) ? SmoothEntry{0.0f, ph} : SmoothEntry{L.curv[pos - R.lo], pos};
+          a[t] = (phantom_here && pos == 4) ? SmoothEntry{0.0f, kPhantom} : SmoothEntry{L.curv[pos - R.lo], pos};
         }
         std_sort_by_value(a, n);
       }
       wave_sync_lds();
     }
-    if (phantom_here && lane == 0) L.misc[M_PH] = a[4 - sp].ind;
+    uint16_t* pm = L.perm + (sp - s);
+    for (int t = lane; t < n; t += 64) {
+      const int ind = a[t].ind;
+      pm[t] = ind == kPhantom ? (uint16_t)0xFFFF : (uint16_t)(ind - R.lo);
+    }
+    if (phantom_here && lane == 0) {
+      const int ind = a[4 - sp].ind;
+      L.misc[M_PH] = ind == kPhantom ? ph : ind;
+    }
+    wave_sync_lds();  // the scratch is refilled for the wave's next sector
   }
   __syncthreads();
   const int newph = L.misc[M_PH];
@@ -475,14 +499,14 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
       int sp, ep, off;
       sector(j, &sp, &ep, &off);
       if (sp >= ep) continue;
-      const SmoothEntry* srt = L.srt + off;
+      const uint16_t* srt = L.perm + (sp - s);
       {
         int cnt = 0;
         bool done = false;
         for (int base = ep; base >= sp && !done; base -= 64) {
           const int k = base - lane;
           bool act = k >= sp;
-          const int ind = act ? entry_ind(srt, sp, ep, k) : -1;
+          const int ind = act ? entry_ind(srt, sp, ep, k, R.lo, ph) : -1;
           if (act && !in_win(R, ind)) { act = false; flags |= 1; }
           while (true) {
             bool el = false;
@@ -515,7 +539,7 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
         for (int base = sp; base <= ep && !done; base += 64) {
           const int k = base + lane;
           bool act = k <= ep;
-          const int ind = act ? entry_ind(srt, sp, ep, k) : -1;
+          const int ind = act ? entry_ind(srt, sp, ep, k, R.lo, ph) : -1;
           if (act && !in_win(R, ind)) { act = false; flags |= 1; }
           while (true) {
             bool el = false;
@@ -564,7 +588,7 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
       }
       int tot;
       const int r = block_rank(f, L.misc + M_WOFF, &tot);
-      if (f) L.lf[L.misc[M_LF] + r] = k;
+      if (f) L.lf[L.misc[M_LF] + r] = (uint16_t)(k - R.lo);  // window positions
       __syncthreads();
       if (tid == 0) L.misc[M_LF] += tot;
       __syncthreads();
@@ -576,7 +600,7 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
   float mn[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
   float mx[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
   for (int t = tid; t < K; t += blockDim.x) {
-    const float4 p = bb.dsk[R.base + L.lf[t]];
+    const float4 p = bb.dsk[R.base + R.lo + L.lf[t]];
     mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
     mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
   }
@@ -611,7 +635,7 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
   __syncthreads();
   int nlf = 0;
   if (K > 0 && L.misc[M_OVF]) {
-    for (int t = tid; t < K; t += blockDim.x) olf[t] = bb.dsk[R.base + L.lf[t]];
+    for (int t = tid; t < K; t += blockDim.x) olf[t] = bb.dsk[R.base + R.lo + L.lf[t]];
     nlf = K;
   } else if (K > 0) {
     const int m = next_pow2(K);
@@ -620,7 +644,7 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
     for (int t = tid; t < m; t += blockDim.x) {
       unsigned long long key = ~0ull;
       if (t < K) {
-        const float4 p = bb.dsk[R.base + L.lf[t]];
+        const float4 p = bb.dsk[R.base + R.lo + L.lf[t]];
         const int i0 = (int)(floorf(p.x * inv) - fb0);
         const int i1 = (int)(floorf(p.y * inv) - fb1);
         const int i2 = (int)(floorf(p.z * inv) - fb2);
@@ -642,7 +666,7 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
         float cx = 0, cy = 0, cz = 0, ci = 0;
         int u = t;
         for (; u < K && (unsigned)(L.vox[u] >> 32) == key; ++u) {
-          const float4 p = bb.dsk[R.base + L.lf[(unsigned)(L.vox[u] & 0xffffffffu)]];
+          const float4 p = bb.dsk[R.base + R.lo + L.lf[(unsigned)(L.vox[u] & 0xffffffffu)]];
           cx += p.x; cy += p.y; cz += p.z; ci += p.w;
         }
         const float cnt = (float)(u - t);

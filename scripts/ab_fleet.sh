@@ -1,0 +1,10 @@
+#!/bin/bash
+# A/B fleet-aux timing of build/ab/A vs build/ab/B on one box (diagnostic).
+set -uo pipefail
+R="${GRAFT_REPO_ROOT:-$(pwd)}"
+cd "$R"
+for r in 1 2; do
+  for v in A B; do
+    LEGO_HIP_LIB_AB=build/ab/$v/liblego_hip.so timeout -k 10 120 python scripts/fleet_probe.py --streams 64 --k 20 --steps 3 2>/dev/null | tail -1 | sed "s/^/$v /" || exit 1
+  done
+done
