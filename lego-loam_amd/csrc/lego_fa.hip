@@ -491,6 +491,10 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
   }
   __syncthreads();
   const int newph = L.misc[M_PH];
+  // picked indices in pick order (sharp, less sharp, flat), in the sort
+  // scratch, which is free until the VoxelGrid keys
+  volatile int* pk = (volatile int*)L.srt;
+  static_assert((kSharpPerRing + kLessSharpPerRing + kFlatPerRing) * 4 <= 16384, "pick lists fit the scratch");
   // ---- picking, sector by sector (wave 0): edge scan k = ep .. sp, then
   // flat scan k = sp .. ep (:699-769)
   if (wave == 0) {
@@ -519,12 +523,11 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
             const int l = __ffsll((long long)msk) - 1;
             cnt++;
             if (cnt > 20) { done = true; break; }
-            if (lane == l) {
+            if (lane == l) {  // the points are copied after the picking (no HBM latency per pick)
               const int w = ind - R.lo;
               label[w] = cnt <= 2 ? 2 : 1;
-              const float4 pt = bb.dsk[R.base + ind];
-              if (cnt <= 2) R.osh[nsh] = pt;
-              R.ols[nls] = pt;
+              if (cnt <= 2) pk[nsh] = ind;
+              pk[kSharpPerRing + nls] = ind;
               suppress(R, picked, L.col, ind);
             }
             if (cnt <= 2) nsh++;
@@ -552,7 +555,7 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
             const int l = __ffsll((long long)msk) - 1;
             if (lane == l) {
               label[ind - R.lo] = -1;
-              R.ofl[nfl] = bb.dsk[R.base + ind];
+              pk[kSharpPerRing + kLessSharpPerRing + nfl] = ind;
             }
             nfl++;
             cnt++;
@@ -566,6 +569,14 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
     if (lane == 0) { L.misc[M_NSH] = nsh; L.misc[M_NLS] = nls; L.misc[M_NFL] = nfl; }
   }
   __syncthreads();
+  {  // the picked points in pick order, all loads independent
+    const int nsh = L.misc[M_NSH], nls = L.misc[M_NLS], nfl = L.misc[M_NFL];
+    for (int t = tid; t < nsh + nls + nfl; t += blockDim.x) {
+      if (t < nsh) R.osh[t] = bb.dsk[R.base + pk[t]];
+      else if (t < nsh + nls) R.ols[t - nsh] = bb.dsk[R.base + pk[kSharpPerRing + t - nsh]];
+      else R.ofl[t - nsh - nls] = bb.dsk[R.base + pk[kSharpPerRing + kLessSharpPerRing + t - nsh - nls]];
+    }
+  }
   // ---- less-flat set: per sector the positions k in [sp, ep] with label <= 0,
   // in order (:771-775); the sectors are consecutive ranges, so one ordered
   // pass over [s, e - 1] restricted to the sectors that ran
