@@ -1041,6 +1041,44 @@ __device__ __forceinline__ void solve_step(float (&AtA)[3][3], float (&AtB)[3], 
 
 __device__ __forceinline__ double r2d(double r) { return r * 180.0 / M_PI; }
 
+// The convergence test of calculateTransformationSurf / Corner (:1362-1368,
+// :1463-1469): deltaR = float(sqrt(sum of rad2deg(x)^2)) < 0.1 and deltaT =
+// float(sqrt(sum of (100 x)^2)) < 0.1.  The squared sums are first bounded
+// with a multiply by 180/pi (a few ulp from the reference's divide): when
+// they are clearly on one side of 0.1^2 the verdict is the reference's; only
+// near the threshold is the exact expression evaluated.
+__device__ __forceinline__ bool conv_exact(bool surf, const float (&X)[3]) {
+  double dR, dT;
+  if (surf) {
+    const double r0 = r2d(X[0]), r1 = r2d(X[1]), t2 = (double)(X[2] * 100);
+    dR = (double)(float)__builtin_sqrt(r0 * r0 + r1 * r1);
+    dT = (double)(float)__builtin_sqrt(t2 * t2);
+  } else {
+    const double r0 = r2d(X[0]), t1 = (double)(X[1] * 100), t2 = (double)(X[2] * 100);
+    dR = (double)(float)__builtin_sqrt(r0 * r0);
+    dT = (double)(float)__builtin_sqrt(t1 * t1 + t2 * t2);
+  }
+  return dR < 0.1 && dT < 0.1;
+}
+__device__ __forceinline__ bool converged3(bool surf, const float (&X)[3]) {
+  constexpr double k = 180.0 / M_PI;
+  double qR, qT;
+  if (surf) {
+    const double r0 = X[0] * k, r1 = X[1] * k, t2 = (double)(X[2] * 100);
+    qR = r0 * r0 + r1 * r1;
+    qT = t2 * t2;
+  } else {
+    const double r0 = X[0] * k, t1 = (double)(X[1] * 100), t2 = (double)(X[2] * 100);
+    qR = r0 * r0;
+    qT = t1 * t1 + t2 * t2;
+  }
+  // float(sqrt(q)) < 0.1 holds for q < 0.0099 and fails for q > 0.0101 (the
+  // float rounding of sqrt and the divide-vs-multiply difference are ~1e-7 relative)
+  if (qR > 0.0101 || qT > 0.0101) return false;
+  if (qR < 0.0099 && qT < 0.0099) return true;
+  return conv_exact(surf, X);
+}
+
 // ---------------------------------------------------------------- exchange
 // The workgroups of a launch run the same serial chain on identical inputs
 // and split only the correspondence searches.  Results travel as 8-byte
@@ -1310,7 +1348,6 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
       float X[3];
       solve_step(AtA, AtB, it, Pm, isDeg, X);
       S.add(it == 0 ? P_T_SOLVE0 : P_T_SOLVE);
-      double dR, dT;
       if (surf) {
         tc[0] += X[0]; tc[2] += X[1]; tc[4] += X[2];
       } else {
@@ -1318,16 +1355,7 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
       }
 #pragma unroll
       for (int i = 0; i < 6; i++) if (__builtin_isnan(tc[i])) tc[i] = 0;
-      if (surf) {
-        const double r0 = r2d(X[0]), r1 = r2d(X[1]), t2 = (double)(X[2] * 100);
-        dR = (double)(float)__builtin_sqrt(r0 * r0 + r1 * r1);
-        dT = (double)(float)__builtin_sqrt(t2 * t2);
-      } else {
-        const double r0 = r2d(X[0]), t1 = (double)(X[1] * 100), t2 = (double)(X[2] * 100);
-        dR = (double)(float)__builtin_sqrt(r0 * r0);
-        dT = (double)(float)__builtin_sqrt(t1 * t1 + t2 * t2);
-      }
-      brk = dR < 0.1 && dT < 0.1;
+      brk = converged3(surf, X);
     }
     S.add(P_SOLVE);
     if (brk) break;
