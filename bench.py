@@ -483,7 +483,7 @@ def main():
         if args.odom_profile:
             prof = (C.c_uint64 * 32)()
             lib.lego_odom_profile(gpu.h, -1, prof)
-            names = ["surf_nn", "surf", "corner_nn", "corner", "solve", "integrate", "to_end",
+            names = ["surf_nn", "to_end w1", "corner_nn", "corner", "solve", "integrate", "to_end",
                      "build", "resident", "", "", "", "nn_shells"]
             nsc = (args.steps + args.warmup) * B
             for i, nm in enumerate(names):

@@ -462,32 +462,35 @@ __device__ __forceinline__ void build_zero(const BuildArgs<Idx>& B) {
   for (int k = tid; k < 2 * B.NK; k += kOdomThreads) { B.kfirst[k] = INT_MAX; B.klast[k] = -1; }
   if (tid == 0) { *B.S.irregular = 0; *B.Cs.irregular = 0; }
 }
+// The keys of index i's neighbours in its cloud: kp of i - 1 (INT_MIN at the
+// cloud's start), kn of i + 1 (INT_MAX at its end), from the .w words wp of
+// point i - 1 and wn of point i + 1 (loaded beside point i itself, so the
+// chunk waits for one load latency).
+__device__ __forceinline__ void nbr_keys(int i, int nS, int n, float wp, float wn, int& kp, int& kn) {
+  kp = i == 0 || i == nS ? INT_MIN : (int)wp;
+  kn = i == nS - 1 || i == n - 1 ? INT_MAX : (int)wn;
+}
 // counts the wave's chunk [i0, i0 + 64) of the combined index range; lane
-// i0 + lane holds point p (ignored past nS + nC).  Wave-uniform call.
+// i0 + lane holds point p (ignored past nS + nC) and its neighbours' keys
+// (nbr_keys).  The clouds come ring after ring, so a key's first / last index
+// is where the key changes: one plain store per run.  A key that decreases
+// along a cloud marks the cloud irregular (the searches then use the literal
+// scan-line loop), as does a key outside [0, NK).
 template <class Idx>
-__device__ __forceinline__ void build_count(const BuildArgs<Idx>& B, int i0, float4 p) {
+__device__ __forceinline__ void build_count(const BuildArgs<Idx>& B, int i0, float4 p, int kp, int kn) {
   const int lane = threadIdx.x & 63, i = i0 + lane, n = B.nS + B.nC;
-  int kk = -1;
   if (i < n) {
     const bool corner = i >= B.nS;
     const int T = corner ? B.TC : B.TS;
     atomicAdd(&B.cnt[(corner ? B.TS : 0) + fine_bucket(cell_of(p.x), cell_of(p.y), cell_of(p.z), T)], 1u);
     const int k = (int)p.w;
-    if (k < 0 || k >= B.NK) *(corner ? B.Cs.irregular : B.S.irregular) = 1;
-    else kk = k + (corner ? B.NK : 0);
-  }
-  // per-key first/last: one atomic per distinct (cloud, key) of the wave
-  unsigned long long todo = __ballot(kk >= 0);
-  while (todo) {
-    const int leader = __ffsll((long long)todo) - 1;
-    const int key = __builtin_amdgcn_readlane(kk, leader);
-    const unsigned long long m = __ballot(kk == key);
-    if (lane == leader) {
-      const int base = key >= B.NK ? B.nS : 0;
-      atomicMin(&B.kfirst[key], i0 + leader - base);
-      atomicMax(&B.klast[key], i0 + 63 - __clzll((long long)m) - base);
+    if (k < 0 || k >= B.NK || kp > k) {
+      *(corner ? B.Cs.irregular : B.S.irregular) = 1;
+    } else {
+      const int kk = k + (corner ? B.NK : 0), j = i - (corner ? B.nS : 0);
+      if (kp != k) B.kfirst[kk] = j;
+      if (kn != k) B.klast[kk] = j;
     }
-    todo &= ~m;
   }
 }
 // key tables, bucket starts, scatter, bucket ends (all threads, after a
@@ -564,11 +567,14 @@ __device__ __forceinline__ void nn_build2(const BuildArgs<Idx>& B, unsigned long
       const int i = j0 + u * kOdomThreads + lane;
       if (i < n) pu[u] = i >= B.nS ? B.ptsC[i - B.nS] : B.ptsS[i];
     }
+    auto w_at = [&](int j) { return j >= B.nS ? B.ptsC[j - B.nS].w : B.ptsS[j].w; };
 #pragma unroll
     for (int u = 0; u < kBuildU; ++u) {
-      const int i0 = j0 + u * kOdomThreads;
+      const int i0 = j0 + u * kOdomThreads, i = i0 + lane;
       if (i0 >= n) break;
-      build_count(B, i0, pu[u]);
+      int kp = 0, kn = 0;
+      if (i < n) nbr_keys(i, B.nS, n, w_at(max(i - 1, 0)), w_at(min(i + 1, n - 1)), kp, kn);
+      build_count(B, i0, pu[u], kp, kn);
     }
   }
   __syncthreads();
@@ -1519,38 +1525,46 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
       else build_zero(BH);
     }
     __syncthreads();
+    const unsigned long long tw = prof && (tid == 0 || tid == 64) ? wall_clock64() : 0;
     if (!init && tid < 64) {
       const float bl[3] = {iq.pitchStart, iq.yawStart, iq.rollStart};
       const float al[3] = {iq.pitchCur, iq.yawCur, iq.rollCur};  // imu*Last = imu*Cur (:1641-1643)
       integrate_wave(st->transformSum, st->transformCur, bl, al);
     }
+    if (prof && tid == 0) prof[P_INTEG] += wall_clock64() - tw;
     // TransformToEnd of less-flat then less-sharp as one index range in
     // wave-uniform chunks, each chunk counted into the next index as it is
     // produced (build_count: no read-back of the clouds for the counting pass)
     auto hand_off = [&](const auto& B) {
       if (t0 >= 0) {
         const int nS = F.nLF, n = F.nLF + F.nLS, lane = tid & 63;
+        auto w_at = [&](int j) { return j < nS ? F.lflat[j].w : F.lsharp[j - nS].w; };
         for (int i0 = t0 - lane; i0 < n; i0 += tstep) {  // wave-uniform
           const int i = i0 + lane;
           float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (i < nS) {
-            p = init ? F.lflat[i] : to_end(F.lflat[i], tcur, et, im);
-            gSn[i] = p;
-            if (lead) sEnd[i] = p;
-            if (fits) L.lastS[i] = p;
-          } else if (i < n) {
-            const int j = i - nS;
-            p = init ? F.lsharp[j] : to_end(F.lsharp[j], tcur, et, im);
-            gCn[j] = p;
-            if (lead) cEnd[j] = p;
-            if (fits) L.lastC[j] = p;
+          int kp = 0, kn = 0;
+          if (i < n) {
+            const bool corner = i >= nS;
+            const float4 r = corner ? F.lsharp[i - nS] : F.lflat[i];
+            if (rebuild) nbr_keys(i, nS, n, w_at(max(i - 1, 0)), w_at(min(i + 1, n - 1)), kp, kn);
+            p = init ? r : to_end(r, tcur, et, im);
+            if (corner) {
+              gCn[i - nS] = p;
+              if (lead) cEnd[i - nS] = p;
+              if (fits) L.lastC[i - nS] = p;
+            } else {
+              gSn[i] = p;
+              if (lead) sEnd[i] = p;
+              if (fits) L.lastS[i] = p;
+            }
           }
-          if (rebuild) build_count(B, i0, p);
+          if (rebuild) build_count(B, i0, p, kp, kn);
         }
       }
     };
     if (fits) hand_off(BL);
     else hand_off(BH);
+    if (prof && tid == 64) prof[P_SURF] += wall_clock64() - tw;
     __syncthreads();
     S.add(P_TOEND);
     if (tid == 0) {
