@@ -122,7 +122,11 @@ struct EndTrig {
   float cx, sx, cy, sy, cz, sz;
 };
 __device__ __forceinline__ EndTrig end_trig(const float* tc) {
-  return {lego_cosf(tc[0]), lego_sinf(tc[0]), lego_cosf(tc[1]), lego_sinf(tc[1]), lego_cosf(tc[2]), lego_sinf(tc[2])};
+  EndTrig e;
+  lego_sincosf(tc[0], &e.sx, &e.cx);
+  lego_sincosf(tc[1], &e.sy, &e.cy);
+  lego_sincosf(tc[2], &e.sz, &e.cz);
+  return e;
 }
 __device__ __forceinline__ float4 to_end(float4 pi, const float* tc, const EndTrig& et, const ImuEnd& im) {
   const float s = 10 * (pi.w - (float)(int)pi.w);
@@ -1539,14 +1543,27 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
       if (t0 >= 0) {
         const int nS = F.nLF, n = F.nLF + F.nLS, lane = tid & 63;
         auto w_at = [&](int j) { return j < nS ? F.lflat[j].w : F.lsharp[j - nS].w; };
+        // the point and its neighbours' .w words, one chunk ahead
+        auto fetch = [&](int i, float4& r, float& wp, float& wn) {
+          if (i < n) {
+            r = i >= nS ? F.lsharp[i - nS] : F.lflat[i];
+            wp = w_at(max(i - 1, 0));
+            wn = w_at(min(i + 1, n - 1));
+          }
+        };
+        float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+        float wp = 0.f, wn = 0.f;
+        fetch(t0, r, wp, wn);
         for (int i0 = t0 - lane; i0 < n; i0 += tstep) {  // wave-uniform
           const int i = i0 + lane;
+          float4 rN = r;
+          float wpN = wp, wnN = wn;
+          fetch(i + tstep, rN, wpN, wnN);
           float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
           int kp = 0, kn = 0;
           if (i < n) {
             const bool corner = i >= nS;
-            const float4 r = corner ? F.lsharp[i - nS] : F.lflat[i];
-            if (rebuild) nbr_keys(i, nS, n, w_at(max(i - 1, 0)), w_at(min(i + 1, n - 1)), kp, kn);
+            if (rebuild) nbr_keys(i, nS, n, wp, wn, kp, kn);
             p = init ? r : to_end(r, tcur, et, im);
             if (corner) {
               gCn[i - nS] = p;
@@ -1559,6 +1576,7 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
             }
           }
           if (rebuild) build_count(B, i0, p, kp, kn);
+          r = rN; wp = wpN; wn = wnN;
         }
       }
     };
