@@ -662,9 +662,27 @@ __device__ __forceinline__ void group_lex_min3(float& d, int& r, int& j) {
   r = rm;
 }
 
+// Exact nearest neighbour with d2 < bound over pts[0, n), by the calling wave.
+// A lane visits ascending indices, so a strict < keeps its lexicographic
+// (distance, index) minimum; the group reduction breaks ties by index.
+__device__ __forceinline__ int nn_brute(const float4* pts, int n, float4 q, float bound, int g) {
+  float bd = bound;
+  int bi = INT_MAX;
+#pragma unroll 4
+  for (int j = g; j < n; j += kGL) {
+    const float d2 = flann_d2(q, pts[j]);
+    if (d2 < bd) { bd = d2; bi = j; }
+  }
+  group_lex_min(bd, bi);
+  return (bi != INT_MAX && bd < bound) ? bi : -1;
+}
+
 // Exact nearest neighbour with d2 < bound, by the calling wave: the fine
 // grid's 27 cells (accepted when the best distance is provably below the one
-// cell they cover), else every point (contiguous, independent loads).
+// cell they cover), else every point (nn_brute, which covers the cells' points
+// too).  Going to nn_brute directly for a query that fell back in the previous
+// NN round measured 1.5% slower: the fallback is VALU-bound and its waves then
+// contend for the SIMDs with the shell searches' latency-bound waves.
 template <class Idx>
 __device__ __forceinline__ int nn_i1(const NNView<Idx>& v, float4 q, float bound, int g, unsigned long long* prof) {
   if (v.n <= 0) return -1;
@@ -692,13 +710,10 @@ __device__ __forceinline__ int nn_i1(const NNView<Idx>& v, float4 q, float bound
   group_lex_min(bd, bi);
   if (bd < kCell * kCell * 0.99999f) {
     if (prof && g == 0) atomicAdd(&prof[P_NN_SHELL1], 1ull);
-  } else {
-    if (prof && g == 0) atomicAdd(&prof[P_NN_BRUTE], 1ull);
-#pragma unroll 4
-    for (int j = g; j < v.n; j += kGL) lex_min(bd, bi, flann_d2(q, v.pts[j]), j);
-    group_lex_min(bd, bi);
+    return (bi != INT_MAX && bd < bound) ? bi : -1;
   }
-  return (bi != INT_MAX && bd < bound) ? bi : -1;
+  if (prof && g == 0) atomicAdd(&prof[P_NN_BRUTE], 1ull);
+  return nn_brute(v.pts, v.n, q, bound, g);
 }
 
 // Scan-line neighbours of closest point ci (corner :1062-1099, surf
@@ -748,14 +763,6 @@ __device__ __forceinline__ bool nn_lines(const NNView<Idx>& v, int ci, int jend,
   return true;
 }
 
-// Exact nearest neighbour by brute force (stale snapshot, rare).
-__device__ __forceinline__ int nn_brute(const float4* pts, int n, float4 q, float bound, int g) {
-  float bd = bound;
-  int bi = INT_MAX;
-  for (int j = g; j < n; j += kGL) lex_min(bd, bi, flann_d2(q, pts[j]), j);
-  group_lex_min(bd, bi);
-  return (bi != INT_MAX && bd < bound) ? bi : -1;
-}
 
 // The reference's sequential loops, kGL indices per step (fallback).  Every
 // lane keeps a lexicographic (distance, visit rank) minimum over the indices
