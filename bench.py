@@ -483,7 +483,7 @@ def main():
         if args.odom_profile:
             prof = (C.c_uint64 * 32)()
             lib.lego_odom_profile(gpu.h, -1, prof)
-            names = ["surf_nn", "to_end w1", "corner_nn", "corner", "solve", "integrate", "to_end",
+            names = ["surf_nn", "surf", "corner_nn", "corner", "solve", "integrate", "to_end",
                      "build", "resident", "", "", "", "nn_shells"]
             nsc = (args.steps + args.warmup) * B
             for i, nm in enumerate(names):
@@ -494,7 +494,7 @@ def main():
                   f" scan-line indexed {prof[20] / nsc:.1f}, scan-line literal {prof[13] / nsc:.1f}",
                   file=sys.stderr)
             for i, nm in ((21, "rows (excl. reduce)"), (22, "solve_qr+eig it0"), (23, "solve_qr it>0"),
-                          (24, "nn local work"), (25, "build (all)"), (26, "build: count pass"),
+                          (24, "nn local work"), (25, "to_end loop (wave 1)"), (26, "build: count pass"),
                           (27, "build: key tables+scan"), (29, "build: scatter pass"), (31, "build: bucket ends")):
                 print(f"  odom.{nm:20s} {prof[i] / 100.0 / nsc:9.2f} us/scan", file=sys.stderr)
             nq0 = max(prof[30], 1)

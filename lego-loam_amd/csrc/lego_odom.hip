@@ -354,7 +354,7 @@ enum { P_SURF_NN = 0, P_SURF = 1, P_CORN_NN = 2, P_CORN = 3, P_SOLVE = 4, P_INTE
        P_TOEND = 6, P_BUILD = 7, P_RESID = 8, P_ITERS_S = 9, P_ITERS_C = 10, P_NNR = 11,
        P_QUERY = 12, P_SCANLINE = 13, P_NN_SHELL1 = 14, P_NN_BRUTE = 15,
        P_G0_TOSTART = 16, P_G0_NN = 17, P_G0_SCAN = 18, P_G0_Q = 19, P_AZLINE = 20,
-       P_T_ROWS = 21, P_T_SOLVE0 = 22, P_T_SOLVE = 23, P_X_LOCAL = 24, P_B_SURF = 25,
+       P_T_ROWS = 21, P_T_SOLVE0 = 22, P_T_SOLVE = 23, P_X_LOCAL = 24, P_TOEND_LOOP = 25,
        P_B_PASS1 = 26, P_B_SCAN = 27, P_B_SCATTER = 29, P_B_ENDS = 31,  // index-build sub-phases
        P_NPROF = 32 };
 struct Stamp {
@@ -937,10 +937,8 @@ __device__ __forceinline__ BuildArgs<uint32_t> hbm_build_args(const OdomLds& L, 
 // Rebuilds both clouds' indexes (all threads) over the current last clouds.
 __device__ __forceinline__ void build_indexes(const OdomLds& L, const OdomBufs& ob, const OdomState* st,
                                               const DevCfg& c, unsigned long long* prof = nullptr) {
-  const unsigned long long t0 = (prof && threadIdx.x == 0) ? wall_clock64() : 0;
   if (st->resident) nn_build2(lds_build_args(L, st, c), prof);
   else nn_build2(hbm_build_args(L, ob, st, c), prof);
-  if (prof && threadIdx.x == 0) prof[P_B_SURF] += wall_clock64() - t0;
 }
 
 // ---------------------------------------------------------------- reduction
@@ -1589,7 +1587,7 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     };
     if (fits) hand_off(BL);
     else hand_off(BH);
-    if (prof && tid == 64) prof[P_SURF] += wall_clock64() - tw;
+    if (prof && tid == 64) prof[P_TOEND_LOOP] += wall_clock64() - tw;  // wave 1's chunks
     __syncthreads();
     S.add(P_TOEND);
     if (tid == 0) {
