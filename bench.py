@@ -162,6 +162,28 @@ def host_info():
     return {"nproc": os.cpu_count(), "affinity": share, "cpu_model": model}
 
 
+def mapping_handoff(gpu, B: int) -> dict:
+    """Auxiliary, outside the timed region: featureAssociation's
+    hand-off to mapping over the last timed batch.  publishCloudsLast sends the
+    last clouds every skipFrameNum + 1 scans (featureAssociation.cpp:1798-1815);
+    lego_batch_fetch brings one scan's outputs (features, the three *_last
+    clouds, the pose) to the host, the step a mapping consumer on another
+    process pays per published scan."""
+    pub, dts, sizes = [], [], []
+    for k in range(B):
+        t0 = time.perf_counter()
+        _, fa = gpu.batch_fetch(k)
+        dts.append((time.perf_counter() - t0) * 1e3)
+        if fa["publish_to_mapping"]:
+            pub.append(k)
+            sizes.append((len(fa["corner_last"]), len(fa["surf_last"]), len(fa["outlier_last"])))
+    gaps = [b - a for a, b in zip(pub, pub[1:])]
+    return {"scans": B, "published": len(pub), "every_n_scans": (statistics.mean(gaps) if gaps else None),
+            "fetch_ms_per_scan": statistics.median(dts),
+            "clouds_per_published_scan": ([round(statistics.mean(c)) for c in zip(*sizes)] if sizes else None),
+            "clouds": "corner_last, surf_last, outlier_last points"}
+
+
 def mapping_bench(L, steps: int, cpu: bool):
     """Auxiliary (not the headline metric): config C5 scan-to-map — a VLS-128
     scan against a fixed synthetic map of 1.0 M surf / 200 k corner points
@@ -454,7 +476,9 @@ def main():
     value = total_scans / dt
     ms_per_step = dt / args.steps * 1e3
 
+    handoff = None
     if rank == 0:
+        handoff = mapping_handoff(gpu, B)
         # the batch runs as chunks (lego_api.hip run_batch): k_odom launches per step
         launches = {k[2:]: v / args.steps for k, v in stage_acc.items() if k.startswith("n:")}
         stage_acc = {k: v for k, v in stage_acc.items() if not k.startswith("n:")}
@@ -506,7 +530,7 @@ def main():
             for k, v in sorted(stage_acc.items(), key=lambda kv: -kv[1]):
                 print(f"  {k:14s} {v / args.steps:9.3f} ms/step  {100 * v / max(tot, 1e-9):5.1f}%",
                       file=sys.stderr)
-        aux = {}
+        aux = {"mapping_handoff": handoff}
         if args.mapping_steps > 0 and world == 1:
             aux["scan_to_map_c5"] = mapping_bench(L, args.mapping_steps, not args.no_cpu)
         if args.fleet_streams > 0 and world == 1:
