@@ -195,6 +195,8 @@ static int make_devcfg(const lego_sensor_cfg* c, DevCfg* d) {
 static int ctx_reset(lego_ctx* x) {
   HIPCHK(hipMemcpyAsync(x->ob.st, x->h_resetSt, sizeof(OdomState) * x->nStreams, hipMemcpyHostToDevice,
                         x->ostream));
+  // the hand-off tags restart with the state: no granule of the old stream may match
+  HIPCHK(hipMemsetAsync(x->ob.xh, 0, x->ob.xhBytes, x->ostream));
   HIPCHK(hipMemcpyAsync(x->d_carry, x->h_resetCarry, sizeof(FaCarry) * x->nStreams, hipMemcpyHostToDevice,
                         x->stream));
   // the next batch's odometry must also follow the reset of its own stream's
@@ -403,6 +405,15 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
     ob.xblock = xb;
     ob.xerr = (unsigned*)xb;
     ob.xg = (unsigned long long*)(xb + 16);
+    ob.capH = ob.capSurf + ob.capCorner;
+    ob.xhBytes = S * sizeof(unsigned long long) * 2 * 3 * (size_t)ob.capH;
+    unsigned char* hb = nullptr;
+    A(hb, ob.xhBytes);
+    ob.xh = (unsigned long long*)hb;
+    if (hipMemset(ob.xh, 0, ob.xhBytes) != hipSuccess) {
+      set_err("hipMemset failed for the hand-off exchange");
+      return fail(LEGO_E_DEVICE);
+    }
   }
   A(ob.sumOut, B * 6);
   A(ob.curOut, B * 6);
@@ -533,6 +544,7 @@ static OdomBufs ob_slice(const OdomBufs& a, const DevCfg& c, int c0, int s0, int
   o.nS.gPts += w * a.capSurf;
   o.qi += w * 3 * a.capQ;
   o.xg += (size_t)s0 * a.roundsCap * 3 * a.capQ;
+  o.xh += (size_t)s0 * 2 * 3 * a.capH;
   o.sumOut += k * 6; o.curOut += k * 6; o.validOut += k; o.pubOut += k;
   o.cornerEnd += k * a.capLS; o.surfEnd += k * c.P;
   return o;

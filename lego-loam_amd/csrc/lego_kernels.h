@@ -86,6 +86,7 @@ struct OdomState {
   int curBuf;    // HBM buffer holding the current last clouds
   int snapBuf;   // HBM buffer holding the indexes' snapshot (== curBuf unless stale)
   int resident;  // current last clouds (and indexes) are LDS-resident
+  unsigned seq;  // hand-offs so far (the hand-off exchange's tag; its granules are zeroed with it)
 };
 
 // Device buffers of the odometry kernel for S independent streams (a fleet;
@@ -111,6 +112,11 @@ struct OdomBufs {
   size_t xbytes;
   unsigned* xerr;
   unsigned long long* xg;
+  // hand-off exchange: per stream 2 (hand-off parity) x 3 x capH granules
+  // {seq, TransformToEnd'ed x / y / z}, zeroed at creation and reset
+  unsigned long long* xh;
+  size_t xhBytes;
+  int capH;  // capSurf + capCorner
   // per-scan outputs of the batch (workgroup 0)
   float* sumOut;        // [B*6]
   float* curOut;        // [B*6]
