@@ -28,7 +28,8 @@ __global__ void __launch_bounds__(512) krow(const float4* gq, const float4* glas
     const float tx = tc[3], ty = tc[4], tz = tc[5];
     double acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     int mloc = 0;
-    for (int q = tid; q < nQ; q += 512) {
+    const int qstep = MODE == 5 ? 64 : 512;  // mode 5: wave 0 takes every row (3 per lane)
+    for (int q = (MODE == 5 && tid >= 64) ? nQ : tid; q < nQ; q += qstep) {
       const float4 po = qp[q];
       float4 sel;
       if (MODE == 2) sel = to_start_t(po, start_s(po), tc, 1.f, 0.f, 1.f, 0.f, 1.f, 0.f);
@@ -84,6 +85,13 @@ __global__ void __launch_bounds__(512) krow(const float4* gq, const float4* glas
       }
     }
     if (MODE == 4) __syncthreads();
+    if (MODE == 5 && tid < 64) {  // the wave's DPP reduction, no barrier
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const double r = row_sum_f64(acc[k]);
+        acc[k] = ((rdlane_f64(r, 0) + rdlane_f64(r, 16)) + rdlane_f64(r, 32)) + rdlane_f64(r, 48);
+      }
+    }
     for (int k = 0; k < 9; ++k) tot += acc[k];
     tot += mloc;
     tc[1] += (float)(acc[0] * 1e-30);  // keep the loop honest; ry changes each iteration
@@ -105,8 +113,8 @@ int main() {
   (void)hipMalloc(&o, 512 * 8); (void)hipMalloc(&t, 8);
   (void)hipMemcpy(dq, hq, sizeof hq, hipMemcpyHostToDevice); (void)hipMemcpy(dl, hl, sizeof hl, hipMemcpyHostToDevice);
   (void)hipMemcpy(dqi, hqi, sizeof hqi, hipMemcpyHostToDevice);
-  const char* nm[5] = {"current", "fma acc", "no trig", "no div", "current+barrier"};
-  for (int mode = 0; mode < 5; ++mode) {
+  const char* nm[6] = {"current", "fma acc", "no trig", "no div", "current+barrier", "one wave + DPP sum"};
+  for (int mode = 0; mode < 6; ++mode) {
     long long ht = 0;
     for (int rep = 0; rep < 2; ++rep) {
       const int iters = 5000;
@@ -116,6 +124,7 @@ int main() {
         case 2: krow<2><<<1, 512>>>(dq, dl, dqi, o, t, iters, nQ); break;
         case 3: krow<3><<<1, 512>>>(dq, dl, dqi, o, t, iters, nQ); break;
         case 4: krow<4><<<1, 512>>>(dq, dl, dqi, o, t, iters, nQ); break;
+        case 5: krow<5><<<1, 512>>>(dq, dl, dqi, o, t, iters, nQ); break;
       }
       (void)hipDeviceSynchronize();
       (void)hipMemcpy(&ht, t, 8, hipMemcpyDeviceToHost);
