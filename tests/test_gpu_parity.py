@@ -316,19 +316,22 @@ def test_concurrent_streams_identical(L):
         assert got[i] == ref[i], i
 
 
-@pytest.mark.parametrize("workgroups", [None, "1"])
-def test_fleet_equals_single_streams(L, workgroups):
+@pytest.mark.parametrize("sensor,seeds,K,cap,workgroups", [
+    ("VLP-16", (4, 8, 9), 8, 40000, None), ("VLP-16", (4, 8, 9), 8, 40000, "1"),
+    ("HDL-64E", (2, 5), 4, 140000, None)])
+def test_fleet_equals_single_streams(L, sensor, seeds, K, cap, workgroups):
     """A fleet context (lego_fleet_create: S streams, one launch per stage for
     all of them) gives each stream the same pose records, byte for byte, as
     the stream's own context, across two stream-major batches (the states
-    and the FA carries cross the launch boundary per stream)."""
+    and the FA carries cross the launch boundary per stream).  HDL-64E: the
+    HBM-resident odometry with its per-stream hand-off exchange."""
     import os
 
-    cfg = L.sensor_cfg("VLP-16", L.hip_lib())
-    K, S = 8, 3
+    cfg = L.sensor_cfg(sensor, L.hip_lib())
+    S = len(seeds)
     streams = []
-    for seed in (4, 8, 9):
-        sc = L.synth_cfg("VLP-16", seed)
+    for seed in seeds:
+        sc = L.synth_cfg(sensor, seed)
         streams.append([L.synth_scan(sc, k) for k in range(K)])
 
     def pack(scans):
@@ -339,14 +342,14 @@ def test_fleet_equals_single_streams(L, workgroups):
 
     ref = []
     for scans in streams:
-        g = L.Lego(cfg, max_points=40000, max_batch=K)
+        g = L.Lego(cfg, max_points=cap, max_batch=K)
         raw = bytes(g.odom_batch(*pack(scans[:K // 2]))) + bytes(g.odom_batch(*pack(scans[K // 2:])))
         g.close()
         ref.append([raw[64 * k:64 * k + 60] for k in range(K)])
     if workgroups:
         os.environ["LEGO_ODOM_WORKGROUPS"] = workgroups
     try:
-        fl = L.Lego(cfg, max_points=40000, max_batch=K // 2, streams=S)
+        fl = L.Lego(cfg, max_points=cap, max_batch=K // 2, streams=S)
     finally:
         os.environ.pop("LEGO_ODOM_WORKGROUPS", None)
     got = [[] for _ in range(S)]
@@ -359,10 +362,36 @@ def test_fleet_equals_single_streams(L, workgroups):
                 got[s].append(raw[64 * r:64 * r + 60])
     # a batch that is not S x K scans is refused
     with pytest.raises(RuntimeError):
-        fl.odom_batch(*pack([streams[0][0], streams[1][0]]))
+        fl.odom_batch(*pack([streams[s][0] for s in range(S)] + [streams[0][1]]))
     fl.close()
     for s in range(S):
         assert got[s] == ref[s], s
+
+
+def test_hbm_reset_clears_handoff_exchange(L):
+    """HBM-resident odometry (HDL-64E): after lego_reset the hand-off sequence
+    restarts, so the exchange's granules must be cleared with it.  A context
+    that ran one stream, was reset and then ran another gives the second
+    stream's records byte for byte as a fresh context."""
+    cfg = L.sensor_cfg("HDL-64E", L.hip_lib())
+
+    def pack(scans):
+        pts = np.concatenate([p for p, _ in scans])
+        off = np.zeros(len(scans) + 1, np.int64)
+        off[1:] = np.cumsum([len(p) for p, _ in scans])
+        return pts, off, np.array([t for _, t in scans])
+
+    a = [L.synth_scan(L.synth_cfg("HDL-64E", 2), k) for k in range(4)]
+    b = [L.synth_scan(L.synth_cfg("HDL-64E", 5), k) for k in range(4)]
+    g = L.Lego(cfg, max_points=140000, max_batch=4)
+    g.odom_batch(*pack(a))
+    g.reset()
+    got = bytes(g.odom_batch(*pack(b)))
+    g.close()
+    f = L.Lego(cfg, max_points=140000, max_batch=4)
+    want = bytes(f.odom_batch(*pack(b)))
+    f.close()
+    assert [got[64 * k:64 * k + 60] for k in range(4)] == [want[64 * k:64 * k + 60] for k in range(4)]
 
 
 def test_async_batches_equal_sync(L):
