@@ -523,7 +523,7 @@ __device__ __forceinline__ void build_finish(const BuildArgs<Idx>& B, unsigned l
   if (tid == 0) { S.sufFirst[NK] = INT_MAX; Cs.sufFirst[NK] = INT_MAX; }
   block_exscan(cnt, TS + TC, B.wtot);  // corner starts come out offset by nS
   stamp(P_B_SCAN);
-  constexpr int kBuildU = 4;  // points per lane in flight
+  constexpr int kBuildU = 8;  // points per lane in flight
   for (int j = tid; j < n; j += kBuildU * kOdomThreads) {
     float4 pu[kBuildU];
 #pragma unroll
