@@ -383,6 +383,9 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
       const int g = std::atoi(e);
       if (g >= 1 && (long)g * (long)n_streams <= (long)cus) ob.G = g;
     }
+    ob.wg = -1;
+    if (const char* e = std::getenv("LEGO_ODOM_SILENT_WG"); e && S == 1) ob.wg = std::atoi(e);
+    const int copies = ob.wg >= 0 ? 2 : 1;  // exchange copies (OdomBufs::wg)
     const size_t G = S * ob.G;  // private copies over all streams' workgroups
     for (int k = 0; k < 2; ++k) {
       A(ob.cornerLast[k], G * ob.capCorner);
@@ -399,20 +402,29 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
     // exchange block: 16-byte error word, then per stream one slot of 3 x capQ
     // granules per NN round a launch can run (10 per scan)
     ob.roundsCap = 10 * (int)((B1 + S - 1) / S);
-    ob.xbytes = 16 + S * sizeof(unsigned long long) * (size_t)ob.roundsCap * 3 * (size_t)ob.capQ;
+    const size_t xslots = S * (size_t)ob.roundsCap * 3 * (size_t)ob.capQ;
+    ob.xbytes = 16 + copies * sizeof(unsigned long long) * xslots;
     unsigned char* xb = nullptr;
     A(xb, ob.xbytes);
     ob.xblock = xb;
     ob.xerr = (unsigned*)xb;
     ob.xg = (unsigned long long*)(xb + 16);
     ob.capH = ob.capSurf + ob.capCorner;
-    ob.xhBytes = S * sizeof(unsigned long long) * 2 * 3 * (size_t)ob.capH;
+    const size_t hslots = S * 2 * 3 * (size_t)ob.capH;
+    ob.xhBytes = copies * sizeof(unsigned long long) * hslots;
     unsigned char* hb = nullptr;
     A(hb, ob.xhBytes);
     ob.xh = (unsigned long long*)hb;
     if (hipMemset(ob.xh, 0, ob.xhBytes) != hipSuccess) {
       set_err("hipMemset failed for the hand-off exchange");
       return fail(LEGO_E_DEVICE);
+    }
+    {  // header: the error word, then the silent workgroup's copy distances
+      const unsigned hdr[4] = {0u, 0u, copies > 1 ? (unsigned)xslots : 0u, copies > 1 ? (unsigned)hslots : 0u};
+      if (hipMemcpy(xb, hdr, sizeof(hdr), hipMemcpyHostToDevice) != hipSuccess) {
+        set_err("hipMemcpy failed for the exchange header");
+        return fail(LEGO_E_DEVICE);
+      }
     }
   }
   A(ob.sumOut, B * 6);

@@ -105,7 +105,13 @@ struct OdomBufs {
   int G;                  // workgroups per stream
   int S;                  // streams
   int roundsCap;          // exchange slots (NN rounds) per stream and launch
-  int wg;                 // set in the kernel: this workgroup's index within its stream
+  // set in the kernel: this workgroup's index within its stream.  On the
+  // host: -1, or the diagnostic LEGO_ODOM_SILENT_WG of a single-stream
+  // context, a workgroup that uses private copies of both exchanges (placed
+  // after the shared ones, distances in xerr[2], xerr[3]): the others never see
+  // its results and take its share through the steal-on-timeout paths, and it
+  // takes theirs the same way (tests)
+  int wg;
   // exchange: an error word shared by the streams (zeroed per batch), then
   // per stream roundsCap x 3 x capQ granules (zeroed per launch)
   void* xblock;
@@ -117,6 +123,7 @@ struct OdomBufs {
   unsigned long long* xh;
   size_t xhBytes;
   int capH;  // capSurf + capCorner
+
   // per-scan outputs of the batch (workgroup 0)
   float* sumOut;        // [B*6]
   float* curOut;        // [B*6]

@@ -1429,7 +1429,12 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
 // is workgroup i % G of stream i / G.
 __device__ __forceinline__ OdomBufs odom_private(OdomBufs ob) {
   const int s = blockIdx.x / ob.G;
+  const int silent = ob.wg;  // the host's value (OdomBufs::wg)
   ob.wg = blockIdx.x - s * ob.G;
+  if (ob.wg == silent) {
+    ob.xg += ob.xerr[2];
+    ob.xh += ob.xerr[3];
+  }
   const size_t w = blockIdx.x;  // index into the [S x G x] arrays
   ob.st += s;
   ob.xg += (size_t)s * ob.roundsCap * 3 * ob.capQ;
@@ -1813,6 +1818,9 @@ int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int K,
   const size_t bytes = ob.S == 1 ? std::min<size_t>(ob.roundsCap, (size_t)10 * K) * slot
                                  : (size_t)ob.S * ob.roundsCap * slot;
   if (ob.G > 1 && hipMemsetAsync(ob.xg, 0, bytes, s) != hipSuccess) return -1;
+  if (ob.wg >= 0 && ob.G > 1 &&  // the diagnostic silent workgroup's copy (single-stream contexts)
+      hipMemsetAsync((unsigned char*)ob.xblock + 16, 0, ob.xbytes - 16, s) != hipSuccess)
+    return -1;
   // A plain launch: the exchange needs no co-residency (see "exchange").
   k_odom<<<ob.S * ob.G, kOdomThreads, odom_lds_bytes(), s>>>(bb, ob, c, K, prof);
   return hipGetLastError() == hipSuccess ? 0 : -1;
