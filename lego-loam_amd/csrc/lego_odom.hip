@@ -1014,6 +1014,34 @@ struct ScanFeat {
   const float4* lflat; int nLF;
 };
 
+// The degeneracy analysis of iteration 0 (:1336-1357, :1437-1458): Jacobi
+// eigen-decomposition, the eigenvalues < 10 zeroed, matP = V^-1 V2.  Out of
+// line: it runs only when eig_min_above cannot rule degeneracy out, and its
+// unrolled Jacobi would otherwise sit inside the LM loop's instruction stream.
+__device__ __attribute__((noinline)) int degeneracy_cold(const float (&AtA)[3][3], float (&P)[3][3]) {
+  float E[3], V[3][3], V2[3][3], Vi[3][3];
+  cv_eigen_sym3(AtA, E, V);
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b) V2[a][b] = V[a][b];
+  int deg = 0;
+  bool stop = false;
+#pragma unroll
+  for (int i = 2; i >= 0; i--) {
+    if (!stop && E[i] < 10) {
+#pragma unroll
+      for (int j = 0; j < 3; j++) V2[i][j] = 0;
+      deg = 1;
+    } else {
+      stop = true;
+    }
+  }
+  cv_inv3(V, Vi);
+  cv_matmul<3>(Vi, V2, P);
+  return deg;
+}
+
 // Shared tail of calculateTransformationSurf / Corner.  Thread 0 only, all in
 // registers (cv_eigen_sym3 is the index-resolved 3x3 Jacobi).
 __device__ __forceinline__ void solve_step(float (&AtA)[3][3], float (&AtB)[3], int iter, float (&P)[3][3],
@@ -1027,27 +1055,7 @@ __device__ __forceinline__ void solve_step(float (&AtA)[3][3], float (&AtB)[3], 
   if (iter == 0 && eig_min_above(AtA, 10.0)) {
     isDeg = 0;  // P is read only while isDeg is set, and the next iteration 0 rewrites both
   } else if (iter == 0) {
-    float E[3], V[3][3], V2[3][3], Vi[3][3];
-    cv_eigen_sym3(AtA, E, V);
-#pragma unroll
-    for (int a = 0; a < 3; ++a)
-#pragma unroll
-      for (int b = 0; b < 3; ++b) V2[a][b] = V[a][b];
-    int deg = 0;
-    bool stop = false;
-#pragma unroll
-    for (int i = 2; i >= 0; i--) {
-      if (!stop && E[i] < 10) {
-#pragma unroll
-        for (int j = 0; j < 3; j++) V2[i][j] = 0;
-        deg = 1;
-      } else {
-        stop = true;
-      }
-    }
-    isDeg = deg;
-    cv_inv3(V, Vi);
-    cv_matmul<3>(Vi, V2, P);
+    isDeg = degeneracy_cold(AtA, P);
   }
   if (isDeg) {
     float X2[3] = {X[0], X[1], X[2]};
