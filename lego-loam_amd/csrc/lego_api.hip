@@ -370,6 +370,7 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
   const size_t S = n_streams;
   ob.S = n_streams;
   A(ob.st, S);
+  A(ob.stIn, S);
   {
     // workgroups of the odometry launch
     int cus = 0;
@@ -385,6 +386,8 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
     }
     ob.wg = -1;
     if (const char* e = std::getenv("LEGO_ODOM_SILENT_WG"); e && S == 1) ob.wg = std::atoi(e);
+    ob.late = -1;
+    if (const char* e = std::getenv("LEGO_ODOM_LATE_WG"); e && S == 1) ob.late = std::atoi(e);
     const int copies = ob.wg >= 0 ? 2 : 1;  // exchange copies (OdomBufs::wg)
     const size_t G = S * ob.G;  // private copies over all streams' workgroups
     for (int k = 0; k < 2; ++k) {
@@ -547,6 +550,7 @@ static OdomBufs ob_slice(const OdomBufs& a, const DevCfg& c, int c0, int s0, int
   OdomBufs o = a;
   o.S = S;
   o.st += s0;
+  o.stIn += s0;
   const size_t w = (size_t)s0 * a.G, k = (size_t)c0;
   for (int i = 0; i < 2; ++i) {
     o.cornerLast[i] += w * a.capCorner;

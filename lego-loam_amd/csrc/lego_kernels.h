@@ -95,7 +95,11 @@ struct OdomState {
 // same serial chain and split only the NN searches); they and st are [S x]
 // over the streams.  The kernel offsets them.
 struct OdomBufs {
-  OdomState* st;          // [S]
+  OdomState* st;          // [S] the state after the last launch (written by each stream's lead workgroup)
+  // [S] read-only copy of st taken on the odometry stream before each launch:
+  // every workgroup starts from it, so one dispatched after its lead finished
+  // still sees the launch's input state (launch_odom)
+  OdomState* stIn;
   float4* cornerLast[2];  // [G x capCorner] double-buffered: current / stale snapshot
   float4* surfLast[2];    // [G x capSurf]
   NNIndexBufs nC, nS;     // [G x] HBM indexes (sensors too large for LDS)
@@ -112,6 +116,11 @@ struct OdomBufs {
   // its results and take its share through the steal-on-timeout paths, and it
   // takes theirs the same way (tests)
   int wg;
+  // diagnostic LEGO_ODOM_LATE_WG of a single-stream context (-1: none): that
+  // workgroup waits at its start until the lead has written the launch's
+  // final state (xerr[1], zeroed per launch), so it replays the whole chain
+  // from the input state and the published rounds (tests)
+  int late;
   // exchange: an error word shared by the streams (zeroed per batch), then
   // per stream roundsCap x 3 x capQ granules (zeroed per launch)
   void* xblock;

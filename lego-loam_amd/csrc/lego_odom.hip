@@ -1,30 +1,34 @@
 // lego_odom.hip — the two-step LM odometry of featureAssociation on gfx950.
 //
-// One persistent 512-thread workgroup walks the batch's scans in stream order
-// (scan k's problem depends on scan k-1's result through transformCur and the
-// TransformToEnd'ed "last" clouds, featureAssociation.cpp:1759-1815), so the
-// per-scan chain never returns to the host.  Per LM iteration:
-//   every 5th iteration: TransformToStart of every query (:860-883, one lane
-//     each), then one 16-lane group per query finds
+// k_odom walks a batch's scans in stream order (scan k's problem depends on
+// scan k-1's result through transformCur and the TransformToEnd'ed "last"
+// clouds, featureAssociation.cpp:1759-1815), so the per-scan chain never
+// returns to the host.  One launch runs G workgroups of 512 threads per
+// stream (48 for VLP-16, odom_workgroups); each runs the whole serial chain
+// redundantly and they split only the correspondence searches, exchanging the
+// results through tagged granules ("exchange" below).  Per LM iteration:
+//   every 5th iteration: each workgroup searches its slice of the queries,
+//     one wave (kGL = 64 lanes) per query:
 //       - the exact nearest neighbour in the last cloud (replaces KdTreeFLANN,
 //         :1054, :1165; ties -> lower index, FLANN's tie order is traversal
-//         dependent): a 0.5 m hash grid, two shells with provable coverage,
-//         then an exact ring x azimuth bucket search;
+//         dependent): a 0.5 m hash grid with provable coverage, else an
+//         exhaustive pass over the cloud;
 //       - the scan-line neighbours (:1062-1099, :1173-1220, incl. the
 //         loop-bound quirk): the reference's sequential loops visit an index
 //         window bounded by ring breaks; the window is read off per-ring
-//         first/last indices, and the minimum over it is searched in the
-//         ring x azimuth buckets with an angular lower bound, keeping the
-//         (distance, visit order) tie rule of the loops;
+//         first/last tables, keeping the (distance, visit order) tie rule;
+//     then publishes (i1, i2, i3) and reads the other slices' granules;
 //   one lane per query: line / plane residual, weight and Jacobian row
 //     (:1106-1151, :1228-1321);
-//   block reduce: AtA, AtB with double accumulation (cv::gemm's float path);
-//   lane 0: QR solve, iteration-0 eigen degeneracy projection (workspace in
-//     LDS), update, NaN reset, convergence test (:1324-1376, :1425-1477).
+//   reduction of AtA, AtB with double accumulation (DPP row sums, one barrier);
+//   every wave: 3x3 QR solve, iteration-0 eigen degeneracy projection, update,
+//     NaN reset, convergence test (:1324-1376, :1425-1477).
 // Then integrateTransformation (:1697-1725) and publishCloudsLast (ToEnd, swap,
 // index rebuild).  For VLP-16-class sensors the last clouds, both NN indexes,
-// the query transforms and correspondences and the state all live in LDS; the
-// same code runs from HBM buffers for larger sensors.
+// the queries, correspondences and the state all live in LDS; the same code
+// runs from per-workgroup HBM copies for larger sensors.  Every workgroup
+// starts from a read-only copy of the stream state (OdomBufs::stIn) and only
+// the lead workgroup writes the state back.
 #include <climits>
 #include <cstdint>
 #include <type_traits>
@@ -1117,6 +1121,7 @@ __device__ __forceinline__ bool converged3(bool surf, const float (&X)[3]) {
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
 constexpr unsigned long long kStealTicks = 4000;  // 40 us at the 100 MHz wall clock
+constexpr unsigned long long kLateTicks = 200000000;  // 2 s: the diagnostic late workgroup's bound
 __device__ __forceinline__ void x_publish(unsigned long long* p, unsigned long long v) {
   __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1445,6 +1450,7 @@ __device__ __forceinline__ OdomBufs odom_private(OdomBufs ob) {
   }
   const size_t w = blockIdx.x;  // index into the [S x G x] arrays
   ob.st += s;
+  ob.stIn += s;
   ob.xg += (size_t)s * ob.roundsCap * 3 * ob.capQ;
   ob.xh += (size_t)s * 2 * 3 * ob.capH;
   ob.cornerLast[0] += w * ob.capCorner;
@@ -1483,7 +1489,17 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
   const int tid = threadIdx.x;
   static_assert(sizeof(OdomState) <= 128, "OdomState LDS slot");
   OdomState* st = L.st;
-  if (tid < (int)(sizeof(OdomState) / 4)) ((int*)st)[tid] = ((const int*)ob.st)[tid];
+  if (ob.wg == ob.late) {  // diagnostic: start only once the lead has finished
+    if (tid == 0) {
+      const unsigned long long t0 = wall_clock64();
+      while (__hip_atomic_load((gu32*)&ob.xerr[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u &&
+             wall_clock64() - t0 < kLateTicks)
+        __builtin_amdgcn_s_sleep(8);
+    }
+    __syncthreads();
+  }
+  // the launch's input state (never the lead's output: ob.st)
+  if (tid < (int)(sizeof(OdomState) / 4)) ((int*)st)[tid] = ((const int*)ob.stIn)[tid];
   if (tid == 0) L.n[N_ROUND] = 0;
   __syncthreads();
   const bool sensorRes = sensor_resident(c);
@@ -1766,6 +1782,10 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
   }
   __syncthreads();
   if (lead && tid < (int)(sizeof(OdomState) / 4)) ((int*)ob.st)[tid] = ((const int*)st)[tid];
+  if (lead && ob.late >= 0) {  // releases the diagnostic late workgroup
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store((gu32*)&ob.xerr[1], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (gprof && tid < P_NPROF) gprof[tid] += sprof[tid];
 }
 
@@ -1826,6 +1846,10 @@ int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int K,
   const size_t bytes = ob.S == 1 ? std::min<size_t>(ob.roundsCap, (size_t)10 * K) * slot
                                  : (size_t)ob.S * ob.roundsCap * slot;
   if (ob.G > 1 && hipMemsetAsync(ob.xg, 0, bytes, s) != hipSuccess) return -1;
+  // the read-only input state of this launch (see OdomBufs::stIn)
+  if (hipMemcpyAsync(ob.stIn, ob.st, sizeof(OdomState) * ob.S, hipMemcpyDeviceToDevice, s) != hipSuccess)
+    return -1;
+  if (ob.late >= 0 && hipMemsetAsync(ob.xerr + 1, 0, sizeof(unsigned), s) != hipSuccess) return -1;
   if (ob.wg >= 0 && ob.G > 1 &&  // the diagnostic silent workgroup's copy (single-stream contexts)
       hipMemsetAsync((unsigned char*)ob.xblock + 16, 0, ob.xbytes - 16, s) != hipSuccess)
     return -1;

@@ -37,3 +37,34 @@ def test_silent_workgroup_is_stolen(L, sensor, seed, n, cap):
     got = bytes(s.odom_batch(*_pack(scans)))
     s.close()
     assert [got[64 * k:64 * k + 60] for k in range(n)] == [want[64 * k:64 * k + 60] for k in range(n)]
+
+
+@pytest.mark.parametrize("sensor,seed,n,cap", [("VLP-16", 7, 12, 40000), ("HDL-64E", 2, 6, 140000)])
+def test_late_workgroup_reads_input_state(L, sensor, seed, n, cap):
+    """A workgroup dispatched after its stream's lead has finished (and written
+    the launch's final OdomState) must still start from the launch's input
+    state (OdomBufs::stIn): LEGO_ODOM_LATE_WG holds one workgroup until the
+    lead is done.  Three launches, so the late workgroup's private last clouds
+    of launch k feed the NN results it publishes in launch k+1."""
+    cfg = L.sensor_cfg(sensor, L.hip_lib())
+    sc = L.synth_cfg(sensor, seed)
+    scans = [L.synth_scan(sc, k) for k in range(n)]
+    per = n // 3
+
+    def run(ctx):
+        out = b""
+        for b in range(3):
+            out += bytes(ctx.odom_batch(*_pack(scans[b * per:(b + 1) * per])))
+        return [out[64 * k:64 * k + 60] for k in range(n)]
+
+    g = L.Lego(cfg, max_points=cap, max_batch=per)
+    want = run(g)
+    g.close()
+    os.environ["LEGO_ODOM_LATE_WG"] = "5"
+    try:
+        s = L.Lego(cfg, max_points=cap, max_batch=per)
+    finally:
+        os.environ.pop("LEGO_ODOM_LATE_WG", None)
+    got = run(s)
+    s.close()
+    assert got == want
