@@ -333,6 +333,28 @@ int lego_cloud_info_serialize(const lego_cloud_info* info, int32_t n_scan, int32
  * keyframe map of mapOptmization.cpp:1001-1056. */
 int lego_mo_set_map(lego_ctx* ctx, const lego_point_xyzi* corner, int32_t n_corner,
                     const lego_point_xyzi* surf, int32_t n_surf);
+/* Mapping options (mapOptimization's compile-time switches, utility.h:104,130). */
+typedef struct lego_mo_opts {
+  /* 1: an installed fixed map goes through the map VoxelGrids and the NN
+   * index build on every mapping step, as extractSurroundingKeyFrames and
+   * scan2MapOptimization do with the surrounding map (mapOptmization.cpp:
+   * 1058-1064, 1333-1334).  0 (default): filtered and indexed once per
+   * lego_mo_set_map (the filter of an unchanged cloud is the same cloud, so
+   * results are identical). */
+  int32_t fixed_map_per_step;
+  /* loopClosureEnableFlag (utility.h:104, default false).  1: the surrounding
+   * map is the most recent surrounding_keyframe_search_num keyframes
+   * (:961-999) instead of the radius search, every saved keyframe goes into
+   * the context's pose graph, an accepted lego_mo_loop_closure adds its loop
+   * factor, and the next mapping step re-optimises the graph and corrects the
+   * keyframe poses (correctPoses :1456-1478).  Keyframe-built map only. */
+  int32_t loop_closure_enable;
+  int32_t surrounding_keyframe_search_num; /* utility.h:130; <= 0 selects 50 */
+  int32_t _pad;
+} lego_mo_opts;
+/* Sets the options; takes effect at the next lego_mo_process.  Switching
+ * loop_closure_enable needs a context with no saved keyframe (LEGO_E_STATE). */
+int lego_mo_configure(lego_ctx* ctx, const lego_mo_opts* opts);
 int lego_mo_process(lego_ctx* ctx, const lego_fa_out* in, lego_mo_out* out);
 /* performLoopClosure over the keyframes the mapping calls have saved (needs
  * the keyframe-built map, i.e. no lego_mo_set_map); LEGO_E_ARG otherwise. */

@@ -127,6 +127,7 @@ struct lego_ctx {
   // scan-to-map (lego_mo_*): buffers allocated by the first lego_mo_set_map
   MoDev mo{};
   bool moAlloc = false, moFixed = false;
+  lego_mo_opts moOpts{};
   double moTimeLast = -1;
   double moTimeOdom = 0;  // timeLaserOdometry: the last hand-off's stamp (laserOdometryHandler :630)
   LcDev lc{};             // loop closure buffers (first lego_mo_loop_closure)
@@ -1114,12 +1115,29 @@ int lego_mo_set_map(lego_ctx* x, const lego_point_xyzi* corner, int32_t n_corner
   MoDev& m = x->mo;
   HIPCHK(hipMemcpyAsync(m.cornerMap, corner, sizeof(float4) * n_corner, hipMemcpyHostToDevice, x->stream));
   HIPCHK(hipMemcpyAsync(m.surfMap, surf, sizeof(float4) * n_surf, hipMemcpyHostToDevice, x->stream));
+  m.nCornerMap = n_corner;
+  m.nSurfMap = n_surf;
   if (mo_set_map_device(m, n_corner, n_surf, x->stream) != 0) {
     set_err("scan-to-map: map voxel filter / index launch failed");
     return LEGO_E_DEVICE;
   }
   HIPCHK(hipStreamSynchronize(x->stream));
   x->moFixed = true;
+  return LEGO_OK;
+}
+
+int lego_mo_configure(lego_ctx* x, const lego_mo_opts* o) {
+  if (!x || !o) return LEGO_E_ARG;
+  if (x->nStreams != 1) {
+    set_err("mapping needs a single-stream context");
+    return LEGO_E_ARG;
+  }
+  if (o->loop_closure_enable) {
+    set_err("loop_closure_enable is not supported by this build");
+    return LEGO_E_ARG;
+  }
+  x->moOpts = *o;
+  x->mo.mapPerStep = o->fixed_map_per_step ? 1 : 0;
   return LEGO_OK;
 }
 

@@ -78,6 +78,8 @@ struct MoDev {
   // fixed map (config C5) and its voxel-filtered form
   float4 *cornerMap, *surfMap, *cornerMapDS, *surfMapDS;
   int mapCornerCap, mapSurfCap;
+  int nCornerMap, nSurfMap;  // the installed map's raw sizes
+  int mapPerStep;            // lego_mo_opts.fixed_map_per_step: filter + index every step
   MoIndex cornerIx, surfIx;
   // the scan's clouds and their filtered forms
   float4 *cornerLast, *surfLast, *outlierLast;

@@ -25,7 +25,9 @@
 //                    once converged
 //   k_mo_finish      transformUpdate (:463-496)
 // The fixed map (config C5, lego_mo_set_map) is voxel-filtered and indexed once
-// per map: the filter of an unchanged cloud is the same cloud every step.
+// per map: the filter of an unchanged cloud is the same cloud every step.  With
+// lego_mo_opts.fixed_map_per_step it is filtered and indexed on every step, the
+// work the reference does on its surrounding map (like-for-like timing).
 #include <hipcub/hipcub.hpp>
 
 #include <cfloat>
@@ -840,6 +842,8 @@ int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, h
   if (!fixedMap) {  // extractSurroundingKeyFrames :1001-1065
     const int st = kf_map(m, radius, s);
     if (st) return st;
+  } else if (m.mapPerStep) {  // the map VoxelGrids (:1058-1064) and kd-tree builds (:1333-1334) of every step
+    if (mo_set_map_device(m, m.nCornerMap, m.nSurfMap, s)) return -1;
   }
   // downsampleCurrentScan :1067-1091
   if (voxel_grid_device(m.cornerLast, a.nCorner, nullptr, 0.2f, m.cornerDS, &m.cnt->cornerDS, m.vg, s)) return -1;

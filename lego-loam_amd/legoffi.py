@@ -102,6 +102,11 @@ class MoOut(C.Structure):
                 ("n_surf_scan_ds", C.c_int32), ("n_rows_last", C.c_int32)]
 
 
+class MoOpts(C.Structure):  # lego_mo_opts
+    _fields_ = [("fixed_map_per_step", C.c_int32), ("loop_closure_enable", C.c_int32),
+                ("surrounding_keyframe_search_num", C.c_int32), ("_pad", C.c_int32)]
+
+
 class LoopOut(C.Structure):  # lego_loop_out (performLoopClosure)
     _fields_ = [("detected", C.c_int32), ("converged", C.c_int32), ("accepted", C.c_int32),
                 ("latest_id", C.c_int32), ("closest_id", C.c_int32), ("iterations", C.c_int32),
@@ -245,7 +250,7 @@ HIP_EXPORTS = ["lego_sensor_preset", "lego_create", "lego_fleet_create", "lego_d
                "lego_imu_push", "lego_odom_batch_submit", "lego_odom_batch_wait", "lego_batch_fetch", "lego_pc2_decode", "lego_ip_process_pc2",
                "lego_odom_batch_pc2", "lego_pc2_encode_xyzi", "lego_cloud_info_serialize",
                "lego_fusion_odometry", "lego_fusion_aft_mapped",
-               "lego_mo_set_map", "lego_mo_process", "lego_mo_loop_closure", "lego_last_error", "lego_stage_times",
+               "lego_mo_set_map", "lego_mo_configure", "lego_mo_process", "lego_mo_loop_closure", "lego_last_error", "lego_stage_times",
                "lego_odom_profile"]
 
 
@@ -281,6 +286,7 @@ def hip_lib() -> C.CDLL:
     lib.lego_batch_fetch.argtypes = [C.c_void_p, C.c_int32, C.POINTER(IpOut), C.POINTER(FaOut)]
     lib.lego_mo_set_map.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32]
     lib.lego_mo_process.argtypes = [C.c_void_p, C.POINTER(FaOut), C.POINTER(MoOut)]
+    lib.lego_mo_configure.argtypes = [C.c_void_p, C.POINTER(MoOpts)]
     lib.lego_mo_loop_closure.argtypes = [C.c_void_p, C.POINTER(LoopOut)]
     lib.lego_last_error.restype = C.c_char_p
     lib.lego_odom_profile.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
@@ -520,6 +526,12 @@ class Lego:
         surf = np.ascontiguousarray(surf, dtype=XYZI_DTYPE)
         check(self.lib.lego_mo_set_map(self.h, corner.ctypes.data, len(corner), surf.ctypes.data, len(surf)),
               "lego_mo_set_map", self.lib)
+
+    def mo_configure(self, fixed_map_per_step: bool = False, loop_closure: bool = False,
+                     keyframe_search_num: int = 0) -> None:
+        """lego_mo_configure (mapOptimization's switches, utility.h:104,130)."""
+        o = MoOpts(int(fixed_map_per_step), int(loop_closure), int(keyframe_search_num), 0)
+        check(self.lib.lego_mo_configure(self.h, C.byref(o)), "lego_mo_configure", self.lib)
 
     def mo(self) -> dict:
         """Scan-to-map on the last fa() output (mapOptimization::run)."""

@@ -18,6 +18,7 @@ int main(void) {
   S(lego_pose_rec); O(lego_pose_rec, n_segmented); O(lego_pose_rec, flags);
   S(lego_loop_out); O(lego_loop_out, fitness); O(lego_loop_out, icp_transform); O(lego_loop_out, from_rotation);
   O(lego_loop_out, between_translation);
+  S(lego_mo_opts); O(lego_mo_opts, loop_closure_enable); O(lego_mo_opts, surrounding_keyframe_search_num);
   S(lego_synth_cfg); O(lego_synth_cfg, seed);
   return 0;
 }

@@ -48,7 +48,7 @@ def test_struct_layouts_match_ctypes(L, tmp_path):
     m = {"lego_point_xyzir": L.PointXYZIR, "lego_point_xyzi": L.PointXYZI, "lego_sensor_cfg": L.SensorCfg,
          "lego_cloud_info": L.CloudInfo, "lego_ip_out": L.IpOut, "lego_fa_out": L.FaOut,
          "lego_mo_out": L.MoOut, "lego_pose_rec": L.PoseRec, "lego_synth_cfg": L.SynthCfg,
-         "lego_loop_out": L.LoopOut}
+         "lego_loop_out": L.LoopOut, "lego_mo_opts": L.MoOpts}
     for key, val in out.items():
         if "." in key:
             t, f = key.split(".")
