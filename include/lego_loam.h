@@ -198,9 +198,14 @@ typedef struct lego_pose_rec {
   int32_t n_segmented;
   int32_t n_sharp, n_less_sharp, n_flat, n_less_flat;
   int32_t odom_valid;
-  int32_t flags;
+  int32_t flags;   /* LEGO_REC_* bits: which paths this scan took (diagnostic) */
   int32_t _pad;
 } lego_pose_rec;
+/* lego_pose_rec.flags */
+#define LEGO_REC_RING0_REDONE 2  /* ring 0 re-extracted with the stream's real carry (SURVEY.md §9.7 residue) */
+#define LEGO_REC_SORT_TIES 4     /* a sector had equal curvatures: sorted by the std::sort restatement
+                                    (featureAssociation.cpp:699), not the bitonic network */
+#define LEGO_REC_ODOM_HBM 8      /* the LM ran on HBM-resident last clouds (LDS caps exceeded) */
 
 typedef struct lego_ctx lego_ctx;
 

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "lego_loam.h"
 #include "lego_numerics.h"
 
 namespace lego {

@@ -470,6 +470,7 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
     if (__ballot(tie)) {
       // equal curvatures: their relative order is std::sort's
       if (lane == 0) {
+        atomicOr(&bb.fa_flags[b], LEGO_REC_SORT_TIES);  // the record shows the fallback ran
         for (int t = 0; t < n; ++t) {
           const int pos = sp + t;
           a[t] = (phantom_here && pos == 4) ? SmoothEntry{0.0f, kPhantom} : SmoothEntry{L.curv[pos - R.lo], pos};
@@ -746,7 +747,7 @@ __global__ void __launch_bounds__(kExtractThreads) k_fa_fixup(BatchBufs bb, DevC
       __syncthreads();
     } else {
       extract_ring(bb, c, b, 0, &cs, L);
-      if (threadIdx.x == 0) bb.fa_flags[b] |= 2;  // ring 0 recomputed with the real carry
+      if (threadIdx.x == 0) atomicOr(&bb.fa_flags[b], LEGO_REC_RING0_REDONE);  // ring 0 recomputed with the real carry
     }
     if (bb.imu && threadIdx.x == 0) {  // the IMU members in stream order (:568-612, 1641-1651)
       ImuScan& o = bb.imuScan[b];

@@ -1752,6 +1752,8 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
       st->cornerLastNum = F.nLS;
       st->surfLastNum = F.nLF;
       st->curBuf = nbuf;
+      // the record's flag: this scan's LM ran on HBM-resident last clouds
+      if (lead && !init && !st->resident) bb.fa_flags[b] |= LEGO_REC_ODOM_HBM;
       st->resident = fits ? 1 : 0;
       if (hx) st->seq = seq;
       if (rebuild) { st->snapBuf = nbuf; st->nnCornerNum = F.nLS; st->nnSurfNum = F.nLF; }
