@@ -234,6 +234,8 @@ def oracle_lib() -> C.CDLL:
     lib.lego_oracle_imu_push.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
     lib.lego_oracle_fusion_odometry.argtypes = [C.c_void_p, C.POINTER(FaOut), C.POINTER(FusionOut)]
     lib.lego_oracle_fusion_aft_mapped.argtypes = [C.c_void_p, C.POINTER(MoOut)]
+    lib.lego_oracle_log_systems.argtypes = [C.c_void_p, C.c_int32]
+    lib.lego_oracle_systems.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.POINTER(C.c_int32)]
     lib.lego_oracle_voxel_grid.argtypes = [C.c_void_p, C.c_int32, C.c_float, C.c_int32,
                                            C.c_void_p, C.POINTER(C.c_int32)]
     for fn in ("atan2f",):
@@ -447,6 +449,20 @@ class Oracle:
         out = LoopOut()
         check(self.lib.lego_oracle_mo_loop_closure(self.h, C.byref(out)), "oracle_mo_loop_closure")
         return loop_to_dict(out)
+
+    def log_systems(self, enable: bool = True) -> None:
+        """Records the dense systems the OpenCV-shaped solvers receive."""
+        check(self.lib.lego_oracle_log_systems(self.h, int(enable)), "oracle_log_systems")
+
+    SYSTEM_WIDTH = {0: 12, 1: 42, 2: 15, 3: 9}  # odometry AtA|AtB, mapping AtA|AtB, plane A0, corner cov
+
+    def systems(self, kind: int) -> np.ndarray:
+        """The logged systems of `kind`, one row each (see SYSTEM_WIDTH)."""
+        n = C.c_int32()
+        check(self.lib.lego_oracle_systems(self.h, kind, None, 0, C.byref(n)), "oracle_systems")
+        out = np.zeros(n.value, np.float32)
+        check(self.lib.lego_oracle_systems(self.h, kind, out.ctypes.data, n.value, C.byref(n)), "oracle_systems")
+        return out.reshape(-1, self.SYSTEM_WIDTH[kind])
 
     def mo(self) -> dict:
         out = MoOut()

@@ -428,10 +428,28 @@ struct ByValue {                                       // utility.h:144-148
   bool operator()(Smooth const& l, Smooth const& r) const { return l.value < r.value; }
 };
 
+// Diagnostic log of the dense systems handed to the OpenCV-shaped solvers, so
+// tests/test_numerics_witness.py can re-solve the real LM systems of a stream
+// with an independent restatement.  Kinds: 0 odometry AtA|AtB (3x3 + 3),
+// 1 mapping AtA|AtB (6x6 + 6), 2 mapping plane fit A0 (5x3, rhs -1),
+// 3 mapping corner covariance (3x3).  Off unless enabled; capped per kind.
+struct SysLog {
+  bool on = false;
+  int cap = 4096;  // systems per kind
+  std::vector<float> v[4];
+  int n[4] = {0, 0, 0, 0};
+  void add(int kind, const float* a, int len) {
+    if (!on || n[kind] >= cap) return;
+    v[kind].insert(v[kind].end(), a, a + len);
+    ++n[kind];
+  }
+};
+
 struct FeatureAssociation {
   lego_sensor_cfg c;
   int N, H, P;
   bool pcl_sort = false;
+  SysLog* log = nullptr;
   // persistent member arrays (:210-223); zero-initialised
   std::vector<float> cloudCurvature;
   std::vector<int> cloudNeighborPicked, cloudLabel;
@@ -1076,6 +1094,12 @@ struct FeatureAssociation {
 
   // the shared tail of calculateTransformationSurf/Corner (:1324-1356, :1425-1457)
   void solve3(float AtA[3][3], float AtB[3], int iter, float X[3]) {
+    if (log) {
+      float rec[12];
+      std::memcpy(rec, AtA, 9 * sizeof(float));
+      std::memcpy(rec + 9, AtB, 3 * sizeof(float));
+      log->add(0, rec, 12);
+    }
     float Acopy[3][3];
     std::memcpy(Acopy, AtA, sizeof(Acopy));
     lego::cv_solve_qr<3, 3>(Acopy, *reinterpret_cast<float(*)[3]>(AtB), *reinterpret_cast<float(*)[3]>(X));
@@ -1317,6 +1341,7 @@ struct lego_oracle {
   std::unique_ptr<oracle::MapOptimization> mo;
   oracle::TransformFusionNode fusion;
   double ip_stamp = 0;
+  oracle::SysLog log;
 };
 
 extern "C" int lego_oracle_sensor_preset(const char* name, lego_sensor_cfg* out) {
@@ -1332,6 +1357,8 @@ extern "C" int lego_oracle_create(const lego_sensor_cfg* cfg, lego_oracle** out)
   o->ip.reset(new oracle::ImageProjection(*cfg));
   o->fa.reset(new oracle::FeatureAssociation(*cfg));
   o->mo.reset(new oracle::MapOptimization(*cfg));
+  o->fa->log = &o->log;
+  o->mo->log = &o->log;
   *out = o;
   return LEGO_OK;
 }
@@ -1487,6 +1514,21 @@ extern "C" int lego_oracle_mo_process(lego_oracle* o, const lego_fa_out* in, leg
   out->n_corner_scan_ds = (int32_t)mo.cornerLastDS.size();
   out->n_surf_scan_ds = (int32_t)mo.surfTotalLastDS.size();
   out->n_rows_last = mo.rowsLast;
+  return LEGO_OK;
+}
+
+extern "C" int lego_oracle_log_systems(lego_oracle* o, int32_t enable) {
+  if (!o) return LEGO_E_ARG;
+  o->log = oracle::SysLog{};
+  o->log.on = enable != 0;
+  return LEGO_OK;
+}
+
+extern "C" int lego_oracle_systems(lego_oracle* o, int32_t kind, float* out, int32_t cap, int32_t* n) {
+  if (!o || !n || kind < 0 || kind > 3) return LEGO_E_ARG;
+  const auto& v = o->log.v[kind];
+  *n = (int32_t)v.size();
+  if (out) std::memcpy(out, v.data(), sizeof(float) * std::min<size_t>(v.size(), (size_t)std::max(cap, 0)));
   return LEGO_OK;
 }
 

@@ -39,6 +39,14 @@ int lego_oracle_imu_push(lego_oracle* o, const lego_imu_msg* msgs, int32_t n);
 /* LM statistics: scans, surf iterations, corner iterations, NN rounds, rows. */
 int lego_oracle_stats(lego_oracle* o, long* out5);
 
+/* Diagnostic: record the dense systems handed to the OpenCV-shaped solvers
+ * (kind 0: odometry AtA|AtB 12 floats; 1: mapping AtA|AtB 42; 2: mapping
+ * plane-fit A0 15; 3: mapping corner covariance 9), up to 4096 per kind.
+ * enable resets the log.  lego_oracle_systems copies up to cap floats of a
+ * kind and reports the total in *n. */
+int lego_oracle_log_systems(lego_oracle* o, int32_t enable);
+int lego_oracle_systems(lego_oracle* o, int32_t kind, float* out, int32_t cap, int32_t* n);
+
 /* Stand-alone pieces for known-answer tests. */
 int lego_oracle_voxel_grid(const lego_point_xyzi* in, int32_t n, float leaf,
                            int32_t pcl_sort, lego_point_xyzi* out, int32_t* n_out);
