@@ -120,9 +120,18 @@ typedef struct lego_ip_out {
   const float* range_image;              /* rangeMat  [P] */
   const int8_t* ground_image;            /* groundMat [P] */
   const int32_t* label_image;            /* labelMat  [P] */
+  /* the topics the reference publishes only with a subscriber
+   * (imageProjection.cpp:480-506); NULL / 0 unless LEGO_IP_GATED is set.
+   * Node-shaped calls (lego_ip_process, lego_ip_process_pc2) only. */
+  const lego_point_xyzi* full_info_cloud;      /* /full_cloud_info [P]: intensity = range (:252-254) */
+  const lego_point_xyzi* ground_cloud;         /* /ground_cloud: groundMat == 1, rows <= groundScanInd (:301-308) */
+  int32_t n_ground;
+  const lego_point_xyzi* segmented_cloud_pure; /* /segmented_cloud_pure: labels, intensity = label (:357-367) */
+  int32_t n_segmented_pure;
 } lego_ip_out;
 
-#define LEGO_IP_IMAGES 1u
+#define LEGO_IP_IMAGES 1u /* full_cloud and the range / ground / label images */
+#define LEGO_IP_GATED 2u  /* full_info_cloud, ground_cloud, segmented_cloud_pure */
 
 typedef struct lego_fa_out {
   double stamp;

@@ -99,6 +99,8 @@ struct lego_ctx {
   std::vector<double> stamps;
   // host staging (library-owned outputs)
   std::vector<lego_point_xyzi> h_seg, h_outl, h_full, h_sharp, h_lsharp, h_flat, h_lflat;
+  GatedBufs gb{};  // LEGO_IP_GATED outputs (first use)
+  std::vector<lego_point_xyzi> h_info, h_gcloud, h_pure;
   std::vector<lego_point_xyzi> h_cornerLast, h_surfLast, h_outlLast;
   std::vector<int32_t> h_sri, h_eri, h_label, h_bad;
   std::vector<uint8_t> h_gflag;
@@ -618,7 +620,7 @@ static int stage_inputs(lego_ctx* x, const lego_point_xyzir* pts, const int64_t*
 
 // Image projection only (lego_ip_process*): slot 0, synchronous.
 static int run_ip(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offsets, int B, int on_device,
-                  int want_labels) {
+                  int want_labels, bool gated = false) {
   if (x->inflight) {
     set_err("node-shaped call while batches are in flight (lego_odom_batch_wait first)");
     return LEGO_E_STATE;
@@ -627,8 +629,20 @@ static int run_ip(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offse
   int st = stage_inputs(x, pts, offsets, B, on_device, bb);
   if (st != LEGO_OK) return st;
   HIPCHK(hipMemsetAsync(bb.bad, 0, sizeof(int) * B, x->stream));
+  if (gated && !x->gb.n) {
+    const size_t P = x->dc.P;
+#define MA(ptr, n) \
+  if (x->alloc(&(ptr), (size_t)(n)) != hipSuccess) { set_err("hipMalloc failed for %s", #ptr); return LEGO_E_DEVICE; }
+    MA(x->gb.info, P); MA(x->gb.ground, P); MA(x->gb.pure, P); MA(x->gb.n, 2);
+#undef MA
+    x->h_info.resize(P); x->h_gcloud.resize(P); x->h_pure.resize(P);
+  }
   x->tm.begin();
-  launch_ip(bb, x->dc, B, want_labels, x->stream, &x->tm);
+  launch_ip(bb, x->dc, B, want_labels || gated ? 1 : 0, x->stream, &x->tm);
+  if (gated) {
+    x->tm.mark("ip.gated", x->stream);
+    launch_gated(bb, x->dc, x->gb, x->stream);
+  }
   x->tm.end(x->stream);
   HIPCHK(hipGetLastError());
   x->h_bad.resize(B);
@@ -755,7 +769,7 @@ static int wait_batch(lego_ctx* x, lego_pose_rec* recs, int cap, int* nOut) {
 }
 
 // copy scan k's image-projection outputs of the last batch into host staging
-static int fetch_ip(lego_ctx* x, int k, bool images, lego_ip_out* o) {
+static int fetch_ip(lego_ctx* x, int k, bool images, lego_ip_out* o, bool gated = false) {
   const DevCfg& c = x->dc;
   const size_t P = c.P, N = c.N;
   int ns = 0, nout = 0;
@@ -772,6 +786,14 @@ static int fetch_ip(lego_ctx* x, int k, bool images, lego_ip_out* o) {
   HIPCHK(hipMemcpyAsync(x->h_col.data(), x->bb.col + k * P, sizeof(uint32_t) * ns, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(x->h_range.data(), x->bb.srange + k * P, sizeof(float) * ns, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(x->h_outl.data(), x->bb.outl + k * P, sizeof(float4) * nout, hipMemcpyDeviceToHost, s));
+  int ng[2] = {0, 0};
+  if (gated) {  // scan 0 of a node-shaped call
+    HIPCHK(hipMemcpyAsync(ng, x->gb.n, sizeof(ng), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(x->h_info.data(), x->gb.info, sizeof(float4) * P, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipMemcpyAsync(x->h_gcloud.data(), x->gb.ground, sizeof(float4) * ng[0], hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(x->h_pure.data(), x->gb.pure, sizeof(float4) * ng[1], hipMemcpyDeviceToHost, s));
+  }
   if (images) {
     HIPCHK(hipMemcpyAsync(x->h_full.data(), x->bb.full + k * P, sizeof(float4) * P, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(x->h_rimg.data(), x->bb.range + k * P, sizeof(float) * P, hipMemcpyDeviceToHost, s));
@@ -799,6 +821,13 @@ static int fetch_ip(lego_ctx* x, int k, bool images, lego_ip_out* o) {
     o->range_image = x->h_rimg.data();
     o->ground_image = x->h_gimg.data();
     o->label_image = x->h_label.data();
+  }
+  if (gated) {
+    o->full_info_cloud = x->h_info.data();
+    o->ground_cloud = x->h_gcloud.data();
+    o->n_ground = ng[0];
+    o->segmented_cloud_pure = x->h_pure.data();
+    o->n_segmented_pure = ng[1];
   }
   return LEGO_OK;
 }
@@ -857,9 +886,10 @@ int lego_ip_process(lego_ctx* x, const lego_point_xyzir* pts, int32_t n, double 
       return LEGO_E_NOT_DENSE;
   int64_t off[2] = {0, n};
   x->stamps.assign(1, stamp);
-  int st = run_ip(x, pts, off, 1, 0, (flags & LEGO_IP_IMAGES) ? 1 : 0);
+  const bool gated = (flags & LEGO_IP_GATED) != 0;
+  int st = run_ip(x, pts, off, 1, 0, (flags & LEGO_IP_IMAGES) ? 1 : 0, gated);
   if (st != LEGO_OK) return st;
-  st = fetch_ip(x, 0, (flags & LEGO_IP_IMAGES) != 0, out);
+  st = fetch_ip(x, 0, (flags & LEGO_IP_IMAGES) != 0, out, gated);
   if (st != LEGO_OK) return st;
   x->lastIp = *out;
   x->lastIpDevice = true;
@@ -1081,7 +1111,8 @@ static int mo_alloc_keyframes(lego_ctx* x) {
   int st = mo_alloc(x, fromCap, fromCap);
   if (st != LEGO_OK) return st;
   MoKeyframes& kf = m.kf;
-  const int kcap = 16384, acap = 16 << 20;
+  int kcap = 16384, acap = 16 << 20;
+  if (const char* e = std::getenv("LEGO_KF_CAP")) kcap = std::max(1, std::min(kcap, std::atoi(e)));  // diagnostic
 #define MA(ptr, n) \
   if (x->alloc(&(ptr), (size_t)(n)) != hipSuccess) { set_err("hipMalloc failed for %s", #ptr); return LEGO_E_DEVICE; }
   MA(kf.pos3, kcap); MA(kf.pose6, kcap * 6); MA(kf.time, kcap); MA(kf.seg, kcap * 6); MA(kf.arena, acap);
@@ -1171,7 +1202,7 @@ int lego_mo_loop_closure(lego_ctx* x, lego_loop_out* out) {
   }
   LcState hs;
   const int rs = mo_loop_closure_device(m, lc, x->moTimeOdom, &hs, x->stream);
-  if (rs == -2) {
+  if (rs == MO_E_MAP_CAP) {
     set_err("loop closure: clouds larger than the loop buffers");
     return LEGO_E_CAPACITY;
   }
@@ -1249,19 +1280,34 @@ int lego_mo_process(lego_ctx* x, const lego_fa_out* in, lego_mo_out* out) {
   a.imuOn = x->moImu.at(in->stamp, x->cfg.scan_period, &a.imuRoll, &a.imuPitch, &moFront) ? 1 : 0;
   if (!a.imuOn) a.imuRoll = a.imuPitch = 0.f;
   const int rs = mo_step_device(m, a, x->moFixed, x->cfg.surrounding_keyframe_search_radius, s);
-  if (rs == -2) {
-    set_err("scan-to-map: keyframe store full");
-    return LEGO_E_CAPACITY;
-  }
-  if (rs != 0) {
-    set_err("scan-to-map launch failed");
-    return LEGO_E_DEVICE;
+  switch (rs) {
+    case MO_OK: break;
+    case MO_E_STORE_FULL:  // sticky: the stream's keyframe history is incomplete from here on
+      set_err("scan-to-map: the keyframe store is full (%d keyframes / %d arena points); lego_reset to go on",
+              m.kf.kcap, m.kf.acap);
+      return LEGO_E_CAPACITY;
+    case MO_E_RADIUS_HITS:  // this step only; nothing of it ran
+      set_err("scan-to-map: more than 8192 key poses within surroundingKeyframeSearchRadius");
+      return LEGO_E_CAPACITY;
+    case MO_E_MAP_CAP:  // this step only; nothing of it ran
+      set_err("scan-to-map: the surrounding map exceeds %d points", m.fromMapCap);
+      return LEGO_E_CAPACITY;
+    default:
+      set_err("scan-to-map launch failed");
+      return LEGO_E_DEVICE;
   }
   MoState hs;
   MoCounts hc;
+  int ovf = 0;
   HIPCHK(hipMemcpyAsync(&hs, m.st, sizeof(hs), hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(&hc, m.cnt, sizeof(hc), hipMemcpyDeviceToHost, s));
+  if (!x->moFixed) HIPCHK(hipMemcpyAsync(&ovf, m.kf.meta + KF_OVF, sizeof(int), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  if (ovf) {  // saveKeyFramesAndFactor of this very step found the store full (k_kf_save)
+    set_err("scan-to-map: the keyframe store is full (%d keyframes / %d arena points): this step's keyframe "
+            "was not saved; lego_reset to go on", m.kf.kcap, m.kf.acap);
+    return LEGO_E_CAPACITY;
+  }
   if (hs.optimized) x->moImu.front = moFront;  // transformUpdate ran (:1345)
   out->processed = 1;
   out->optimized = hs.optimized;
@@ -1357,9 +1403,10 @@ int lego_ip_process_pc2(lego_ctx* x, const lego_pc2_msg* msg, uint32_t flags, le
   int st = pc2_stage(x, msg, 1, false, off);
   if (st != LEGO_OK) return st;
   x->stamps.assign(1, msg->stamp);
-  st = run_ip(x, x->d_pts, x->d_off, 1, 1, (flags & LEGO_IP_IMAGES) ? 1 : 0);
+  const bool gated = (flags & LEGO_IP_GATED) != 0;
+  st = run_ip(x, x->d_pts, x->d_off, 1, 1, (flags & LEGO_IP_IMAGES) ? 1 : 0, gated);
   if (st != LEGO_OK) return st;
-  st = fetch_ip(x, 0, (flags & LEGO_IP_IMAGES) != 0, out);
+  st = fetch_ip(x, 0, (flags & LEGO_IP_IMAGES) != 0, out, gated);
   if (st != LEGO_OK) return st;
   x->lastIp = *out;
   x->lastIpDevice = true;

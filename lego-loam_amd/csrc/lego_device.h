@@ -83,6 +83,15 @@ struct FaCarry {
 };
 
 // Batch-wide device pointers (filled by the host, passed by value).
+// The gated imageProjection topics of one scan (lego_ip_process with
+// LEGO_IP_GATED), allocated on first use.
+struct GatedBufs {
+  float4* info;    // [P] /full_cloud_info
+  float4* ground;  // [P] /ground_cloud
+  float4* pure;    // [P] /segmented_cloud_pure
+  int* n;          // [2] ground, pure counts
+};
+
 struct BatchBufs {
   int B;
   const ImuSnap* imu;        // [B] or null: no IMU message delivered to this batch's stream(s)

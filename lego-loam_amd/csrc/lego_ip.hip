@@ -292,6 +292,45 @@ __global__ void __launch_bounds__(1024) k_compact(BatchBufs bb, DevCfg c, int wa
   }
 }
 
+// The gated topics of publishCloud (imageProjection.cpp:480-506) for scan 0 of
+// the batch, one 1024-thread workgroup walking the image row-major:
+// /full_cloud_info (the full cloud with intensity = range, :252-254), the
+// ground cloud (groundMat == 1 in rows <= groundScanInd, :301-308) and the
+// pure segmented cloud (labels > 0 and != 999999, intensity = label,
+// :357-367).  Needs the final label image (k_compact with want_labels).
+__global__ void __launch_bounds__(1024) k_gated(BatchBufs bb, DevCfg c, GatedBufs gb) {
+  __shared__ int lds[64];
+  int ng = 0, np = 0;
+  for (int t0 = 0; t0 < c.P; t0 += blockDim.x) {
+    const int p = t0 + threadIdx.x;
+    bool gnd = false, pure = false;
+    int L = 0;
+    float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p < c.P) {
+      f = bb.full[p];
+      const float r = bb.range[p];
+      gb.info[p] = r == FLT_MAX ? f : make_float4(f.x, f.y, f.z, r);
+      L = bb.label[p];
+      gnd = p / c.H <= c.g && bb.ground[p] == 1;
+      pure = L > 0 && L != 999999;
+    }
+    Scan3 in{{gnd ? 1 : 0, pure ? 1 : 0, 0}}, tot;
+    const Scan3 ex = block_scan3(in, &tot, lds);
+    if (gnd) gb.ground[ng + ex.v[0]] = f;
+    if (pure) gb.pure[np + ex.v[1]] = make_float4(f.x, f.y, f.z, (float)L);
+    ng += tot.v[0];
+    np += tot.v[1];
+  }
+  if (threadIdx.x == 0) {
+    gb.n[0] = ng;
+    gb.n[1] = np;
+  }
+}
+
+void launch_gated(const BatchBufs& bb, const DevCfg& c, const GatedBufs& gb, hipStream_t s) {
+  k_gated<<<1, 1024, 0, s>>>(bb, c, gb);
+}
+
 void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hipStream_t s,
                StageTimer* tm) {
   const int P = c.P;

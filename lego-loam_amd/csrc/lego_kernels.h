@@ -143,6 +143,7 @@ struct OdomBufs {
   int capLS;
 };
 
+void launch_gated(const BatchBufs& bb, const DevCfg& c, const GatedBufs& gb, hipStream_t s);
 void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hipStream_t s,
                StageTimer* tm);
 // B = S x K scans, stream-major (scans [s*K, s*K + K) are stream s's, in

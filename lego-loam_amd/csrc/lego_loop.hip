@@ -349,7 +349,7 @@ int mo_loop_closure_device(MoDev& m, LcDev& lc, double tnow, LcState* hostState,
   if (hipMemcpyAsync(hostState, lc.st, sizeof(LcState), hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
   if (hipStreamSynchronize(s) != hipSuccess) return -1;
   if (!hostState->detected) return 0;
-  if (hostState->nSrcRaw > lc.cap || hostState->nTgtRaw > lc.cap || hostState->nTgtRaw > m.vg.cap) return -2;
+  if (hostState->nSrcRaw > lc.cap || hostState->nTgtRaw > lc.cap || hostState->nTgtRaw > m.vg.cap) return MO_E_MAP_CAP;
   k_lc_gather<<<hostState->nPlan, 256, 0, s>>>(m.kf, lc.st, lc.srcRaw, lc.tgtRaw);
   k_lc_compact<<<1, 1024, 0, s>>>(lc.srcRaw, lc.st, lc.src, lc.cur);
   if (voxel_grid_device(lc.tgtRaw, hostState->nTgtRaw, nullptr, 0.4f, lc.tgt, &lc.st->nTgt, m.vg, s)) return -1;

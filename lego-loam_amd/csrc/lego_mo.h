@@ -64,12 +64,15 @@ struct MoKeyframes {
   float4* sur;       // [kcap] surrounding key poses (radius hits, distance order)
   float4* surDS;     // [kcap] their 1 m voxel filter
   unsigned long long* sortKeys;  // [kcap] (distance bits, index) of the hits
-  int* meta;         // [kKfMeta] K, arenaTop, nEx, nSur, nSurDS, nCornerFromMap, nSurfFromMap, overflow, saved
+  int* meta;         // [kKfMeta] K, arenaTop, nEx, nSur, nSurDS, nCornerFromMap, nSurfFromMap, store full
+                     // (sticky), saved this step, radius hits over the sort capacity (this step)
   float* robot;      // previousRobotPos xyz, currentRobotPos xyz
   int kcap, acap;
 };
 enum { KF_K = 0, KF_TOP = 1, KF_NEX = 2, KF_NSUR = 3, KF_NSURDS = 4, KF_NCM = 5, KF_NSM = 6, KF_OVF = 7,
-       kKfMeta = 16 };
+       KF_SAVED = 8, KF_HITOVF = 9, kKfMeta = 16 };
+// mo_step_device / mo_loop_closure_device status codes
+enum { MO_OK = 0, MO_E_LAUNCH = -1, MO_E_STORE_FULL = -2, MO_E_RADIUS_HITS = -3, MO_E_MAP_CAP = -4 };
 
 struct MoDev {
   MoState* st;
@@ -130,11 +133,15 @@ int voxel_grid_device(const float4* in, int n, const int* nDev, float leaf, floa
 int mo_set_map_device(MoDev& m, int nCornerMap, int nSurfMap, hipStream_t s);
 int index_build_device(const float4* pts, int n, const int* nDev, MoIndex& ix, const VgScratch& v, hipStream_t s);
 // One performLoopClosure over the keyframe store (tnow = timeLaserOdometry).
-// Returns 0 (hostState holds the result), -1 on a launch failure, -2 when the
-// clouds exceed the loop buffers.
+// Returns MO_OK (hostState holds the result), MO_E_LAUNCH, or MO_E_MAP_CAP when
+// the clouds exceed the loop buffers.
 int mo_loop_closure_device(MoDev& m, LcDev& lc, double tnow, LcState* hostState, hipStream_t s);
 // One mapping step.  fixedMap: the installed map; otherwise the keyframe map.
-// Returns 0, -1 on a launch failure, -2 when the keyframe store is full.
+// Returns MO_OK, MO_E_LAUNCH, MO_E_STORE_FULL (an earlier step could not save
+// its keyframe), MO_E_RADIUS_HITS (more key poses within the search radius
+// than the sort holds) or MO_E_MAP_CAP (the surrounding map exceeds its
+// buffers), the last three before anything of the step ran.  That a keyframe
+// of THIS step did not fit is reported through meta[KF_OVF] after the step.
 int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, hipStream_t s);
 
 }  // namespace lego

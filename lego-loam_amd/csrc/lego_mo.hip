@@ -670,7 +670,7 @@ __global__ void __launch_bounds__(1024) k_kf_select(MoKeyframes kf, float radius
   __shared__ int nHit;
   const int tid = threadIdx.x;
   const int K = kf.meta[KF_K];
-  if (tid == 0) nHit = 0;
+  if (tid == 0) { nHit = 0; kf.meta[KF_HITOVF] = 0; }
   __syncthreads();
   const float cx = kf.robot[3], cy = kf.robot[4], cz = kf.robot[5];
   const double r = (double)radius;
@@ -705,7 +705,7 @@ __global__ void __launch_bounds__(1024) k_kf_select(MoKeyframes kf, float radius
   for (int i = tid; i < n; i += blockDim.x) kf.sur[i] = kf.pos3[(int)(keys[i] & 0xffffffffu)];
   if (tid == 0) {
     kf.meta[KF_NSUR] = n;
-    if (nHit > kKfSortCap) kf.meta[KF_OVF] = 1;
+    if (nHit > kKfSortCap) kf.meta[KF_HITOVF] = 1;  // the step is refused (MO_E_RADIUS_HITS)
   }
 }
 
@@ -779,7 +779,7 @@ __global__ void k_kf_save(MoKeyframes kf, MoState* st, const MoCounts* cnt, doub
   const float dx = prev[0] - cur[0], dy = prev[1] - cur[1], dz = prev[2] - cur[2];
   const bool save = !(__builtin_sqrtf(dx * dx + dy * dy + dz * dz) < 0.3f);
   const int K = kf.meta[KF_K];
-  kf.meta[KF_OVF + 1] = 0;  // no copy unless saved
+  kf.meta[KF_SAVED] = 0;  // no copy unless saved
   if (!save && K > 0) return;
   const int top = kf.meta[KF_TOP];
   const int nc = cnt->cornerDS, ns = cnt->surfDS, no = cnt->outlierDS;
@@ -801,10 +801,10 @@ __global__ void k_kf_save(MoKeyframes kf, MoState* st, const MoCounts* cnt, doub
   sg[0] = top; sg[1] = nc; sg[2] = top + nc; sg[3] = ns; sg[4] = top + nc + ns; sg[5] = no;
   kf.meta[KF_TOP] = top + nc + ns + no;
   kf.meta[KF_K] = K + 1;
-  kf.meta[KF_OVF + 1] = 1;
+  kf.meta[KF_SAVED] = 1;
 }
 __global__ void k_kf_copy(MoKeyframes kf, const float4* cornerDS, const float4* surfDS, const float4* outlierDS) {
-  if (!kf.meta[KF_OVF + 1]) return;
+  if (!kf.meta[KF_SAVED]) return;
   const int* sg = kf.seg + 6 * (kf.meta[KF_K] - 1);
   for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < sg[1] + sg[3] + sg[5]; j += gridDim.x * blockDim.x) {
     float4 p;
@@ -825,7 +825,9 @@ static int kf_map(MoDev& m, float radius, hipStream_t s) {
   int meta[kKfMeta];
   if (hipMemcpyAsync(meta, kf.meta, sizeof(meta), hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
   if (hipStreamSynchronize(s) != hipSuccess) return -1;
-  if (meta[KF_OVF] || meta[KF_NCM] > m.fromMapCap || meta[KF_NSM] > m.fromMapCap) return -2;
+  if (meta[KF_OVF]) return MO_E_STORE_FULL;
+  if (meta[KF_HITOVF]) return MO_E_RADIUS_HITS;
+  if (meta[KF_NCM] > m.fromMapCap || meta[KF_NSM] > m.fromMapCap) return MO_E_MAP_CAP;
   if (meta[KF_NEX] > 0) k_kf_gather<<<meta[KF_NEX], 256, 0, s>>>(kf, m.cornerFromMap, m.surfFromMap);
   if (voxel_grid_device(m.cornerFromMap, meta[KF_NCM], nullptr, 0.2f, m.cornerMapDS, &m.cnt->cornerMapDS, m.vg, s))
     return -1;

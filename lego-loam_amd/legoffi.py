@@ -29,6 +29,7 @@ ORACLE_LIB = REPO / "oracle" / "build" / "liblego_oracle.so"
 
 LEGO_OK, LEGO_E_NOT_DENSE, LEGO_E_CAPACITY, LEGO_E_DEVICE, LEGO_E_ARG, LEGO_E_STATE = range(6)
 LEGO_IP_IMAGES = 1
+LEGO_IP_GATED = 2
 
 f32p = C.POINTER(C.c_float)
 
@@ -77,7 +78,10 @@ class IpOut(C.Structure):
                 ("n_segmented", C.c_int32), ("outlier_cloud", C.POINTER(PointXYZI)),
                 ("n_outlier", C.c_int32), ("full_cloud", C.POINTER(PointXYZI)),
                 ("range_image", f32p), ("ground_image", C.POINTER(C.c_int8)),
-                ("label_image", C.POINTER(C.c_int32))]
+                ("label_image", C.POINTER(C.c_int32)),
+                ("full_info_cloud", C.POINTER(PointXYZI)), ("ground_cloud", C.POINTER(PointXYZI)),
+                ("n_ground", C.c_int32), ("segmented_cloud_pure", C.POINTER(PointXYZI)),
+                ("n_segmented_pure", C.c_int32)]
 
 
 class FaOut(C.Structure):
@@ -384,6 +388,10 @@ def ip_to_dict(o: IpOut, cfg: SensorCfg, images: bool = False) -> dict:
         d["ground_image"] = _arr(o.ground_image, P, np.int8)
         d["label_image"] = _arr(o.label_image, P, np.int32)
         d["full_cloud"] = _arr(o.full_cloud, P, XYZI_DTYPE)
+    if o.full_info_cloud:  # LEGO_IP_GATED
+        d["full_info_cloud"] = _arr(o.full_info_cloud, P, XYZI_DTYPE)
+        d["ground_cloud"] = _arr(o.ground_cloud, o.n_ground, XYZI_DTYPE)
+        d["segmented_cloud_pure"] = _arr(o.segmented_cloud_pure, o.n_segmented_pure, XYZI_DTYPE)
     return d
 
 
@@ -423,10 +431,10 @@ class Oracle:
             self.lib.lego_oracle_destroy(self.h)
             self.h = None
 
-    def ip(self, pts: np.ndarray, stamp: float, images: bool = False) -> dict:
+    def ip(self, pts: np.ndarray, stamp: float, images: bool = False, gated: bool = False) -> dict:
         pts = np.ascontiguousarray(pts, dtype=XYZIR_DTYPE)
-        check(self.lib.lego_oracle_ip_process(self.h, pts.ctypes.data, len(pts), stamp,
-                                              LEGO_IP_IMAGES if images else 0, C.byref(self._ip)),
+        flags = (LEGO_IP_IMAGES if images else 0) | (LEGO_IP_GATED if gated else 0)
+        check(self.lib.lego_oracle_ip_process(self.h, pts.ctypes.data, len(pts), stamp, flags, C.byref(self._ip)),
               "oracle_ip")
         return ip_to_dict(self._ip, self.cfg, images)
 
@@ -525,10 +533,10 @@ class Lego:
     def reset(self):
         check(self.lib.lego_reset(self.h), "lego_reset", self.lib)
 
-    def ip(self, pts: np.ndarray, stamp: float, images: bool = False) -> dict:
+    def ip(self, pts: np.ndarray, stamp: float, images: bool = False, gated: bool = False) -> dict:
         pts = np.ascontiguousarray(pts, dtype=XYZIR_DTYPE)
-        check(self.lib.lego_ip_process(self.h, pts.ctypes.data, len(pts), stamp,
-                                       LEGO_IP_IMAGES if images else 0, C.byref(self._ip)),
+        flags = (LEGO_IP_IMAGES if images else 0) | (LEGO_IP_GATED if gated else 0)
+        check(self.lib.lego_ip_process(self.h, pts.ctypes.data, len(pts), stamp, flags, C.byref(self._ip)),
               "lego_ip_process", self.lib)
         return ip_to_dict(self._ip, self.cfg, images)
 

@@ -403,7 +403,7 @@ struct ImageProjection {
         }
   }
 
-  int process(const lego_point_xyzir* in, int n, bool images) {
+  int process(const lego_point_xyzir* in, int n, bool images, bool gated = false) {
     if (n <= 0 || !in) return LEGO_E_ARG;
     for (int i = 0; i < n; ++i)
       if (!std::isfinite(in[i].x) || !std::isfinite(in[i].y) || !std::isfinite(in[i].z))
@@ -411,8 +411,8 @@ struct ImageProjection {
     reset();
     findStartEndAngle(in, n);
     project(in, n);
-    groundRemoval(images);
-    cloudSegmentation(images);
+    groundRemoval(gated);
+    cloudSegmentation(gated);
     return LEGO_OK;
   }
 };
@@ -1379,7 +1379,7 @@ extern "C" int lego_oracle_ip_process(lego_oracle* o, const lego_point_xyzir* pt
                                       double stamp, uint32_t flags, lego_ip_out* out) {
   if (!o || !out) return LEGO_E_ARG;
   auto& ip = *o->ip;
-  int st = ip.process(pts, n, (flags & LEGO_IP_IMAGES) != 0);
+  int st = ip.process(pts, n, (flags & LEGO_IP_IMAGES) != 0, (flags & LEGO_IP_GATED) != 0);
   if (st != LEGO_OK) return st;
   std::memset(out, 0, sizeof(*out));
   out->info.stamp = stamp;
@@ -1400,6 +1400,13 @@ extern "C" int lego_oracle_ip_process(lego_oracle* o, const lego_point_xyzir* pt
     out->range_image = ip.rangeMat.data();
     out->ground_image = ip.groundMat.data();
     out->label_image = ip.labelMat.data();
+  }
+  if (flags & LEGO_IP_GATED) {  // publishCloud :480-506
+    out->full_info_cloud = ip.fullInfoCloud.data();
+    out->ground_cloud = ip.groundCloud.data();
+    out->n_ground = (int32_t)ip.groundCloud.size();
+    out->segmented_cloud_pure = ip.segmentedCloudPure.data();
+    out->n_segmented_pure = (int32_t)ip.segmentedCloudPure.size();
   }
   return LEGO_OK;
 }

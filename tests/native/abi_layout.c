@@ -12,6 +12,7 @@ int main(void) {
   S(lego_sensor_cfg); O(lego_sensor_cfg, mapping_process_interval); O(lego_sensor_cfg, skip_frame_num);
   S(lego_cloud_info); O(lego_cloud_info, segmented_cloud_range);
   S(lego_ip_out); O(lego_ip_out, n_segmented); O(lego_ip_out, label_image);
+  O(lego_ip_out, full_info_cloud); O(lego_ip_out, n_ground); O(lego_ip_out, n_segmented_pure);
   S(lego_fa_out); O(lego_fa_out, odom_valid); O(lego_fa_out, odom_quat); O(lego_fa_out, publish_to_mapping);
   O(lego_fa_out, n_outlier_last);
   S(lego_mo_out); O(lego_mo_out, transform_bef_mapped); O(lego_mo_out, n_rows_last);

@@ -47,6 +47,25 @@ def test_ip_parity(L, sensor, seed, extra):
     gpu.close()
 
 
+@pytest.mark.parametrize("sensor,seed", [("VLP-16", 0), ("HDL-64E", 2), ("VLS-128", 3)])
+def test_gated_topics_parity(L, sensor, seed):
+    """LEGO_IP_GATED: /full_cloud_info, /ground_cloud and /segmented_cloud_pure
+    (imageProjection.cpp:480-506) byte for byte against the oracle, with the
+    regular outputs unchanged."""
+    sc = L.synth_cfg(sensor, seed)
+    pts, stamp = L.synth_scan(sc, 0)
+    gpu = L.Lego(L.sensor_cfg(sensor, L.hip_lib()), max_points=len(pts) + 16)
+    ora = L.Oracle(L.sensor_cfg(sensor))
+    g = gpu.ip(pts, stamp, gated=True)
+    o = ora.ip(pts, stamp, gated=True)
+    assert_ip_equal(g, o, images=False)
+    for k in ("full_info_cloud", "ground_cloud", "segmented_cloud_pure"):
+        assert g[k].shape == o[k].shape, (k, g[k].shape, o[k].shape)
+        assert np.array_equal(bits(g[k]), bits(o[k])), k
+    assert "full_info_cloud" not in gpu.ip(pts, stamp)  # not materialised unless asked
+    gpu.close()
+
+
 @pytest.mark.parametrize("sensor,seed,nscans", [("VLP-16", 1, 12), ("HDL-64E", 2, 3)])
 def test_stream_parity_node_api(L, sensor, seed, nscans):
     """ip -> fa per scan through the node-shaped calls; features bit-exact,
@@ -253,6 +272,48 @@ def test_scan_to_map_keyframe_parity(L):
     print(f"keyframe scan-to-map: {steps} steps, {optimized} optimized, worst |dpose| = {worst:.3g}")
     assert steps >= 5 and optimized >= 3
     gpu.close()
+
+
+def test_keyframe_store_full_is_reported(L):
+    """The keyframe store's capacity (LEGO_KF_CAP shrinks it, diagnostic):
+    the step whose keyframe does not fit returns LEGO_E_CAPACITY itself (not
+    a later one), every later step does too (the history is incomplete), and
+    lego_reset recovers the context: the stream then matches a fresh one."""
+    import os
+
+    sc = L.synth_cfg("VLP-16", 6)
+    scans = [L.synth_scan(sc, k) for k in range(30)]
+    os.environ["LEGO_KF_CAP"] = "3"
+    try:
+        gpu = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=40000)
+        saved_ok, failed_at, msgs = 0, None, []
+        for k, (pts, stamp) in enumerate(scans):
+            gpu.ip(pts, stamp)
+            gpu.fa()
+            try:
+                saved_ok += gpu.mo()["processed"]
+            except RuntimeError as e:
+                msgs.append(str(e))
+                if failed_at is None:
+                    failed_at = k
+        assert failed_at is not None and "keyframe store is full" in msgs[0], msgs[:1]
+        assert "was not saved" in msgs[0] and len(msgs) >= 2, msgs  # reported at its own step, then sticky
+        assert f"status {L.LEGO_E_CAPACITY}" in msgs[0]
+        gpu.reset()
+        got = []
+        for pts, stamp in scans[:10]:
+            gpu.ip(pts, stamp)
+            gpu.fa()
+            got.append(gpu.mo()["transform_aft_mapped"])
+        gpu.close()
+    finally:
+        os.environ.pop("LEGO_KF_CAP", None)
+    fresh = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=40000)
+    for (pts, stamp), g in zip(scans[:10], got):
+        fresh.ip(pts, stamp)
+        fresh.fa()
+        assert np.array_equal(fresh.mo()["transform_aft_mapped"], g)
+    fresh.close()
 
 
 def test_concurrent_streams_identical(L):

@@ -309,3 +309,28 @@ def test_oracle_loop_closure_on_a_circle(L):
     for key in ("from_rotation", "to_rotation", "between_rotation"):
         R = o[key].reshape(3, 3)
         assert np.allclose(R @ R.T, np.eye(3), atol=1e-6) and abs(np.linalg.det(R) - 1) < 1e-6, key
+
+
+def test_gated_topics_follow_the_images(L):
+    """publishCloud's gated topics (imageProjection.cpp:480-506) restated from
+    the images they are cut from: /full_cloud_info is the full cloud with
+    intensity = range where a point was written (:252-254, else the NaN point
+    with intensity -1), /ground_cloud the full-cloud points with groundMat == 1
+    in rows <= groundScanInd in row-major order (:301-308), and
+    /segmented_cloud_pure the points with a valid label, intensity = label
+    (:357-367)."""
+    sc = L.synth_cfg("VLP-16", 0)
+    pts, stamp = L.synth_scan(sc, 0)
+    o = L.Oracle(L.sensor_cfg("VLP-16")).ip(pts, stamp, images=True, gated=True)
+    full, rng, gnd, lab = o["full_cloud"], o["range_image"], o["ground_image"], o["label_image"]
+    written = rng != np.finfo(np.float32).max
+    info = full.copy()
+    info["intensity"][written] = rng[written]
+    assert np.array_equal(o["full_info_cloud"].view(np.uint8), info.view(np.uint8))
+    rows = np.arange(N * H) // H
+    assert np.array_equal(o["ground_cloud"].view(np.uint8), full[(gnd == 1) & (rows <= G)].view(np.uint8))
+    sel = (lab > 0) & (lab != 999999)
+    pure = full[sel].copy()
+    pure["intensity"] = lab[sel].astype(np.float32)
+    assert np.array_equal(o["segmented_cloud_pure"].view(np.uint8), pure.view(np.uint8))
+    assert len(o["ground_cloud"]) > 100 and len(o["segmented_cloud_pure"]) > 100
