@@ -11,8 +11,10 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <array>
 #include <atomic>
 #include <cstring>
+#include <deque>
 #include <new>
 #include <string>
 #include <vector>
@@ -23,6 +25,7 @@
 #include "lego_kernels.h"
 #include "lego_mo.h"
 #include "lego_loam.h"
+#include "lego_pgo_host.h"
 #include "lego_wire.h"
 
 using namespace lego;
@@ -133,6 +136,20 @@ struct lego_ctx {
   double moTimeLast = -1;
   double moTimeOdom = 0;  // timeLaserOdometry: the last hand-off's stamp (laserOdometryHandler :630)
   LcDev lc{};             // loop closure buffers (first lego_mo_loop_closure)
+  // loop-closure mode (lego_mo_opts.loop_closure_enable): the pose graph, the
+  // recent-keyframe queue (key + the pose it was transformed with) and host
+  // mirrors of the saved keyframes' poses and arena segments
+  struct RecentKf {
+    int key;
+    std::array<float, 6> pose;
+  };
+  PoseGraph pg;
+  std::deque<RecentKf> recent;
+  int latestFrameID = 0;  // mapOptmization.cpp:373
+  bool aLoopIsClosed = false;
+  float transformLast[6] = {0, 0, 0, 0, 0, 0};
+  std::vector<std::array<float, 6>> kfPose;  // x y z roll pitch yaw (cloudKeyPoses6D)
+  std::vector<std::array<int, 6>> kfSeg;
   std::vector<std::string> tnames;
   std::vector<float> tms;
 
@@ -219,6 +236,13 @@ static int ctx_reset(lego_ctx* x) {
   }
   x->moTimeLast = -1;
   x->moTimeOdom = 0;
+  x->pg.clear();
+  x->recent.clear();
+  x->latestFrameID = 0;
+  x->aLoopIsClosed = false;
+  std::memset(x->transformLast, 0, sizeof(x->transformLast));
+  x->kfPose.clear();
+  x->kfSeg.clear();
   return LEGO_OK;
 }
 
@@ -1116,7 +1140,7 @@ static int mo_alloc_keyframes(lego_ctx* x) {
 #define MA(ptr, n) \
   if (x->alloc(&(ptr), (size_t)(n)) != hipSuccess) { set_err("hipMalloc failed for %s", #ptr); return LEGO_E_DEVICE; }
   MA(kf.pos3, kcap); MA(kf.pose6, kcap * 6); MA(kf.time, kcap); MA(kf.seg, kcap * 6); MA(kf.arena, acap);
-  MA(kf.exID, kcap); MA(kf.plan, kcap * 4); MA(kf.sur, kcap); MA(kf.surDS, kcap); MA(kf.sortKeys, kcap);
+  MA(kf.exID, kcap); MA(kf.plan, kcap * 4); MA(kf.planPose, kcap * 6); MA(kf.sur, kcap); MA(kf.surDS, kcap); MA(kf.sortKeys, kcap);
   MA(kf.meta, kKfMeta); MA(kf.robot, 8);
   MA(m.cornerFromMap, fromCap); MA(m.surfFromMap, fromCap);
 #undef MA
@@ -1163,9 +1187,14 @@ int lego_mo_configure(lego_ctx* x, const lego_mo_opts* o) {
     set_err("mapping needs a single-stream context");
     return LEGO_E_ARG;
   }
-  if (o->loop_closure_enable) {
-    set_err("loop_closure_enable is not supported by this build");
-    return LEGO_E_ARG;
+  if ((o->loop_closure_enable != 0) != (x->moOpts.loop_closure_enable != 0) && x->mo.kf.kcap) {
+    int K = 0;
+    HIPCHK(hipSetDevice(x->device));
+    HIPCHK(hipMemcpy(&K, x->mo.kf.meta + KF_K, sizeof(int), hipMemcpyDeviceToHost));
+    if (K > 0) {
+      set_err("loop_closure_enable changes the keyframe bookkeeping: lego_reset first");
+      return LEGO_E_STATE;
+    }
   }
   x->moOpts = *o;
   x->mo.mapPerStep = o->fixed_map_per_step ? 1 : 0;
@@ -1233,7 +1262,138 @@ int lego_mo_loop_closure(lego_ctx* x, lego_loop_out* out) {
     std::memcpy(out->to_translation, f.toT, sizeof(f.toT));
     std::memcpy(out->between_rotation, f.betweenR, sizeof(f.betweenR));
     std::memcpy(out->between_translation, f.betweenT, sizeof(f.betweenT));
+    if (x->moOpts.loop_closure_enable) {  // gtSAMgraph.add + isam->update (:930-944)
+      const double noise = (double)(float)hs.fitness;  // float noiseScore (:931)
+      const double var[6] = {noise, noise, noise, noise, noise, noise};
+      Pose3d z;
+      std::memcpy(z.R, f.betweenR, sizeof(z.R));
+      std::memcpy(z.t, f.betweenT, sizeof(z.t));
+      x->pg.add_between(hs.latest, hs.closest, z, var, true);
+      x->aLoopIsClosed = true;
+    }
   }
+  return LEGO_OK;
+}
+
+// loopClosureEnableFlag's extractSurroundingKeyFrames (mapOptmization.cpp:
+// 961-999): the queue of the most recent keyframes, each with the pose its
+// clouds were transformed with, and the gather plan of the map it makes
+// (corner clouds, then surf + outlier per key), uploaded on the stream.
+static int lc_recent_plan(lego_ctx* x, MoStepArgs& a) {
+  const int K = (int)x->kfPose.size();
+  const int num = x->moOpts.surrounding_keyframe_search_num > 0 ? x->moOpts.surrounding_keyframe_search_num : 50;
+  a.nPlan = a.nCM = a.nSM = 0;
+  if (K == 0) return LEGO_OK;  // cloudKeyPoses3D empty: no map (:958-959)
+  auto& q = x->recent;
+  if ((int)q.size() < num) {  // not full: rebuilt from the newest keys (:963-977)
+    q.clear();
+    for (int i = K - 1; i >= 0; --i) {
+      q.push_front({i, x->kfPose[i]});
+      if ((int)q.size() >= num) break;
+    }
+  } else if (x->latestFrameID != K - 1) {  // full: the oldest out, the newest in (:978-991)
+    q.pop_front();
+    x->latestFrameID = K - 1;
+    q.push_back({K - 1, x->kfPose[K - 1]});
+  }
+  const int n = (int)q.size();
+  std::vector<int> plan((size_t)n * 4);
+  std::vector<float> pose((size_t)n * 6);
+  int oc = 0, os = 0;
+  for (int i = 0; i < n; ++i) {
+    const int key = q[i].key;
+    plan[4 * i] = key;
+    plan[4 * i + 1] = oc;
+    plan[4 * i + 2] = os;
+    plan[4 * i + 3] = 0;
+    std::memcpy(&pose[6 * i], q[i].pose.data(), sizeof(float) * 6);
+    oc += x->kfSeg[key][1];
+    os += x->kfSeg[key][3] + x->kfSeg[key][5];
+  }
+  MoKeyframes& kf = x->mo.kf;
+  HIPCHK(hipMemcpyAsync(kf.plan, plan.data(), sizeof(int) * plan.size(), hipMemcpyHostToDevice, x->stream));
+  HIPCHK(hipMemcpyAsync(kf.planPose, pose.data(), sizeof(float) * pose.size(), hipMemcpyHostToDevice, x->stream));
+  HIPCHK(hipStreamSynchronize(x->stream));  // the host vectors go out of scope
+  a.nPlan = n;
+  a.nCM = oc;
+  a.nSM = os;
+  return LEGO_OK;
+}
+
+static std::array<float, 6> t6_of_pose6(const std::array<float, 6>& p) {  // x y z r p y -> transform order
+  return {p[3], p[4], p[5], p[0], p[1], p[2]};
+}
+
+// Writes keyframe i's pose (transform order r p y x y z) to the device store
+// (cloudKeyPoses3D / 6D) and the host mirror.
+static int lc_put_key(lego_ctx* x, int i, const float (&t)[6]) {
+  MoKeyframes& kf = x->mo.kf;
+  const std::array<float, 6> p6 = {t[3], t[4], t[5], t[0], t[1], t[2]};
+  const float4 p3 = make_float4(t[3], t[4], t[5], (float)i);
+  x->kfPose[i] = p6;
+  HIPCHK(hipMemcpyAsync(kf.pose6 + 6 * i, p6.data(), sizeof(float) * 6, hipMemcpyHostToDevice, x->stream));
+  HIPCHK(hipMemcpyAsync(kf.pos3 + i, &p3, sizeof(float4), hipMemcpyHostToDevice, x->stream));
+  HIPCHK(hipStreamSynchronize(x->stream));
+  return LEGO_OK;
+}
+
+// saveKeyFramesAndFactor's graph part and correctPoses (:1372-1438, 1456-1478)
+// after the device saved (or not) this step's keyframe; hs is updated to what
+// the reference publishes.
+static int lc_after_step(lego_ctx* x, MoState& hs, int saved, int K) {
+  MoDev& m = x->mo;
+  if (saved) {
+    std::array<float, 6> p6;
+    std::array<int, 6> sg;
+    HIPCHK(hipMemcpyAsync(p6.data(), m.kf.pose6 + 6 * (K - 1), sizeof(float) * 6, hipMemcpyDeviceToHost, x->stream));
+    HIPCHK(hipMemcpyAsync(sg.data(), m.kf.seg + 6 * (K - 1), sizeof(int) * 6, hipMemcpyDeviceToHost, x->stream));
+    HIPCHK(hipStreamSynchronize(x->stream));
+    x->kfPose.push_back(p6);
+    x->kfSeg.push_back(sg);
+    const double(&var)[6] = pgo_odometry_variances();
+    if (K == 1) {
+      float t[6];
+      for (int i = 0; i < 6; ++i) t[i] = hs.transformTobeMapped[i];
+      x->pg.add_prior(pose_from_transform(t), var);
+      x->pg.insert(pose_from_transform(t));
+      std::memcpy(x->transformLast, t, sizeof(t));
+    } else {
+      float aft[6];
+      for (int i = 0; i < 6; ++i) aft[i] = hs.transformAftMapped[i];
+      x->pg.add_between(K - 2, K - 1, pose_between(pose_from_transform(x->transformLast), pose_from_transform(aft)),
+                        var);
+      x->pg.insert(pose_from_transform(aft));
+    }
+    if (x->pg.loops > 0) {  // otherwise the estimate is the chain the device already stored
+      x->pg.optimize();
+      float t[6];
+      transform_from_pose(x->pg.est[K - 1], t);
+      int st = lc_put_key(x, K - 1, t);
+      if (st != LEGO_OK) return st;
+      if (K > 1) {  // transformAftMapped = transformTobeMapped = transformLast = latestEstimate
+        for (int i = 0; i < 6; ++i) hs.transformAftMapped[i] = hs.transformTobeMapped[i] = t[i];
+        HIPCHK(hipMemcpyAsync((char*)m.st + offsetof(MoState, transformAftMapped), t, sizeof(t),
+                              hipMemcpyHostToDevice, x->stream));
+        HIPCHK(hipMemcpyAsync((char*)m.st + offsetof(MoState, transformTobeMapped), t, sizeof(t),
+                              hipMemcpyHostToDevice, x->stream));
+        HIPCHK(hipStreamSynchronize(x->stream));  // t is a stack array
+        std::memcpy(x->transformLast, t, sizeof(t));
+      }
+    } else if (K > 1) {
+      for (int i = 0; i < 6; ++i) x->transformLast[i] = hs.transformAftMapped[i];
+    }
+  }
+  if (x->aLoopIsClosed) {  // correctPoses: the estimate of the last save, every key
+    x->recent.clear();
+    for (int i = 0; i < (int)x->pg.est.size(); ++i) {
+      float t[6];
+      transform_from_pose(x->pg.est[i], t);
+      const int st = lc_put_key(x, i, t);
+      if (st != LEGO_OK) return st;
+    }
+    x->aLoopIsClosed = false;
+  }
+  HIPCHK(hipStreamSynchronize(x->stream));
   return LEGO_OK;
 }
 
@@ -1279,6 +1439,11 @@ int lego_mo_process(lego_ctx* x, const lego_fa_out* in, lego_mo_out* out) {
   int moFront = x->moImu.front;
   a.imuOn = x->moImu.at(in->stamp, x->cfg.scan_period, &a.imuRoll, &a.imuPitch, &moFront) ? 1 : 0;
   if (!a.imuOn) a.imuRoll = a.imuPitch = 0.f;
+  const bool lcMode = x->moOpts.loop_closure_enable && !x->moFixed;
+  if (lcMode) {
+    const int st = lc_recent_plan(x, a);
+    if (st != LEGO_OK) return st;
+  }
   const int rs = mo_step_device(m, a, x->moFixed, x->cfg.surrounding_keyframe_search_radius, s);
   switch (rs) {
     case MO_OK: break;
@@ -1298,15 +1463,19 @@ int lego_mo_process(lego_ctx* x, const lego_fa_out* in, lego_mo_out* out) {
   }
   MoState hs;
   MoCounts hc;
-  int ovf = 0;
+  int meta[kKfMeta] = {};
   HIPCHK(hipMemcpyAsync(&hs, m.st, sizeof(hs), hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(&hc, m.cnt, sizeof(hc), hipMemcpyDeviceToHost, s));
-  if (!x->moFixed) HIPCHK(hipMemcpyAsync(&ovf, m.kf.meta + KF_OVF, sizeof(int), hipMemcpyDeviceToHost, s));
+  if (!x->moFixed) HIPCHK(hipMemcpyAsync(meta, m.kf.meta, sizeof(meta), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  if (ovf) {  // saveKeyFramesAndFactor of this very step found the store full (k_kf_save)
+  if (meta[KF_OVF]) {  // saveKeyFramesAndFactor of this very step found the store full (k_kf_save)
     set_err("scan-to-map: the keyframe store is full (%d keyframes / %d arena points): this step's keyframe "
             "was not saved; lego_reset to go on", m.kf.kcap, m.kf.acap);
     return LEGO_E_CAPACITY;
+  }
+  if (lcMode) {
+    const int st = lc_after_step(x, hs, meta[KF_SAVED], meta[KF_K]);
+    if (st != LEGO_OK) return st;
   }
   if (hs.optimized) x->moImu.front = moFront;  // transformUpdate ran (:1345)
   out->processed = 1;

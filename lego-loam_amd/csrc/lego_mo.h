@@ -61,6 +61,7 @@ struct MoKeyframes {
   float4* arena;     // [acap] keyframe clouds
   int* exID;         // [kcap] surroundingExistingKeyPosesID
   int* plan;         // [kcap * 4] per existing key: key, corner offset, surf offset, -
+  float* planPose;   // [kcap * 6] loop-closure mode: the pose each planned key is transformed with
   float4* sur;       // [kcap] surrounding key poses (radius hits, distance order)
   float4* surDS;     // [kcap] their 1 m voxel filter
   unsigned long long* sortKeys;  // [kcap] (distance bits, index) of the hits
@@ -103,6 +104,10 @@ struct MoStepArgs {
   int imuOn;              // transformUpdate's IMU blend (:465-490), roll / pitch from the host queue
   float imuRoll, imuPitch;
   double stamp;           // timeLaserOdometry (the keyframe's time)
+  // loop-closure mode's recent-keyframe map: nPlan >= 0 entries of kf.plan /
+  // kf.planPose (uploaded by the host), nCM / nSM the map clouds' sizes;
+  // nPlan = -1: the radius-search map
+  int nPlan = -1, nCM = 0, nSM = 0;
 };
 
 // Loop closure (lego_loop.hip): the detection result and gather plan, the

@@ -743,12 +743,14 @@ __global__ void k_kf_plan(MoKeyframes kf) {
   kf.meta[KF_NSM] = os;
 }
 
-// transformPointCloud (:529-575) of every existing key's clouds into the map
-// clouds, one workgroup per key: corner, then surf followed by outlier.
-__global__ void k_kf_gather(MoKeyframes kf, float4* cornerFromMap, float4* surfFromMap) {
+// transformPointCloud (:529-575) of every planned key's clouds into the map
+// clouds, one workgroup per key: corner, then surf followed by outlier.  The
+// pose is the key's current one, or (planPose) the one the recent-keyframe
+// queue transformed it with when it was queued (:961-999).
+__global__ void k_kf_gather(MoKeyframes kf, const float* planPose, float4* cornerFromMap, float4* surfFromMap) {
   const int i = blockIdx.x;
   const int key = kf.plan[4 * i + 0], oc = kf.plan[4 * i + 1], os = kf.plan[4 * i + 2];
-  const float* pose = kf.pose6 + 6 * key;
+  const float* pose = planPose ? planPose + 6 * i : kf.pose6 + 6 * key;
   const float ctRoll = lego_cosf(pose[3]), stRoll = lego_sinf(pose[3]);
   const float ctPitch = lego_cosf(pose[4]), stPitch = lego_sinf(pose[4]);
   const float ctYaw = lego_cosf(pose[5]), stYaw = lego_sinf(pose[5]);
@@ -815,6 +817,15 @@ __global__ void k_kf_copy(MoKeyframes kf, const float4* cornerDS, const float4* 
   }
 }
 
+// The surrounding map's VoxelGrids (:1058-1064) and NN indexes.
+static int kf_map_filter(MoDev& m, int nCM, int nSM, hipStream_t s) {
+  if (voxel_grid_device(m.cornerFromMap, nCM, nullptr, 0.2f, m.cornerMapDS, &m.cnt->cornerMapDS, m.vg, s)) return -1;
+  if (voxel_grid_device(m.surfFromMap, nSM, nullptr, 0.4f, m.surfMapDS, &m.cnt->surfMapDS, m.vg, s)) return -1;
+  if (index_build_device(m.cornerMapDS, nCM, &m.cnt->cornerMapDS, m.cornerIx, m.vg, s)) return -1;
+  if (index_build_device(m.surfMapDS, nSM, &m.cnt->surfMapDS, m.surfIx, m.vg, s)) return -1;
+  return 0;
+}
+
 // The surrounding map of the keyframe store, filtered and indexed.
 static int kf_map(MoDev& m, float radius, hipStream_t s) {
   MoKeyframes& kf = m.kf;
@@ -828,20 +839,25 @@ static int kf_map(MoDev& m, float radius, hipStream_t s) {
   if (meta[KF_OVF]) return MO_E_STORE_FULL;
   if (meta[KF_HITOVF]) return MO_E_RADIUS_HITS;
   if (meta[KF_NCM] > m.fromMapCap || meta[KF_NSM] > m.fromMapCap) return MO_E_MAP_CAP;
-  if (meta[KF_NEX] > 0) k_kf_gather<<<meta[KF_NEX], 256, 0, s>>>(kf, m.cornerFromMap, m.surfFromMap);
-  if (voxel_grid_device(m.cornerFromMap, meta[KF_NCM], nullptr, 0.2f, m.cornerMapDS, &m.cnt->cornerMapDS, m.vg, s))
-    return -1;
-  if (voxel_grid_device(m.surfFromMap, meta[KF_NSM], nullptr, 0.4f, m.surfMapDS, &m.cnt->surfMapDS, m.vg, s))
-    return -1;
-  if (index_build_device(m.cornerMapDS, meta[KF_NCM], &m.cnt->cornerMapDS, m.cornerIx, m.vg, s)) return -1;
-  if (index_build_device(m.surfMapDS, meta[KF_NSM], &m.cnt->surfMapDS, m.surfIx, m.vg, s)) return -1;
-  return 0;
+  if (meta[KF_NEX] > 0) k_kf_gather<<<meta[KF_NEX], 256, 0, s>>>(kf, nullptr, m.cornerFromMap, m.surfFromMap);
+  return kf_map_filter(m, meta[KF_NCM], meta[KF_NSM], s);
+}
+
+// The recent-keyframe map of loopClosureEnableFlag (:961-999): the host's
+// queue plan (kf.plan / kf.planPose, uploaded on stream s) of nPlan keys.
+static int kf_map_recent(MoDev& m, const MoStepArgs& a, hipStream_t s) {
+  if (a.nCM > m.fromMapCap || a.nSM > m.fromMapCap) return MO_E_MAP_CAP;
+  if (a.nPlan > 0) k_kf_gather<<<a.nPlan, 256, 0, s>>>(m.kf, m.kf.planPose, m.cornerFromMap, m.surfFromMap);
+  return kf_map_filter(m, a.nCM, a.nSM, s);
 }
 
 int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, hipStream_t s) {
   k_mo_associate<<<1, 64, 0, s>>>(m.st, a.quat[0], a.quat[1], a.quat[2], a.quat[3], a.pos[0], a.pos[1], a.pos[2]);
   if (hipGetLastError() != hipSuccess) return -1;
-  if (!fixedMap) {  // extractSurroundingKeyFrames :1001-1065
+  if (!fixedMap && a.nPlan >= 0) {  // extractSurroundingKeyFrames, loop-closure branch :961-999
+    const int st = kf_map_recent(m, a, s);
+    if (st) return st;
+  } else if (!fixedMap) {  // extractSurroundingKeyFrames :1001-1065
     const int st = kf_map(m, radius, s);
     if (st) return st;
   } else if (m.mapPerStep) {  // the map VoxelGrids (:1058-1064) and kd-tree builds (:1333-1334) of every step

@@ -235,6 +235,7 @@ def oracle_lib() -> C.CDLL:
     lib.lego_oracle_mo_set_map.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32]
     lib.lego_oracle_mo_process.argtypes = [C.c_void_p, C.POINTER(FaOut), C.POINTER(MoOut)]
     lib.lego_oracle_mo_loop_closure.argtypes = [C.c_void_p, C.POINTER(LoopOut)]
+    lib.lego_oracle_mo_configure.argtypes = [C.c_void_p, C.POINTER(MoOpts)]
     lib.lego_oracle_imu_push.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
     lib.lego_oracle_fusion_odometry.argtypes = [C.c_void_p, C.POINTER(FaOut), C.POINTER(FusionOut)]
     lib.lego_oracle_fusion_aft_mapped.argtypes = [C.c_void_p, C.POINTER(MoOut)]
@@ -452,6 +453,11 @@ class Oracle:
     def mo_set_map(self, corner: np.ndarray, surf: np.ndarray) -> None:
         check(self.lib.lego_oracle_mo_set_map(self.h, corner.ctypes.data, len(corner),
                                               surf.ctypes.data, len(surf)), "oracle_mo_set_map")
+
+    def mo_configure(self, fixed_map_per_step: bool = False, loop_closure: bool = False,
+                     keyframe_search_num: int = 0) -> None:
+        o = MoOpts(int(fixed_map_per_step), int(loop_closure), int(keyframe_search_num), 0)
+        check(self.lib.lego_oracle_mo_configure(self.h, C.byref(o)), "oracle_mo_configure")
 
     def loop_closure(self) -> dict:
         out = LoopOut()

@@ -14,12 +14,14 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <limits>
 #include <memory>
 #include <vector>
 
 #include "../lego-loam_amd/csrc/lego_numerics.h"
 #include "../lego-loam_amd/csrc/lego_icp.h"
+#include "../lego-loam_amd/csrc/lego_pgo_host.h"
 
 using lego::lego_atan2f;
 using lego::lego_cosf;
@@ -1494,6 +1496,15 @@ extern "C" int lego_oracle_mo_set_map(lego_oracle* o, const lego_point_xyzi* cor
   mo.fixedCorner.assign(corner, corner + n_corner);
   mo.fixedSurf.assign(surf, surf + n_surf);
   return LEGO_OK;
+}
+
+extern "C" int lego_oracle_mo_configure(lego_oracle* o, const lego_mo_opts* opts) {
+  if (!o || !opts) return LEGO_E_ARG;
+  if ((opts->loop_closure_enable != 0) != o->mo->loopClosureEnable && !o->mo->keyPoses3D.empty())
+    return LEGO_E_STATE;
+  o->mo->loopClosureEnable = opts->loop_closure_enable != 0;
+  o->mo->keyframeSearchNum = opts->surrounding_keyframe_search_num > 0 ? opts->surrounding_keyframe_search_num : 50;
+  return LEGO_OK;  // fixed_map_per_step: the oracle filters the map every step anyway
 }
 
 extern "C" int lego_oracle_mo_loop_closure(lego_oracle* o, lego_loop_out* out) {

@@ -30,6 +30,7 @@ int lego_oracle_mo_set_map(lego_oracle* o, const lego_point_xyzi* corner, int32_
                            const lego_point_xyzi* surf, int32_t n_surf);
 int lego_oracle_mo_process(lego_oracle* o, const lego_fa_out* in, lego_mo_out* out);
 int lego_oracle_mo_loop_closure(lego_oracle* o, lego_loop_out* out);
+int lego_oracle_mo_configure(lego_oracle* o, const lego_mo_opts* opts);
 /* transformFusion's two handlers. */
 int lego_oracle_fusion_odometry(lego_oracle* o, const lego_fa_out* odom, lego_fusion_out* out);
 int lego_oracle_fusion_aft_mapped(lego_oracle* o, const lego_mo_out* mo);
