@@ -390,6 +390,57 @@ int lego_fusion_odometry(lego_ctx* ctx, const lego_fa_out* odom, lego_fusion_out
  * processed lego_mo_out (mapOptmization.cpp:654-679 publishTF). */
 int lego_fusion_aft_mapped(lego_ctx* ctx, const lego_mo_out* mo);
 
+/* ---- featureAssociation's hand-off to the serial mapping consumer
+ * (publishCloudsLast, featureAssociation.cpp:1790-1815) as one packet per
+ * batch, so streams running on other GPUs can be mapped on rank 0.
+ *
+ * Packet (little-endian, 8-byte aligned): a lego_handoff_hdr, nscans
+ * lego_handoff_scan entries, then for every scan with publish_to_mapping set
+ * its /laser_cloud_corner_last, /laser_cloud_surf_last and
+ * /outlier_cloud_last points (lego_point_xyzi, the published forms, the
+ * outliers axis-swapped as adjustOutlierCloud does, :1746-1757) at the entry's
+ * offset, in that order. */
+#define LEGO_HANDOFF_MAGIC 0x4f48474cu /* "LGHO" */
+typedef struct lego_handoff_hdr {
+  uint32_t magic, version; /* LEGO_HANDOFF_MAGIC, 1 */
+  int32_t nscans, npub;    /* scans of the batch, scans published to mapping */
+  uint64_t bytes;          /* the whole packet */
+  uint64_t _pad;
+} lego_handoff_hdr;
+typedef struct lego_handoff_scan {
+  lego_pose_rec rec;       /* the batch record of the scan */
+  float transform_cur[6];
+  int32_t publish_to_mapping;
+  int32_t n_corner_last, n_surf_last, n_outlier_last; /* 0 unless published */
+  uint64_t offset;         /* byte offset of the corner points in the packet */
+  uint64_t _pad[2];
+} lego_handoff_scan;
+/* Packs the last batch lego_odom_batch / lego_odom_batch_wait returned into a
+ * device buffer owned by the context (*packet, *bytes), complete when the
+ * call returns; valid until the next batch call on the context. */
+int lego_handoff_pack(lego_ctx* ctx, const void** packet, uint64_t* bytes);
+/* Host-side view of scan k of a packet in host memory: its record and, in
+ * out, the lego_fa_out lego_mo_process consumes (stamp, transform_sum /
+ * _cur, odom_quat / _pos, publish flag, the three clouds pointing into the
+ * packet; the feature clouds are not part of the hand-off and stay NULL).
+ * Needs no device.  LEGO_E_ARG for a malformed packet or k out of range. */
+int lego_handoff_unpack(const void* packet, uint64_t bytes, int32_t k, lego_pose_rec* rec, lego_fa_out* out);
+
+/* Native collective for the hand-off (RCCL over xGMI): one communicator per
+ * process and GPU, ranks 0..nranks-1 sharing the unique id rank 0 created
+ * (the caller broadcasts the 128 bytes, e.g. over MPI or torch.distributed). */
+typedef struct lego_comm lego_comm;
+int lego_comm_unique_id(uint8_t id[128]);
+int lego_comm_create(const uint8_t id[128], int32_t nranks, int32_t rank, int32_t device, lego_comm** out);
+int lego_comm_destroy(lego_comm* comm);
+/* Collective over all ranks: every rank packs its context's last batch
+ * (lego_handoff_pack) and root receives every rank's packet (ncclGather of
+ * the sizes, then ncclSend / ncclRecv of the packets in one group). */
+int lego_comm_gather_handoff(lego_comm* comm, lego_ctx* ctx, int32_t root);
+/* On root after lego_comm_gather_handoff: rank r's packet in host memory,
+ * valid until the next gather on the communicator. */
+int lego_comm_handoff(lego_comm* comm, int32_t rank, const void** packet, uint64_t* bytes);
+
 /* Last device error string (static storage). */
 const char* lego_last_error(void);
 

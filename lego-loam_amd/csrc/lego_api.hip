@@ -69,6 +69,14 @@ hipError_t dalloc(T** p, size_t n) {
 
 }  // namespace
 
+// for the other translation units of the library (lego_comm.hip)
+void lego_set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
 struct lego_ctx {
   lego_sensor_cfg cfg;
   DevCfg dc;
@@ -103,6 +111,9 @@ struct lego_ctx {
   // host staging (library-owned outputs)
   std::vector<lego_point_xyzi> h_seg, h_outl, h_full, h_sharp, h_lsharp, h_flat, h_lflat;
   GatedBufs gb{};  // LEGO_IP_GATED outputs (first use)
+  uint8_t* d_handoff = nullptr;  // lego_handoff_pack's packet (grown on demand)
+  size_t handoffCap = 0;
+  std::vector<uint8_t> h_handoffHead;
   std::vector<lego_point_xyzi> h_info, h_gcloud, h_pure;
   std::vector<lego_point_xyzi> h_cornerLast, h_surfLast, h_outlLast;
   std::vector<int32_t> h_sri, h_eri, h_label, h_bad;
@@ -112,6 +123,7 @@ struct lego_ctx {
   std::vector<int8_t> h_gimg;
   lego_ip_out lastIp{};
   bool lastIpDevice = false;  // lastIp describes batch slot 0 on device
+  bool lastBatch = false;     // lastB / lastBase describe a waited batch (lego_handoff_pack)
   // /imu_raw: featureAssociation's and mapOptimization's queues (host), the
   // per-scan snapshots of the former for a batch
   // raw PointCloud2 staging (lego_*_pc2): grown on demand
@@ -164,6 +176,7 @@ struct lego_ctx {
     if (stream) (void)hipStreamSynchronize(stream);  // batches still in flight
     if (ostream) (void)hipStreamSynchronize(ostream);
     if (d_raw) (void)hipFree(d_raw);
+    if (d_handoff) (void)hipFree(d_handoff);
     if (h_pack) (void)hipHostFree(h_pack);
     if (h_offp) (void)hipHostFree(h_offp);
     if (h_resetSt) (void)hipHostFree(h_resetSt);
@@ -223,6 +236,7 @@ static int ctx_reset(lego_ctx* x) {
   // carry: it already waits for that batch's extraction (faDone)
   x->lastIpDevice = false;
   x->lastB = 0;
+  x->lastBatch = false;
   x->faImu = FaImuQueue{};
   x->moImu = MoImuQueue{};
   x->fusion = Fusion{};
@@ -650,6 +664,7 @@ static int run_ip(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offse
     return LEGO_E_STATE;
   }
   BatchBufs bb = x->bb;
+  x->lastBatch = false;
   int st = stage_inputs(x, pts, offsets, B, on_device, bb);
   if (st != LEGO_OK) return st;
   HIPCHK(hipMemsetAsync(bb.bad, 0, sizeof(int) * B, x->stream));
@@ -757,6 +772,7 @@ static int wait_batch(lego_ctx* x, lego_pose_rec* recs, int cap, int* nOut) {
     x->tms.push_back((float)cnt[i]);
   }
   x->lastB = 0;
+  x->lastBatch = false;
   if (pk[B].bad) {
     set_err("odometry exchange overflow (more NN rounds than slots)");
     return LEGO_E_DEVICE;
@@ -788,6 +804,7 @@ static int wait_batch(lego_ctx* x, lego_pose_rec* recs, int cap, int* nOut) {
   x->stamps = stamps;
   x->lastB = B;
   x->lastBase = h * x->maxBatch;
+  x->lastBatch = true;
   if (nOut) *nOut = B;
   return LEGO_OK;
 }
@@ -1596,6 +1613,109 @@ int lego_odom_batch_pc2(lego_ctx* x, const lego_pc2_msg* msgs, int32_t nscans, i
   std::vector<double> stamps(nscans);
   for (int k = 0; k < nscans; ++k) stamps[k] = msgs[k].stamp;
   return lego_odom_batch(x, x->d_pts, x->d_off, stamps.data(), nscans, 1, recs);
+}
+
+// ---------------------------------------------------------------- hand-off packet
+int lego_handoff_pack(lego_ctx* x, const void** packet, uint64_t* bytes) {
+  if (!x || !packet || !bytes) return LEGO_E_ARG;
+  const int B = x->lastB;
+  if (B <= 0 || !x->lastBatch) {
+    set_err("lego_handoff_pack: no batch result (lego_odom_batch / lego_odom_batch_wait first)");
+    return LEGO_E_STATE;
+  }
+  HIPCHK(hipSetDevice(x->device));
+  const int slot = x->lastBase / x->maxBatch;
+  const PackedRec* pk = x->h_pack + (size_t)slot * (x->maxBatch + 1);
+  const size_t head = sizeof(lego_handoff_hdr) + sizeof(lego_handoff_scan) * (size_t)B;
+  x->h_handoffHead.assign(head, 0);
+  lego_handoff_hdr* h = reinterpret_cast<lego_handoff_hdr*>(x->h_handoffHead.data());
+  lego_handoff_scan* e = reinterpret_cast<lego_handoff_scan*>(h + 1);
+  uint64_t off = head, npub = 0;
+  for (int k = 0; k < B; ++k) {
+    const PackedRec& p = pk[k];
+    lego_pose_rec& r = e[k].rec;
+    r.stamp = k < (int)x->stamps.size() ? x->stamps[k] : 0.0;
+    for (int i = 0; i < 6; ++i) { r.transform_sum[i] = p.sum[i]; e[k].transform_cur[i] = p.cur[i]; }
+    r.n_segmented = p.ns;
+    r.n_sharp = p.cnt[0]; r.n_less_sharp = p.cnt[1]; r.n_flat = p.cnt[2]; r.n_less_flat = p.cnt[3];
+    r.odom_valid = p.valid;
+    r.flags = p.flags;
+    e[k].publish_to_mapping = p.pub;
+    e[k].offset = off;
+    if (p.pub) {  // publishCloudsLast: less-sharp / less-flat after TransformToEnd, the outliers
+      e[k].n_corner_last = p.cnt[1];
+      e[k].n_surf_last = p.cnt[3];
+      e[k].n_outlier_last = p.nout;
+      off += sizeof(lego_point_xyzi) * (uint64_t)(p.cnt[1] + p.cnt[3] + p.nout);
+      ++npub;
+    }
+  }
+  h->magic = LEGO_HANDOFF_MAGIC;
+  h->version = 1;
+  h->nscans = B;
+  h->npub = (int32_t)npub;
+  h->bytes = off;
+  if (off > x->handoffCap) {
+    if (x->d_handoff) HIPCHK(hipFree(x->d_handoff));
+    x->d_handoff = nullptr;
+    x->handoffCap = 0;
+    HIPCHK(hipMalloc(&x->d_handoff, off));
+    x->handoffCap = off;
+  }
+  hipStream_t s = x->stream;
+  HIPCHK(hipMemcpyAsync(x->d_handoff, x->h_handoffHead.data(), head, hipMemcpyHostToDevice, s));
+  launch_pack_handoff(bb_slice(x->bb, x->dc, x->lastBase, B), ob_slice(x->ob, x->dc, x->lastBase, 0, x->nStreams), B,
+                      x->dc.P, x->d_handoff, s);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));
+  *packet = x->d_handoff;
+  *bytes = off;
+  return LEGO_OK;
+}
+
+int lego_handoff_unpack(const void* packet, uint64_t bytes, int32_t k, lego_pose_rec* rec, lego_fa_out* out) {
+  if (!packet || bytes < sizeof(lego_handoff_hdr)) return LEGO_E_ARG;
+  const uint8_t* base = static_cast<const uint8_t*>(packet);
+  const lego_handoff_hdr* h = reinterpret_cast<const lego_handoff_hdr*>(base);
+  if (h->magic != LEGO_HANDOFF_MAGIC || h->version != 1 || h->bytes != bytes || h->nscans < 0 ||
+      sizeof(lego_handoff_hdr) + sizeof(lego_handoff_scan) * (uint64_t)h->nscans > bytes) {
+    set_err("lego_handoff_unpack: not a version-1 hand-off packet of %llu bytes", (unsigned long long)bytes);
+    return LEGO_E_ARG;
+  }
+  if (k < 0 || k >= h->nscans) return LEGO_E_ARG;
+  const lego_handoff_scan& e = reinterpret_cast<const lego_handoff_scan*>(h + 1)[k];
+  const uint64_t n = (uint64_t)e.n_corner_last + (uint64_t)e.n_surf_last + (uint64_t)e.n_outlier_last;
+  if (e.n_corner_last < 0 || e.n_surf_last < 0 || e.n_outlier_last < 0 || e.offset > bytes ||
+      n * sizeof(lego_point_xyzi) > bytes - e.offset) {
+    set_err("lego_handoff_unpack: scan %d's clouds lie outside the packet", k);
+    return LEGO_E_ARG;
+  }
+  if (rec) *rec = e.rec;
+  if (out) {
+    std::memset(out, 0, sizeof(*out));
+    out->stamp = e.rec.stamp;
+    out->n_sharp = e.rec.n_sharp;
+    out->n_less_sharp = e.rec.n_less_sharp;
+    out->n_flat = e.rec.n_flat;
+    out->n_less_flat = e.rec.n_less_flat;
+    out->odom_valid = e.rec.odom_valid;
+    for (int i = 0; i < 6; ++i) {
+      out->transform_sum[i] = e.rec.transform_sum[i];
+      out->transform_cur[i] = e.transform_cur[i];
+    }
+    odom_quat(e.rec.transform_sum, out->odom_quat, out->odom_pos);  // publishOdometry (:1727-1744)
+    out->publish_to_mapping = e.publish_to_mapping;
+    if (e.publish_to_mapping) {
+      const lego_point_xyzi* p = reinterpret_cast<const lego_point_xyzi*>(base + e.offset);
+      out->corner_last = p;
+      out->n_corner_last = e.n_corner_last;
+      out->surf_last = p + e.n_corner_last;
+      out->n_surf_last = e.n_surf_last;
+      out->outlier_last = p + e.n_corner_last + e.n_surf_last;
+      out->n_outlier_last = e.n_outlier_last;
+    }
+  }
+  return LEGO_OK;
 }
 
 // ---------------------------------------------------------------- transformFusion

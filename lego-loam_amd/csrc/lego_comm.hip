@@ -1,0 +1,174 @@
+// lego_comm.hip — the stream-per-GPU hand-off collective behind
+// the C-ABI: every rank's batch packet (lego_handoff_pack: pose records plus
+// the published corner / surf / outlier "last" clouds of
+// featureAssociation.cpp:1790-1815) gathered to the rank that runs the serial
+// mapping consumer, over RCCL (xGMI between the GPUs of a node).
+//
+// One collective per batch: ncclGather of the 8-byte packet sizes, then one
+// group of ncclSend (every other rank) / ncclRecv (root, one per peer), so
+// each peer's packet travels on its own link.  Root's own packet is a
+// device-to-device copy.  The received packets are copied to pinned host
+// memory for the host-side consumers (lego_handoff_unpack -> lego_mo_process).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "lego_loam.h"
+
+void lego_set_error(const char* fmt, ...);  // lego_api.hip
+
+struct lego_comm {
+  ncclComm_t nc = nullptr;
+  int nranks = 0, rank = 0, device = 0;
+  hipStream_t s = nullptr;
+  uint64_t* dSize = nullptr;   // [1] this rank's packet size
+  uint64_t* dSizes = nullptr;  // [nranks] gathered on root
+  uint8_t* dRecv = nullptr;    // root: every packet, back to back
+  size_t recvCap = 0;
+  uint8_t* hRecv = nullptr;    // pinned copy of dRecv
+  size_t hCap = 0;
+  std::vector<uint64_t> sizes, offs;
+  bool haveResult = false;
+  ~lego_comm() {
+    if (device >= 0) (void)hipSetDevice(device);
+    if (s) (void)hipStreamSynchronize(s);
+    if (nc) (void)ncclCommDestroy(nc);
+    if (dSize) (void)hipFree(dSize);
+    if (dSizes) (void)hipFree(dSizes);
+    if (dRecv) (void)hipFree(dRecv);
+    if (hRecv) (void)hipHostFree(hRecv);
+    if (s) (void)hipStreamDestroy(s);
+  }
+};
+
+#define COMM_HIP(call)                                                      \
+  do {                                                                      \
+    hipError_t e_ = (call);                                                 \
+    if (e_ != hipSuccess) {                                                 \
+      lego_set_error("%s: %s", #call, hipGetErrorString(e_));               \
+      return LEGO_E_DEVICE;                                                 \
+    }                                                                       \
+  } while (0)
+#define COMM_NCCL(call)                                                     \
+  do {                                                                      \
+    ncclResult_t r_ = (call);                                               \
+    if (r_ != ncclSuccess) {                                                \
+      lego_set_error("%s: %s", #call, ncclGetErrorString(r_));              \
+      return LEGO_E_DEVICE;                                                 \
+    }                                                                       \
+  } while (0)
+
+extern "C" {
+
+int lego_comm_unique_id(uint8_t id[128]) {
+  if (!id) return LEGO_E_ARG;
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+  ncclUniqueId u;
+  COMM_NCCL(ncclGetUniqueId(&u));
+  std::memcpy(id, &u, sizeof(u));
+  return LEGO_OK;
+}
+
+int lego_comm_create(const uint8_t id[128], int32_t nranks, int32_t rank, int32_t device, lego_comm** out) {
+  if (!id || !out || nranks <= 0 || rank < 0 || rank >= nranks || device < 0) return LEGO_E_ARG;
+  *out = nullptr;
+  lego_comm* c = new lego_comm;
+  c->nranks = nranks;
+  c->rank = rank;
+  c->device = device;
+  auto fail = [&](int st) {
+    delete c;
+    return st;
+  };
+  if (hipSetDevice(device) != hipSuccess) {
+    lego_set_error("lego_comm_create: no HIP device %d", device);
+    return fail(LEGO_E_DEVICE);
+  }
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u));
+  ncclResult_t r = ncclCommInitRank(&c->nc, nranks, u, rank);
+  if (r != ncclSuccess) {
+    c->nc = nullptr;
+    lego_set_error("ncclCommInitRank: %s", ncclGetErrorString(r));
+    return fail(LEGO_E_DEVICE);
+  }
+  if (hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&c->dSize, sizeof(uint64_t)) != hipSuccess ||
+      hipMalloc(&c->dSizes, sizeof(uint64_t) * nranks) != hipSuccess) {
+    lego_set_error("lego_comm_create: stream / buffer allocation failed");
+    return fail(LEGO_E_DEVICE);
+  }
+  c->sizes.assign(nranks, 0);
+  c->offs.assign(nranks + 1, 0);
+  *out = c;
+  return LEGO_OK;
+}
+
+int lego_comm_destroy(lego_comm* c) {
+  delete c;
+  return LEGO_OK;
+}
+
+int lego_comm_gather_handoff(lego_comm* c, lego_ctx* ctx, int32_t root) {
+  if (!c || !ctx || root < 0 || root >= c->nranks) return LEGO_E_ARG;
+  c->haveResult = false;
+  const void* pkt = nullptr;
+  uint64_t bytes = 0;
+  const int st = lego_handoff_pack(ctx, &pkt, &bytes);  // complete on return
+  if (st != LEGO_OK) return st;
+  COMM_HIP(hipSetDevice(c->device));
+  COMM_HIP(hipMemcpyAsync(c->dSize, &bytes, sizeof(bytes), hipMemcpyHostToDevice, c->s));
+  COMM_NCCL(ncclGather(c->dSize, c->dSizes, 1, ncclUint64, root, c->nc, c->s));
+  const bool isRoot = c->rank == root;
+  if (isRoot) {
+    COMM_HIP(hipMemcpyAsync(c->sizes.data(), c->dSizes, sizeof(uint64_t) * c->nranks, hipMemcpyDeviceToHost, c->s));
+    COMM_HIP(hipStreamSynchronize(c->s));
+    for (int r = 0; r < c->nranks; ++r) c->offs[r + 1] = c->offs[r] + ((c->sizes[r] + 255) & ~(uint64_t)255);
+    const size_t need = c->offs[c->nranks];
+    if (need > c->recvCap) {
+      if (c->dRecv) COMM_HIP(hipFree(c->dRecv));
+      c->dRecv = nullptr;
+      c->recvCap = 0;
+      COMM_HIP(hipMalloc(&c->dRecv, need));
+      c->recvCap = need;
+    }
+    if (need > c->hCap) {
+      if (c->hRecv) COMM_HIP(hipHostFree(c->hRecv));
+      c->hRecv = nullptr;
+      c->hCap = 0;
+      COMM_HIP(hipHostMalloc(&c->hRecv, need, hipHostMallocDefault));
+      c->hCap = need;
+    }
+    COMM_HIP(hipMemcpyAsync(c->dRecv + c->offs[root], pkt, bytes, hipMemcpyDeviceToDevice, c->s));
+  }
+  COMM_NCCL(ncclGroupStart());
+  if (isRoot) {
+    for (int r = 0; r < c->nranks; ++r)
+      if (r != root && c->sizes[r])
+        COMM_NCCL(ncclRecv(c->dRecv + c->offs[r], c->sizes[r], ncclUint8, r, c->nc, c->s));
+  } else if (bytes) {
+    COMM_NCCL(ncclSend(pkt, bytes, ncclUint8, root, c->nc, c->s));
+  }
+  COMM_NCCL(ncclGroupEnd());
+  if (isRoot) COMM_HIP(hipMemcpyAsync(c->hRecv, c->dRecv, c->offs[c->nranks], hipMemcpyDeviceToHost, c->s));
+  COMM_HIP(hipStreamSynchronize(c->s));
+  c->haveResult = isRoot;
+  return LEGO_OK;
+}
+
+int lego_comm_handoff(lego_comm* c, int32_t rank, const void** packet, uint64_t* bytes) {
+  if (!c || !packet || !bytes || rank < 0 || rank >= c->nranks) return LEGO_E_ARG;
+  if (!c->haveResult) {
+    lego_set_error("lego_comm_handoff: no gathered result on this rank (root, after lego_comm_gather_handoff)");
+    return LEGO_E_STATE;
+  }
+  *packet = c->hRecv + c->offs[rank];
+  *bytes = c->sizes[rank];
+  return LEGO_OK;
+}
+
+}  // extern "C"

@@ -161,7 +161,12 @@ int odom_workgroups(int N, int cusAvailable);
 struct PackedRec {
   float sum[6];
   int ns, cnt[4], valid, flags, bad;
+  float cur[6];
+  int pub, nout;  // publish_to_mapping, outlier cloud size (the hand-off packet)
 };
+// The hand-off packet's clouds (lego_handoff_pack): scan b of the batch reads
+// its lego_handoff_scan entry at packet + 32 + 128 b.
+void launch_pack_handoff(const BatchBufs& bb, const OdomBufs& ob, int B, int maxPts, uint8_t* packet, hipStream_t s);
 void launch_pack_recs(const BatchBufs& bb, const OdomBufs& ob, int B, PackedRec* out, hipStream_t s);
 // HBM index sizes for clouds of up to capCorner / capSurf points.
 void odom_index_caps(int capCorner, int capSurf, int* gTC, int* gTS);

@@ -1819,8 +1819,38 @@ __global__ void k_pack_recs(BatchBufs bb, OdomBufs ob, int B, PackedRec* out) {
     r.valid = ob.validOut[b];
     r.flags = bb.fa_flags[b];
     r.bad = bb.bad[b];
+    for (int i = 0; i < 6; ++i) r.cur[i] = ob.curOut[b * 6 + i];
+    r.pub = ob.pubOut[b];
+    r.nout = bb.nout[b];
   }
   out[b] = r;
+}
+
+// publishCloudsLast's clouds into the hand-off packet (lego_handoff_pack): one
+// y-block row per scan, the entries (offsets, counts) already in the packet.
+__global__ void k_pack_handoff(BatchBufs bb, OdomBufs ob, int P, uint8_t* packet) {
+  const int b = blockIdx.y;
+  const lego_handoff_scan& e = *reinterpret_cast<const lego_handoff_scan*>(packet + sizeof(lego_handoff_hdr) +
+                                                                           sizeof(lego_handoff_scan) * b);
+  if (!e.publish_to_mapping) return;
+  const int nc = e.n_corner_last, ns = e.n_surf_last, no = e.n_outlier_last;
+  float4* dst = reinterpret_cast<float4*>(packet + e.offset);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nc + ns + no; i += gridDim.x * blockDim.x) {
+    float4 p;
+    if (i < nc) {
+      p = ob.cornerEnd[(size_t)b * ob.capLS + i];
+    } else if (i < nc + ns) {
+      p = ob.surfEnd[(size_t)b * P + i - nc];
+    } else {
+      const float4 q = bb.outl[(size_t)b * P + i - nc - ns];
+      p = make_float4(q.y, q.z, q.x, q.w);  // adjustOutlierCloud :1746-1757
+    }
+    dst[i] = p;
+  }
+}
+
+void launch_pack_handoff(const BatchBufs& bb, const OdomBufs& ob, int B, int P, uint8_t* packet, hipStream_t s) {
+  k_pack_handoff<<<dim3(16, B), 256, 0, s>>>(bb, ob, P, packet);
 }
 
 void launch_pack_recs(const BatchBufs& bb, const OdomBufs& ob, int B, PackedRec* out, hipStream_t s) {

@@ -141,6 +141,21 @@ class PoseRec(C.Structure):
 assert C.sizeof(PoseRec) == 64
 
 
+class HandoffHdr(C.Structure):  # lego_handoff_hdr
+    _fields_ = [("magic", C.c_uint32), ("version", C.c_uint32), ("nscans", C.c_int32), ("npub", C.c_int32),
+                ("bytes", C.c_uint64), ("_pad", C.c_uint64)]
+
+
+class HandoffScan(C.Structure):  # lego_handoff_scan
+    _fields_ = [("rec", PoseRec), ("transform_cur", C.c_float * 6), ("publish_to_mapping", C.c_int32),
+                ("n_corner_last", C.c_int32), ("n_surf_last", C.c_int32), ("n_outlier_last", C.c_int32),
+                ("offset", C.c_uint64), ("_pad", C.c_uint64 * 2)]
+
+
+assert C.sizeof(HandoffHdr) == 32 and C.sizeof(HandoffScan) == 128
+HANDOFF_MAGIC = 0x4F48474C
+
+
 # lego_imu_msg (include/lego_loam.h): the sensor_msgs/Imu fields the handlers read
 IMU_DTYPE = np.dtype([("stamp", np.float64), ("orientation", np.float64, 4),
                       ("angular_velocity", np.float64, 3), ("linear_acceleration", np.float64, 3)])
@@ -258,7 +273,8 @@ HIP_EXPORTS = ["lego_sensor_preset", "lego_create", "lego_fleet_create", "lego_d
                "lego_odom_batch_pc2", "lego_pc2_encode_xyzi", "lego_cloud_info_serialize",
                "lego_fusion_odometry", "lego_fusion_aft_mapped",
                "lego_mo_set_map", "lego_mo_configure", "lego_mo_process", "lego_mo_loop_closure", "lego_last_error", "lego_stage_times",
-               "lego_odom_profile"]
+               "lego_odom_profile", "lego_handoff_pack", "lego_handoff_unpack", "lego_comm_unique_id",
+               "lego_comm_create", "lego_comm_destroy", "lego_comm_gather_handoff", "lego_comm_handoff"]
 
 
 def hip_lib() -> C.CDLL:
@@ -295,11 +311,44 @@ def hip_lib() -> C.CDLL:
     lib.lego_mo_process.argtypes = [C.c_void_p, C.POINTER(FaOut), C.POINTER(MoOut)]
     lib.lego_mo_configure.argtypes = [C.c_void_p, C.POINTER(MoOpts)]
     lib.lego_mo_loop_closure.argtypes = [C.c_void_p, C.POINTER(LoopOut)]
+    lib.lego_handoff_pack.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]
+    lib.lego_handoff_unpack.argtypes = [C.c_void_p, C.c_uint64, C.c_int32, C.POINTER(PoseRec), C.POINTER(FaOut)]
+    lib.lego_comm_unique_id.argtypes = [C.c_void_p]
+    lib.lego_comm_create.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]
+    lib.lego_comm_destroy.argtypes = [C.c_void_p]
+    lib.lego_comm_gather_handoff.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
+    lib.lego_comm_handoff.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]
     lib.lego_last_error.restype = C.c_char_p
     lib.lego_odom_profile.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
     lib.lego_stage_times.argtypes = [C.c_void_p, C.POINTER(C.c_char_p), f32p, C.c_int32,
                                      C.POINTER(C.c_int32)]
     return lib
+
+
+_hiprt = None
+
+
+def hip_memcpy_d2h(dst: int, src: int, n: int) -> int:
+    """hipMemcpy device -> host through the HIP runtime already loaded."""
+    global _hiprt
+    if _hiprt is None:
+        _hiprt = C.CDLL("libamdhip64.so.7")
+        _hiprt.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    return _hiprt.hipMemcpy(C.c_void_p(dst), C.c_void_p(src), n, 2)  # hipMemcpyDeviceToHost
+
+
+def handoff_unpack(packet: np.ndarray, k: int, lib: C.CDLL | None = None) -> tuple:
+    """lego_handoff_unpack of scan k of a host packet: (PoseRec, fa dict)."""
+    lib = lib or hip_lib()
+    rec, fa = PoseRec(), FaOut()
+    packet = np.ascontiguousarray(packet, np.uint8)
+    check(lib.lego_handoff_unpack(packet.ctypes.data, packet.nbytes, k, C.byref(rec), C.byref(fa)),
+          "lego_handoff_unpack", lib)
+    return rec, fa_to_dict(fa)
+
+
+def handoff_header(packet: np.ndarray) -> HandoffHdr:
+    return HandoffHdr.from_buffer_copy(bytes(packet[:C.sizeof(HandoffHdr)]))
 
 
 def check(st: int, what: str, lib: C.CDLL | None = None) -> None:
@@ -637,6 +686,26 @@ class Lego:
         check(self.lib.lego_batch_fetch(self.h, k, C.byref(self._ip), C.byref(self._fa)),
               "lego_batch_fetch", self.lib)
         return ip_to_dict(self._ip, self.cfg, images), fa_to_dict(self._fa)
+
+    def handoff_packet(self) -> np.ndarray:
+        """lego_handoff_pack of the last waited batch, copied to the host
+        (uint8 array)."""
+        ptr, n = C.c_void_p(), C.c_uint64()
+        check(self.lib.lego_handoff_pack(self.h, C.byref(ptr), C.byref(n)), "lego_handoff_pack", self.lib)
+        out = np.zeros(n.value, np.uint8)
+        err = hip_memcpy_d2h(out.ctypes.data, ptr.value, n.value)
+        assert err == 0, err
+        return out
+
+    def mo_handoff(self, packet: np.ndarray, k: int) -> dict:
+        """mapOptimization::run on scan k of a hand-off packet (another
+        stream's, e.g. gathered from another GPU): lego_handoff_unpack into
+        the context's lego_fa_out, then lego_mo_process."""
+        packet = np.ascontiguousarray(packet, np.uint8)
+        self._handoff_keep = packet  # the fa_out points into it
+        check(self.lib.lego_handoff_unpack(packet.ctypes.data, packet.nbytes, k, None, C.byref(self._fa)),
+              "lego_handoff_unpack", self.lib)
+        return self.mo()
 
     def stage_times(self) -> dict:
         names = (C.c_char_p * 64)()

@@ -1,11 +1,15 @@
-"""Stream-per-GPU sharding and the pose-record hand-off.
+"""Stream-per-GPU sharding and the hand-off to rank 0.
 
 Each lidar stream is an independent unit: scans of one stream are serially
 dependent through the odometry state, so a stream never spans GPUs.  Stream s
-runs on rank s mod world.  The only exchange is the gather of the fixed 64-B
-`lego_pose_rec`s of every step to rank 0, the serial consumer (the reference's
-mapOptimization / transformFusion nodes).  On ROCm the "nccl" backend is RCCL
-over xGMI; the CPU tests drive the same code over gloo.
+runs on rank s mod world.  The only exchange is the hand-off to rank 0, the
+serial consumer (the reference's mapOptimization / transformFusion nodes):
+the fixed 64-B `lego_pose_rec`s of every step (`gather_pose_records`, the
+bench's per-step gather) and the batch's hand-off packet with the published
+corner / surf / outlier clouds (`gather_packets` over torch.distributed, or
+`native_gather_handoff`, the C-ABI's RCCL collective, lego_comm.hip), which
+rank 0 maps with `Lego.mo_handoff`.  On ROCm the "nccl" backend is RCCL over
+xGMI; the CPU tests drive the same code over gloo.
 """
 from __future__ import annotations
 
@@ -59,3 +63,69 @@ def gather_pose_records(raw: np.ndarray, dist, device=None):
     if rank != 0:
         return None
     return [g.cpu().numpy() for g in glist]
+
+
+def gather_packets(packet: np.ndarray, dist, device=None):
+    """Gathers every rank's variable-size uint8 hand-off packet
+    (lego_handoff_pack) to rank 0 over torch.distributed: the sizes first,
+    then the packets padded to the largest.  Returns the list of per-rank
+    packets on rank 0, None elsewhere.  The native RCCL path is
+    `native_gather_handoff`."""
+    import torch
+
+    world, rank = dist.get_world_size(), dist.get_rank()
+    n = torch.tensor([packet.size], dtype=torch.int64, device=device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    sizes = [int(s.item()) for s in sizes]
+    buf = np.zeros(max(sizes), np.uint8)
+    buf[:packet.size] = packet
+    t = torch.from_numpy(buf)
+    if device is not None:
+        t = t.to(device)
+    glist = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
+    dist.gather(t, glist, dst=0)
+    if rank != 0:
+        return None
+    return [g.cpu().numpy()[:sizes[r]].copy() for r, g in enumerate(glist)]
+
+
+def native_comm(L, dist, device: int):
+    """A lego_comm (RCCL) over the ranks of `dist`: rank 0's unique id is
+    broadcast with torch.distributed, then every rank joins on its device."""
+    import ctypes as C
+
+    lib = L.hip_lib()
+    uid = (C.c_uint8 * 128)()
+    if dist.get_rank() == 0:
+        L.check(lib.lego_comm_unique_id(uid), "lego_comm_unique_id", lib)
+    box = [bytes(uid)]
+    dist.broadcast_object_list(box, src=0)
+    C.memmove(uid, box[0], 128)
+    comm = C.c_void_p()
+    L.check(lib.lego_comm_create(uid, dist.get_world_size(), dist.get_rank(), device, C.byref(comm)),
+            "lego_comm_create", lib)
+    return comm
+
+
+def native_gather_handoff(L, comm, ctx, root: int = 0):
+    """lego_comm_gather_handoff: every rank's last batch packet to root over
+    RCCL.  Returns the host packets on root (list per rank), None elsewhere."""
+    import ctypes as C
+
+    lib = L.hip_lib()
+    L.check(lib.lego_comm_gather_handoff(comm, ctx.h, root), "lego_comm_gather_handoff", lib)
+    out = []
+    r = 0
+    while True:
+        ptr, n = C.c_void_p(), C.c_uint64()
+        st = lib.lego_comm_handoff(comm, r, C.byref(ptr), C.byref(n))
+        if st == L.LEGO_E_STATE:
+            return None  # not root
+        if st != L.LEGO_OK:
+            break  # past the last rank
+        pkt = np.zeros(n.value, np.uint8)
+        C.memmove(pkt.ctypes.data, ptr.value, n.value)
+        out.append(pkt)
+        r += 1
+    return out

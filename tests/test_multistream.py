@@ -84,3 +84,105 @@ def test_gather_world2_gloo(L, tmp_path):
     out = tmp_path / "rank0.txt"
     mp.spawn(_worker, args=(2, _free_port(), str(out)), nprocs=2, join=True)
     assert out.read_text() == "ok"
+
+
+# ---------------------------------------------------------------- hand-off packets
+def oracle_packet(L, stream, n=K + 3):
+    """A version-1 hand-off packet (include/lego_loam.h) written here from the
+    oracle's run of `stream`: what the product's lego_handoff_pack emits for
+    the same scans (its GPU test checks that side).  Test-side writer of the
+    documented format."""
+    sc = L.synth_cfg("VLP-16", ms.stream_seed(stream))
+    ora = L.Oracle(L.sensor_cfg("VLP-16"))
+    ents, clouds = [], []
+    for k in range(n):
+        pts, stamp = L.synth_scan(sc, k)
+        ora.ip(pts, stamp)
+        fa = ora.fa()
+        e = L.HandoffScan()
+        e.rec.stamp = stamp
+        for i in range(6):
+            e.rec.transform_sum[i] = float(fa["transform_sum"][i])
+            e.transform_cur[i] = float(fa["transform_cur"][i])
+        e.rec.n_sharp, e.rec.n_less_sharp = len(fa["sharp"]), len(fa["less_sharp"])
+        e.rec.n_flat, e.rec.n_less_flat = len(fa["flat"]), len(fa["less_flat"])
+        e.rec.odom_valid = int(fa["odom_valid"])
+        e.publish_to_mapping = int(fa["publish_to_mapping"])
+        c = [fa["corner_last"], fa["surf_last"], fa["outlier_last"]] if e.publish_to_mapping else [None] * 3
+        if e.publish_to_mapping:
+            e.n_corner_last, e.n_surf_last, e.n_outlier_last = (len(x) for x in c)
+        ents.append(e)
+        clouds.append(c)
+    head = L.C.sizeof(L.HandoffHdr) + L.C.sizeof(L.HandoffScan) * n
+    off, body = head, []
+    for e, c in zip(ents, clouds):
+        e.offset = off
+        if e.publish_to_mapping:
+            blob = b"".join(x.tobytes() for x in c)
+            body.append(blob)
+            off += len(blob)
+    h = L.HandoffHdr(L.HANDOFF_MAGIC, 1, n, sum(e.publish_to_mapping for e in ents), off, 0)
+    raw = bytes(h) + b"".join(bytes(e) for e in ents) + b"".join(body)
+    assert len(raw) == off
+    return np.frombuffer(raw, np.uint8).copy(), ents, clouds
+
+
+def test_handoff_unpack_format(L):
+    """lego_handoff_unpack (host code of the product library, no device) on a
+    packet written from the format description: records, flags and the three
+    published clouds come back as a lego_fa_out; malformed packets are refused."""
+    pkt, ents, clouds = oracle_packet(L, 0)
+    assert L.handoff_header(pkt).npub >= 2
+    for k, (e, c) in enumerate(zip(ents, clouds)):
+        rec, fa = L.handoff_unpack(pkt, k)
+        assert bytes(rec) == bytes(e.rec)
+        assert fa["publish_to_mapping"] == e.publish_to_mapping and fa["odom_valid"] == e.rec.odom_valid
+        assert np.array_equal(fa["transform_cur"], np.array(list(e.transform_cur), np.float32))
+        if e.publish_to_mapping:
+            for key, x in zip(("corner_last", "surf_last", "outlier_last"), c):
+                assert np.array_equal(fa[key].view(np.uint8), x.view(np.uint8)), (k, key)
+        # the /laser_odom_to_init quaternion is recomputed from transformSum as the node publishes it
+        assert np.isclose(np.linalg.norm(fa["odom_quat"]), 1.0)
+    for bad in (pkt[:-16], np.r_[np.zeros(4, np.uint8), pkt[4:]]):  # truncated / wrong magic
+        with pytest.raises(RuntimeError):
+            L.handoff_unpack(bad, 0)
+    with pytest.raises(RuntimeError):
+        L.handoff_unpack(pkt, len(ents))
+
+
+def _packet_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    sys.path.insert(0, str(REPO / "tests"))
+    from conftest import _load_ffi, ensure_built
+
+    ensure_built()
+    L = _load_ffi()
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine, _, _ = oracle_packet(L, rank)
+        got = ms.gather_packets(mine, dist)
+        if rank == 0:
+            assert len(got) == world
+            for r in range(world):
+                exp, ents, clouds = oracle_packet(L, r)
+                assert np.array_equal(got[r], exp)
+                for k, e in enumerate(ents):
+                    rec, fa = L.handoff_unpack(got[r], k)
+                    assert bytes(rec) == bytes(e.rec)
+                    if e.publish_to_mapping:
+                        assert np.array_equal(fa["surf_last"].view(np.uint8), clouds[k][1].view(np.uint8))
+            Path(out).write_text("ok")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_handoff_packets_world2_gloo(L, tmp_path):
+    """The variable-size packet gather (sizes, then padded packets) at world
+    size 2 over gloo, unpacked on rank 0."""
+    import torch.multiprocessing as mp
+
+    out = tmp_path / "rank0.txt"
+    mp.spawn(_packet_worker, args=(2, _free_port(), str(out)), nprocs=2, join=True)
+    assert out.read_text() == "ok"
