@@ -6,7 +6,8 @@ Workload (BASELINE.json configs[1]): one synthetic VLP-16
 two-step LM odometry for every scan, in stream order.  A "step" is one batch
 of `--batch` consecutive scans of the stream through lego_odom_batch with the
 points already resident in HBM.  With --gpus N each rank runs its own stream
-(seed 10 + rank, config C4) and the 64-B pose records of every step are
+(seed 10 + rank, config C4) and every step's hand-off packet (the 64-B pose
+records plus the corner / surf / outlier clouds published to mapping) is
 gathered to rank 0 over RCCL (the hand-off to the serial pose graph).
 
 Prints ONE JSON line on rank 0 (contract in the task statement).
@@ -443,7 +444,10 @@ def main():
         gpu.wait(recs)
         cp = (L.PoseRec * B)()
         C.memmove(cp, recs, C.sizeof(recs))
-        return i, gpu.stage_times(), cp
+        # N > 1: the step's hand-off packet (pose records + the published
+        # corner / surf / outlier clouds) packed into HBM before the slot is reused
+        pkt = gpu.handoff_tensor(dev) if dist else None
+        return i, gpu.stage_times(), cp, pkt
 
     def submit(i):
         j = i % nb
@@ -472,13 +476,13 @@ def main():
 
     def account(done):
         nonlocal alg_bytes, gathered
-        for i, st, rc in done:
+        for i, st, rc, pkt in done:
             gpu_recs[i % nb] = rc
             for k, v in st.items():
                 stage_acc[k] = stage_acc.get(k, 0.0) + v
             alg_bytes += odom_alg_bytes(rc)
-            if dist:  # hand-off of the step's pose records to the serial consumer on rank 0
-                gathered = ms.gather_pose_records(ms.recs_to_bytes(rc), dist, dev if backend == "nccl" else None)
+            if dist:  # hand-off of the step to the serial consumer on rank 0 (RCCL over xGMI)
+                gathered = ms.gather_packets(pkt if backend == "nccl" else pkt.cpu(), dist, to_host=False)
 
     for i in range(args.steps):
         account(submit(args.warmup + i))
@@ -499,6 +503,13 @@ def main():
     handoff = None
     if rank == 0:
         handoff = mapping_handoff(gpu, B)
+        if gathered is not None:  # the last step's packets as rank 0 received them
+            hdrs = [L.handoff_header(g.cpu().numpy()) for g in gathered]
+            handoff["gathered_to_rank0"] = {
+                "ranks": len(hdrs), "scans_per_rank": [h.nscans for h in hdrs],
+                "published_per_rank": [h.npub for h in hdrs], "bytes_per_rank": [h.bytes for h in hdrs],
+                "valid": all(h.magic == L.HANDOFF_MAGIC and h.nscans == B for h in hdrs),
+                "transport": f"torch.distributed gather ({backend}) of lego_handoff_pack_into packets, in the timed region"}
         # the batch runs as chunks (lego_api.hip run_batch): k_odom launches per step
         launches = {k[2:]: v / args.steps for k, v in stage_acc.items() if k.startswith("n:")}
         stage_acc = {k: v for k, v in stage_acc.items() if not k.startswith("n:")}
@@ -575,10 +586,14 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (seeded ray-cast VLP-16 stream, 1 m/s + 5 deg/s)",
-            "config": {"workload": f"C2: {args.sensor} stream @10Hz, full per-scan pipeline incl. "
-                                   f"2-step LM odometry, {B} scans/step",
+            "config": {"workload": (f"C2: {args.sensor} stream @10Hz, full per-scan pipeline incl. "
+                                    f"2-step LM odometry, {B} scans/step" if world == 1 else
+                                    f"C4: one {args.sensor} stream per GPU (seeds 10..{9 + world}) @10Hz, full "
+                                    f"per-scan pipeline incl. 2-step LM odometry, {B} scans/step, hand-off "
+                                    "gathered to rank 0 every step"),
                        "scans_per_step": B, "stream_len": args.stream_len,
-                       "parallelism": f"stream-per-gpu x{world}"},
+                       "parallelism": f"stream-per-gpu x{world}",
+                       "gather": "per step: pose records + published clouds to rank 0" if world > 1 else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_odom", "launch_ms": odom_ms / n_odom, "launches_per_step": n_odom,

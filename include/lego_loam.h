@@ -419,6 +419,9 @@ typedef struct lego_handoff_scan {
  * device buffer owned by the context (*packet, *bytes), complete when the
  * call returns; valid until the next batch call on the context. */
 int lego_handoff_pack(lego_ctx* ctx, const void** packet, uint64_t* bytes);
+/* The same into caller-owned device memory dst (cap bytes, on the context's
+ * device; LEGO_E_CAPACITY if smaller); dst == NULL only sets *bytes. */
+int lego_handoff_pack_into(lego_ctx* ctx, void* dst, uint64_t cap, uint64_t* bytes);
 /* Host-side view of scan k of a packet in host memory: its record and, in
  * out, the lego_fa_out lego_mo_process consumes (stamp, transform_sum /
  * _cur, odom_quat / _pos, publish flag, the three clouds pointing into the

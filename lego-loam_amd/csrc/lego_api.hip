@@ -112,6 +112,7 @@ struct lego_ctx {
   std::vector<lego_point_xyzi> h_seg, h_outl, h_full, h_sharp, h_lsharp, h_flat, h_lflat;
   GatedBufs gb{};  // LEGO_IP_GATED outputs (first use)
   uint8_t* d_handoff = nullptr;  // lego_handoff_pack's packet (grown on demand)
+  hipStream_t hstream = nullptr; // the hand-off packing (first use)
   size_t handoffCap = 0;
   std::vector<uint8_t> h_handoffHead;
   std::vector<lego_point_xyzi> h_info, h_gcloud, h_pure;
@@ -187,6 +188,8 @@ struct lego_ctx {
       if (faDone[i]) (void)hipEventDestroy(faDone[i]);
       if (recsDone[i]) (void)hipEventDestroy(recsDone[i]);
     }
+    if (hstream) (void)hipStreamSynchronize(hstream);
+    if (hstream) (void)hipStreamDestroy(hstream);
     if (ostream) (void)hipStreamDestroy(ostream);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -1616,14 +1619,15 @@ int lego_odom_batch_pc2(lego_ctx* x, const lego_pc2_msg* msgs, int32_t nscans, i
 }
 
 // ---------------------------------------------------------------- hand-off packet
-int lego_handoff_pack(lego_ctx* x, const void** packet, uint64_t* bytes) {
-  if (!x || !packet || !bytes) return LEGO_E_ARG;
+// Packs the last waited batch into dst (cap bytes) or, dst == NULL, into the
+// context's buffer, on the hand-off stream (the batch is complete: no other
+// stream's work is waited for).
+static int handoff_pack(lego_ctx* x, uint8_t* dst, uint64_t cap, const void** packet, uint64_t* bytes) {
   const int B = x->lastB;
   if (B <= 0 || !x->lastBatch) {
     set_err("lego_handoff_pack: no batch result (lego_odom_batch / lego_odom_batch_wait first)");
     return LEGO_E_STATE;
   }
-  HIPCHK(hipSetDevice(x->device));
   const int slot = x->lastBase / x->maxBatch;
   const PackedRec* pk = x->h_pack + (size_t)slot * (x->maxBatch + 1);
   const size_t head = sizeof(lego_handoff_hdr) + sizeof(lego_handoff_scan) * (size_t)B;
@@ -1655,22 +1659,44 @@ int lego_handoff_pack(lego_ctx* x, const void** packet, uint64_t* bytes) {
   h->nscans = B;
   h->npub = (int32_t)npub;
   h->bytes = off;
-  if (off > x->handoffCap) {
-    if (x->d_handoff) HIPCHK(hipFree(x->d_handoff));
-    x->d_handoff = nullptr;
-    x->handoffCap = 0;
-    HIPCHK(hipMalloc(&x->d_handoff, off));
-    x->handoffCap = off;
+  *bytes = off;
+  if (!packet && !dst) return LEGO_OK;  // lego_handoff_pack_into size query
+  if (dst && cap < off) {
+    set_err("lego_handoff_pack_into: %llu bytes needed, %llu given", (unsigned long long)off,
+            (unsigned long long)cap);
+    return LEGO_E_CAPACITY;
   }
-  hipStream_t s = x->stream;
-  HIPCHK(hipMemcpyAsync(x->d_handoff, x->h_handoffHead.data(), head, hipMemcpyHostToDevice, s));
+  if (!dst) {
+    if (off > x->handoffCap) {
+      if (x->d_handoff) HIPCHK(hipFree(x->d_handoff));
+      x->d_handoff = nullptr;
+      x->handoffCap = 0;
+      HIPCHK(hipMalloc(&x->d_handoff, off));
+      x->handoffCap = off;
+    }
+    dst = x->d_handoff;
+  }
+  if (!x->hstream) HIPCHK(hipStreamCreateWithFlags(&x->hstream, hipStreamNonBlocking));
+  hipStream_t s = x->hstream;
+  HIPCHK(hipMemcpyAsync(dst, x->h_handoffHead.data(), head, hipMemcpyHostToDevice, s));
   launch_pack_handoff(bb_slice(x->bb, x->dc, x->lastBase, B), ob_slice(x->ob, x->dc, x->lastBase, 0, x->nStreams), B,
-                      x->dc.P, x->d_handoff, s);
+                      x->dc.P, dst, s);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s));
-  *packet = x->d_handoff;
-  *bytes = off;
+  if (packet) *packet = dst;
   return LEGO_OK;
+}
+
+int lego_handoff_pack(lego_ctx* x, const void** packet, uint64_t* bytes) {
+  if (!x || !packet || !bytes) return LEGO_E_ARG;
+  HIPCHK(hipSetDevice(x->device));
+  return handoff_pack(x, nullptr, 0, packet, bytes);
+}
+
+int lego_handoff_pack_into(lego_ctx* x, void* dst, uint64_t cap, uint64_t* bytes) {
+  if (!x || !bytes) return LEGO_E_ARG;
+  HIPCHK(hipSetDevice(x->device));
+  return handoff_pack(x, static_cast<uint8_t*>(dst), dst ? cap : 0, nullptr, bytes);
 }
 
 int lego_handoff_unpack(const void* packet, uint64_t bytes, int32_t k, lego_pose_rec* rec, lego_fa_out* out) {

@@ -273,7 +273,7 @@ HIP_EXPORTS = ["lego_sensor_preset", "lego_create", "lego_fleet_create", "lego_d
                "lego_odom_batch_pc2", "lego_pc2_encode_xyzi", "lego_cloud_info_serialize",
                "lego_fusion_odometry", "lego_fusion_aft_mapped",
                "lego_mo_set_map", "lego_mo_configure", "lego_mo_process", "lego_mo_loop_closure", "lego_last_error", "lego_stage_times",
-               "lego_odom_profile", "lego_handoff_pack", "lego_handoff_unpack", "lego_comm_unique_id",
+               "lego_odom_profile", "lego_handoff_pack", "lego_handoff_pack_into", "lego_handoff_unpack", "lego_comm_unique_id",
                "lego_comm_create", "lego_comm_destroy", "lego_comm_gather_handoff", "lego_comm_handoff"]
 
 
@@ -312,6 +312,7 @@ def hip_lib() -> C.CDLL:
     lib.lego_mo_configure.argtypes = [C.c_void_p, C.POINTER(MoOpts)]
     lib.lego_mo_loop_closure.argtypes = [C.c_void_p, C.POINTER(LoopOut)]
     lib.lego_handoff_pack.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]
+    lib.lego_handoff_pack_into.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
     lib.lego_handoff_unpack.argtypes = [C.c_void_p, C.c_uint64, C.c_int32, C.POINTER(PoseRec), C.POINTER(FaOut)]
     lib.lego_comm_unique_id.argtypes = [C.c_void_p]
     lib.lego_comm_create.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]
@@ -696,6 +697,18 @@ class Lego:
         err = hip_memcpy_d2h(out.ctypes.data, ptr.value, n.value)
         assert err == 0, err
         return out
+
+    def handoff_tensor(self, device):
+        """lego_handoff_pack_into a torch uint8 tensor in HBM (the packet of
+        the last waited batch, ready for a device-side gather)."""
+        import torch
+
+        n = C.c_uint64()
+        check(self.lib.lego_handoff_pack_into(self.h, None, 0, C.byref(n)), "lego_handoff_pack_into", self.lib)
+        t = torch.empty(n.value, dtype=torch.uint8, device=device)
+        check(self.lib.lego_handoff_pack_into(self.h, C.c_void_p(t.data_ptr()), n.value, C.byref(n)),
+              "lego_handoff_pack_into", self.lib)
+        return t
 
     def mo_handoff(self, packet: np.ndarray, k: int) -> dict:
         """mapOptimization::run on scan k of a hand-off packet (another

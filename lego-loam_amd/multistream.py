@@ -65,29 +65,31 @@ def gather_pose_records(raw: np.ndarray, dist, device=None):
     return [g.cpu().numpy() for g in glist]
 
 
-def gather_packets(packet: np.ndarray, dist, device=None):
+def gather_packets(packet, dist, device=None, to_host: bool = True):
     """Gathers every rank's variable-size uint8 hand-off packet
-    (lego_handoff_pack) to rank 0 over torch.distributed: the sizes first,
+    (lego_handoff_pack; a numpy array, or a torch tensor already in HBM from
+    Lego.handoff_tensor) to rank 0 over torch.distributed: the sizes first,
     then the packets padded to the largest.  Returns the list of per-rank
-    packets on rank 0, None elsewhere.  The native RCCL path is
-    `native_gather_handoff`."""
+    packets on rank 0 (numpy, or device tensors with to_host=False), None
+    elsewhere.  The native RCCL path is `native_gather_handoff`."""
     import torch
 
     world, rank = dist.get_world_size(), dist.get_rank()
-    n = torch.tensor([packet.size], dtype=torch.int64, device=device)
+    t = packet if isinstance(packet, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(packet))
+    if device is not None:
+        t = t.to(device)
+    n = torch.tensor([t.numel()], dtype=torch.int64, device=t.device)
     sizes = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(sizes, n)
     sizes = [int(s.item()) for s in sizes]
-    buf = np.zeros(max(sizes), np.uint8)
-    buf[:packet.size] = packet
-    t = torch.from_numpy(buf)
-    if device is not None:
-        t = t.to(device)
+    if t.numel() < max(sizes):
+        t = torch.cat([t, torch.zeros(max(sizes) - t.numel(), dtype=torch.uint8, device=t.device)])
     glist = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
     dist.gather(t, glist, dst=0)
     if rank != 0:
         return None
-    return [g.cpu().numpy()[:sizes[r]].copy() for r, g in enumerate(glist)]
+    out = [g[:sizes[r]] for r, g in enumerate(glist)]
+    return [g.cpu().numpy().copy() for g in out] if to_host else out
 
 
 def native_comm(L, dist, device: int):
