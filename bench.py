@@ -142,9 +142,21 @@ def cpu_all_cores(L, sensor, threads, nscans, budget_s):
     [x.start() for x in th]
     [x.join() for x in th]
     dt = time.perf_counter() - t0
+    quota = cgroup_cpus()
     return {"value": sum(done) / dt, "unit": "scans/s", "cores": threads, "kind": "port",
-            "sample": f"{sum(done)} scans: {threads} threads, each its own {nscans}-scan {sensor} stream "
-                      f"(seeds 10..{9 + threads}) through oracle ip+fa incl. LM, ~{budget_s:.0f} s"}
+            "cgroup_cpu_quota": quota,
+            "sample": f"{sum(done)} scans: {threads} threads (min(streams, cores), BASELINE.md), each its own "
+                      f"{nscans}-scan {sensor} stream (seeds 10..{9 + threads}) through oracle ip+fa incl. LM, "
+                      f"~{budget_s:.0f} s" + (f"; the cgroup caps the process at {quota:g} cores" if quota else "")}
+
+
+def cgroup_cpus():
+    """The CPU quota of this process's cgroup (cpu.max), in cores, or None."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        return None
 
 
 def host_info():
@@ -160,7 +172,7 @@ def host_info():
         share = len(os.sched_getaffinity(0))
     except AttributeError:
         share = os.cpu_count() or 1
-    return {"nproc": os.cpu_count(), "affinity": share, "cpu_model": model}
+    return {"nproc": os.cpu_count(), "affinity": share, "cgroup_cpu_quota": cgroup_cpus(), "cpu_model": model}
 
 
 def mapping_handoff(gpu, B: int) -> dict:
@@ -301,7 +313,7 @@ def loop_bench(L, nscans: int, calls: int, cpu: bool):
     return res
 
 
-def dense_bench(L, nscans: int, batch: int, device: int):
+def dense_bench(L, nscans: int, batch: int, device: int, cpu: bool = False, budget_s: float = 5.0):
     """Auxiliary (not the headline metric): config C3, the HDL-64E-shaped
     synthetic stream (64 x 2048) through the same pipeline
     on one GPU, two batches in flight.  Host wall clock, like the headline."""
@@ -329,8 +341,23 @@ def dense_bench(L, nscans: int, batch: int, device: int):
     dt = time.perf_counter() - t0
     g.close()
     n = (nb - 1) * batch
-    return {"workload": f"C3: HDL-64E 64x2048 synthetic stream (seed 2), {batch} scans per call, two in flight",
-            "scans": n, "scans_per_s": n / dt, "ms_per_scan": dt / n * 1e3, "points_per_scan": int(maxn)}
+    res = {"workload": f"C3: HDL-64E 64x2048 synthetic stream (seed 2), {batch} scans per call, two in flight",
+           "scans": n, "scans_per_s": n / dt, "ms_per_scan": dt / n * 1e3, "points_per_scan": int(maxn)}
+    if cpu:  # the oracle on one core over the same stream (scans synthesised beforehand) until ~budget_s
+        sc = L.synth_cfg("HDL-64E", 2)
+        scans = [L.synth_scan(sc, k) for k in range(min(nscans, 40))]
+        ora = L.Oracle(L.sensor_cfg("HDL-64E"))
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < budget_s and done < len(scans):
+            ora.ip(*scans[done])
+            ora.fa()
+            done += 1
+        v = done / (time.perf_counter() - t0)
+        res["cpu_baseline"] = {"value": v, "unit": "scans/s", "cores": 1, "kind": "port",
+                               "sample": f"the first {done} scans of the same HDL-64E stream through oracle ip+fa "
+                                         "incl. LM, 1 thread"}
+        res["gpu_over_cpu"] = res["scans_per_s"] / v
+    return res
 
 
 def fleet_bench(L, streams: int, k: int, steps: int, device: int):
@@ -516,13 +543,19 @@ def main():
         odom_ms = stage_acc.get("odom.lm", 0.0) / args.steps
         n_odom = max(1.0, launches.get("odom.lm", 1.0))
         achieved = (alg_bytes / args.steps) / (odom_ms * 1e-3) / 1e9 if odom_ms > 0 else 0.0
-        traffic = None
-        pmc = REPO / "profiles" / "r01_pmc_summary.json"
-        if pmc.exists():
-            try:
-                traffic = json.loads(pmc.read_text()).get("k_odom_hbm_bytes_per_launch")
-            except Exception:  # noqa: BLE001
-                traffic = None
+        # roofline.traffic: the PMC figure (FETCH_SIZE x2 + WRITE_SIZE, separate
+        # rocprofv3 passes over this command, scripts/gpu_profile.sh) of the newest
+        # committed summary, labelled with the commit it was measured at
+        traffic, traffic_src = None, None
+        for pmc in (REPO / "profiles" / "r02_pmc_summary.json", REPO / "profiles" / "r01_pmc_summary.json"):
+            if pmc.exists():
+                try:
+                    js = json.loads(pmc.read_text())
+                    traffic = js.get("k_odom_hbm_bytes_per_launch")
+                    traffic_src = f"profiles/{pmc.name} (measured at commit {js.get('commit', '?')}, not in this run)"
+                except Exception:  # noqa: BLE001
+                    traffic = None
+                break
         cpu = None
         cpu_all = None
         pose_delta = None
@@ -532,8 +565,8 @@ def main():
             cpu = {"value": v, "unit": "scans/s", "cores": 1, "kind": "port",
                    "sample": f"{n} scans ({passes} pass(es) over the {args.stream_len}-scan "
                              f"{args.sensor} stream, seed {seed}) through oracle ip+fa incl. LM, 1 thread"}
-            # the box's CPU share is 16 cores per GPU (the machine's nproc is larger)
-            thr = max(1, min(16, host_info()["affinity"]))
+            # min(streams, cores) threads, the streams being the fleet line's
+            thr = max(1, min(max(args.fleet_streams, 1), host_info()["affinity"]))
             cpu_all = cpu_all_cores(L, args.sensor, thr, 60, args.cpu_budget)
         if args.odom_profile:
             prof = (C.c_uint64 * 32)()
@@ -567,7 +600,7 @@ def main():
         if args.fleet_streams > 0 and world == 1:
             aux["fleet_vlp16"] = fleet_bench(L, args.fleet_streams, 20, 3, local)
         if args.dense_scans > 0 and world == 1:
-            aux["dense_hdl64_c3"] = dense_bench(L, args.dense_scans, 20, local)
+            aux["dense_hdl64_c3"] = dense_bench(L, args.dense_scans, 20, local, cpu=not args.no_cpu)
         if args.loop_scans > 0 and world == 1:
             aux["loop_closure"] = loop_bench(L, args.loop_scans, 5, not args.no_cpu)
         if cpu_all:
@@ -595,7 +628,9 @@ def main():
                        "parallelism": f"stream-per-gpu x{world}",
                        "gather": "per step: pose records + published clouds to rank 0" if world > 1 else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                         "traffic_over_alg": (traffic / (alg_bytes / args.steps * 1.0 / n_odom)
+                                              if traffic and alg_bytes else None),
                          "kernel": "k_odom", "launch_ms": odom_ms / n_odom, "launches_per_step": n_odom,
                          "kernel_ms_per_step": odom_ms},
             "cpu_baseline": cpu,

@@ -2,7 +2,7 @@
 """HBM bytes per launch from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE;
 scripts/gpu_profile.sh), with MI355X_MICROARCH.md's gfx950 correction:
 FETCH_SIZE x2 (it reports half of wide coalesced reads), WRITE_SIZE as
-reported, KiB -> bytes.  Usage: pmc_summary.py <run dir> <out.json> <source note>"""
+reported, KiB -> bytes.  Usage: pmc_summary.py <run dir> <out.json> <source note> [commit]"""
 import csv
 import json
 import sys
@@ -27,7 +27,7 @@ def main():
     run, out, note = Path(sys.argv[1]), Path(sys.argv[2]), sys.argv[3]
     f = per_launch(run / "pmc_fetch" / "run_counter_collection.csv", "FETCH_SIZE")
     w = per_launch(run / "pmc_write" / "run_counter_collection.csv", "WRITE_SIZE")
-    res = {"source": note,
+    res = {"source": note, "commit": sys.argv[4] if len(sys.argv) > 4 else None,
            "correction": "FETCH_SIZE x2 (gfx950 reports half of wide coalesced reads, MI355X_MICROARCH.md HBM "
                          "section); WRITE_SIZE as reported; KiB -> bytes",
            "per_launch": {}}

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Copies one GPU session's evidence (scripts/gpu_check.sh + gpu_profile.sh
 under gpurun_out/<tag>, the phase profile of gpu_quick.sh under
-gpurun_out/<tag>_q) into profiles/r01_* and prints the numbers DESIGN.md
-quotes.  Usage: refresh_profiles.py <tag>"""
+gpurun_out/<tag>_q) into profiles/<round>_*, stamps the summaries with the
+commit the session ran, and prints the numbers DESIGN.md quotes.
+Usage: refresh_profiles.py <tag> [round (r02)] [commit (HEAD)]"""
 import json
 import shutil
 import subprocess
@@ -11,25 +12,30 @@ from pathlib import Path
 
 REPO = Path(__file__).resolve().parents[1]
 tag = sys.argv[1]
+rnd = sys.argv[2] if len(sys.argv) > 2 else "r02"
+commit = sys.argv[3] if len(sys.argv) > 3 else subprocess.run(["git", "rev-parse", "--short", "HEAD"], cwd=REPO,
+                                                             capture_output=True, text=True).stdout.strip()
 src = REPO / "gpurun_out" / tag
 prof = REPO / "profiles"
-shutil.copy(src / "bench.json", prof / "r01_bench.json")
-shutil.copy(src / "gpu_tests.log", prof / "r01_gpu_tests.log")
-shutil.copy(src / "prof_stats" / "run_kernel_stats.csv", prof / "r01_kernel_stats.csv")
-subprocess.run([sys.executable, str(REPO / "scripts" / "pmc_summary.py"), str(src), str(prof / "r01_pmc_summary.json"),
+shutil.copy(src / "bench.json", prof / f"{rnd}_bench.json")
+shutil.copy(src / "gpu_tests.log", prof / f"{rnd}_gpu_tests.log")
+shutil.copy(src / "prof_stats" / "run_kernel_stats.csv", prof / f"{rnd}_kernel_stats.csv")
+subprocess.run([sys.executable, str(REPO / "scripts" / "pmc_summary.py"), str(src), str(prof / f"{rnd}_pmc_summary.json"),
                 "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes over bench.py --no-cpu "
                 "--mapping-steps 0 --fleet-streams 0 --dense-scans 0 --loop-scans 0 --steps 2 --warmup 1 "
-                "(3 launches per kernel, 100 VLP-16 scans each; k_odom = 48 workgroups, plain launch)"], check=True)
+                "(3 launches per kernel, 100 VLP-16 scans each; k_odom = 48 workgroups, plain launch)", commit],
+               check=True)
 q = REPO / "gpurun_out" / (tag + "_q") / "prof.txt"
 if q.exists():
-    (prof / "r01_odom_phase_profile.txt").write_text(
+    (prof / f"{rnd}_odom_phase_profile.txt").write_text(
         "".join(line for line in q.read_text().splitlines(True) if "amdgpu" not in line))
-d = json.loads((prof / "r01_bench.json").read_text())
+d = json.loads((prof / f"{rnd}_bench.json").read_text())
 import csv  # noqa: E402
 
-rows = list(csv.DictReader(open(prof / "r01_kernel_stats.csv")))
+rows = list(csv.DictReader(open(prof / f"{rnd}_kernel_stats.csv")))
 kod = next(r for r in rows if r["Name"].startswith("lego::k_odom"))
-pmc = json.loads((prof / "r01_pmc_summary.json").read_text())
+pmc = json.loads((prof / f"{rnd}_pmc_summary.json").read_text())
+(prof / f"{rnd}_COMMIT").write_text(f"{commit}\n")
 print(json.dumps({
     "value": d["value"], "launch_ms": d["roofline"]["launch_ms"], "rocprof_k_odom_ms": float(kod["AverageNs"]) / 1e6,
     "achieved_GBs": d["roofline"]["achieved"], "frac": d["roofline"]["frac"],
