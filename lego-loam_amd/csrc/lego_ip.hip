@@ -50,10 +50,16 @@ __global__ void k_project(BatchBufs bb, DevCfg c) {
   atomicMax(&bb.owner[(size_t)b * c.P + row * c.H + col], i);
 }
 
-__global__ void k_pixels(BatchBufs bb, DevCfg c) {
-  const int b = blockIdx.y;
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= c.P) return;
+// One workgroup per 4 rows x 64 columns (a wave per row): the stores stay
+// row-contiguous, and the records a wave gathers (16 rings apart in firing
+// order) share their 128-B lines with the other three waves' at the same
+// columns, so each line is fetched once per workgroup instead of once per row
+// (rocprofv3 FETCH_SIZE calibration: scripts/mb/mb_gather.hip).
+__global__ void __launch_bounds__(256) k_pixels(BatchBufs bb, DevCfg c) {
+  const int b = blockIdx.z;
+  const int row = blockIdx.y * 4 + (threadIdx.x >> 6), col = blockIdx.x * 64 + (threadIdx.x & 63);
+  if (row >= c.N || col >= c.H) return;
+  const int p = row * c.H + col;
   const size_t gp = (size_t)b * c.P + p;
   const int o = bb.owner[gp];
   if (o < 0) {
@@ -62,7 +68,6 @@ __global__ void k_pixels(BatchBufs bb, DevCfg c) {
     bb.full[gp] = make_float4(qn, qn, qn, -1.0f);
     return;
   }
-  const int row = p / c.H, col = p - row * c.H;
   const float4 xyz = *(const float4*)((const lego_point_xyzir*)bb.pts + bb.off[b] + o);
   const float range = __builtin_sqrtf(xyz.x * xyz.x + xyz.y * xyz.y + xyz.z * xyz.z);
   const float inten = (float)((double)(float)row + (double)(float)col / 10000.0);  // :250
@@ -343,7 +348,7 @@ void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hip
   dim3 gpts((bb.Nmax + 255) / 256, B), gpix((P + 255) / 256, B), gcol((c.H + 255) / 256, B);
   k_project<<<gpts, 256, 0, s>>>(bb, c);
   tm->mark("ip.pixels", s);
-  k_pixels<<<gpix, 256, 0, s>>>(bb, c);
+  k_pixels<<<dim3((c.H + 63) / 64, (c.N + 3) / 4, B), 256, 0, s>>>(bb, c);
   tm->mark("ip.ground", s);
   k_ground<<<gcol, 256, 0, s>>>(bb, c);
   tm->mark("ip.ccl", s);

@@ -15,7 +15,8 @@
 //                    within 1 m, :1101, :1183), so the 27 cells around a query
 //                    hold every candidate; ties resolve to the lower index.
 //   per LM iteration (<= 10, :1337-1345):
-//     k_mo_rows      one lane per query: pointAssociateToMap (:513-527), 5-NN,
+//     k_mo_rows      one 32-lane group per query: pointAssociateToMap (:513-527), 5-NN
+//                    (a lane per cell of the 3x3x3 block, then a group merge),
 //                    corner line fit (mean, covariance, 3x3 Jacobi, :1093-1174)
 //                    or surf plane fit (5x3 QR, :1176-1227), weight and
 //                    Jacobian row (:1244-1270)
@@ -30,6 +31,7 @@
 // work the reference does on its surrounding map (like-for-like timing).
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <cfloat>
 #include <climits>
 
@@ -75,9 +77,20 @@ __global__ void k_vg_minmax(const float4* in, int n, const int* nDev, VgScratch 
       mx[k] = max(mx[k], __shfl_xor(mx[k], off, 64));
     }
   }
-  if ((threadIdx.x & 63) == 0) {
+  // the block's waves through LDS, then one atomic per block and component
+  // (a few hundred blocks: per-wave atomics on the same six words serialise)
+  __shared__ int red[6][16];
+  const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if ((threadIdx.x & 63) == 0)
 #pragma unroll
-    for (int k = 0; k < 3; ++k) { atomicMin(&v.mm[k], mn[k]); atomicMax(&v.mm[3 + k], mx[k]); }
+    for (int k = 0; k < 3; ++k) { red[k][wave] = mn[k]; red[3 + k][wave] = mx[k]; }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const int k = threadIdx.x;
+    int r = red[k][0];
+    for (int w = 1; w < nw; ++w) r = k < 3 ? min(r, red[k][w]) : max(r, red[k][w]);
+    if (k < 3) atomicMin(&v.mm[k], r);
+    else atomicMax(&v.mm[k], r);
   }
 }
 
@@ -173,7 +186,7 @@ int voxel_grid_device(const float4* in, int n, const int* nDev, float leaf, floa
   }
   if (n > v.cap) return -1;
   k_vg_init<<<1, 64, 0, s>>>(v);
-  k_vg_minmax<<<grid_for(n), 256, 0, s>>>(in, n, nDev, v);
+  k_vg_minmax<<<std::min(grid_for(n), 512), 256, 0, s>>>(in, n, nDev, v);
   k_vg_keys<<<grid_for(n), 256, 0, s>>>(in, n, nDev, leaf, v);
   size_t tb = v.tmpBytes;
   if (hipcub::DeviceRadixSort::SortPairs(v.tmp, tb, v.keys, v.keys2, v.vals, v.vals2, n, 0, 32, s) != hipSuccess)
@@ -246,37 +259,62 @@ int index_build_device(const float4* pts, int n, const int* nDev, MoIndex& ix, c
 }
 
 // The 5 nearest map points with squared distance < 1 (FLANN L2_Simple order),
-// sorted by (distance, index).  Returns how many were found (<= 5).
-__device__ __forceinline__ int knn5(const MoIndex& ix, float4 q, int* oi, float* od) {
+// sorted by (distance, index), found by a 32-lane group: lane l < 27 scans cell
+// l of the 3x3x3 block around the query into its own sorted top 5, then five
+// rounds of a group-wide lexicographic minimum pick the overall five (the
+// result depends only on the (distance, index) order, not on the split).
+// Every lane of the group returns the same list; the count (<= 5) is returned.
+constexpr int kKnnLanes = 32;
+__device__ __forceinline__ bool knn_less(float da, int ia, float db, int ib) {
+  return da < db || (da == db && ia < ib);
+}
+__device__ __forceinline__ int knn5_group(const MoIndex& ix, float4 q, int* oi, float* od) {
+  const int gl = threadIdx.x & (kKnnLanes - 1);
+  float ld[5];
+  int li[5];
   int n = 0;
-  const int cx = cell1(q.x), cy = cell1(q.y), cz = cell1(q.z);
-  for (int dz = -1; dz <= 1; ++dz)
-    for (int dy = -1; dy <= 1; ++dy)
-      for (int dx = -1; dx <= 1; ++dx) {
-        const int bx = cx + dx, by = cy + dy, bz = cz + dz;
-        const unsigned b = mo_cell_hash(bx, by, bz) & (unsigned)(ix.T - 1);
-        const int lo = ix.begin[b], hi = ix.end[b];
-        for (int t = lo; t < hi; ++t) {
-          const float4 p = ix.sorted[t];
-          if (cell1(p.x) != bx || cell1(p.y) != by || cell1(p.z) != bz) continue;  // another cell's bucket mate
-          float d2 = 0.f, d;
-          d = q.x - p.x; d2 += d * d;
-          d = q.y - p.y; d2 += d * d;
-          d = q.z - p.z; d2 += d * d;
-          if (!(d2 < 1.0f)) continue;
-          const int id = __float_as_int(p.w);
-          if (n == 5 && !(d2 < od[4] || (d2 == od[4] && id < oi[4]))) continue;
-          int pos = n < 5 ? n++ : 4;
-          while (pos > 0 && (d2 < od[pos - 1] || (d2 == od[pos - 1] && id < oi[pos - 1]))) {
-            od[pos] = od[pos - 1];
-            oi[pos] = oi[pos - 1];
-            --pos;
-          }
-          od[pos] = d2;
-          oi[pos] = id;
-        }
+  if (gl < 27) {
+    const int bx = cell1(q.x) + gl % 3 - 1, by = cell1(q.y) + (gl / 3) % 3 - 1, bz = cell1(q.z) + gl / 9 - 1;
+    const unsigned b = mo_cell_hash(bx, by, bz) & (unsigned)(ix.T - 1);
+    const int lo = ix.begin[b], hi = ix.end[b];
+    for (int t = lo; t < hi; ++t) {
+      const float4 p = ix.sorted[t];
+      if (cell1(p.x) != bx || cell1(p.y) != by || cell1(p.z) != bz) continue;  // another cell's bucket mate
+      float d2 = 0.f, d;
+      d = q.x - p.x; d2 += d * d;
+      d = q.y - p.y; d2 += d * d;
+      d = q.z - p.z; d2 += d * d;
+      if (!(d2 < 1.0f)) continue;
+      const int id = __float_as_int(p.w);
+      if (n == 5 && !knn_less(d2, id, ld[4], li[4])) continue;
+      int pos = n < 5 ? n++ : 4;
+      while (pos > 0 && knn_less(d2, id, ld[pos - 1], li[pos - 1])) {
+        ld[pos] = ld[pos - 1];
+        li[pos] = li[pos - 1];
+        --pos;
       }
-  return n;
+      ld[pos] = d2;
+      li[pos] = id;
+    }
+  }
+  int head = 0, found = 0;
+  for (int r = 0; r < 5; ++r) {
+    float cd = head < n ? ld[head] : FLT_MAX;
+    int ci = head < n ? li[head] : INT_MAX;
+    float md = cd;
+    int mi = ci;
+    for (int o = kKnnLanes / 2; o > 0; o >>= 1) {
+      const float d2 = __shfl_xor(md, o, kKnnLanes);
+      const int i2 = __shfl_xor(mi, o, kKnnLanes);
+      if (knn_less(d2, i2, md, mi)) { md = d2; mi = i2; }
+    }
+    if (mi == INT_MAX) break;  // fewer than five points within 1 m
+    od[r] = md;
+    oi[r] = mi;
+    ++found;
+    if (head < n && ci == mi) ++head;  // indices are unique: exactly one lane advances
+  }
+  return found;
 }
 
 // ---------------------------------------------------------------- state
@@ -428,23 +466,21 @@ __device__ __forceinline__ float4 associate_to_map(float4 pi, const MoState* st)
                      pi.w);
 }
 
-// One lane per query: corner queries [0, nCornerDS), then surf+outlier
-// queries.  Row r = {arx, ary, arz, cf.x, cf.y, cf.z, B, valid}.
-__global__ void k_mo_rows(MoState* st, const MoCounts* cnt, const float4* cornerDS, const float4* surfTotalDS,
-                          MoIndex cornerIx, MoIndex surfIx, const float4* cornerMap, const float4* surfMap,
-                          float* rows, int qcap) {
-  if (!st->optimized || st->converged) return;
-  const int nC = cnt->cornerDS, nS = cnt->surfTotalDS;
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= nC + nS || q >= qcap) return;
+// One 32-lane group per query: corner queries [0, nCornerDS), then
+// surf+outlier queries.  Row r = {arx, ary, arz, cf.x, cf.y, cf.z, B, valid},
+// written by the group's lane 0 (the fit runs on every lane of the group).
+__device__ __forceinline__ void mo_row(MoState* st, int nC, const float4* cornerDS, const float4* surfTotalDS,
+                                       const MoIndex& cornerIx, const MoIndex& surfIx, const float4* cornerMap,
+                                       const float4* surfMap, float* rows, int q) {
+  const bool lead = (threadIdx.x & (kKnnLanes - 1)) == 0;
   float* row = rows + (size_t)q * 8;
-  row[7] = 0.f;
+  if (lead) row[7] = 0.f;
   const bool corner = q < nC;
   const float4 po = corner ? cornerDS[q] : surfTotalDS[q - nC];
   const float4 sel = associate_to_map(po, st);
   int ind[5];
   float sq[5];
-  if (knn5(corner ? cornerIx : surfIx, sel, ind, sq) < 5) return;
+  if (knn5_group(corner ? cornerIx : surfIx, sel, ind, sq) < 5) return;
   float4 cf;
   if (corner) {  // cornerOptimization :1093-1174
     float cx = 0, cy = 0, cz = 0;
@@ -519,10 +555,25 @@ __global__ void k_mo_rows(MoState* st, const MoCounts* cnt, const float4* corner
   const float arz = ((crz * srx * sry - cry * srz) * po.x + (-cry * crz - srx * sry * srz) * po.y) * cf.x +
                     (crx * crz * po.x - crx * srz * po.y) * cf.y +
                     ((sry * srz + cry * crz * srx) * po.x + (crz * sry - cry * srx * srz) * po.y) * cf.z;
+  if (!lead) return;
   row[0] = arx; row[1] = ary; row[2] = arz;
   row[3] = cf.x; row[4] = cf.y; row[5] = cf.z;
   row[6] = -cf.w;
   row[7] = 1.f;
+}
+
+constexpr int kMoRowsThreads = 256;
+__global__ void __launch_bounds__(kMoRowsThreads) k_mo_rows(MoState* st, const MoCounts* cnt, const float4* cornerDS,
+                                                           const float4* surfTotalDS, MoIndex cornerIx,
+                                                           MoIndex surfIx, const float4* cornerMap,
+                                                           const float4* surfMap, float* rows, int qcap) {
+  if (!st->optimized || st->converged) return;
+  const int nC = cnt->cornerDS, nQ = min(nC + cnt->surfTotalDS, qcap);
+  constexpr int kGroups = kMoRowsThreads / kKnnLanes;
+  for (int q0 = blockIdx.x * kGroups; q0 < nQ; q0 += gridDim.x * kGroups) {  // group-uniform
+    const int q = q0 + (int)threadIdx.x / kKnnLanes;
+    if (q < nQ) mo_row(st, nC, cornerDS, surfTotalDS, cornerIx, surfIx, cornerMap, surfMap, rows, q);
+  }
 }
 
 // ---------------------------------------------------------------- LM solve
@@ -877,7 +928,8 @@ int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, h
   if (qcap > m.rowCap) return -1;
   for (int it = 0; it < 10; ++it) {
     if (qcap > 0)
-      k_mo_rows<<<grid_for(qcap, 128), 128, 0, s>>>(m.st, m.cnt, m.cornerDS, m.surfTotalDS, m.cornerIx, m.surfIx,
+      k_mo_rows<<<grid_for(qcap, kMoRowsThreads / kKnnLanes), kMoRowsThreads, 0, s>>>(
+          m.st, m.cnt, m.cornerDS, m.surfTotalDS, m.cornerIx, m.surfIx,
                                                    m.cornerMapDS, m.surfMapDS, m.rows, qcap);
     k_mo_solve<<<1, kMoSolveThreads, 0, s>>>(m.st, m.cnt, m.rows, qcap, it);
   }
