@@ -460,6 +460,11 @@ int lego_stage_times(lego_ctx* ctx, const char** names, float* ms, int32_t cap,
  *  nn query, -, #shell-1 queries, #brute-force queries, then group-0 splits of
  *  the NN loop: to_start, grid NN, scan-line, #queries; 12 spare}. */
 int lego_odom_profile(lego_ctx* ctx, int32_t enable, uint64_t* out32);
+/* Diagnostic phase stamps of the feature-extraction kernel (one workgroup per
+ * scan and ring), summed over workgroups while lego_odom_profile stamping is
+ * on (wall clock at 100 MHz): {window load + sector sorts, picking walk,
+ * picked copies + less-flat set, per-ring VoxelGrid, #rings, 3 spare}. */
+int lego_extract_profile(lego_ctx* ctx, uint64_t* out8);
 
 #ifdef __cplusplus
 }

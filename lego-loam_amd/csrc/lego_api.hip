@@ -491,7 +491,7 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
     x->h_resetSt[i].frameCount = cfg->skip_frame_num;  // frameCount = skipFrameNum (:314)
     x->h_resetCarry[i] = FaCarry{};  // fresh member arrays: phantom {0.0f, 0}, picked[0] = 0
   }
-  A(x->d_prof, 32);
+  A(x->d_prof, 40);  // [0, 32) k_odom phases, [32, 40) k_extract phases
 #undef A
   bb.pts = x->d_pts;
   bb.off = x->d_off;
@@ -725,6 +725,7 @@ static int submit_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t*
   StageTimer& otm = x->sotm[h];
   tm.enabled = otm.enabled = x->tm.enabled;
   HIPCHK(hipMemsetAsync(bb.bad, 0, sizeof(int) * B, x->stream));
+  bb.xprof = x->profOn ? x->d_prof + 32 : nullptr;
   tm.begin();
   otm.begin();
   launch_ip(bb, x->dc, B, 0, x->stream, &tm);
@@ -1772,8 +1773,15 @@ int lego_odom_profile(lego_ctx* x, int32_t enable, uint64_t* out32) {
   }
   if (enable >= 0) {
     x->profOn = enable != 0;
-    HIPCHK(hipMemset(x->d_prof, 0, 32 * sizeof(uint64_t)));
+    HIPCHK(hipMemset(x->d_prof, 0, 40 * sizeof(uint64_t)));
   }
+  return LEGO_OK;
+}
+
+int lego_extract_profile(lego_ctx* x, uint64_t* out8) {
+  if (!x || !out8) return LEGO_E_ARG;
+  HIPCHK(hipSetDevice(x->device));
+  HIPCHK(hipMemcpy(out8, x->d_prof + 32, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return LEGO_OK;
 }
 

@@ -135,6 +135,7 @@ struct BatchBufs {
   int* r_cnt;                // [B*N*4]
   FaCarry* spec_out;         // [B] carry produced under S*
   int* fa_flags;             // [B]
+  unsigned long long* xprof; // k_extract phase stamps (lego_extract_profile) or nullptr
   float4* f_sharp;           // [B*N*12]
   float4* f_lsharp;          // [B*N*120]
   float4* f_flat;            // [B*N*24]

@@ -396,6 +396,15 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ns = bb.ns[b];
   const int s = bb.sri[b * c.N + ring], e = bb.eri[b * c.N + ring];
+  unsigned long long* const xp = bb.xprof;  // diagnostic phase stamps (thread 0, 100 MHz)
+  unsigned long long tp = (xp && tid == 0) ? wall_clock64() : 0;
+  auto stamp = [&](int slot) {
+    if (xp && tid == 0) {
+      const unsigned long long now = wall_clock64();
+      atomicAdd(xp + slot, now - tp);
+      tp = now;
+    }
+  };
   RingCtx R;
   R.b = b; R.ring = ring; R.ns = ns;
   R.base = (size_t)b * c.P;
@@ -491,6 +500,7 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
     wave_sync_lds();  // the scratch is refilled for the wave's next sector
   }
   __syncthreads();
+  stamp(0);  // window load + the six sector sorts
   const int newph = L.misc[M_PH];
   // picked indices in pick order (sharp, less sharp, flat), in the sort
   // scratch, which is free until the VoxelGrid keys
@@ -570,6 +580,7 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
     if (lane == 0) { L.misc[M_NSH] = nsh; L.misc[M_NLS] = nls; L.misc[M_NFL] = nfl; }
   }
   __syncthreads();
+  stamp(1);  // the serial picking walk (wave 0)
   {  // the picked points in pick order, all loads independent
     const int nsh = L.misc[M_NSH], nls = L.misc[M_NLS], nfl = L.misc[M_NFL];
     for (int t = tid; t < nsh + nls + nfl; t += blockDim.x) {
@@ -606,6 +617,7 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
       __syncthreads();
     }
   }
+  stamp(2);  // picked-point copies + the ordered less-flat set
   // ---- per-ring VoxelGrid 0.2 m on the less-flat set (:778-782)
   const int K = L.misc[M_LF];
   const float inv = 1.0f / 0.2f;
@@ -689,6 +701,8 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
     nlf = outc;
   }
   __syncthreads();
+  stamp(3);  // the VoxelGrid (bounds, keys, sort, centroids)
+  if (xp && tid == 0) atomicAdd(xp + 4, 1ull);
   if (tid == 0) {
     int* cnt = bb.r_cnt + ((size_t)b * c.N + ring) * 4;
     cnt[0] = L.misc[M_NSH];

@@ -273,7 +273,7 @@ HIP_EXPORTS = ["lego_sensor_preset", "lego_create", "lego_fleet_create", "lego_d
                "lego_odom_batch_pc2", "lego_pc2_encode_xyzi", "lego_cloud_info_serialize",
                "lego_fusion_odometry", "lego_fusion_aft_mapped",
                "lego_mo_set_map", "lego_mo_configure", "lego_mo_process", "lego_mo_loop_closure", "lego_last_error", "lego_stage_times",
-               "lego_odom_profile", "lego_handoff_pack", "lego_handoff_pack_into", "lego_handoff_unpack", "lego_comm_unique_id",
+               "lego_odom_profile", "lego_extract_profile", "lego_handoff_pack", "lego_handoff_pack_into", "lego_handoff_unpack", "lego_comm_unique_id",
                "lego_comm_create", "lego_comm_destroy", "lego_comm_gather_handoff", "lego_comm_handoff"]
 
 
@@ -321,6 +321,7 @@ def hip_lib() -> C.CDLL:
     lib.lego_comm_handoff.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]
     lib.lego_last_error.restype = C.c_char_p
     lib.lego_odom_profile.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
+    lib.lego_extract_profile.argtypes = [C.c_void_p, C.c_void_p]
     lib.lego_stage_times.argtypes = [C.c_void_p, C.POINTER(C.c_char_p), f32p, C.c_int32,
                                      C.POINTER(C.c_int32)]
     return lib

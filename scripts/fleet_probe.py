@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--distinct", type=int, default=4)
     ap.add_argument("--workgroups", type=int, default=0)
+    ap.add_argument("--extract-profile", action="store_true", help="k_extract phase stamps (diagnostic)")
     args = ap.parse_args()
     import torch
 
@@ -61,6 +62,8 @@ def main():
         d_pts, d_off, st = wins[0]
         fl.odom_batch_device(d_pts.data_ptr(), d_off.data_ptr(), st, S * K, recs)  # warm-up
         torch.cuda.synchronize()
+        if args.extract_profile:
+            lib.lego_odom_profile(fl.h, 1, None)
         t0 = time.perf_counter()
         for i in range(args.steps):
             d_pts, d_off, st = wins[1 + i]
@@ -68,10 +71,19 @@ def main():
         dt = time.perf_counter() - t0
         stg = fl.stage_times()
         valid = sum(r.odom_valid for r in recs)
+        xph = None
+        if args.extract_profile:
+            xp = (C.c_uint64 * 8)()
+            lib.lego_extract_profile(fl.h, xp)
+            rings = max(xp[4], 1)
+            xph = {nm: round(xp[i] / 100.0 / rings, 2) for i, nm in
+                   enumerate(("sorts", "picking", "copies+lessflat", "voxelgrid"))}
+            xph["rings"] = xp[4]
         fl.close()
         print(json.dumps({"streams": S, "k": K, "scans_per_s": S * K * args.steps / dt,
                           "ms_per_call": dt / args.steps * 1e3, "valid_last": valid,
-                          "stages_ms_last": {k: round(v, 3) for k, v in stg.items()}}), flush=True)
+                          "stages_ms_last": {k: round(v, 3) for k, v in stg.items()},
+                          "extract_us_per_ring_workgroup": xph}), flush=True)
         del wins
 
 
