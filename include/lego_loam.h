@@ -463,7 +463,9 @@ int lego_odom_profile(lego_ctx* ctx, int32_t enable, uint64_t* out32);
 /* Diagnostic phase stamps of the feature-extraction kernel (one workgroup per
  * scan and ring), summed over workgroups while lego_odom_profile stamping is
  * on (wall clock at 100 MHz): {window load + sector sorts, picking walk,
- * picked copies + less-flat set, per-ring VoxelGrid, #rings, 3 spare}. */
+ * picked copies + less-flat set, per-ring VoxelGrid, #rings, #sector
+ * re-walks of the speculative picking, #rings picked speculatively, sum over
+ * workgroups of the workgroups in flight when each started}. */
 int lego_extract_profile(lego_ctx* ctx, uint64_t* out8);
 
 #ifdef __cplusplus

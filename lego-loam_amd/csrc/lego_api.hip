@@ -491,7 +491,7 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
     x->h_resetSt[i].frameCount = cfg->skip_frame_num;  // frameCount = skipFrameNum (:314)
     x->h_resetCarry[i] = FaCarry{};  // fresh member arrays: phantom {0.0f, 0}, picked[0] = 0
   }
-  A(x->d_prof, 40);  // [0, 32) k_odom phases, [32, 40) k_extract phases
+  A(x->d_prof, 48);  // [0, 32) k_odom phases, [32, 40) k_extract phases, [40] its in-flight counter
 #undef A
   bb.pts = x->d_pts;
   bb.off = x->d_off;
@@ -1773,7 +1773,7 @@ int lego_odom_profile(lego_ctx* x, int32_t enable, uint64_t* out32) {
   }
   if (enable >= 0) {
     x->profOn = enable != 0;
-    HIPCHK(hipMemset(x->d_prof, 0, 40 * sizeof(uint64_t)));
+    HIPCHK(hipMemset(x->d_prof, 0, 48 * sizeof(uint64_t)));
   }
   return LEGO_OK;
 }

@@ -239,7 +239,9 @@ __host__ __device__ inline int next_pow2(int x) {
 // The sectors are sorted in per-wave scratch buffers (one sector per wave at a
 // time) and kept as index permutations (uint16, the ring window's positions);
 // the scratch region is reused by the VoxelGrid keys after the picking.
-__host__ __device__ inline int extract_sector_cap(int H) { return next_pow2((H + 32) / 6 + 2); }
+// a sector of n <= (H + 32) / 6 + 2 entries plus the fallback sort's stack
+// (kIntroStack words) behind it
+__host__ __device__ inline int extract_sector_cap(int H) { return next_pow2((H + 32) / 6 + 2 + (kIntroStack + 1) / 2); }
 __host__ __device__ inline size_t extract_sort_region(int H) {
   const size_t W = (size_t)H + 32;
   const size_t vox = (size_t)next_pow2((int)W) * 8;
@@ -280,7 +282,9 @@ __device__ __forceinline__ ExtractLds carve(unsigned char* base, int H) {
 }
 
 enum { M_TIE = 0, M_LF = 1, M_OVF = 2, M_NSH = 3, M_NLS = 4, M_NFL = 5, M_D0 = 6, M_D1 = 7,
-       M_MB0 = 8, M_MB1 = 9, M_MB2 = 10, M_PH = 11, M_WOFF = 16 };
+       M_MB0 = 8, M_MB1 = 9, M_MB2 = 10, M_PH = 11, M_REWALK = 12, M_WOFF = 16, M_SEC = 24, M_NEF = 48 };
+// per-sector pick list: 2 sharp, 20 less sharp, 4 flat (featureAssociation.cpp:709-748)
+constexpr int kPickListStride = 32;
 
 // Bitonic sort of m (power of two) entries in LDS by value, all threads.
 __device__ __forceinline__ void bitonic_entries(SmoothEntry* a, int m) {
@@ -331,6 +335,50 @@ __device__ __forceinline__ void bitonic_u64(unsigned long long* a, int m) {
       __syncthreads();
     }
   }
+}
+
+// The same network with the block barriers only where a pass crosses waves:
+// wave w owns the aligned chunk [w*C, (w+1)*C), C = m / waves, and every pass
+// with j < C pairs elements inside one chunk, so the wave that owns the chunk
+// runs it alone behind a wave-level LDS fence.  Only the passes with j >= C
+// (log2(waves) per merge stage above C) sit between two __syncthreads: for
+// m = 2048 on 4 waves that is 3 block passes instead of 66.  Same compare-
+// exchange sequence per element pair as bitonic_u64, so the result is the
+// same sorted array (the keys are unique).
+__device__ __forceinline__ void bitonic_u64_chunked(unsigned long long* a, int m) {
+  const int nw = blockDim.x >> 6, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int C = m / nw;
+  if (C < 128) {
+    bitonic_u64(a, m);
+    return;
+  }
+  unsigned long long* w = a + wave * C;
+  const int base = wave * C;
+  for (int k = 2; k <= m; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j >= C) {
+        __syncthreads();
+        for (int t = threadIdx.x; t < m / 2; t += blockDim.x) {
+          const int i = (t / j) * 2 * j + (t % j);
+          const int l = i + j;
+          const bool up = (i & k) == 0;
+          const unsigned long long x = a[i], y = a[l];
+          if ((x > y) == up) { a[i] = y; a[l] = x; }
+        }
+        __syncthreads();
+      } else {
+        for (int t = lane; t < C / 2; t += 64) {
+          const int i = (t / j) * 2 * j + (t % j);
+          const int l = i + j;
+          const bool up = ((base + i) & k) == 0;
+          const unsigned long long x = w[i], y = w[l];
+          if ((x > y) == up) { w[i] = y; w[l] = x; }
+        }
+        wave_sync_lds();
+      }
+    }
+  }
+  __syncthreads();
 }
 
 // Ordered block compaction helper: returns this thread's exclusive rank among
@@ -398,6 +446,7 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
   const int s = bb.sri[b * c.N + ring], e = bb.eri[b * c.N + ring];
   unsigned long long* const xp = bb.xprof;  // diagnostic phase stamps (thread 0, 100 MHz)
   unsigned long long tp = (xp && tid == 0) ? wall_clock64() : 0;
+  if (xp && tid == 0) atomicAdd(xp + 7, atomicAdd(xp + 8, 1ull) + 1);  // workgroups in flight
   auto stamp = [&](int slot) {
     if (xp && tid == 0) {
       const unsigned long long now = wall_clock64();
@@ -450,17 +499,78 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
   };
   // ---- the six sector sorts, one wave per sector at a time (they do not
   // depend on the picking; only the picking runs in sector order).  Each is
-  // sorted in its wave's scratch and kept as window positions in perm (the
-  // phantom entry of ring 0, whose index is the carried one, as 0xFFFF).
+  // sorted in its wave's scratch and kept as window positions in perm.
+  //
+  // Rings other than ring 0 sort only what a walk can pick: the edge walk
+  // (:704-734) takes points with curvature > edge_thr off the ground, the flat
+  // walk (:736-769) points with curvature < surf_thr on the ground, and it
+  // passes over every other point without effect.  So the edge candidates
+  // and the flat candidates are each sorted by value alone and kept back to
+  // back in perm (counts in misc): the walks over them see the candidates in
+  // the same order as over the whole sorted sector.  Equal values within a
+  // candidate list fall back to std::sort of the whole sector, filtered in
+  // its order.  Ring 0 sorts the whole sector: its phantom entry (the carried
+  // index, perm 0xFFFF) is not a position of the sector.
   const int nw = blockDim.x >> 6;
   constexpr int kPhantom = -2;
   const int secCap = extract_sector_cap(c.H);
+  const bool filtered = ring != 0;
   for (int j = wave; j < 6; j += nw) {
     int sp, ep, off;
     sector(j, &sp, &ep, &off);
     if (sp >= ep) continue;
-    const int n = ep - sp, m = next_pow2(n);
+    const int n = ep - sp;
     SmoothEntry* a = L.srt + wave * secCap;
+    uint16_t* pm = L.perm + (sp - s);
+    if (filtered) {
+      int nl[2] = {0, 0};
+      for (int list = 0; list < 2; ++list) {
+        auto cand = [&](int w, float v) {
+          return list == 0 ? (v > c.edge_thr && L.gfl[w] == 0) : (v < c.surf_thr && L.gfl[w] == 1);
+        };
+        int cnt = 0;
+        for (int t0 = 0; t0 < n; t0 += 64) {  // ordered wave compaction
+          const int t = t0 + lane;
+          bool f = false;
+          float v = 0.0f;
+          if (t < n) {
+            v = L.curv[sp + t - R.lo];
+            f = cand(sp + t - R.lo, v);
+          }
+          const unsigned long long msk = __ballot(f);
+          if (f) a[cnt + __popcll(msk & ((1ull << lane) - 1))] = SmoothEntry{v, sp + t};
+          cnt += __popcll(msk);
+        }
+        nl[list] = cnt;
+        if (cnt == 0) continue;
+        const int m = next_pow2(cnt);
+        for (int t = cnt + lane; t < m; t += 64) a[t] = {__builtin_inff(), INT_MAX};
+        wave_sync_lds();
+        wave_bitonic_entries(a, m);
+        bool tie = false;
+        for (int t = lane; t < cnt - 1; t += 64) tie |= a[t].value == a[t + 1].value;
+        uint16_t* out = pm + (list == 0 ? 0 : nl[0]);
+        if (__ballot(tie)) {
+          if (lane == 0) {
+            atomicOr(&bb.fa_flags[b], LEGO_REC_SORT_TIES);  // the record shows the fallback ran
+            for (int t = 0; t < n; ++t) a[t] = SmoothEntry{L.curv[sp + t - R.lo], sp + t};
+            std_sort_by_value(a, n, (uint32_t*)(a + n));  // stack in the scratch behind the sector
+            int k = 0;
+            for (int t = 0; t < n; ++t)
+              if (cand(a[t].ind - R.lo, a[t].value)) out[k++] = (uint16_t)(a[t].ind - R.lo);
+          }
+        } else {
+          for (int t = lane; t < cnt; t += 64) out[t] = (uint16_t)(a[t].ind - R.lo);
+        }
+        wave_sync_lds();  // the scratch is refilled for the next list
+      }
+      if (lane == 0) {
+        L.misc[M_NEF + 2 * j] = nl[0];
+        L.misc[M_NEF + 2 * j + 1] = nl[1];
+      }
+      continue;
+    }
+    const int m = next_pow2(n);
     const bool phantom_here = (ring == 0 && sp <= 4 && 4 < ep);
     for (int t = lane; t < m; t += 64) {
       SmoothEntry en;
@@ -484,11 +594,10 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
           const int pos = sp + t;
           a[t] = (phantom_here && pos == 4) ? SmoothEntry{0.0f, kPhantom} : SmoothEntry{L.curv[pos - R.lo], pos};
         }
-        std_sort_by_value(a, n);
+        std_sort_by_value(a, n, (uint32_t*)(a + n));  // stack in the scratch behind the sector
       }
       wave_sync_lds();
     }
-    uint16_t* pm = L.perm + (sp - s);
     for (int t = lane; t < n; t += 64) {
       const int ind = a[t].ind;
       pm[t] = ind == kPhantom ? (uint16_t)0xFFFF : (uint16_t)(ind - R.lo);
@@ -502,92 +611,193 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
   __syncthreads();
   stamp(0);  // window load + the six sector sorts
   const int newph = L.misc[M_PH];
-  // picked indices in pick order (sharp, less sharp, flat), in the sort
-  // scratch, which is free until the VoxelGrid keys
-  volatile int* pk = (volatile int*)L.srt;
-  static_assert((kSharpPerRing + kLessSharpPerRing + kFlatPerRing) * 4 <= 16384, "pick lists fit the scratch");
-  // ---- picking, sector by sector (wave 0): edge scan k = ep .. sp, then
-  // flat scan k = sp .. ep (:699-769)
-  if (wave == 0) {
+  // per-sector pick lists (sharp, less sharp, flat) in pick order, in the
+  // sort scratch, which is free until the VoxelGrid keys; the counts and the
+  // spill masks in misc
+  int* const pk = (int*)L.srt;
+  static_assert(6 * kPickListStride * 4 <= 1024, "pick lists fit the scratch head");
+  // ---- picking (:699-769).  Sector j's walk only interacts with sector j+1
+  // through the suppression of its picks near ep_j (positions sp_{j+1} ..
+  // sp_{j+1}+4).  Rings other than ring 0 (whose phantom entry may point
+  // anywhere in the window) with every sector at least 8 long run the six
+  // walks speculatively in parallel (one wave per sector, suppression kept
+  // inside the sector and the rest recorded as spill bits), then validate in
+  // sector order: sector j's walk is exactly the serial one unless sector
+  // j-1's final spill marks a position that sector j's walk picked (a position
+  // the walk reached and found eligible; one it skipped or never reached
+  // changes nothing).  Such a sector is re-walked by wave 0 from its initial
+  // state plus the spill.  Ring 0 and short rings walk serially on wave 0.
+  bool parallel = !(ring == 0);
+  for (int j = 0; j < 6 && parallel; ++j) {
+    int sp, ep, off;
+    sector(j, &sp, &ep, &off);
+    parallel = ep - sp >= 8;
+  }
+  if (parallel) {  // the initial picked state, for re-walks
+    uint8_t* p0 = (uint8_t*)L.srt + 1024;
+    for (int t = tid; t < R.Wn; t += blockDim.x) p0[t] = picked[t];
+  }
+  if (tid < 6 * 4) L.misc[M_SEC + tid] = 0;
+  __syncthreads();
+  auto walk = [&](int j, bool local) {
+    int sp, ep, off;
+    sector(j, &sp, &ep, &off);
+    if (sp >= ep) return;
+    int* const lst = pk + j * kPickListStride;
+    int* const cnt3 = L.misc + M_SEC + 4 * j;
+    const int lo = local ? sp - R.lo : 0, hi = local ? ep - R.lo : R.Wn - 1;
+    const uint16_t* srt = L.perm + (sp - s);
+    // the walks' items: position ep (scanned, never sorted, :699-702) first
+    // in the edge walk and last in the flat walk, the sorted entries between
+    const int nE = filtered ? L.misc[M_NEF + 2 * j] : 0, nF = filtered ? L.misc[M_NEF + 2 * j + 1] : 0;
+    const int nEdge = filtered ? nE + 1 : ep - sp + 1, nFlat = filtered ? nF + 1 : ep - sp + 1;
+    auto edge_item = [&](int q) {
+      if (!filtered) return entry_ind(srt, sp, ep, ep - q, R.lo, ph);
+      return q == 0 ? ep : (int)srt[nE - q] + R.lo;
+    };
+    auto flat_item = [&](int q) {
+      if (!filtered) return entry_ind(srt, sp, ep, sp + q, R.lo, ph);
+      return q == nF ? ep : (int)srt[nE + q] + R.lo;
+    };
     int nsh = 0, nls = 0, nfl = 0;
-    for (int j = 0; j < 6; j++) {
-      int sp, ep, off;
-      sector(j, &sp, &ep, &off);
-      if (sp >= ep) continue;
-      const uint16_t* srt = L.perm + (sp - s);
-      {
-        int cnt = 0;
-        bool done = false;
-        for (int base = ep; base >= sp && !done; base -= 64) {
-          const int k = base - lane;
-          bool act = k >= sp;
-          const int ind = act ? entry_ind(srt, sp, ep, k, R.lo, ph) : -1;
-          if (act && !in_win(R, ind)) { act = false; flags |= 1; }
-          while (true) {
-            bool el = false;
-            if (act) {
-              const int w = ind - R.lo;
-              el = picked[w] == 0 && L.curv[w] > c.edge_thr && L.gfl[w] == 0;
-            }
-            const unsigned long long msk = __ballot(el);
-            if (msk == 0) break;
-            const int l = __ffsll((long long)msk) - 1;
-            cnt++;
-            if (cnt > 20) { done = true; break; }
-            if (lane == l) {  // the points are copied after the picking (no HBM latency per pick)
-              const int w = ind - R.lo;
-              label[w] = cnt <= 2 ? 2 : 1;
-              if (cnt <= 2) pk[nsh] = ind;
-              pk[kSharpPerRing + nls] = ind;
-              suppress(R, picked, L.col, ind);
-            }
-            if (cnt <= 2) nsh++;
-            nls++;
-            act = act && lane > l;
-          }
-        }
+    unsigned spill = 0;  // bit i: position ep+1+i suppressed; bit 8+i: sp-1-i
+    auto sup = [&](int ind) {
+      const int w = ind - R.lo;
+      picked[w] = 1;
+      for (int l = 1; l <= 5; l++) {
+        const int q = w + l;
+        if (q >= R.Wn) break;
+        if (abs((int)L.col[q] - (int)L.col[q - 1]) > 10) break;
+        if (q <= hi) picked[q] = 1;
+        else spill |= 1u << (q - hi - 1);
       }
-      {
-        int cnt = 0;
-        bool done = false;
-        for (int base = sp; base <= ep && !done; base += 64) {
-          const int k = base + lane;
-          bool act = k <= ep;
-          const int ind = act ? entry_ind(srt, sp, ep, k, R.lo, ph) : -1;
-          if (act && !in_win(R, ind)) { act = false; flags |= 1; }
-          while (true) {
-            bool el = false;
-            if (act) {
-              const int w = ind - R.lo;
-              el = picked[w] == 0 && L.curv[w] < c.surf_thr && L.gfl[w] == 1;
-            }
-            const unsigned long long msk = __ballot(el);
-            if (msk == 0) break;
-            const int l = __ffsll((long long)msk) - 1;
-            if (lane == l) {
-              label[ind - R.lo] = -1;
-              pk[kSharpPerRing + kLessSharpPerRing + nfl] = ind;
-            }
-            nfl++;
-            cnt++;
-            if (cnt >= 4) { done = true; break; }
-            if (lane == l) suppress(R, picked, L.col, ind);
-            act = act && lane > l;
+      for (int l = -1; l >= -5; l--) {
+        const int q = w + l;
+        if (ind + l < 0 || q < 0) break;
+        if (abs((int)L.col[q] - (int)L.col[q + 1]) > 10) break;
+        if (q >= lo) picked[q] = 1;
+        else spill |= 1u << (8 + lo - 1 - q);
+      }
+    };
+    {
+      int cnt = 0;
+      bool done = false;
+      for (int q0 = 0; q0 < nEdge && !done; q0 += 64) {
+        const int q = q0 + lane;
+        bool act = q < nEdge;
+        const int ind = act ? edge_item(q) : -1;
+        if (act && !in_win(R, ind)) { act = false; flags |= 1; }
+        while (true) {
+          bool el = false;
+          if (act) {
+            const int w = ind - R.lo;
+            el = picked[w] == 0 && L.curv[w] > c.edge_thr && L.gfl[w] == 0;
           }
+          const unsigned long long msk = __ballot(el);
+          if (msk == 0) break;
+          const int l = __ffsll((long long)msk) - 1;
+          cnt++;
+          if (cnt > 20) { done = true; break; }
+          if (lane == l) {  // the points are copied after the picking (no HBM latency per pick)
+            label[ind - R.lo] = cnt <= 2 ? 2 : 1;
+            if (cnt <= 2) lst[nsh] = ind;
+            lst[2 + nls] = ind;
+            sup(ind);
+          }
+          if (cnt <= 2) nsh++;
+          nls++;
+          act = act && lane > l;
         }
       }
     }
-    if (lane == 0) { L.misc[M_NSH] = nsh; L.misc[M_NLS] = nls; L.misc[M_NFL] = nfl; }
+    {
+      int cnt = 0;
+      bool done = false;
+      for (int q0 = 0; q0 < nFlat && !done; q0 += 64) {
+        const int q = q0 + lane;
+        bool act = q < nFlat;
+        const int ind = act ? flat_item(q) : -1;
+        if (act && !in_win(R, ind)) { act = false; flags |= 1; }
+        while (true) {
+          bool el = false;
+          if (act) {
+            const int w = ind - R.lo;
+            el = picked[w] == 0 && L.curv[w] < c.surf_thr && L.gfl[w] == 1;
+          }
+          const unsigned long long msk = __ballot(el);
+          if (msk == 0) break;
+          const int l = __ffsll((long long)msk) - 1;
+          if (lane == l) {
+            label[ind - R.lo] = -1;
+            lst[22 + nfl] = ind;
+          }
+          nfl++;
+          cnt++;
+          if (cnt >= 4) { done = true; break; }
+          if (lane == l) sup(ind);
+          act = act && lane > l;
+        }
+      }
+    }
+    unsigned sm = 0;
+    for (int bit = 0; bit < 16; ++bit)
+      if (__ballot((spill >> bit) & 1u)) sm |= 1u << bit;
+    if (lane == 0) { cnt3[0] = nsh; cnt3[1] = nls; cnt3[2] = nfl; cnt3[3] = (int)sm; }
+    wave_sync_lds();
+  };
+  if (parallel) {
+    for (int j = wave; j < 6; j += nw) walk(j, true);
+    __syncthreads();
+    if (wave == 0) {
+      const uint8_t* p0 = (const uint8_t*)L.srt + 1024;
+      for (int j = 1; j < 6; ++j) {
+        int sp, ep, off;
+        sector(j, &sp, &ep, &off);
+        const unsigned in = (unsigned)L.misc[M_SEC + 4 * (j - 1) + 3] & 0x1fu;
+        bool bad = false;
+        for (int i = 0; i < 5; ++i) bad |= ((in >> i) & 1u) && label[sp + i - R.lo] != 0;
+        if (!bad) continue;
+        // re-walk: the sector's initial state plus the spill, labels cleared
+        for (int t = sp + lane; t <= ep; t += 64) {
+          const int w = t - R.lo;
+          picked[w] = p0[w] | ((t - sp < 5 && ((in >> (t - sp)) & 1u)) ? 1 : 0);
+          label[w] = 0;
+        }
+        wave_sync_lds();
+        if (lane == 0) atomicAdd(&L.misc[M_REWALK], 1);
+        walk(j, true);
+      }
+    }
+  } else if (wave == 0) {
+    for (int j = 0; j < 6; j++) walk(j, false);
   }
   __syncthreads();
-  stamp(1);  // the serial picking walk (wave 0)
-  {  // the picked points in pick order, all loads independent
-    const int nsh = L.misc[M_NSH], nls = L.misc[M_NLS], nfl = L.misc[M_NFL];
-    for (int t = tid; t < nsh + nls + nfl; t += blockDim.x) {
-      if (t < nsh) R.osh[t] = bb.dsk[R.base + pk[t]];
-      else if (t < nsh + nls) R.ols[t - nsh] = bb.dsk[R.base + pk[kSharpPerRing + t - nsh]];
-      else R.ofl[t - nsh - nls] = bb.dsk[R.base + pk[kSharpPerRing + kLessSharpPerRing + t - nsh - nls]];
+  stamp(1);  // the picking walks
+  if (xp && tid == 0) {
+    atomicAdd(xp + 5, (unsigned long long)L.misc[M_REWALK]);
+    if (parallel) atomicAdd(xp + 6, 1ull);
+  }
+  {  // the picked points in pick order (sector by sector), all loads independent
+    int nsh = 0, nls = 0, nfl = 0;
+    for (int j = 0; j < 6; ++j) {
+      nsh += L.misc[M_SEC + 4 * j];
+      nls += L.misc[M_SEC + 4 * j + 1];
+      nfl += L.misc[M_SEC + 4 * j + 2];
     }
+    auto at = [&](int t, int which, int head) {  // t-th entry of list `which` over the sectors
+      for (int j = 0;; ++j) {
+        const int n = L.misc[M_SEC + 4 * j + which];
+        if (t < n || j == 5) return pk[j * kPickListStride + head + t];
+        t -= n;
+      }
+    };
+    for (int t = tid; t < nsh + nls + nfl; t += blockDim.x) {
+      if (t < nsh) R.osh[t] = bb.dsk[R.base + at(t, 0, 0)];
+      else if (t < nsh + nls) R.ols[t - nsh] = bb.dsk[R.base + at(t - nsh, 1, 2)];
+      else R.ofl[t - nsh - nls] = bb.dsk[R.base + at(t - nsh - nls, 2, 22)];
+    }
+    __syncthreads();
+    if (tid == 0) { L.misc[M_NSH] = nsh; L.misc[M_NLS] = nls; L.misc[M_NFL] = nfl; }
   }
   // ---- less-flat set: per sector the positions k in [sp, ep] with label <= 0,
   // in order (:771-775); the sectors are consecutive ranges, so one ordered
@@ -678,7 +888,7 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
       L.vox[t] = key;
     }
     __syncthreads();
-    bitonic_u64(L.vox, m);
+    bitonic_u64_chunked(L.vox, m);
     int outc = 0;
     for (int t0 = 0; t0 < K; t0 += blockDim.x) {
       const int t = t0 + tid;
@@ -687,13 +897,26 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
       const int r = block_rank(head, L.misc + M_WOFF, &tot);
       if (head) {
         const unsigned key = (unsigned)(L.vox[t] >> 32);
+        // the voxel's points in sorted order (PCL's accumulation order),
+        // four loads in flight per round instead of one per add
         float cx = 0, cy = 0, cz = 0, ci = 0;
-        int u = t;
-        for (; u < K && (unsigned)(L.vox[u] >> 32) == key; ++u) {
-          const float4 p = bb.dsk[R.base + R.lo + L.lf[(unsigned)(L.vox[u] & 0xffffffffu)]];
-          cx += p.x; cy += p.y; cz += p.z; ci += p.w;
+        int u = t, n = 0;
+        bool more = true;
+        while (more) {
+          float4 q[4];
+          bool in[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            in[i] = u + i < K && (unsigned)(L.vox[u + i] >> 32) == key;
+            if (in[i]) q[i] = bb.dsk[R.base + R.lo + L.lf[(unsigned)(L.vox[u + i] & 0xffffffffu)]];
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (in[i]) { cx += q[i].x; cy += q[i].y; cz += q[i].z; ci += q[i].w; ++n; }
+          more = in[3];
+          u += 4;
         }
-        const float cnt = (float)(u - t);
+        const float cnt = (float)n;
         olf[outc + r] = make_float4(cx / cnt, cy / cnt, cz / cnt, ci / cnt);
       }
       outc += tot;
@@ -702,7 +925,10 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
   }
   __syncthreads();
   stamp(3);  // the VoxelGrid (bounds, keys, sort, centroids)
-  if (xp && tid == 0) atomicAdd(xp + 4, 1ull);
+  if (xp && tid == 0) {
+    atomicAdd(xp + 4, 1ull);
+    atomicAdd(xp + 8, ~0ull);  // leaves the in-flight count
+  }
   if (tid == 0) {
     int* cnt = bb.r_cnt + ((size_t)b * c.N + ring) * 4;
     cnt[0] = L.misc[M_NSH];

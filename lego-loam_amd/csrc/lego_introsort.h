@@ -103,14 +103,17 @@ struct IntroSort {
       pop_heap(first, last, last);
     }
   }
-  LEGO_HD void introsort_loop(int first, int last, int depth) const {
-    // the recursion on the right part becomes an explicit stack (depth <= 2*lg n)
-    int st_first[64], st_last[64], st_depth[64];
+  // The recursion on the right part becomes an explicit stack of packed frames
+  // (first | last << 13 | depth << 26; n < 8192).  A frame's depth is below
+  // every frame under it, so the stack never holds more than 2 lg n + 1 <=
+  // kIntroStack frames.  The caller provides the stack: on the device a slice
+  // of LDS, so the kernel needs no private (scratch) memory.
+  LEGO_HD void introsort_loop(int first, int last, int depth, uint32_t* st) const {
     int sp = 0;
-    st_first[sp] = first; st_last[sp] = last; st_depth[sp] = depth; ++sp;
+    st[sp++] = (uint32_t)first | ((uint32_t)last << 13) | ((uint32_t)depth << 26);
     while (sp > 0) {
-      --sp;
-      first = st_first[sp]; last = st_last[sp]; depth = st_depth[sp];
+      const uint32_t f = st[--sp];
+      first = (int)(f & 8191u); last = (int)((f >> 13) & 8191u); depth = (int)(f >> 26);
       while (last - first > 16) {
         if (depth == 0) {
           heap_sort(first, last);
@@ -121,7 +124,7 @@ struct IntroSort {
         // std: __introsort_loop(cut, last, depth) first, then continue on [first, cut)
         // Order matters only for when sub-ranges are processed; they are
         // disjoint, so results are identical whichever runs first.
-        st_first[sp] = cut; st_last[sp] = last; st_depth[sp] = depth; ++sp;
+        st[sp++] = (uint32_t)cut | ((uint32_t)last << 13) | ((uint32_t)depth << 26);
         last = cut;
       }
     }
@@ -156,18 +159,21 @@ struct IntroSort {
       insertion_sort(first, last);
     }
   }
-  LEGO_HD void sort(int first, int last) const {
+  LEGO_HD void sort(int first, int last, uint32_t* st) const {
     if (last - first > 1) {
-      introsort_loop(first, last, lg(last - first) * 2);
+      introsort_loop(first, last, lg(last - first) * 2, st);
       final_insertion_sort(first, last);
     }
   }
 };
 
+constexpr int kIntroStack = 28;  // frames: 2 lg n + 1 for n < 8192
+
+// n < 8192; `stack` holds kIntroStack words
 template <typename Ptr>
-LEGO_HD void std_sort_by_value(Ptr a, int n) {
+LEGO_HD void std_sort_by_value(Ptr a, int n, uint32_t* stack) {
   IntroSort<Ptr> s{a};
-  s.sort(0, n);
+  s.sort(0, n, stack);
 }
 
 }  // namespace lego

@@ -1022,7 +1022,22 @@ struct ScanFeat {
 // eigen-decomposition, the eigenvalues < 10 zeroed, matP = V^-1 V2.  Out of
 // line: it runs only when eig_min_above cannot rule degeneracy out, and its
 // unrolled Jacobi would otherwise sit inside the LM loop's instruction stream.
-__device__ __attribute__((noinline)) int degeneracy_cold(const float (&AtA)[3][3], float (&P)[3][3]) {
+// Arguments and result by value: a reference into the caller's matrices
+// would give them an address and keep them in scratch memory for the whole
+// LM loop.
+struct Mat3 {
+  float m[3][3];
+};
+struct DegOut {
+  Mat3 P;
+  int deg;
+};
+__device__ __attribute__((noinline)) DegOut degeneracy_cold(const Mat3 in) {
+  float AtA[3][3], P[3][3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b) AtA[a][b] = in.m[a][b];
   float E[3], V[3][3], V2[3][3], Vi[3][3];
   cv_eigen_sym3(AtA, E, V);
 #pragma unroll
@@ -1043,7 +1058,13 @@ __device__ __attribute__((noinline)) int degeneracy_cold(const float (&AtA)[3][3
   }
   cv_inv3(V, Vi);
   cv_matmul<3>(Vi, V2, P);
-  return deg;
+  DegOut o;
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b) o.P.m[a][b] = P[a][b];
+  o.deg = deg;
+  return o;
 }
 
 // Shared tail of calculateTransformationSurf / Corner.  Thread 0 only, all in
@@ -1059,7 +1080,17 @@ __device__ __forceinline__ void solve_step(float (&AtA)[3][3], float (&AtB)[3], 
   if (iter == 0 && eig_min_above(AtA, 10.0)) {
     isDeg = 0;  // P is read only while isDeg is set, and the next iteration 0 rewrites both
   } else if (iter == 0) {
-    isDeg = degeneracy_cold(AtA, P);
+    Mat3 a;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) a.m[i][j] = AtA[i][j];
+    const DegOut d = degeneracy_cold(a);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) P[i][j] = d.P.m[i][j];
+    isDeg = d.deg;
   }
   if (isDeg) {
     float X2[3] = {X[0], X[1], X[2]};
@@ -1233,7 +1264,8 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
     {  // lanes 0-2 the sines, 3-5 the cosines: one fused evaluation, no divergence
       const int l = tid & 63;
       float sv, cv;
-      lego_sincosf(tc[l % 3], &sv, &cv);
+      const int l3 = l % 3;  // selects, not tc[l % 3]: a lane-varying index would put tc in scratch
+      lego_sincosf(l3 == 0 ? tc[0] : (l3 == 1 ? tc[1] : tc[2]), &sv, &cv);
       trig = l < 3 ? sv : cv;
     }
     const float srx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(trig), 0));

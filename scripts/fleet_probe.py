@@ -79,6 +79,9 @@ def main():
             xph = {nm: round(xp[i] / 100.0 / rings, 2) for i, nm in
                    enumerate(("sorts", "picking", "copies+lessflat", "voxelgrid"))}
             xph["rings"] = xp[4]
+            xph["rings_parallel_picking"] = xp[6]
+            xph["sector_rewalks"] = xp[5]
+            xph["mean_workgroups_in_flight_at_start"] = round(xp[7] / rings, 1)
         fl.close()
         print(json.dumps({"streams": S, "k": K, "scans_per_s": S * K * args.steps / dt,
                           "ms_per_call": dt / args.steps * 1e3, "valid_last": valid,

@@ -33,7 +33,8 @@ int main(int argc, char** argv) {
       b[i] = {v, i};
     }
     std::sort(a.begin(), a.end(), by_value());
-    lego::std_sort_by_value(b.data(), n);
+    uint32_t stk[lego::kIntroStack];
+    lego::std_sort_by_value(b.data(), n, stk);
     for (int i = 0; i < n; ++i)
       if ((int)a[i].ind != b[i].ind) { ++bad; break; }
   }
