@@ -667,6 +667,7 @@ __device__ __forceinline__ void group_lex_min3(float& d, int& r, int& j) {
   r = rm;
 }
 
+constexpr int kBruteSmall = 4 * kGL;
 // Exact nearest neighbour with d2 < bound over pts[0, n), by the calling wave.
 // A lane visits ascending indices, so a strict < keeps its lexicographic
 // (distance, index) minimum; the group reduction breaks ties by index.
@@ -691,6 +692,9 @@ __device__ __forceinline__ int nn_brute(const float4* pts, int n, float4 q, floa
 template <class Idx>
 __device__ __forceinline__ int nn_i1(const NNView<Idx>& v, float4 q, float bound, int g, unsigned long long* prof) {
   if (v.n <= 0) return -1;
+  // a small cloud (the corner clouds: ~100-200 points) is searched whole:
+  // four points per lane cost less than the bucket lookups the shell needs
+  if (v.n <= kBruteSmall) return nn_brute(v.pts, v.n, q, bound, g);
   float bd = bound;
   int bi = INT_MAX;
   const int cx = cell_of(q.x), cy = cell_of(q.y), cz = cell_of(q.z);
@@ -1290,14 +1294,26 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
       const bool w0 = S.prof && tid == 0;
       // findCorresponding{Surf,Corner}Features for query q by one wave
       auto search = [&](int q, int& i1, int& i2, int& i3) {
+        // wave 0's sub-phase stamps (diagnostic): to_start, closest point, scan-line neighbours
+        unsigned long long tq = w0 ? wall_clock64() : 0;
+        auto sub = [&](int k) {
+          if (w0) {
+            const unsigned long long n = wall_clock64();
+            S.prof[k] += n - tq;
+            tq = n;
+          }
+        };
         const float4 sel = to_start(qp[q], tc);
+        sub(P_G0_TOSTART);
         i1 = stale ? nn_brute(snap, snapN, sel, c.nn_sq, g) : nn_i1(nn, sel, c.nn_sq, g, S.prof);
         if (i1 >= lastN) i1 = -1;  // an index past a stale snapshot's cloud
+        sub(P_G0_NN);
         i2 = -1; i3 = -1;
         if (i1 >= 0 && (stale || !nn_lines(nn, i1, jend, sel, surf, c.nn_sq, g, &i2, &i3))) {
           if (S.prof && g == 0) atomicAdd(&S.prof[P_SCANLINE], 1ull);
           scanline_group(last, jend, i1, sel, surf, c.nn_sq, g, &i2, &i3);
         }
+        sub(P_G0_SCAN);
       };
       const int qa = xch ? q0 : 0, qb = xch ? q1 : nQ;  // no exchange: every query here
       for (int q = qa + grp; q < qb; q += kNGrp) {
