@@ -332,6 +332,149 @@ __global__ void __launch_bounds__(1024) k_gated(BatchBufs bb, DevCfg c, GatedBuf
   }
 }
 
+// ---------------------------------------------------------------------------
+// Segmentation of one scan in LDS (labelComponents + the cloudSegmentation
+// compaction, imageProjection.cpp:300-460), one 1024-thread workgroup per
+// scan, for images of at most kSegLdsMaxP pixels and 16 rows (VLP-16 class):
+// the union-find parents live in LDS instead of HBM, so the unions are LDS
+// compare-and-swaps, and the per-component size and rows are LDS words
+// instead of HBM atomics read back through two dependent gathers per pixel.
+//
+//  1. parent[p] = p for the unlabelled pixels (labelMat 0), -1 otherwise;
+//  2. unions over the right (wrapping) and down neighbours whose angle test
+//     passes (:397-427), linking the larger root under the smaller, so every
+//     component's root is its smallest pixel index — the BFS seed;
+//  3. each pixel's root (path-compressed) to HBM (root[], read back by
+//     step 5 in pixel order);
+//  4. per root one LDS word: the component's size (bits 0-14) and the rows of
+//     its pushed (non-seed) pixels (bits 15-30, lineCountFlag :431);
+//  5. k_compact's ordered pass, the validity test (:441-451) on the root's
+//     word; a valid root's word becomes -(its label) when its chunk is
+//     scanned, which its later pixels read (the root precedes them).
+// Results equal the HBM kernels' (k_ccl_* + k_compact) bit for bit.
+constexpr int kSegLdsMaxP = 32767;  // counts fit 15 bits; 128 KB of parents
+constexpr int kSegLdsMaxN = 16;     // the row mask fits 16 bits
+bool seg_lds_ok(const DevCfg& c) { return c.N <= kSegLdsMaxN && c.P <= kSegLdsMaxP; }
+
+__device__ __forceinline__ int lds_find(volatile int* par, int x) {
+  while (true) {
+    const int p = par[x];
+    if (p == x) return x;
+    x = p;
+  }
+}
+__device__ __forceinline__ void lds_unite(int* par, int a, int b) {
+  while (true) {
+    a = lds_find(par, a);
+    b = lds_find(par, b);
+    if (a == b) return;
+    if (a < b) { const int t = a; a = b; b = t; }  // the larger root under the smaller
+    if (atomicCAS(&par[a], a, b) == a) return;
+  }
+}
+
+__global__ void __launch_bounds__(1024) k_seg_lds(BatchBufs bb, DevCfg c, int want_labels) {
+  extern __shared__ int par[];  // [P]
+  __shared__ int lds[64];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const size_t base = (size_t)b * c.P;
+  const int P = c.P, H = c.H;
+  volatile int* vpar = par;
+  for (int p = tid; p < P; p += blockDim.x) par[p] = bb.label[base + p] == 0 ? p : -1;
+  __syncthreads();
+  for (int p = tid; p < P; p += blockDim.x) {
+    if (vpar[p] < 0) continue;  // candidates keep a parent >= 0 throughout
+    const int row = p / H, col = p - row * H;
+    const float r = bb.range[base + p];
+    const int qr = row * H + (col + 1 == H ? 0 : col + 1);  // column wrap :403-406
+    if (vpar[qr] >= 0 && seg_edge(r, bb.range[base + qr], c.sinAX, c.cosAX, c.theta)) lds_unite(par, p, qr);
+    if (row + 1 < c.N) {
+      const int qd = p + H;
+      if (vpar[qd] >= 0 && seg_edge(r, bb.range[base + qd], c.sinAY, c.cosAY, c.theta)) lds_unite(par, p, qd);
+    }
+  }
+  __syncthreads();
+  for (int p = tid; p < P; p += blockDim.x) bb.root[base + p] = vpar[p] < 0 ? -1 : lds_find(vpar, p);
+  __syncthreads();  // every find done before the parents become words
+  for (int p = tid; p < P; p += blockDim.x) par[p] = 0;
+  __syncthreads();
+  for (int p = tid; p < P; p += blockDim.x) {
+    const int r = bb.root[base + p];  // this thread's own write
+    if (r < 0) continue;
+    atomicAdd(&par[r], 1);
+    if (r != p) atomicOr(&par[r], 1 << (15 + p / H));
+  }
+  __syncthreads();
+  int segc = 0, outc = 0, labc = 0;
+  for (int t0 = 0; t0 < P; t0 += blockDim.x) {
+    const int p = t0 + tid;
+    bool keep = false, outl = false, vroot = false, inseg = false, valid = false;
+    int r = -1;
+    int row = 0, col = 0;
+    if (p < P) {
+      row = p / H;
+      col = p - row * H;
+      const int L0 = bb.label[base + p];
+      const int8_t G = bb.ground[base + p];
+      r = bb.root[base + p];
+      if (L0 == 0) {
+        inseg = true;
+        const int w = vpar[r];
+        if (w < 0) {
+          valid = true;  // the root, an earlier chunk's pixel, was found valid
+        } else {
+          const int sz = w & 0x7fff;
+          const int lines = __popc((unsigned)w >> 15);
+          valid = sz >= 30 || (sz >= c.valid_pt && lines >= c.valid_line);  // :441-451
+        }
+        vroot = valid && r == p;
+        keep = valid;
+        outl = !valid && row > c.g && col % 5 == 0;                      // :328-334
+      } else if (G == 1) {
+        keep = !(col % 5 != 0 && col > 5 && col < H - 5);                // :337-340
+      }
+    }
+    Scan3 in{{keep ? 1 : 0, outl ? 1 : 0, vroot ? 1 : 0}}, tot;
+    Scan3 ex = block_scan3(in, &tot, lds);
+    if (p < P) {
+      if (col == 0) {  // ring boundaries (:323, :354)
+        bb.sri[b * c.N + row] = segc + ex.v[0] - 1 + 5;
+        if (row > 0) bb.eri[b * c.N + row - 1] = segc + ex.v[0] - 1 - 5;
+      }
+      if (vroot) par[p] = -(labc + ex.v[2] + 1);  // a valid root's label, negated
+    }
+    __syncthreads();
+    if (p < P) {
+      if (want_labels && inseg) bb.label[base + p] = valid ? -vpar[r] : 999999;  // the final labelMat
+      if (keep) {
+        const int pos = segc + ex.v[0];
+        bb.seg[base + pos] = bb.full[base + p];
+        bb.gflag[base + pos] = (bb.ground[base + p] == 1) ? 1 : 0;
+        bb.col[base + pos] = (uint32_t)col;
+        bb.srange[base + pos] = bb.range[base + p];
+      }
+      if (outl) bb.outl[base + outc + ex.v[1]] = bb.full[base + p];
+    }
+    segc += tot.v[0];
+    outc += tot.v[1];
+    labc += tot.v[2];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    bb.ns[b] = segc;
+    bb.nout[b] = outc;
+    bb.eri[b * c.N + c.N - 1] = segc - 1 - 5;
+    // findStartEndAngle :199-209
+    const float so = bb.rawang[2 * b];
+    float eo = (float)((double)bb.rawang[2 * b + 1] + 2 * M_PI);
+    if ((double)(eo - so) > 3 * M_PI) eo = (float)((double)eo - 2 * M_PI);
+    else if ((double)(eo - so) < M_PI) eo = (float)((double)eo + 2 * M_PI);
+    bb.orient[3 * b] = so;
+    bb.orient[3 * b + 1] = eo;
+    bb.orient[3 * b + 2] = eo - so;
+  }
+}
+
 void launch_gated(const BatchBufs& bb, const DevCfg& c, const GatedBufs& gb, hipStream_t s) {
   k_gated<<<1, 1024, 0, s>>>(bb, c, gb);
 }
@@ -341,9 +484,12 @@ void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hip
   const int P = c.P;
   tm->mark("ip.memset", s);
   // launch-path errors are sticky: the caller checks hipGetLastError() after the batch
+  const bool segLds = seg_lds_ok(c);
   (void)hipMemsetAsync(bb.owner, 0xff, sizeof(int) * (size_t)B * P, s);
-  (void)hipMemsetAsync(bb.csize, 0, sizeof(int) * (size_t)B * P, s);
-  (void)hipMemsetAsync(bb.rowmask, 0, sizeof(unsigned long long) * 2 * (size_t)B * P, s);
+  if (!segLds) {  // the HBM union-find's size and row counters
+    (void)hipMemsetAsync(bb.csize, 0, sizeof(int) * (size_t)B * P, s);
+    (void)hipMemsetAsync(bb.rowmask, 0, sizeof(unsigned long long) * 2 * (size_t)B * P, s);
+  }
   tm->mark("ip.project", s);
   dim3 gpts((bb.Nmax + 255) / 256, B), gpix((P + 255) / 256, B), gcol((c.H + 255) / 256, B);
   k_project<<<gpts, 256, 0, s>>>(bb, c);
@@ -351,6 +497,11 @@ void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hip
   k_pixels<<<dim3((c.H + 63) / 64, (c.N + 3) / 4, B), 256, 0, s>>>(bb, c);
   tm->mark("ip.ground", s);
   k_ground<<<gcol, 256, 0, s>>>(bb, c);
+  if (segLds) {
+    tm->mark("ip.seg_lds", s);
+    k_seg_lds<<<B, 1024, (size_t)P * sizeof(int), s>>>(bb, c, want_labels);
+    return;
+  }
   tm->mark("ip.ccl", s);
   k_ccl_init<<<gpix, 256, 0, s>>>(bb, c);
   k_ccl_union<<<gpix, 256, 0, s>>>(bb, c);
