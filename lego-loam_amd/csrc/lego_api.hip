@@ -208,6 +208,9 @@ static int make_devcfg(const lego_sensor_cfg* c, DevCfg* d) {
   d->min_range = c->sensor_minimum_range;
   d->mount_angle = c->sensor_mount_angle;
   d->theta = c->segment_theta;
+  d->tanLo = std::tan((double)d->theta - 1e-5);
+  d->tanHi = std::tan((double)d->theta + 1e-5);
+  d->quad1 = (double)d->theta < M_PI / 2 - 1e-3 ? 1 : 0;
   // labelComponents re-evaluates sin/cos(alpha) per edge (imageProjection.cpp:421);
   // they are per-sensor constants, evaluated with the same libm restatement.
   d->sinAX = lego_sinf(c->segment_alpha_x);

@@ -33,6 +33,10 @@ struct DevCfg {
   int valid_pt, valid_line;
   float edge_thr, surf_thr, nn_sq, scan_period;
   int skip;  // skipFrameNum (featureAssociation.cpp:284)
+  // the segmentation angle test's quotient band (seg_edge_fast, lego_ip.hip):
+  // tan(theta -+ 1e-5), and whether theta < pi / 2 - 1e-3
+  double tanLo, tanHi;
+  int quad1;
 };
 
 // ---- IMU (featureAssociation.cpp:84-159, 317-459, 525-614)

@@ -112,10 +112,33 @@ __global__ void k_ground(BatchBufs bb, DevCfg c) {
   }
 }
 
-__device__ __forceinline__ bool seg_edge(float ra, float rb, float sa, float ca, float theta) {
+// The segmentation angle test (:421-423): with d1 / d2 the larger / smaller
+// of the two ranges, atan2f(d2 sin(alpha), d1 - d2 cos(alpha)) > theta.  The
+// verdict is decided without atan2f away from the threshold: for
+// x > 0, y >= 0 the angle is atan(y / x), and a quotient beyond tan(theta +-
+// 1e-5) puts it 1e-5 rad from theta, far outside atan2f's 2-ulp error and
+// the quotient's rounding (< 4e-7 rad together); for x <= 0 < y it is at least
+// pi / 2 > theta.  Everything else, and every quotient in the band, takes
+// atan2f itself.  tb = {tan(theta - 1e-5), tan(theta + 1e-5)} (DevCfg).
+struct TanBand {
+  double lo, hi;
+  bool quad1;  // theta < pi / 2 - 1e-3: the x <= 0 shortcut holds
+};
+__device__ __forceinline__ TanBand seg_tan_band(const DevCfg& c) {  // computed on the host
+  return TanBand{c.tanLo, c.tanHi, c.quad1 != 0};
+}
+__device__ __forceinline__ bool seg_edge_fast(float ra, float rb, float sa, float ca, float theta, const TanBand& tb) {
   const float d1 = (ra < rb) ? rb : ra;  // std::max
   const float d2 = (rb < ra) ? rb : ra;  // std::min
-  return lego_atan2f(d2 * sa, (d1 - d2 * ca)) > theta;                 // :421-423
+  const float y = d2 * sa, x = d1 - d2 * ca;
+  if (tb.quad1 && y >= 0.f && x > 0.f) {
+    const double q = (double)(y / x);
+    if (q > tb.hi) return true;
+    if (q < tb.lo) return false;
+  } else if (tb.quad1 && y > 0.f && x <= 0.f) {
+    return true;
+  }
+  return lego_atan2f(y, x) > theta;
 }
 
 __global__ void k_ccl_init(BatchBufs bb, DevCfg c) {
@@ -130,10 +153,11 @@ __global__ void k_ccl_init(BatchBufs bb, DevCfg c) {
     const int row = p / c.H, col = p - row * c.H;
     const float r = bb.range[base + p];
     const int qr = row * c.H + (col + 1 == c.H ? 0 : col + 1);        // column wrap :403-406
-    if (bb.label[base + qr] == 0 && seg_edge(r, bb.range[base + qr], c.sinAX, c.cosAX, c.theta)) e |= 1;
+    const TanBand tb = seg_tan_band(c);
+    if (bb.label[base + qr] == 0 && seg_edge_fast(r, bb.range[base + qr], c.sinAX, c.cosAX, c.theta, tb)) e |= 1;
     if (row + 1 < c.N) {
       const int qd = p + c.H;
-      if (bb.label[base + qd] == 0 && seg_edge(r, bb.range[base + qd], c.sinAY, c.cosAY, c.theta)) e |= 2;
+      if (bb.label[base + qd] == 0 && seg_edge_fast(r, bb.range[base + qd], c.sinAY, c.cosAY, c.theta, tb)) e |= 2;
     }
   }
   bb.edges[base + p] = e;
@@ -332,6 +356,30 @@ __global__ void __launch_bounds__(1024) k_gated(BatchBufs bb, DevCfg c, GatedBuf
   }
 }
 
+// Exclusive block prefix of three 0/1 flags (any block size up to 16 waves):
+// ballots within a wave, the wave totals through LDS (one barrier).  The
+// caller separates two calls with a barrier (lds is reused).
+__device__ __forceinline__ Scan3 block_scan3_bits(bool f0, bool f1, bool f2, Scan3* total, int* lds /*48*/) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const unsigned long long lt = (1ull << lane) - 1;
+  const unsigned long long m0 = __ballot(f0), m1 = __ballot(f1), m2 = __ballot(f2);
+  if (lane == 0) {
+    lds[wave] = (int)__popcll(m0);
+    lds[16 + wave] = (int)__popcll(m1);
+    lds[32 + wave] = (int)__popcll(m2);
+  }
+  __syncthreads();
+  Scan3 out{{(int)__popcll(m0 & lt), (int)__popcll(m1 & lt), (int)__popcll(m2 & lt)}};
+  Scan3 t{{0, 0, 0}};
+  for (int w = 0; w < nw; ++w) {
+    const int a = lds[w], b = lds[16 + w], c = lds[32 + w];
+    if (w < wave) { out.v[0] += a; out.v[1] += b; out.v[2] += c; }
+    t.v[0] += a; t.v[1] += b; t.v[2] += c;
+  }
+  *total = t;
+  return out;
+}
+
 // ---------------------------------------------------------------------------
 // Segmentation of one scan in LDS (labelComponents + the cloudSegmentation
 // compaction, imageProjection.cpp:300-460), one 1024-thread workgroup per
@@ -354,6 +402,7 @@ __global__ void __launch_bounds__(1024) k_gated(BatchBufs bb, DevCfg c, GatedBuf
 // Results equal the HBM kernels' (k_ccl_* + k_compact) bit for bit.
 constexpr int kSegLdsMaxP = 32767;  // counts fit 15 bits; 128 KB of parents
 constexpr int kSegLdsMaxN = 16;     // the row mask fits 16 bits
+constexpr int kSegK = (kSegLdsMaxP + 1023) / 1024;  // 1024-pixel chunks per scan
 bool seg_lds_ok(const DevCfg& c) { return c.N <= kSegLdsMaxN && c.P <= kSegLdsMaxP; }
 
 __device__ __forceinline__ int lds_find(volatile int* par, int x) {
@@ -374,93 +423,165 @@ __device__ __forceinline__ void lds_unite(int* par, int a, int b) {
 }
 
 __global__ void __launch_bounds__(1024) k_seg_lds(BatchBufs bb, DevCfg c, int want_labels) {
-  extern __shared__ int par[];  // [P]
-  __shared__ int lds[64];
-  const int b = blockIdx.x, tid = threadIdx.x;
+  extern __shared__ int par[];          // [P]
+  __shared__ int wpre[kSegK][3][16];    // per chunk and flag: the waves' exclusive prefixes
+  __shared__ int cpre[kSegK + 1][3];    // per chunk and flag: the chunks' exclusive prefixes
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const size_t base = (size_t)b * c.P;
-  const int P = c.P, H = c.H;
+  const int P = c.P, H = c.H, K = (P + 1023) >> 10;
   volatile int* vpar = par;
-  for (int p = tid; p < P; p += blockDim.x) par[p] = bb.label[base + p] == 0 ? p : -1;
+  const TanBand tb = seg_tan_band(c);
+  // pixel k * 1024 + tid of chunk k: loads coalesced, chunk-ordered
+#pragma unroll
+  for (int k = 0; k < kSegK; ++k) {
+    const int p = (k << 10) + tid;
+    if (k < K && p < P) par[p] = bb.label[base + p] == 0 ? p : -1;
+  }
   __syncthreads();
-  for (int p = tid; p < P; p += blockDim.x) {
-    if (vpar[p] < 0) continue;  // candidates keep a parent >= 0 throughout
-    const int row = p / H, col = p - row * H;
-    const float r = bb.range[base + p];
-    const int qr = row * H + (col + 1 == H ? 0 : col + 1);  // column wrap :403-406
-    if (vpar[qr] >= 0 && seg_edge(r, bb.range[base + qr], c.sinAX, c.cosAX, c.theta)) lds_unite(par, p, qr);
-    if (row + 1 < c.N) {
-      const int qd = p + H;
-      if (vpar[qd] >= 0 && seg_edge(r, bb.range[base + qd], c.sinAY, c.cosAY, c.theta)) lds_unite(par, p, qd);
+  // unions over the right (wrapping) and down neighbours, four chunks' ranges in flight
+  for (int k0 = 0; k0 < K; k0 += 4) {
+    float rp[4], rr_[4], rd[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = ((k0 + u) << 10) + tid;
+      rp[u] = rr_[u] = rd[u] = 0.f;
+      if (k0 + u < K && p < P) {
+        const int row = p / H, col = p - row * H;
+        rp[u] = bb.range[base + p];
+        rr_[u] = bb.range[base + row * H + (col + 1 == H ? 0 : col + 1)];
+        if (row + 1 < c.N) rd[u] = bb.range[base + p + H];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = ((k0 + u) << 10) + tid;
+      if (k0 + u >= K || p >= P || vpar[p] < 0) continue;  // candidates keep a parent >= 0 throughout
+      const int row = p / H, col = p - row * H;
+      const int qr = row * H + (col + 1 == H ? 0 : col + 1);  // column wrap :403-406
+      if (vpar[qr] >= 0 && seg_edge_fast(rp[u], rr_[u], c.sinAX, c.cosAX, c.theta, tb)) lds_unite(par, p, qr);
+      if (row + 1 < c.N) {
+        const int qd = p + H;
+        if (vpar[qd] >= 0 && seg_edge_fast(rp[u], rd[u], c.sinAY, c.cosAY, c.theta, tb)) lds_unite(par, p, qd);
+      }
     }
   }
   __syncthreads();
-  for (int p = tid; p < P; p += blockDim.x) bb.root[base + p] = vpar[p] < 0 ? -1 : lds_find(vpar, p);
+  int rt[kSegK];  // each pixel's root (-1: not a candidate), in registers
+#pragma unroll
+  for (int k = 0; k < kSegK; ++k) {
+    const int p = (k << 10) + tid;
+    rt[k] = (k < K && p < P && vpar[p] >= 0) ? lds_find(vpar, p) : -1;
+  }
   __syncthreads();  // every find done before the parents become words
-  for (int p = tid; p < P; p += blockDim.x) par[p] = 0;
-  __syncthreads();
-  for (int p = tid; p < P; p += blockDim.x) {
-    const int r = bb.root[base + p];  // this thread's own write
-    if (r < 0) continue;
-    atomicAdd(&par[r], 1);
-    if (r != p) atomicOr(&par[r], 1 << (15 + p / H));
+#pragma unroll
+  for (int k = 0; k < kSegK; ++k) {
+    const int p = (k << 10) + tid;
+    if (k < K && p < P) par[p] = 0;
   }
   __syncthreads();
-  int segc = 0, outc = 0, labc = 0;
-  for (int t0 = 0; t0 < P; t0 += blockDim.x) {
-    const int p = t0 + tid;
-    bool keep = false, outl = false, vroot = false, inseg = false, valid = false;
-    int r = -1;
-    int row = 0, col = 0;
-    if (p < P) {
-      row = p / H;
-      col = p - row * H;
-      const int L0 = bb.label[base + p];
-      const int8_t G = bb.ground[base + p];
-      r = bb.root[base + p];
-      if (L0 == 0) {
-        inseg = true;
-        const int w = vpar[r];
-        if (w < 0) {
-          valid = true;  // the root, an earlier chunk's pixel, was found valid
-        } else {
+#pragma unroll
+  for (int k = 0; k < kSegK; ++k) {
+    const int p = (k << 10) + tid;
+    if (rt[k] < 0) continue;
+    atomicAdd(&par[rt[k]], 1);
+    if (rt[k] != p) atomicOr(&par[rt[k]], 1 << (15 + p / H));
+  }
+  __syncthreads();
+  // flags per chunk: kept in the segmented cloud, outlier, valid root; the
+  // waves' counts per chunk into wpre
+  unsigned mkeep = 0, mout = 0, mroot = 0;
+#pragma unroll
+  for (int k0 = 0; k0 < kSegK; k0 += 8) {
+    int8_t G[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int p = ((k0 + u) << 10) + tid;
+      G[u] = (k0 + u < K && p < P) ? bb.ground[base + p] : (int8_t)0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + u, p = (k << 10) + tid;
+      if (k >= K) break;
+      bool keep = false, outl = false, vroot = false;
+      if (p < P) {
+        const int row = p / H, col = p - row * H;
+        if (rt[k] >= 0) {
+          const int w = vpar[rt[k]];
           const int sz = w & 0x7fff;
           const int lines = __popc((unsigned)w >> 15);
-          valid = sz >= 30 || (sz >= c.valid_pt && lines >= c.valid_line);  // :441-451
+          const bool valid = sz >= 30 || (sz >= c.valid_pt && lines >= c.valid_line);  // :441-451
+          vroot = valid && rt[k] == p;
+          keep = valid;
+          outl = !valid && row > c.g && col % 5 == 0;                                // :328-334
+        } else if (G[u] == 1) {
+          keep = !(col % 5 != 0 && col > 5 && col < H - 5);                          // :337-340
         }
-        vroot = valid && r == p;
-        keep = valid;
-        outl = !valid && row > c.g && col % 5 == 0;                      // :328-334
-      } else if (G == 1) {
-        keep = !(col % 5 != 0 && col > 5 && col < H - 5);                // :337-340
+      }
+      mkeep |= (keep ? 1u : 0u) << k;
+      mout |= (outl ? 1u : 0u) << k;
+      mroot |= (vroot ? 1u : 0u) << k;
+      const unsigned long long b0 = __ballot(keep), b1 = __ballot(outl), b2 = __ballot(vroot);
+      if (lane == 0) {
+        wpre[k][0][wave] = (int)__popcll(b0);
+        wpre[k][1][wave] = (int)__popcll(b1);
+        wpre[k][2][wave] = (int)__popcll(b2);
       }
     }
-    Scan3 in{{keep ? 1 : 0, outl ? 1 : 0, vroot ? 1 : 0}}, tot;
-    Scan3 ex = block_scan3(in, &tot, lds);
-    if (p < P) {
-      if (col == 0) {  // ring boundaries (:323, :354)
-        bb.sri[b * c.N + row] = segc + ex.v[0] - 1 + 5;
-        if (row > 0) bb.eri[b * c.N + row - 1] = segc + ex.v[0] - 1 - 5;
-      }
-      if (vroot) par[p] = -(labc + ex.v[2] + 1);  // a valid root's label, negated
+  }
+  __syncthreads();
+  const int nw = blockDim.x >> 6;
+  if (tid < 3 * K) {  // per (chunk, flag): the waves' exclusive prefix, the chunk's total
+    const int k = tid / 3, f = tid - 3 * k;
+    int run = 0;
+    for (int w = 0; w < nw; ++w) {
+      const int v = wpre[k][f][w];
+      wpre[k][f][w] = run;
+      run += v;
     }
+    cpre[k][f] = run;
+  }
+  __syncthreads();
+  if (tid < 3) {  // the chunks' exclusive prefix (cpre[K]: the totals)
+    int run = 0;
+    for (int k = 0; k <= K; ++k) {
+      const int v = k < K ? cpre[k][tid] : 0;
+      cpre[k][tid] = run;
+      run += v;
+    }
+  }
+  __syncthreads();
+  // outputs at their ordered positions (cloudSegmentation :318-357)
+  const unsigned long long lt = (1ull << lane) - 1;
+  for (int k = 0; k < K; ++k) {
+    const int p = (k << 10) + tid;
+    const bool keep = (mkeep >> k) & 1u, outl = (mout >> k) & 1u, vroot = (mroot >> k) & 1u;
+    const unsigned long long b0 = __ballot(keep), b1 = __ballot(outl), b2 = __ballot(vroot);
+    if (p >= P) continue;
+    const int row = p / H, col = p - row * H;
+    const int pos = cpre[k][0] + wpre[k][0][wave] + (int)__popcll(b0 & lt);  // kept pixels before p
+    if (col == 0) {  // ring boundaries (:323, :354)
+      bb.sri[b * c.N + row] = pos - 1 + 5;
+      if (row > 0) bb.eri[b * c.N + row - 1] = pos - 1 - 5;
+    }
+    if (vroot) par[p] = -(cpre[k][2] + wpre[k][2][wave] + (int)__popcll(b2 & lt) + 1);  // its label, negated
+    if (keep) {
+      bb.seg[base + pos] = bb.full[base + p];
+      bb.gflag[base + pos] = (bb.ground[base + p] == 1) ? 1 : 0;
+      bb.col[base + pos] = (uint32_t)col;
+      bb.srange[base + pos] = bb.range[base + p];
+    }
+    if (outl) bb.outl[base + cpre[k][1] + wpre[k][1][wave] + (int)__popcll(b1 & lt)] = bb.full[base + p];
+  }
+  if (want_labels) {  // the final labelMat: a valid segment's label, 999999 for the rest
     __syncthreads();
-    if (p < P) {
-      if (want_labels && inseg) bb.label[base + p] = valid ? -vpar[r] : 999999;  // the final labelMat
-      if (keep) {
-        const int pos = segc + ex.v[0];
-        bb.seg[base + pos] = bb.full[base + p];
-        bb.gflag[base + pos] = (bb.ground[base + p] == 1) ? 1 : 0;
-        bb.col[base + pos] = (uint32_t)col;
-        bb.srange[base + pos] = bb.range[base + p];
-      }
-      if (outl) bb.outl[base + outc + ex.v[1]] = bb.full[base + p];
+#pragma unroll
+    for (int k = 0; k < kSegK; ++k) {
+      const int p = (k << 10) + tid;
+      if (rt[k] >= 0) bb.label[base + p] = ((mkeep >> k) & 1u) ? -vpar[rt[k]] : 999999;
     }
-    segc += tot.v[0];
-    outc += tot.v[1];
-    labc += tot.v[2];
-    __syncthreads();
   }
   if (tid == 0) {
+    const int segc = cpre[K][0], outc = cpre[K][1];
     bb.ns[b] = segc;
     bb.nout[b] = outc;
     bb.eri[b * c.N + c.N - 1] = segc - 1 - 5;
