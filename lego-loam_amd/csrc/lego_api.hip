@@ -26,6 +26,7 @@
 #include "lego_mo.h"
 #include "lego_loam.h"
 #include "lego_pgo_host.h"
+#include "lego_seg.h"
 #include "lego_wire.h"
 
 using namespace lego;
@@ -208,9 +209,11 @@ static int make_devcfg(const lego_sensor_cfg* c, DevCfg* d) {
   d->min_range = c->sensor_minimum_range;
   d->mount_angle = c->sensor_mount_angle;
   d->theta = c->segment_theta;
-  d->tanLo = std::tan((double)d->theta - 1e-5);
-  d->tanHi = std::tan((double)d->theta + 1e-5);
-  d->quad1 = (double)d->theta < M_PI / 2 - 1e-3 ? 1 : 0;
+  const TanBand tb = seg_tan_band_host(d->theta);  // seg_edge_fast's quotient band (lego_seg.h)
+  d->tanLo = tb.lo;
+  d->tanHi = tb.hi;
+  d->quad1 = tb.quad1 ? 1 : 0;
+  d->segHbm = std::getenv("LEGO_SEG_HBM") ? 1 : 0;  // diagnostic: the k_seg_lds cross-check
   // labelComponents re-evaluates sin/cos(alpha) per edge (imageProjection.cpp:421);
   // they are per-sensor constants, evaluated with the same libm restatement.
   d->sinAX = lego_sinf(c->segment_alpha_x);

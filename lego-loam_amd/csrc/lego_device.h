@@ -37,6 +37,7 @@ struct DevCfg {
   // tan(theta -+ 1e-5), and whether theta < pi / 2 - 1e-3
   double tanLo, tanHi;
   int quad1;
+  int segHbm;  // diagnostic (LEGO_SEG_HBM): the HBM union-find for every image size
 };
 
 // ---- IMU (featureAssociation.cpp:84-159, 317-459, 525-614)

@@ -18,6 +18,7 @@
 
 #include "lego_device.h"
 #include "lego_kernels.h"
+#include "lego_seg.h"
 #include "lego_loam.h"
 
 namespace lego {
@@ -112,33 +113,8 @@ __global__ void k_ground(BatchBufs bb, DevCfg c) {
   }
 }
 
-// The segmentation angle test (:421-423): with d1 / d2 the larger / smaller
-// of the two ranges, atan2f(d2 sin(alpha), d1 - d2 cos(alpha)) > theta.  The
-// verdict is decided without atan2f away from the threshold: for
-// x > 0, y >= 0 the angle is atan(y / x), and a quotient beyond tan(theta +-
-// 1e-5) puts it 1e-5 rad from theta, far outside atan2f's 2-ulp error and
-// the quotient's rounding (< 4e-7 rad together); for x <= 0 < y it is at least
-// pi / 2 > theta.  Everything else, and every quotient in the band, takes
-// atan2f itself.  tb = {tan(theta - 1e-5), tan(theta + 1e-5)} (DevCfg).
-struct TanBand {
-  double lo, hi;
-  bool quad1;  // theta < pi / 2 - 1e-3: the x <= 0 shortcut holds
-};
 __device__ __forceinline__ TanBand seg_tan_band(const DevCfg& c) {  // computed on the host
   return TanBand{c.tanLo, c.tanHi, c.quad1 != 0};
-}
-__device__ __forceinline__ bool seg_edge_fast(float ra, float rb, float sa, float ca, float theta, const TanBand& tb) {
-  const float d1 = (ra < rb) ? rb : ra;  // std::max
-  const float d2 = (rb < ra) ? rb : ra;  // std::min
-  const float y = d2 * sa, x = d1 - d2 * ca;
-  if (tb.quad1 && y >= 0.f && x > 0.f) {
-    const double q = (double)(y / x);
-    if (q > tb.hi) return true;
-    if (q < tb.lo) return false;
-  } else if (tb.quad1 && y > 0.f && x <= 0.f) {
-    return true;
-  }
-  return lego_atan2f(y, x) > theta;
 }
 
 __global__ void k_ccl_init(BatchBufs bb, DevCfg c) {
@@ -403,7 +379,7 @@ __device__ __forceinline__ Scan3 block_scan3_bits(bool f0, bool f1, bool f2, Sca
 constexpr int kSegLdsMaxP = 32767;  // counts fit 15 bits; 128 KB of parents
 constexpr int kSegLdsMaxN = 16;     // the row mask fits 16 bits
 constexpr int kSegK = (kSegLdsMaxP + 1023) / 1024;  // 1024-pixel chunks per scan
-bool seg_lds_ok(const DevCfg& c) { return c.N <= kSegLdsMaxN && c.P <= kSegLdsMaxP; }
+bool seg_lds_ok(const DevCfg& c) { return c.N <= kSegLdsMaxN && c.P <= kSegLdsMaxP && !c.segHbm; }
 
 __device__ __forceinline__ int lds_find(volatile int* par, int x) {
   while (true) {

@@ -532,3 +532,30 @@ def test_reset_in_flight(L):
     for k in range(K):
         assert r1[64 * k:64 * k + 60] == g1[64 * k:64 * k + 60], k
         assert r2[64 * k:64 * k + 60] == g2[64 * k:64 * k + 60], k
+
+
+@pytest.mark.parametrize("seed,extra", [(0, {}), (1, {}), (2, {"dup_frac": 0.05})])
+def test_seg_lds_equals_hbm_union_find(L, seed, extra):
+    """VLP-16 images are segmented in LDS (k_seg_lds); LEGO_SEG_HBM (diagnostic)
+    sends them through the HBM union-find (k_ccl_* + k_compact) that the
+    larger sensors use.  Both equal the oracle and each other, labels, images
+    and clouds byte for byte, on 12 consecutive scans."""
+    import os
+
+    sc = L.synth_cfg("VLP-16", seed, **extra)
+    scans = [L.synth_scan(sc, k) for k in range(12)]
+    ora = L.Oracle(L.sensor_cfg("VLP-16"))
+    ref = [ora.ip(p, s, images=True) for p, s in scans]
+    outs = {}
+    for mode in ("lds", "hbm"):
+        if mode == "hbm":
+            os.environ["LEGO_SEG_HBM"] = "1"
+        try:
+            gpu = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=max(len(p) for p, _ in scans) + 16)
+            outs[mode] = [gpu.ip(p, s, images=True) for p, s in scans]
+            gpu.close()
+        finally:
+            os.environ.pop("LEGO_SEG_HBM", None)
+    for k in range(len(scans)):
+        assert_ip_equal(outs["lds"][k], ref[k])
+        assert_ip_equal(outs["hbm"][k], ref[k])
