@@ -801,14 +801,20 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
   }
   // ---- less-flat set: per sector the positions k in [sp, ep] with label <= 0,
   // in order (:771-775); the sectors are consecutive ranges, so one ordered
-  // pass over [s, e - 1] restricted to the sectors that ran
+  // pass over [s, e - 1] restricted to the sectors that ran.  One block scan
+  // for the whole range: a flag per position in 256-position chunks (a bit
+  // per chunk), the waves' counts per chunk through LDS (L.red, free until
+  // the VoxelGrid bounds), then every position's rank.
   {
     int sp0, ep0, o0;
     sector(0, &sp0, &ep0, &o0);
     int sp5, ep5, o5;
     sector(5, &sp5, &ep5, &o5);
-    for (int k0 = sp0; k0 <= ep5; k0 += blockDim.x) {
-      const int k = k0 + tid;
+    const int nC = ep5 >= sp0 ? (ep5 - sp0 + blockDim.x) / blockDim.x : 0;  // <= 16 (W <= 4096)
+    int* cnt = (int*)L.red;  // [chunk][wave], nC * nw <= 64
+    unsigned fm = 0;
+    for (int ch = 0; ch < nC; ++ch) {
+      const int k = sp0 + ch * (int)blockDim.x + tid;
       bool f = false;
       if (k <= ep5 && label[k - R.lo] <= 0) {
         int j = 0;
@@ -819,13 +825,26 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
         }
         f = j < 6 && k >= sp && sp < ep;
       }
-      int tot;
-      const int r = block_rank(f, L.misc + M_WOFF, &tot);
-      if (f) L.lf[L.misc[M_LF] + r] = (uint16_t)(k - R.lo);  // window positions
-      __syncthreads();
-      if (tid == 0) L.misc[M_LF] += tot;
-      __syncthreads();
+      fm |= (f ? 1u : 0u) << ch;
+      const unsigned long long m = __ballot(f);
+      if (lane == 0) cnt[ch * nw + wave] = (int)__popcll(m);
     }
+    __syncthreads();
+    const unsigned long long lt = (1ull << lane) - 1;
+    int total = 0;
+    for (int ch = 0; ch < nC; ++ch) {
+      int base = total;
+      for (int w = 0; w < nw; ++w) {
+        const int v = cnt[ch * nw + w];
+        if (w < wave) base += v;
+        total += v;
+      }
+      const bool f = (fm >> ch) & 1u;
+      const unsigned long long m = __ballot(f);
+      if (f) L.lf[base + (int)__popcll(m & lt)] = (uint16_t)(sp0 + ch * (int)blockDim.x + tid - R.lo);  // window positions
+    }
+    if (tid == 0) L.misc[M_LF] = total;
+    __syncthreads();
   }
   stamp(2);  // picked-point copies + the ordered less-flat set
   // ---- per-ring VoxelGrid 0.2 m on the less-flat set (:778-782)
@@ -833,7 +852,25 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
   const float inv = 1.0f / 0.2f;
   float mn[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
   float mx[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
-  for (int t = tid; t < K; t += blockDim.x) {
+  // the less-flat points, gathered once: the thread's first kLfRegs in
+  // registers for the keys below, the rest (rings wider than
+  // kLfRegs * 256 points) gathered again there
+  constexpr int kLfRegs = 8;
+  float4 lp[kLfRegs];
+#pragma unroll
+  for (int i = 0; i < kLfRegs; ++i) {
+    const int t = tid + i * (int)blockDim.x;
+    lp[i] = t < K ? bb.dsk[R.base + R.lo + L.lf[t]] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int i = 0; i < kLfRegs; ++i) {
+    if (tid + i * (int)blockDim.x < K) {
+      const float4 p = lp[i];
+      mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+      mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+    }
+  }
+  for (int t = tid + kLfRegs * (int)blockDim.x; t < K; t += blockDim.x) {
     const float4 p = bb.dsk[R.base + R.lo + L.lf[t]];
     mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
     mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
@@ -875,10 +912,17 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
     const int m = next_pow2(K);
     const int d0 = L.misc[M_D0], d1 = L.misc[M_D1];
     const float fb0 = (float)L.misc[M_MB0], fb1 = (float)L.misc[M_MB1], fb2 = (float)L.misc[M_MB2];
-    for (int t = tid; t < m; t += blockDim.x) {
+    for (int t = tid, i = 0; t < m; t += blockDim.x, ++i) {
       unsigned long long key = ~0ull;
       if (t < K) {
-        const float4 p = bb.dsk[R.base + R.lo + L.lf[t]];
+        float4 p;
+        if (i < kLfRegs) {  // a register, selected without a dynamic index
+#pragma unroll
+          for (int u = 0; u < kLfRegs; ++u)
+            if (u == i) p = lp[u];
+        } else {
+          p = bb.dsk[R.base + R.lo + L.lf[t]];
+        }
         const int i0 = (int)(floorf(p.x * inv) - fb0);
         const int i1 = (int)(floorf(p.y * inv) - fb1);
         const int i2 = (int)(floorf(p.z * inv) - fb2);
