@@ -25,6 +25,10 @@ subprocess.run([sys.executable, str(REPO / "scripts" / "pmc_summary.py"), str(sr
                 "--mapping-steps 0 --fleet-streams 0 --dense-scans 0 --loop-scans 0 --steps 2 --warmup 1 "
                 "(3 launches per kernel, 100 VLP-16 scans each; k_odom = 48 workgroups, plain launch)", commit],
                check=True)
+for sub, name in (("prof_fleet", "fleet_kernel_stats.csv"), ("prof_c5", "c5_kernel_stats.csv")):
+    f = src / sub / "run_kernel_stats.csv"
+    if f.exists():
+        shutil.copy(f, prof / f"{rnd}_{name}")
 q = REPO / "gpurun_out" / (tag + "_q") / "prof.txt"
 if q.exists():
     (prof / f"{rnd}_odom_phase_profile.txt").write_text(
