@@ -993,6 +993,7 @@ int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
   }
   x->stamps.assign(1, in->info.stamp);
   BatchBufs bb = x->bb;
+  bb.xprof = x->profOn ? x->d_prof + 32 : nullptr;  // k_extract's stamps (lego_extract_profile)
   HIPCHK(hipEventRecord(x->oJoin, x->ostream));  // e.g. a reset of the odometry state
   HIPCHK(hipStreamWaitEvent(x->stream, x->oJoin, 0));
   {

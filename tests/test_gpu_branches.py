@@ -14,7 +14,12 @@ branch was taken (include/lego_loam.h LEGO_REC_*):
   LDS cap downwards and back up mid-stream (a denser far-wall scene, seed 23).
   LEGO_REC_ODOM_HBM must be set exactly on the scans whose previous scan's
   clouds exceeded the caps, and the poses must match the oracle across both
-  switches."""
+  switches;
+* the speculative sector-parallel picking of k_extract (rings other than 0
+  walk their six sectors at once and re-walk a sector whose predecessor's
+  boundary suppression reached a position it picked): lego_extract_profile's
+  counters prove both the parallel walks and re-walks ran, and the four
+  feature clouds must equal the oracle's byte for byte."""
 import numpy as np
 import pytest
 
@@ -105,3 +110,27 @@ def test_lds_hbm_switch_mid_stream(L):
     gpu.close()
     assert [bool(r.flags & REC_ODOM_HBM) for r in recs] == expect_hbm, [r.flags for r in recs]
     _check_recs(recs, ref, "LDS <-> HBM residency switch")
+
+
+def test_speculative_picking_rewalks_match_oracle(L):
+    import ctypes as C
+
+    sc = L.synth_cfg("VLP-16", 12)
+    scans = [L.synth_scan(sc, k) for k in range(10)]
+    ora = L.Oracle(L.sensor_cfg("VLP-16"))
+    lib = L.hip_lib()
+    gpu = L.Lego(L.sensor_cfg("VLP-16", lib), max_points=max(len(p) for p, _ in scans) + 16)
+    L.check(lib.lego_odom_profile(gpu.h, 1, None), "lego_odom_profile", lib)
+    for k, (p, s) in enumerate(scans):
+        gpu.ip(p, s)
+        g = gpu.fa()
+        ora.ip(p, s)
+        o = ora.fa()
+        for key in ("sharp", "less_sharp", "flat", "less_flat"):
+            assert np.array_equal(bits(g[key]), bits(o[key])), (k, key)
+    xp = (C.c_uint64 * 8)()
+    L.check(lib.lego_extract_profile(gpu.h, xp), "lego_extract_profile", lib)
+    gpu.close()
+    rings, rewalks, parallel = xp[4], xp[5], xp[6]
+    print(f"rings {rings}, picked in parallel {parallel}, sector re-walks {rewalks}")
+    assert rings >= 10 * 16 and parallel > 0 and rewalks > 0
