@@ -320,6 +320,7 @@ def dense_bench(L, nscans: int, batch: int, device: int, cpu: bool = False, budg
     import torch
 
     cfg = L.sensor_cfg("HDL-64E", L.hip_lib())
+    nscans = max(nscans, 2 * batch)  # a warm-up batch and at least one timed one
     pts, off, stamps, maxn = make_stream(L, "HDL-64E", 2, nscans)
     nb = nscans // batch
     d_pts = torch.from_numpy(pts.view(np.uint8)).to(device)

@@ -1053,31 +1053,40 @@ __global__ void __launch_bounds__(kExtractThreads) k_fa_fixup(BatchBufs bb, DevC
   if (threadIdx.x == 0) *carry = cs;
 }
 
+// One workgroup per (scan, ring): the ring's offsets are the sums of the
+// earlier rings' counts (wave 0, a lane per ring), then its four slots are
+// copied.  (A workgroup per scan walking its rings serially cost ~185 us on
+// a single VLS-128 scan: 128 dependent rounds of small copies.)
 __global__ void k_fa_compact(BatchBufs bb, DevCfg c) {
-  __shared__ int off[4][kMaxRings + 1];
-  const int b = blockIdx.x;
+  __shared__ int off[4];
+  const int r = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   const int* cnt = bb.r_cnt + (size_t)b * c.N * 4;
-  if (threadIdx.x < 4) {
-    int s = 0;
-    for (int r = 0; r < c.N; ++r) {
-      off[threadIdx.x][r] = s;
-      s += cnt[r * 4 + threadIdx.x];
+  if (tid < 64) {
+    int s[4] = {0, 0, 0, 0};
+    for (int q = tid; q < r; q += 64)
+#pragma unroll
+      for (int f = 0; f < 4; ++f) s[f] += cnt[q * 4 + f];
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+      for (int o = 32; o > 0; o >>= 1) s[f] += __shfl_xor(s[f], o, 64);
+    if (tid == 0) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        off[f] = s[f];
+        if (r == c.N - 1) bb.f_cnt[b * 4 + f] = s[f] + cnt[r * 4 + f];
+      }
     }
-    off[threadIdx.x][c.N] = s;
-    bb.f_cnt[b * 4 + threadIdx.x] = s;
   }
   __syncthreads();
-  for (int r = 0; r < c.N; ++r) {
-    const size_t rb = (size_t)b * c.N + r;
-    for (int t = threadIdx.x; t < cnt[r * 4 + 0]; t += blockDim.x)
-      bb.f_sharp[(size_t)b * c.N * kSharpPerRing + off[0][r] + t] = bb.r_sharp[rb * kSharpPerRing + t];
-    for (int t = threadIdx.x; t < cnt[r * 4 + 1]; t += blockDim.x)
-      bb.f_lsharp[(size_t)b * c.N * kLessSharpPerRing + off[1][r] + t] = bb.r_lsharp[rb * kLessSharpPerRing + t];
-    for (int t = threadIdx.x; t < cnt[r * 4 + 2]; t += blockDim.x)
-      bb.f_flat[(size_t)b * c.N * kFlatPerRing + off[2][r] + t] = bb.r_flat[rb * kFlatPerRing + t];
-    for (int t = threadIdx.x; t < cnt[r * 4 + 3]; t += blockDim.x)
-      bb.f_lflat[(size_t)b * c.P + off[3][r] + t] = bb.r_lflat[(size_t)b * c.P + (size_t)r * c.H + t];
-  }
+  const size_t rb = (size_t)b * c.N + r;
+  for (int t = tid; t < cnt[r * 4 + 0]; t += blockDim.x)
+    bb.f_sharp[(size_t)b * c.N * kSharpPerRing + off[0] + t] = bb.r_sharp[rb * kSharpPerRing + t];
+  for (int t = tid; t < cnt[r * 4 + 1]; t += blockDim.x)
+    bb.f_lsharp[(size_t)b * c.N * kLessSharpPerRing + off[1] + t] = bb.r_lsharp[rb * kLessSharpPerRing + t];
+  for (int t = tid; t < cnt[r * 4 + 2]; t += blockDim.x)
+    bb.f_flat[(size_t)b * c.N * kFlatPerRing + off[2] + t] = bb.r_flat[rb * kFlatPerRing + t];
+  for (int t = tid; t < cnt[r * 4 + 3]; t += blockDim.x)
+    bb.f_lflat[(size_t)b * c.P + off[3] + t] = bb.r_lflat[(size_t)b * c.P + (size_t)r * c.H + t];
 }
 
 void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_carry, hipStream_t s,
@@ -1095,7 +1104,7 @@ void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_ca
   tm->mark("fa.fixup", s);
   k_fa_fixup<<<S, kExtractThreads, lds, s>>>(bb, c, B / S, d_carry);
   tm->mark("fa.compact", s);
-  k_fa_compact<<<B, 256, 0, s>>>(bb, c);
+  k_fa_compact<<<dim3(c.N, B), 256, 0, s>>>(bb, c);
 }
 
 }  // namespace lego

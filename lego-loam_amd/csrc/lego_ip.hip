@@ -5,12 +5,16 @@
 //               (imageProjection.cpp:219-256)
 //   k_pixels    1 lane / pixel: rangeMat + fullCloud (:248-255)
 //   k_ground    1 lane / column: the sequential ground-pair walk (:267-301)
-//   k_ccl_*     BFS segmentation as connected components (:312-317, 370-460):
-//               symmetric edge predicate -> union-find with CAS on roots; the
-//               root is the component's minimum raster index = the BFS seed
-//   k_compact   1 workgroup / scan: component validity, label ranking,
-//               row-major compaction into segmented cloud + cloud_info,
-//               outlier cloud (:319-355)
+//   k_seg_lds   VLP-16-class images: 1 workgroup / scan, BFS segmentation
+//               as union-find in LDS + the ordered compaction (below)
+//   k_ccl_*     larger images: BFS segmentation as connected components
+//               (:312-317, 370-460): symmetric edge predicate -> union-find
+//               with CAS on roots in HBM; the root is the component's minimum
+//               raster index = the BFS seed
+//   k_seg_flags / _scan / _write / _labels
+//               their compaction, one 1024-pixel chunk per workgroup:
+//               component validity, label ranking, row-major compaction into
+//               segmented cloud + cloud_info, outlier cloud (:319-355)
 //
 // All float expressions mirror the reference's mixed float/double evaluation
 // (SURVEY.md §9.2); compiled with -ffp-contract=off.
@@ -224,65 +228,107 @@ __device__ __forceinline__ Scan3 block_scan3(Scan3 in, Scan3* total, int* lds /*
   return out;
 }
 
-__global__ void __launch_bounds__(1024) k_compact(BatchBufs bb, DevCfg c, int want_labels) {
+// Exclusive block prefix of three 0/1 flags (any block size up to 16 waves):
+// ballots within a wave, the wave totals through LDS (one barrier).  The
+// caller separates two calls with a barrier (lds is reused).
+__device__ __forceinline__ Scan3 block_scan3_bits(bool f0, bool f1, bool f2, Scan3* total, int* lds /*48*/) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const unsigned long long lt = (1ull << lane) - 1;
+  const unsigned long long m0 = __ballot(f0), m1 = __ballot(f1), m2 = __ballot(f2);
+  if (lane == 0) {
+    lds[wave] = (int)__popcll(m0);
+    lds[16 + wave] = (int)__popcll(m1);
+    lds[32 + wave] = (int)__popcll(m2);
+  }
+  __syncthreads();
+  Scan3 out{{(int)__popcll(m0 & lt), (int)__popcll(m1 & lt), (int)__popcll(m2 & lt)}};
+  Scan3 t{{0, 0, 0}};
+  for (int w = 0; w < nw; ++w) {
+    const int a = lds[w], b = lds[16 + w], c = lds[32 + w];
+    if (w < wave) { out.v[0] += a; out.v[1] += b; out.v[2] += c; }
+    t.v[0] += a; t.v[1] += b; t.v[2] += c;
+  }
+  *total = t;
+  return out;
+}
+
+// cloudSegmentation's compaction (:318-367) after the HBM union-find, over
+// the whole batch at once: one 1024-pixel chunk per workgroup.
+//  k_seg_flags  each pixel's flags (kept in the segmented cloud, outlier,
+//               valid root, valid, in a segment) into edges[] (free after the
+//               unions), and the chunk's three counts into parent[] (free
+//               after the roots: 3 ints per chunk at the scan's base);
+//  k_seg_scan   per scan the chunks' exclusive prefixes, in place, and the
+//               scan's totals (segmented / outlier counts, the last ring's end,
+//               findStartEndAngle);
+//  k_seg_write  each chunk's outputs at their ordered positions, and a valid
+//               root's label, negated, into root[] at the root;
+//  k_seg_labels (labels wanted) the final labelMat.
+// The results equal the single-workgroup walk of round 1 and k_seg_lds.
+enum { SF_KEEP = 1, SF_OUTL = 2, SF_VROOT = 4, SF_VALID = 8, SF_INSEG = 16 };
+
+__device__ __forceinline__ void block_counts3(bool f0, bool f1, bool f2, int* lds /*48*/, int* out3) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const unsigned long long m0 = __ballot(f0), m1 = __ballot(f1), m2 = __ballot(f2);
+  if (lane == 0) {
+    lds[wave] = (int)__popcll(m0);
+    lds[16 + wave] = (int)__popcll(m1);
+    lds[32 + wave] = (int)__popcll(m2);
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    int t = 0;
+    for (int w = 0; w < nw; ++w) t += lds[16 * threadIdx.x + w];
+    out3[threadIdx.x] = t;
+  }
+}
+
+__global__ void __launch_bounds__(1024) k_seg_flags(BatchBufs bb, DevCfg c) {
+  __shared__ int lds[48];
+  const int b = blockIdx.y, ch = blockIdx.x;
+  const int p = ch * blockDim.x + threadIdx.x;
+  const size_t base = (size_t)b * c.P;
+  bool keep = false, outl = false, vroot = false, valid = false, inseg = false;
+  if (p < c.P) {
+    const int row = p / c.H, col = p - row * c.H;
+    const int L0 = bb.label[base + p];
+    if (L0 == 0) {
+      inseg = true;
+      const int r = bb.root[base + p];
+      const int sz = bb.csize[base + r];
+      const unsigned long long* rm = &bb.rowmask[(base + r) * 2];
+      const int lines = __popcll(rm[0]) + __popcll(rm[1]);
+      valid = sz >= 30 || (sz >= c.valid_pt && lines >= c.valid_line);  // :441-451
+      vroot = valid && r == p;
+      keep = valid;
+      outl = !valid && row > c.g && col % 5 == 0;                      // :328-334
+    } else if (bb.ground[base + p] == 1) {
+      keep = !(col % 5 != 0 && col > 5 && col < c.H - 5);              // :337-340
+    }
+    bb.edges[base + p] = (uint8_t)((keep ? SF_KEEP : 0) | (outl ? SF_OUTL : 0) | (vroot ? SF_VROOT : 0) |
+                                   (valid ? SF_VALID : 0) | (inseg ? SF_INSEG : 0));
+  }
+  block_counts3(keep, outl, vroot, lds, bb.parent + base + 3 * ch);
+}
+
+__global__ void __launch_bounds__(1024) k_seg_scan(BatchBufs bb, DevCfg c) {
   __shared__ int lds[64];
   const int b = blockIdx.x;
   const size_t base = (size_t)b * c.P;
-  int segc = 0, outc = 0, labc = 0;
-  for (int t0 = 0; t0 < c.P; t0 += blockDim.x) {
-    const int p = t0 + threadIdx.x;
-    bool keep = false, outl = false, vroot = false, inseg = false, valid = false;
-    int r = -1;
-    int row = 0, col = 0;
-    if (p < c.P) {
-      row = p / c.H;
-      col = p - row * c.H;
-      const int L0 = bb.label[base + p];
-      const int8_t G = bb.ground[base + p];
-      if (L0 == 0) {
-        inseg = true;
-        r = bb.root[base + p];
-        const int sz = bb.csize[base + r];
-        const unsigned long long* rm = &bb.rowmask[(base + r) * 2];
-        const int lines = __popcll(rm[0]) + __popcll(rm[1]);
-        valid = sz >= 30 || (sz >= c.valid_pt && lines >= c.valid_line);  // :441-451
-        vroot = valid && r == p;
-        keep = valid;
-        outl = !valid && row > c.g && col % 5 == 0;                      // :328-334
-      } else if (G == 1) {
-        keep = !(col % 5 != 0 && col > 5 && col < c.H - 5);              // :337-340
-      }
-    }
-    Scan3 in{{keep ? 1 : 0, outl ? 1 : 0, vroot ? 1 : 0}}, tot;
-    Scan3 ex = block_scan3(in, &tot, lds);
-    if (p < c.P) {
-      if (col == 0) {  // ring boundaries (:323, :354)
-        bb.sri[b * c.N + row] = segc + ex.v[0] - 1 + 5;
-        if (row > 0) bb.eri[b * c.N + row - 1] = segc + ex.v[0] - 1 - 5;
-      }
-      if (vroot) bb.root[base + p] = -(labc + ex.v[2] + 1);  // label of a valid root, stored negated
-    }
-    __syncthreads();
-    if (p < c.P) {
-      if (want_labels && inseg) {
-        const int lr = valid ? -bb.root[base + r] : 999999;
-        bb.label[base + p] = lr;  // the final labelMat (root array holds -label at roots)
-      }
-      if (keep) {
-        const int pos = segc + ex.v[0];
-        bb.seg[base + pos] = bb.full[base + p];
-        bb.gflag[base + pos] = (bb.ground[base + p] == 1) ? 1 : 0;
-        bb.col[base + pos] = (uint32_t)col;
-        bb.srange[base + pos] = bb.range[base + p];
-      }
-      if (outl) bb.outl[base + outc + ex.v[1]] = bb.full[base + p];
-    }
-    segc += tot.v[0];
-    outc += tot.v[1];
-    labc += tot.v[2];
-    __syncthreads();
+  const int nCh = (c.P + 1023) / 1024;
+  int* cnt = bb.parent + base;
+  int run[3] = {0, 0, 0};
+  for (int c0 = 0; c0 < nCh; c0 += blockDim.x) {
+    const int ch = c0 + threadIdx.x;
+    Scan3 in{{0, 0, 0}}, tot;
+    if (ch < nCh) in = Scan3{{cnt[3 * ch], cnt[3 * ch + 1], cnt[3 * ch + 2]}};
+    const Scan3 ex = block_scan3(in, &tot, lds);
+    if (ch < nCh)
+      for (int f = 0; f < 3; ++f) cnt[3 * ch + f] = run[f] + ex.v[f];
+    for (int f = 0; f < 3; ++f) run[f] += tot.v[f];
   }
   if (threadIdx.x == 0) {
+    const int segc = run[0], outc = run[1];
     bb.ns[b] = segc;
     bb.nout[b] = outc;
     bb.eri[b * c.N + c.N - 1] = segc - 1 - 5;
@@ -297,12 +343,50 @@ __global__ void __launch_bounds__(1024) k_compact(BatchBufs bb, DevCfg c, int wa
   }
 }
 
+__global__ void __launch_bounds__(1024) k_seg_write(BatchBufs bb, DevCfg c) {
+  __shared__ int lds[64];
+  const int b = blockIdx.y, ch = blockIdx.x;
+  const int p = ch * blockDim.x + threadIdx.x;
+  const size_t base = (size_t)b * c.P;
+  const int f = p < c.P ? bb.edges[base + p] : 0;
+  const bool keep = f & SF_KEEP, outl = f & SF_OUTL, vroot = f & SF_VROOT;
+  Scan3 tot;
+  const Scan3 ex = block_scan3_bits(keep, outl, vroot, &tot, lds);
+  if (p >= c.P) return;
+  const int* off = bb.parent + base + 3 * ch;
+  const int row = p / c.H, col = p - row * c.H;
+  const int pos = off[0] + ex.v[0];  // kept pixels before p
+  if (col == 0) {  // ring boundaries (:323, :354)
+    bb.sri[b * c.N + row] = pos - 1 + 5;
+    if (row > 0) bb.eri[b * c.N + row - 1] = pos - 1 - 5;
+  }
+  if (vroot) bb.root[base + p] = -(off[2] + ex.v[2] + 1);  // a valid root's label, negated
+  if (keep) {
+    bb.seg[base + pos] = bb.full[base + p];
+    bb.gflag[base + pos] = (bb.ground[base + p] == 1) ? 1 : 0;
+    bb.col[base + pos] = (uint32_t)col;
+    bb.srange[base + pos] = bb.range[base + p];
+  }
+  if (outl) bb.outl[base + off[1] + ex.v[1]] = bb.full[base + p];
+}
+
+__global__ void k_seg_labels(BatchBufs bb, DevCfg c) {
+  const int b = blockIdx.y;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= c.P) return;
+  const size_t base = (size_t)b * c.P;
+  const int f = bb.edges[base + p];
+  if (!(f & SF_INSEG)) return;
+  const int v = bb.root[base + p];  // -(label) at a valid root, else the root index
+  bb.label[base + p] = v < 0 ? -v : ((f & SF_VALID) ? -bb.root[base + v] : 999999);  // the final labelMat
+}
+
 // The gated topics of publishCloud (imageProjection.cpp:480-506) for scan 0 of
 // the batch, one 1024-thread workgroup walking the image row-major:
 // /full_cloud_info (the full cloud with intensity = range, :252-254), the
 // ground cloud (groundMat == 1 in rows <= groundScanInd, :301-308) and the
 // pure segmented cloud (labels > 0 and != 999999, intensity = label,
-// :357-367).  Needs the final label image (k_compact with want_labels).
+// :357-367).  Needs the final label image (want_labels).
 __global__ void __launch_bounds__(1024) k_gated(BatchBufs bb, DevCfg c, GatedBufs gb) {
   __shared__ int lds[64];
   int ng = 0, np = 0;
@@ -332,30 +416,6 @@ __global__ void __launch_bounds__(1024) k_gated(BatchBufs bb, DevCfg c, GatedBuf
   }
 }
 
-// Exclusive block prefix of three 0/1 flags (any block size up to 16 waves):
-// ballots within a wave, the wave totals through LDS (one barrier).  The
-// caller separates two calls with a barrier (lds is reused).
-__device__ __forceinline__ Scan3 block_scan3_bits(bool f0, bool f1, bool f2, Scan3* total, int* lds /*48*/) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const unsigned long long lt = (1ull << lane) - 1;
-  const unsigned long long m0 = __ballot(f0), m1 = __ballot(f1), m2 = __ballot(f2);
-  if (lane == 0) {
-    lds[wave] = (int)__popcll(m0);
-    lds[16 + wave] = (int)__popcll(m1);
-    lds[32 + wave] = (int)__popcll(m2);
-  }
-  __syncthreads();
-  Scan3 out{{(int)__popcll(m0 & lt), (int)__popcll(m1 & lt), (int)__popcll(m2 & lt)}};
-  Scan3 t{{0, 0, 0}};
-  for (int w = 0; w < nw; ++w) {
-    const int a = lds[w], b = lds[16 + w], c = lds[32 + w];
-    if (w < wave) { out.v[0] += a; out.v[1] += b; out.v[2] += c; }
-    t.v[0] += a; t.v[1] += b; t.v[2] += c;
-  }
-  *total = t;
-  return out;
-}
-
 // ---------------------------------------------------------------------------
 // Segmentation of one scan in LDS (labelComponents + the cloudSegmentation
 // compaction, imageProjection.cpp:300-460), one 1024-thread workgroup per
@@ -372,10 +432,10 @@ __device__ __forceinline__ Scan3 block_scan3_bits(bool f0, bool f1, bool f2, Sca
 //     step 5 in pixel order);
 //  4. per root one LDS word: the component's size (bits 0-14) and the rows of
 //     its pushed (non-seed) pixels (bits 15-30, lineCountFlag :431);
-//  5. k_compact's ordered pass, the validity test (:441-451) on the root's
+//  5. the ordered compaction pass, the validity test (:441-451) on the root's
 //     word; a valid root's word becomes -(its label) when its chunk is
 //     scanned, which its later pixels read (the root precedes them).
-// Results equal the HBM kernels' (k_ccl_* + k_compact) bit for bit.
+// Results equal the HBM kernels' (k_ccl_* + k_seg_flags/_scan/_write) bit for bit.
 constexpr int kSegLdsMaxP = 32767;  // counts fit 15 bits; 128 KB of parents
 constexpr int kSegLdsMaxN = 16;     // the row mask fits 16 bits
 constexpr int kSegK = (kSegLdsMaxP + 1023) / 1024;  // 1024-pixel chunks per scan
@@ -604,7 +664,11 @@ void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hip
   k_ccl_union<<<gpix, 256, 0, s>>>(bb, c);
   k_ccl_root<<<gpix, 256, 0, s>>>(bb, c);
   tm->mark("ip.compact", s);
-  k_compact<<<B, 1024, 0, s>>>(bb, c, want_labels);
+  const dim3 gch((P + 1023) / 1024, B);
+  k_seg_flags<<<gch, 1024, 0, s>>>(bb, c);
+  k_seg_scan<<<B, 1024, 0, s>>>(bb, c);
+  k_seg_write<<<gch, 1024, 0, s>>>(bb, c);
+  if (want_labels) k_seg_labels<<<gpix, 256, 0, s>>>(bb, c);
 }
 
 }  // namespace lego
