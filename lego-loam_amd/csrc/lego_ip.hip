@@ -382,38 +382,71 @@ __global__ void k_seg_labels(BatchBufs bb, DevCfg c) {
 }
 
 // The gated topics of publishCloud (imageProjection.cpp:480-506) for scan 0 of
-// the batch, one 1024-thread workgroup walking the image row-major:
+// the batch, one 1024-pixel chunk per workgroup in row-major order:
 // /full_cloud_info (the full cloud with intensity = range, :252-254), the
 // ground cloud (groundMat == 1 in rows <= groundScanInd, :301-308) and the
 // pure segmented cloud (labels > 0 and != 999999, intensity = label,
-// :357-367).  Needs the final label image (want_labels).
-__global__ void __launch_bounds__(1024) k_gated(BatchBufs bb, DevCfg c, GatedBufs gb) {
+// :357-367).  Needs the final label image (want_labels).  k_gated_flags
+// writes the info cloud and each chunk's two counts (into parent[], free
+// after the segmentation), k_gated_scan their exclusive prefixes and the
+// totals, k_gated_write both clouds at their ordered positions.
+__device__ __forceinline__ void gated_flags(const BatchBufs& bb, const DevCfg& c, int p, bool& gnd, bool& pure) {
+  gnd = pure = false;
+  if (p < c.P) {
+    const int L = bb.label[p];
+    gnd = p / c.H <= c.g && bb.ground[p] == 1;
+    pure = L > 0 && L != 999999;
+  }
+}
+
+__global__ void __launch_bounds__(1024) k_gated_flags(BatchBufs bb, DevCfg c, GatedBufs gb) {
+  __shared__ int lds[48];
+  const int ch = blockIdx.x, p = ch * blockDim.x + threadIdx.x;
+  if (p < c.P) {
+    const float4 f = bb.full[p];
+    const float r = bb.range[p];
+    gb.info[p] = r == FLT_MAX ? f : make_float4(f.x, f.y, f.z, r);
+  }
+  bool gnd, pure;
+  gated_flags(bb, c, p, gnd, pure);
+  block_counts3(gnd, pure, false, lds, bb.parent + 3 * ch);
+}
+
+__global__ void __launch_bounds__(1024) k_gated_scan(BatchBufs bb, DevCfg c, GatedBufs gb) {
   __shared__ int lds[64];
-  int ng = 0, np = 0;
-  for (int t0 = 0; t0 < c.P; t0 += blockDim.x) {
-    const int p = t0 + threadIdx.x;
-    bool gnd = false, pure = false;
-    int L = 0;
-    float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (p < c.P) {
-      f = bb.full[p];
-      const float r = bb.range[p];
-      gb.info[p] = r == FLT_MAX ? f : make_float4(f.x, f.y, f.z, r);
-      L = bb.label[p];
-      gnd = p / c.H <= c.g && bb.ground[p] == 1;
-      pure = L > 0 && L != 999999;
-    }
-    Scan3 in{{gnd ? 1 : 0, pure ? 1 : 0, 0}}, tot;
+  const int nCh = (c.P + 1023) / 1024;
+  int* cnt = bb.parent;
+  int run[2] = {0, 0};
+  for (int c0 = 0; c0 < nCh; c0 += blockDim.x) {
+    const int ch = c0 + threadIdx.x;
+    Scan3 in{{0, 0, 0}}, tot;
+    if (ch < nCh) in = Scan3{{cnt[3 * ch], cnt[3 * ch + 1], 0}};
     const Scan3 ex = block_scan3(in, &tot, lds);
-    if (gnd) gb.ground[ng + ex.v[0]] = f;
-    if (pure) gb.pure[np + ex.v[1]] = make_float4(f.x, f.y, f.z, (float)L);
-    ng += tot.v[0];
-    np += tot.v[1];
+    if (ch < nCh) {
+      cnt[3 * ch] = run[0] + ex.v[0];
+      cnt[3 * ch + 1] = run[1] + ex.v[1];
+    }
+    run[0] += tot.v[0];
+    run[1] += tot.v[1];
   }
   if (threadIdx.x == 0) {
-    gb.n[0] = ng;
-    gb.n[1] = np;
+    gb.n[0] = run[0];
+    gb.n[1] = run[1];
   }
+}
+
+__global__ void __launch_bounds__(1024) k_gated_write(BatchBufs bb, DevCfg c, GatedBufs gb) {
+  __shared__ int lds[64];
+  const int ch = blockIdx.x, p = ch * blockDim.x + threadIdx.x;
+  bool gnd, pure;
+  gated_flags(bb, c, p, gnd, pure);
+  Scan3 tot;
+  const Scan3 ex = block_scan3_bits(gnd, pure, false, &tot, lds);
+  if (!gnd && !pure) return;
+  const int* off = bb.parent + 3 * ch;
+  const float4 f = bb.full[p];
+  if (gnd) gb.ground[off[0] + ex.v[0]] = f;
+  if (pure) gb.pure[off[1] + ex.v[1]] = make_float4(f.x, f.y, f.z, (float)bb.label[p]);
 }
 
 // ---------------------------------------------------------------------------
@@ -633,7 +666,10 @@ __global__ void __launch_bounds__(1024) k_seg_lds(BatchBufs bb, DevCfg c, int wa
 }
 
 void launch_gated(const BatchBufs& bb, const DevCfg& c, const GatedBufs& gb, hipStream_t s) {
-  k_gated<<<1, 1024, 0, s>>>(bb, c, gb);
+  const int nCh = (c.P + 1023) / 1024;
+  k_gated_flags<<<nCh, 1024, 0, s>>>(bb, c, gb);
+  k_gated_scan<<<1, 1024, 0, s>>>(bb, c, gb);
+  k_gated_write<<<nCh, 1024, 0, s>>>(bb, c, gb);
 }
 
 void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hipStream_t s,

@@ -82,6 +82,14 @@ def main():
             xph["rings_parallel_picking"] = xp[6]
             xph["sector_rewalks"] = xp[5]
             xph["mean_workgroups_in_flight_at_start"] = round(xp[7] / rings, 1)
+            op = (C.c_uint64 * 32)()
+            lib.lego_odom_profile(fl.h, -1, op)
+            nsc = S * K * (args.steps + 1)  # stamps of every workgroup 0 of a stream... summed over all workgroups
+            xph["odom_us_per_scan_summed_over_workgroups"] = {
+                nm: round(op[i] / 100.0 / nsc, 2) for i, nm in
+                ((0, "surf_nn"), (2, "corner_nn"), (3, "corner"), (4, "solve"), (5, "integrate"), (6, "to_end"),
+                 (7, "build"), (12, "nn_shells"), (21, "rows"), (23, "solve_qr"), (24, "nn_local"))}
+            xph["odom_iters_per_scan"] = {"surf": op[9] / nsc, "corner": op[10] / nsc, "nn": op[11] / nsc}
         fl.close()
         print(json.dumps({"streams": S, "k": K, "scans_per_s": S * K * args.steps / dt,
                           "ms_per_call": dt / args.steps * 1e3, "valid_last": valid,
