@@ -234,55 +234,65 @@ __host__ __device__ inline int next_pow2(int x) {
   return m;
 }
 
-// LDS of one (scan, ring) workgroup, sized so that four fit a CU for
-// VLP-16-class rings (occupancy: the picking is a serial, latency-bound walk).
-// The sectors are sorted in per-wave scratch buffers (one sector per wave at a
-// time) and kept as index permutations (uint16, the ring window's positions);
-// the scratch region is reused by the VoxelGrid keys after the picking.
-// a sector of n <= (H + 32) / 6 + 2 entries plus the fallback sort's stack
-// (kIntroStack words) behind it
+// LDS of one (scan, ring) workgroup, laid out by phase so that five fit a CU
+// for VLP-16-class rings (W = H + 32 window positions; the kernel's time
+// scales with the resident workgroups: two per CU took 1.86x the time of
+// four).  Region A, then region B, then misc / red:
+//   sorts    A: the waves' sector scratch          B: curv, perm, gfl
+//   picking  A: pick lists [0, 1 KB), the initial  B: curv, perm, gfl
+//               picked copy, picked, label, col
+//   less-flat                                      B: lf (its tail)
+//   VoxelGrid   the keys from offset 0 over A and B's head, lf in B's tail
+// col, picked and label are loaded once the sorts are done.
+// A sector holds n <= (H + 32) / 6 + 2 entries plus the fallback sort's
+// stack (kIntroStack words) behind it.
 __host__ __device__ inline int extract_sector_cap(int H) { return next_pow2((H + 32) / 6 + 2 + (kIntroStack + 1) / 2); }
-__host__ __device__ inline size_t extract_sort_region(int H) {
+struct ExtractLayout {
+  size_t A, B, colOff, lfOff;  // region sizes; col's offset in A, lf's in B
+};
+__host__ __device__ inline ExtractLayout extract_layout(int H) {
   const size_t W = (size_t)H + 32;
-  const size_t vox = (size_t)next_pow2((int)W) * 8;
+  ExtractLayout e;
   const size_t sec = (size_t)(kExtractThreads / 64) * extract_sector_cap(H) * 8;
-  return vox > sec ? vox : sec;
+  e.colOff = (1024 + 3 * W + 1) & ~(size_t)1;  // after the pick lists, the picked copy, picked, label
+  size_t a = e.colOff + 2 * W;
+  if (sec > a) a = sec;
+  e.lfOff = (5 * W + 1) & ~(size_t)1;          // over perm / gfl, dead once the walks are done
+  e.B = (e.lfOff + 2 * W + 15) & ~(size_t)15;
+  const size_t vox = (size_t)next_pow2((int)W) * 8;  // keys from A's start up to lf
+  if (vox > a + e.lfOff) a = vox - e.lfOff;
+  e.A = (a + 15) & ~(size_t)15;
+  return e;
 }
 __host__ __device__ inline size_t extract_lds_bytes(int H) {
-  const size_t W = (size_t)H + 32;
-  size_t s = 0;
-  s += W * 4;                     // curv
-  s += W * 2;                     // lf
-  s += W * 2;                     // perm (the sectors' sorted positions)
-  s += extract_sort_region(H);    // sort scratch / vox
-  s += 64 * 4 + 64 * 4;           // misc + red
-  s += W * 2;                     // col
-  s += W * 3;                     // picked, label, gfl
-  return (s + 15) & ~(size_t)15;
+  const ExtractLayout e = extract_layout(H);
+  return e.A + e.B + 64 * 4 + 64 * 4;  // + misc + red
 }
 
 __device__ __forceinline__ ExtractLds carve(unsigned char* base, int H) {
   const size_t W = (size_t)H + 32;
+  const ExtractLayout e = extract_layout(H);
   ExtractLds L;
-  size_t o = 0;
-  L.vox = (unsigned long long*)(base + o);
-  L.srt = (SmoothEntry*)(base + o);
+  unsigned char* A = base;
+  unsigned char* B = base + e.A;
+  L.vox = (unsigned long long*)A;
+  L.srt = (SmoothEntry*)A;
   L.orig = nullptr;
-  o += extract_sort_region(H);
-  L.curv = (float*)(base + o); o += W * 4;
-  L.lf = (uint16_t*)(base + o); o += W * 2;
-  L.perm = (uint16_t*)(base + o); o += W * 2;
-  L.misc = (int*)(base + o); o += 64 * 4;
-  L.red = (float*)(base + o); o += 64 * 4;
-  L.col = (uint16_t*)(base + o); o += W * 2;
-  L.picked = base + o; o += W;
-  L.label = (int8_t*)(base + o); o += W;
-  L.gfl = base + o; o += W;
+  L.picked = A + 1024 + W;  // [1024, 1024 + W): the initial picked copy of the speculative walks
+  L.label = (int8_t*)(A + 1024 + 2 * W);
+  L.col = (uint16_t*)(A + e.colOff);
+  L.curv = (float*)B;
+  L.perm = (uint16_t*)(B + 4 * W);
+  L.gfl = B + 6 * W;
+  L.lf = (uint16_t*)(B + e.lfOff);
+  L.misc = (int*)(B + e.B);
+  L.red = (float*)(B + e.B + 64 * 4);
   return L;
 }
 
 enum { M_TIE = 0, M_LF = 1, M_OVF = 2, M_NSH = 3, M_NLS = 4, M_NFL = 5, M_D0 = 6, M_D1 = 7,
-       M_MB0 = 8, M_MB1 = 9, M_MB2 = 10, M_PH = 11, M_REWALK = 12, M_WOFF = 16, M_SEC = 24, M_NEF = 48 };
+       M_MB0 = 8, M_MB1 = 9, M_MB2 = 10, M_PH = 11, M_REWALK = 12, M_P0 = 13, M_WOFF = 16, M_SEC = 24,
+       M_NEF = 48 };
 // per-sector pick list: 2 sharp, 20 less sharp, 4 flat (featureAssociation.cpp:709-748)
 constexpr int kPickListStride = 32;
 
@@ -467,21 +477,15 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
   float4* olf = bb.r_lflat + R.base + (size_t)ring * c.H;
   volatile uint8_t* picked = L.picked;
   volatile int8_t* label = L.label;
-  for (int t = tid; t < R.Wn; t += blockDim.x) {
+  for (int t = tid; t < R.Wn; t += blockDim.x) {  // what the sorts read (col, picked, label: after them)
     const size_t g = R.base + R.lo + t;
     L.curv[t] = bb.curv[g];
-    L.col[t] = (uint16_t)bb.col[g];
-    L.picked[t] = bb.pick0[g];
-    L.label[t] = 0;
     L.gfl[t] = bb.gflag[g];
   }
   if (tid < 64) L.misc[tid] = 0;
   __syncthreads();
   int ph = 0;
-  if (ring == 0 && carry) {
-    ph = carry->phantom_ind;
-    if (tid == 0 && R.lo == 0 && R.Wn > 0 && carry->picked0) L.picked[0] = 1;
-  }
+  if (ring == 0 && carry) ph = carry->phantom_ind;
   if (tid == 0) L.misc[M_PH] = ph;  // the phantom entry's index unless a sector sort replaces it
   __syncthreads();
   int flags = 0;
@@ -608,6 +612,16 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
     }
     wave_sync_lds();  // the scratch is refilled for the wave's next sector
   }
+  __syncthreads();
+  // the walks' arrays, in the sort scratch now that the sorts are done
+  for (int t = tid; t < R.Wn; t += blockDim.x) {
+    const size_t g = R.base + R.lo + t;
+    L.col[t] = (uint16_t)bb.col[g];
+    L.picked[t] = bb.pick0[g];
+    L.label[t] = 0;
+  }
+  __syncthreads();
+  if (ring == 0 && carry && tid == 0 && R.lo == 0 && R.Wn > 0 && carry->picked0) L.picked[0] = 1;
   __syncthreads();
   stamp(0);  // window load + the six sector sorts
   const int newph = L.misc[M_PH];
@@ -846,6 +860,7 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
     if (tid == 0) L.misc[M_LF] = total;
     __syncthreads();
   }
+  if (tid == 0) L.misc[M_P0] = (R.Wn > 0 && L.picked[0]) ? 1 : 0;  // the carry's, before the keys overwrite picked
   stamp(2);  // picked-point copies + the ordered less-flat set
   // ---- per-ring VoxelGrid 0.2 m on the less-flat set (:778-782)
   const int K = L.misc[M_LF];
@@ -985,7 +1000,7 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
     int fl = __ballot(flags != 0) ? 1 : 0;
     if (tid == 0) {
       carry->phantom_ind = newph;
-      carry->picked0 = (R.lo == 0 && R.Wn > 0) ? (L.picked[0] ? 1 : 0) : carry->picked0;
+      carry->picked0 = (R.lo == 0 && R.Wn > 0) ? L.misc[M_P0] : carry->picked0;
       carry->flags |= fl;
     }
   }
@@ -1099,7 +1114,7 @@ void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_ca
   if (bb.imu) k_fa_imu_start<<<(B + 63) / 64, 64, 0, s>>>(bb, c);
   k_fa_point<<<gpts, 256, 0, s>>>(bb, c);
   tm->mark("fa.extract", s);
-  const size_t lds = extract_lds_bytes(c.H);
+  const size_t lds = extract_lds_bytes(c.H) + (std::getenv("LEGO_XLDS_PAD") ? (size_t)std::atoi(std::getenv("LEGO_XLDS_PAD")) : 0);
   k_extract<<<dim3(c.N, B), kExtractThreads, lds, s>>>(bb, c);
   tm->mark("fa.fixup", s);
   k_fa_fixup<<<S, kExtractThreads, lds, s>>>(bb, c, B / S, d_carry);
