@@ -234,7 +234,7 @@ __host__ __device__ inline int next_pow2(int x) {
   return m;
 }
 
-// LDS of one (scan, ring) workgroup, laid out by phase so that five fit a CU
+// LDS of one (scan, ring) workgroup, laid out by phase so that six fit a CU
 // for VLP-16-class rings (W = H + 32 window positions; the kernel's time
 // scales with the resident workgroups: two per CU took 1.86x the time of
 // four).  Region A, then region B, then misc / red:
@@ -247,13 +247,14 @@ __host__ __device__ inline int next_pow2(int x) {
 // A sector holds n <= (H + 32) / 6 + 2 entries plus the fallback sort's
 // stack (kIntroStack words) behind it.
 __host__ __device__ inline int extract_sector_cap(int H) { return next_pow2((H + 32) / 6 + 2 + (kIntroStack + 1) / 2); }
+constexpr int kSortWaves = 3;  // waves sorting sectors at once (the scratch holds their sectors)
 struct ExtractLayout {
   size_t A, B, colOff, lfOff;  // region sizes; col's offset in A, lf's in B
 };
 __host__ __device__ inline ExtractLayout extract_layout(int H) {
   const size_t W = (size_t)H + 32;
   ExtractLayout e;
-  const size_t sec = (size_t)(kExtractThreads / 64) * extract_sector_cap(H) * 8;
+  const size_t sec = (size_t)kSortWaves * extract_sector_cap(H) * 8;
   e.colOff = (1024 + 3 * W + 1) & ~(size_t)1;  // after the pick lists, the picked copy, picked, label
   size_t a = e.colOff + 2 * W;
   if (sec > a) a = sec;
@@ -519,7 +520,9 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
   constexpr int kPhantom = -2;
   const int secCap = extract_sector_cap(c.H);
   const bool filtered = ring != 0;
-  for (int j = wave; j < 6; j += nw) {
+  // three waves sort (two rounds of three sectors, as four waves would take
+  // two rounds too), so the scratch holds three sectors
+  for (int j = wave; j < 6 && wave < kSortWaves; j += kSortWaves) {
     int sp, ep, off;
     sector(j, &sp, &ep, &off);
     if (sp >= ep) continue;
@@ -870,7 +873,7 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
   // the less-flat points, gathered once: the thread's first kLfRegs in
   // registers for the keys below, the rest (rings wider than
   // kLfRegs * 256 points) gathered again there
-  constexpr int kLfRegs = 8;
+  constexpr int kLfRegs = 4;
   float4 lp[kLfRegs];
 #pragma unroll
   for (int i = 0; i < kLfRegs; ++i) {
@@ -1007,7 +1010,7 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
   __syncthreads();
 }
 
-__global__ void __launch_bounds__(kExtractThreads) k_extract(BatchBufs bb, DevCfg c) {
+__global__ void __launch_bounds__(kExtractThreads, 6) k_extract(BatchBufs bb, DevCfg c) {  // six waves per SIMD: six workgroups per CU
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   const ExtractLds L = carve(lds_raw, c.H);
   const int ring = blockIdx.x, b = blockIdx.y;
