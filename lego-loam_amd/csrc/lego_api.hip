@@ -417,6 +417,10 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
   ob.capLS = (int)(N * kLessSharpPerRing);
   ob.capCorner = ob.capLS;
   ob.capSurf = (int)P;
+  if (ob.capSurf >= (1 << 21) - 1 || ob.capCorner >= (1 << 21) - 1) {  // the NN exchange's 21-bit indices
+    set_err("max_points too large for the odometry exchange (< 2097151 points per scan)");
+    return fail(LEGO_E_ARG);
+  }
   const size_t S = n_streams;
   ob.S = n_streams;
   A(ob.st, S);
@@ -452,10 +456,10 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
     A(ob.nS.gPts, G * ob.capSurf);
     ob.capQ = (int)(N * kFlatPerRing);
     A(ob.qi, G * 3 * ob.capQ);
-    // exchange block: 16-byte error word, then per stream one slot of 3 x capQ
+    // exchange block: 16-byte error word, then per stream one slot of capQ
     // granules per NN round a launch can run (10 per scan)
     ob.roundsCap = 10 * (int)((B1 + S - 1) / S);
-    const size_t xslots = S * (size_t)ob.roundsCap * 3 * (size_t)ob.capQ;
+    const size_t xslots = S * (size_t)ob.roundsCap * (size_t)ob.capQ;
     ob.xbytes = 16 + copies * sizeof(unsigned long long) * xslots;
     unsigned char* xb = nullptr;
     A(xb, ob.xbytes);
@@ -609,7 +613,7 @@ static OdomBufs ob_slice(const OdomBufs& a, const DevCfg& c, int c0, int s0, int
   o.nC.gPts += w * a.capCorner;
   o.nS.gPts += w * a.capSurf;
   o.qi += w * 3 * a.capQ;
-  o.xg += (size_t)s0 * a.roundsCap * 3 * a.capQ;
+  o.xg += (size_t)s0 * a.roundsCap * a.capQ;
   o.xh += (size_t)s0 * 2 * 3 * a.capH;
   o.sumOut += k * 6; o.curOut += k * 6; o.validOut += k; o.pubOut += k;
   o.cornerEnd += k * a.capLS; o.surfEnd += k * c.P;

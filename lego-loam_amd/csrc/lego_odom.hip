@@ -1144,10 +1144,10 @@ __device__ __forceinline__ bool converged3(bool surf, const float (&X)[3]) {
 
 // ---------------------------------------------------------------- exchange
 // The workgroups of a launch run the same serial chain on identical inputs
-// and split only the correspondence searches.  Results travel as 8-byte
-// {tag = round + 1, value} granules (MI355X L2s are per XCD: agent-scope
-// relaxed atomics, the data is its own flag), one slot per NN round of the
-// launch, zeroed before the launch.  Nothing assumes the launch's workgroups
+// and split only the correspondence searches.  Results travel as one 8-byte
+// granule per query (x_pack: the three indices and a valid bit; MI355X L2s
+// are per XCD: agent-scope relaxed atomics, the data is its own flag), one
+// slot per NN round of the launch, zeroed before the launch.  Nothing assumes the launch's workgroups
 // are resident together: a granule that has not arrived within kStealTicks is
 // computed by the waiting wave itself (the search is deterministic: the same
 // bits as its owner's), and a workgroup that starts late replays the chain
@@ -1160,14 +1160,25 @@ constexpr unsigned long long kLateTicks = 200000000;  // 2 s: the diagnostic lat
 __device__ __forceinline__ void x_publish(unsigned long long* p, unsigned long long v) {
   __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// The NN exchange's granule: (i1, i2, i3) of one query, each + 1 in 21 bits,
+// and bit 63 set (the round's slots are zeroed before the launch, so a
+// nonzero granule is a published one).  Clouds stay below 2^21 - 1 points
+// (checked at context creation).
+__device__ __forceinline__ unsigned long long x_pack(int i1, int i2, int i3) {
+  return (1ull << 63) | ((unsigned long long)(unsigned)(i1 + 1) << 42) |
+         ((unsigned long long)(unsigned)(i2 + 1) << 21) | (unsigned long long)(unsigned)(i3 + 1);
+}
+__device__ __forceinline__ int x_field(unsigned long long x, int k) {  // k = 0: i1, 1: i2, 2: i3
+  return (int)((x >> (42 - 21 * k)) & 0x1fffffu) - 1;
+}
 // Bounded wait for a granule; false when it did not arrive in time.  The
 // clock (an SMEM read) is consulted only every 32 polls.
-__device__ __forceinline__ bool x_try(const unsigned long long* p, unsigned long long tag, int* v) {
+__device__ __forceinline__ bool x_try(const unsigned long long* p, unsigned long long* v) {
   unsigned long long t0 = 0;
   for (unsigned n = 0;; ++n) {
     const unsigned long long x = __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if ((x & 0xffffffff00000000ull) == tag) {
-      *v = (int)(unsigned)x;
+    if (x >> 63) {
+      *v = x;
       return true;
     }
     if ((n & 31) == 0) {
@@ -1289,8 +1300,7 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
       int round = L.n[N_ROUND];
       const bool xch = G > 1 && round < ob.roundsCap;
       if (G > 1 && !xch && tid == 0) *ob.xerr = 1;  // more rounds than the slots (cannot happen: 10 per scan)
-      unsigned long long* xg = ob.xg + (size_t)round * 3 * ob.capQ;  // this stream's (odom_private)
-      const unsigned long long tag = (unsigned long long)(round + 1) << 32;
+      unsigned long long* xg = ob.xg + (size_t)round * ob.capQ;  // this stream's (odom_private)
       const bool w0 = S.prof && tid == 0;
       // findCorresponding{Surf,Corner}Features for query q by one wave
       auto search = [&](int q, int& i1, int& i2, int& i3) {
@@ -1303,7 +1313,22 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
             tq = n;
           }
         };
-        const float4 sel = to_start(qp[q], tc);
+        // TransformToStart of the wave's query: the three sines / cosines on
+        // lanes 0-2 at once (the same calls as to_start), then broadcast
+        const float4 pq = qp[q];
+        const float s = start_s(pq);
+        float sv, cv;
+        {
+          const int l3 = g % 3;  // selects, not tc[l3] (a lane-varying index would put tc in scratch)
+          lego_sincosf(s * (l3 == 0 ? tc[0] : (l3 == 1 ? tc[1] : tc[2])), &sv, &cv);
+        }
+        const float sx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sv), 0));
+        const float sy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sv), 1));
+        const float sz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sv), 2));
+        const float cx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cv), 0));
+        const float cy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cv), 1));
+        const float cz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cv), 2));
+        const float4 sel = to_start_t(pq, s, tc, cx, sx, cy, sy, cz, sz);
         sub(P_G0_TOSTART);
         i1 = stale ? nn_brute(snap, snapN, sel, c.nn_sq, g) : nn_i1(nn, sel, c.nn_sq, g, S.prof);
         if (i1 >= lastN) i1 = -1;  // an index past a stale snapshot's cloud
@@ -1325,40 +1350,35 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
         }
         if (g == 0) {
           qi[q] = i1; qi[qs + q] = i2; qi[2 * qs + q] = i3;
-          if (xch) {
-            x_publish(xg + 3 * q + 0, tag | (unsigned)i1);
-            x_publish(xg + 3 * q + 1, tag | (unsigned)i2);
-            x_publish(xg + 3 * q + 2, tag | (unsigned)i3);
-          }
+          if (xch) x_publish(xg + q, x_pack(i1, i2, i3));
         }
       }
       S.add(P_X_LOCAL);
       if (xch) {
-        // the other slices: lane l of a wave waits for granule l % 3 of query
-        // base + l / 3 (21 queries per pass); what does not arrive in time the
+        // the other slices: lane l of a wave waits for the granule of query
+        // base + l (64 queries per pass); what does not arrive in time the
         // wave computes itself
-        constexpr int kQPer = 21;
-        for (int base = grp * kQPer; base < nQ; base += kNGrp * kQPer) {
-          const int q = base + g / 3, k = g - 3 * (g / 3);
-          const bool want = g < 3 * kQPer && q < nQ && !(q >= q0 && q < q1);
+        for (int base = grp * kGL; base < nQ; base += kNGrp * kGL) {
+          const int q = base + g;
+          const bool want = q < nQ && !(q >= q0 && q < q1);
           bool got = !want;
           if (want) {
-            int v;
-            got = x_try(xg + 3 * q + k, tag, &v);
-            if (got) qi[k * qs + q] = v;
+            unsigned long long x;
+            got = x_try(xg + q, &x);
+            if (got) {
+              qi[q] = x_field(x, 0); qi[qs + q] = x_field(x, 1); qi[2 * qs + q] = x_field(x, 2);
+            }
           }
           unsigned long long miss = __ballot(!got);
           while (miss) {
-            const int qm = base + (__ffsll((long long)miss) - 1) / 3;
+            const int qm = base + __ffsll((long long)miss) - 1;
             int i1, i2, i3;
             search(qm, i1, i2, i3);
             if (g == 0) {
               qi[qm] = i1; qi[qs + qm] = i2; qi[2 * qs + qm] = i3;
-              x_publish(xg + 3 * qm + 0, tag | (unsigned)i1);
-              x_publish(xg + 3 * qm + 1, tag | (unsigned)i2);
-              x_publish(xg + 3 * qm + 2, tag | (unsigned)i3);
+              x_publish(xg + qm, x_pack(i1, i2, i3));
             }
-            miss &= ~(7ull << (3 * (qm - base)));
+            miss &= miss - 1;
           }
         }
       }
@@ -1499,7 +1519,7 @@ __device__ __forceinline__ OdomBufs odom_private(OdomBufs ob) {
   const size_t w = blockIdx.x;  // index into the [S x G x] arrays
   ob.st += s;
   ob.stIn += s;
-  ob.xg += (size_t)s * ob.roundsCap * 3 * ob.capQ;
+  ob.xg += (size_t)s * ob.roundsCap * ob.capQ;
   ob.xh += (size_t)s * 2 * 3 * ob.capH;
   ob.cornerLast[0] += w * ob.capCorner;
   ob.cornerLast[1] += w * ob.capCorner;
@@ -1922,7 +1942,7 @@ int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int K,
                 unsigned long long* prof) {
   tm->mark("odom.lm", s);
   // zero the exchange slots of the rounds this launch can use (10 per scan)
-  const size_t slot = (size_t)3 * ob.capQ * sizeof(unsigned long long);
+  const size_t slot = (size_t)ob.capQ * sizeof(unsigned long long);
   const size_t bytes = ob.S == 1 ? std::min<size_t>(ob.roundsCap, (size_t)10 * K) * slot
                                  : (size_t)ob.S * ob.roundsCap * slot;
   if (ob.G > 1 && hipMemsetAsync(ob.xg, 0, bytes, s) != hipSuccess) return -1;
