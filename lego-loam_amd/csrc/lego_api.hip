@@ -438,6 +438,11 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
       const int g = std::atoi(e);
       if (g >= 1 && (long)g * (long)n_streams <= (long)cus) ob.G = g;
     }
+    // without grids an NN round's wave searches its query's whole LDS cloud:
+    // worth it when that is about one query per wave (the grids' build is on
+    // every scan's chain); a fleet's few workgroups per stream keep them
+    ob.gridless = ob.G >= kGridlessMinWG ? 1 : 0;
+    if (const char* e = std::getenv("LEGO_ODOM_GRIDLESS")) ob.gridless = std::atoi(e) ? 1 : 0;  // diagnostic
     ob.wg = -1;
     if (const char* e = std::getenv("LEGO_ODOM_SILENT_WG"); e && S == 1) ob.wg = std::atoi(e);
     ob.late = -1;

@@ -109,6 +109,10 @@ struct OdomBufs {
   int G;                  // workgroups per stream
   int S;                  // streams
   int roundsCap;          // exchange slots (NN rounds) per stream and launch
+  // LDS-resident clouds without hash grids (host: G large enough that an NN
+  // round is about one query per wave): the closest point is an exhaustive
+  // pass over the LDS cloud and the index build keeps only the key tables
+  int gridless;
   // set in the kernel: this workgroup's index within its stream.  On the
   // host: -1, or the diagnostic LEGO_ODOM_SILENT_WG of a single-stream
   // context, a workgroup that uses private copies of both exchanges (placed
@@ -122,7 +126,7 @@ struct OdomBufs {
   // from the input state and the published rounds (tests)
   int late;
   // exchange: an error word shared by the streams (zeroed per batch), then
-  // per stream roundsCap x 3 x capQ granules (zeroed per launch)
+  // per stream roundsCap x capQ granules (zeroed per launch)
   void* xblock;
   size_t xbytes;
   unsigned* xerr;
@@ -155,6 +159,8 @@ void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_ca
 int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int K, hipStream_t s,
                 StageTimer* tm, unsigned long long* prof);
 int odom_workgroups(int N, int cusAvailable);
+// workgroups per stream from which the LDS-resident odometry runs without grids
+constexpr int kGridlessMinWG = 16;
 
 // One scan's pose-record fields, gathered on the device so a batch returns in
 // one copy; slot B of the array carries the exchange timeout word in `bad`.

@@ -388,6 +388,7 @@ struct NNView {
   const int* sufFirst;  // [NK + 1] first index whose key >= k (INT_MAX if none)
   const int* preLast;   // [NK]     last index whose key <= k (-1 if none)
   int irregular;        // a key outside [0, NK): tables unusable
+  int gridless;         // no grid (OdomBufs::gridless): exhaustive closest-point search
 };
 
 template <class Idx>
@@ -454,19 +455,22 @@ struct BuildArgs {
   NNStore<Idx> S, Cs;
   unsigned* cnt;
   int *wtot, *kfirst, *klast;
+  int gridless;  // key tables only (OdomBufs::gridless)
 };
 template <class Idx>
 __device__ __forceinline__ BuildArgs<Idx> build_args(const float4* ptsS, int nS, const NNStore<Idx>& S,
                                                      const float4* ptsC, int nC, const NNStore<Idx>& Cs, int NK,
-                                                     unsigned* cnt, int* wtot, int* kfirst, int* klast) {
+                                                     unsigned* cnt, int* wtot, int* kfirst, int* klast,
+                                                     int gridless = 0) {
   return BuildArgs<Idx>{ptsS, ptsC, nS, nC, fine_T(nS, S.Tcap), fine_T(nC, Cs.Tcap), NK, S, Cs,
-                        cnt, wtot, kfirst, klast};
+                        cnt, wtot, kfirst, klast, gridless};
 }
 // zeroes the counters and key tables (all threads; the caller's barrier follows)
 template <class Idx>
 __device__ __forceinline__ void build_zero(const BuildArgs<Idx>& B) {
   const int tid = threadIdx.x;
-  for (int b = tid; b < B.TS + B.TC; b += kOdomThreads) B.cnt[b] = 0;
+  if (!B.gridless)
+    for (int b = tid; b < B.TS + B.TC; b += kOdomThreads) B.cnt[b] = 0;
   for (int k = tid; k < 2 * B.NK; k += kOdomThreads) { B.kfirst[k] = INT_MAX; B.klast[k] = -1; }
   if (tid == 0) { *B.S.irregular = 0; *B.Cs.irregular = 0; }
 }
@@ -491,7 +495,8 @@ __device__ __forceinline__ void build_count(const BuildArgs<Idx>& B, int i0, flo
   if (i < n && active) {
     const bool corner = i >= B.nS;
     const int T = corner ? B.TC : B.TS;
-    atomicAdd(&B.cnt[(corner ? B.TS : 0) + fine_bucket(cell_of(p.x), cell_of(p.y), cell_of(p.z), T)], 1u);
+    if (!B.gridless)
+      atomicAdd(&B.cnt[(corner ? B.TS : 0) + fine_bucket(cell_of(p.x), cell_of(p.y), cell_of(p.z), T)], 1u);
     const int k = (int)p.w;
     if (k < 0 || k >= B.NK || kp > k) {
       *(corner ? B.Cs.irregular : B.S.irregular) = 1;
@@ -525,6 +530,10 @@ __device__ __forceinline__ void build_finish(const BuildArgs<Idx>& B, unsigned l
     (c0 ? Cs : S).preLast[k] = M;
   }
   if (tid == 0) { S.sufFirst[NK] = INT_MAX; Cs.sufFirst[NK] = INT_MAX; }
+  if (B.gridless) {
+    __syncthreads();
+    return;
+  }
   block_exscan(cnt, TS + TC, B.wtot);  // corner starts come out offset by nS
   stamp(P_B_SCAN);
   constexpr int kBuildU = 8;  // points per lane in flight
@@ -694,7 +703,7 @@ __device__ __forceinline__ int nn_i1(const NNView<Idx>& v, float4 q, float bound
   if (v.n <= 0) return -1;
   // a small cloud (the corner clouds: ~100-200 points) is searched whole:
   // four points per lane cost less than the bucket lookups the shell needs
-  if (v.n <= kBruteSmall) return nn_brute(v.pts, v.n, q, bound, g);
+  if (v.n <= kBruteSmall || v.gridless) return nn_brute(v.pts, v.n, q, bound, g);
   float bd = bound;
   int bi = INT_MAX;
   const int cx = cell_of(q.x), cy = cell_of(q.y), cz = cell_of(q.z);
@@ -898,12 +907,13 @@ __device__ __forceinline__ bool sensor_resident(const DevCfg& c) {
 }
 
 // Views of the current indexes (valid when the snapshot is current).
-__device__ __forceinline__ NNView<uint16_t> view_lds(bool surf, const OdomLds& L, const OdomState* st, const DevCfg& c) {
+__device__ __forceinline__ NNView<uint16_t> view_lds(bool surf, const OdomLds& L, const OdomState* st, const DevCfg& c,
+                                                    int gridless) {
   if (surf)
     return NNView<uint16_t>{L.lastS, st->surfLastNum, L.gEndS, L.gOrdS, nullptr, fine_T(st->surfLastNum, kLdsGridS),
-                            c.N, L.sufS, L.preS, L.n[N_IRR_S]};
+                            c.N, L.sufS, L.preS, L.n[N_IRR_S], gridless};
   return NNView<uint16_t>{L.lastC, st->cornerLastNum, L.gEndC, L.gOrdC, nullptr, fine_T(st->cornerLastNum, kLdsGridC),
-                          c.N, L.sufC, L.preC, L.n[N_IRR_C]};
+                          c.N, L.sufC, L.preC, L.n[N_IRR_C], gridless};
 }
 // HBM-resident clouds: the LDS that holds the clouds, queries and counters of
 // the resident layout (lastS .. cnt, contiguous) is free, and takes both
@@ -917,19 +927,19 @@ __device__ __forceinline__ NNView<uint32_t> view_hbm(bool surf, const OdomLds& L
   const int TS = fine_T(st->surfLastNum, ob.gTS);
   if (surf)
     return NNView<uint32_t>{buf2(ob.surfLast, st->curBuf), st->surfLastNum, ends, nullptr, ob.nS.gPts, TS, c.N,
-                            L.sufS, L.preS, L.n[N_IRR_S]};
+                            L.sufS, L.preS, L.n[N_IRR_S], 0};
   return NNView<uint32_t>{buf2(ob.cornerLast, st->curBuf), st->cornerLastNum, ends + TS, nullptr, ob.nC.gPts,
-                          fine_T(st->cornerLastNum, ob.gTC), c.N, L.sufC, L.preC, L.n[N_IRR_C]};
+                          fine_T(st->cornerLastNum, ob.gTC), c.N, L.sufC, L.preC, L.n[N_IRR_C], 0};
 }
 
 // The build arguments of both clouds' indexes over the current last clouds
 // (st->curBuf, st->*LastNum) in the layout `resident` selects.
 __device__ __forceinline__ BuildArgs<uint16_t> lds_build_args(const OdomLds& L, const OdomState* st,
-                                                              const DevCfg& c) {
+                                                              const DevCfg& c, int gridless) {
   NNStore<uint16_t> sS{L.gEndS, L.gOrdS, nullptr, L.sufS, L.preS, &L.n[N_IRR_S], kLdsGridS};
   NNStore<uint16_t> sC{L.gEndC, L.gOrdC, nullptr, L.sufC, L.preC, &L.n[N_IRR_C], kLdsGridC};
   return build_args<uint16_t>(L.lastS, st->surfLastNum, sS, L.lastC, st->cornerLastNum, sC, c.N, L.cnt, L.wtot,
-                              L.kfirst, L.klast);
+                              L.kfirst, L.klast, gridless);
 }
 __device__ __forceinline__ BuildArgs<uint32_t> hbm_build_args(const OdomLds& L, const OdomBufs& ob,
                                                               const OdomState* st, const DevCfg& c) {
@@ -946,7 +956,7 @@ __device__ __forceinline__ BuildArgs<uint32_t> hbm_build_args(const OdomLds& L, 
 // Rebuilds both clouds' indexes (all threads) over the current last clouds.
 __device__ __forceinline__ void build_indexes(const OdomLds& L, const OdomBufs& ob, const OdomState* st,
                                               const DevCfg& c, unsigned long long* prof = nullptr) {
-  if (st->resident) nn_build2(lds_build_args(L, st, c), prof);
+  if (st->resident) nn_build2(lds_build_args(L, st, c, ob.gridless), prof);
   else nn_build2(hbm_build_args(L, ob, st, c), prof);
 }
 
@@ -1243,7 +1253,7 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
   if constexpr (R) {
     last = surf ? L.lastS : L.lastC;
     qi = L.qi; qs = kLdsQ;
-    nn = view_lds(surf, L, st, c);
+    nn = view_lds(surf, L, st, c, ob.gridless);
   } else {
     last = surf ? buf2(ob.surfLast, st->curBuf) : buf2(ob.cornerLast, st->curBuf);
     qi = ob.qi; qs = ob.capQ;
@@ -1658,7 +1668,7 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     NNStore<uint16_t> nsS{L.gEndS, L.gOrdS, nullptr, L.sufS, L.preS, &L.n[N_IRR_S], kLdsGridS};
     NNStore<uint16_t> nsC{L.gEndC, L.gOrdC, nullptr, L.sufC, L.preC, &L.n[N_IRR_C], kLdsGridC};
     const BuildArgs<uint16_t> BL = build_args<uint16_t>(L.lastS, F.nLF, nsS, L.lastC, F.nLS, nsC, c.N, L.cnt,
-                                                        L.wtot, L.kfirst, L.klast);
+                                                        L.wtot, L.kfirst, L.klast, ob.gridless);
     unsigned* hcnt = hbm_grid_ends(L);
     const int hTS = fine_T(F.nLF, ob.gTS);
     NNStore<uint32_t> hsS{hcnt, nullptr, ob.nS.gPts, L.sufS, L.preS, &L.n[N_IRR_S], ob.gTS};

@@ -95,3 +95,28 @@ def test_dense_stream_host_batches(L, sensor, seed, n, B):
         recs.extend(g.odom_batch(pts[a:b], off[i * B:(i + 1) * B + 1] - a, stamps[i * B:(i + 1) * B]))
     g.close()
     _check(recs, ref, f"{sensor} seed {seed}")
+
+
+@pytest.mark.parametrize("gridless", ["0", "1"])
+def test_vlp16_grid_and_gridless_odometry(L, gridless):
+    """Both closest-point searches of the LDS-resident odometry against the
+    oracle: the hashed 0.5 m grids (what a fleet with few workgroups per stream
+    runs) and the gridless mode (exhaustive pass over the LDS cloud, key tables
+    only; what a single stream's 48 workgroups run).  LEGO_ODOM_GRIDLESS
+    overrides the host's choice (OdomBufs::gridless)."""
+    import os
+
+    n, B = 40, 20
+    scans, pts, off, stamps = _stream(L, "VLP-16", 4, n)
+    ref = _oracle_recs(L, "VLP-16", scans)
+    os.environ["LEGO_ODOM_GRIDLESS"] = gridless
+    try:
+        g = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=int(np.max(np.diff(off))) + 16, max_batch=B)
+    finally:
+        os.environ.pop("LEGO_ODOM_GRIDLESS", None)
+    recs = []
+    for i in range(n // B):
+        a, b = off[i * B], off[(i + 1) * B]
+        recs.extend(g.odom_batch(pts[a:b], off[i * B:(i + 1) * B + 1] - a, stamps[i * B:(i + 1) * B]))
+    g.close()
+    _check(recs, ref, f"VLP-16 seed 4 gridless={gridless}")
