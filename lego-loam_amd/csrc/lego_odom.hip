@@ -132,7 +132,7 @@ __device__ __forceinline__ EndTrig end_trig(const float* tc) {
   lego_sincosf(tc[2], &e.sz, &e.cz);
   return e;
 }
-__device__ __forceinline__ float4 to_end(float4 pi, const float* tc, const EndTrig& et, const ImuEnd& im) {
+__device__ __forceinline__ float4 to_end_t(float4 pi, const float* tc, const EndTrig& et, const ImuEnd& im) {
   const float s = 10 * (pi.w - (float)(int)pi.w);
   float tx = s * tc[3], ty = s * tc[4], tz = s * tc[5];
   float cx, sx, cy, sy, cz, sz;
@@ -176,6 +176,14 @@ __device__ __forceinline__ float4 to_end(float4 pi, const float* tc, const EndTr
   const float z11 = -im.sPL * y10 + im.cPL * z10;
   return make_float4(im.cRL * x11 + im.sRL * y11, -im.sRL * x11 + im.cRL * y11, z11,
                      (float)(int)pi.w);
+}
+
+// The IMU terms of an IMU-less stream are cos 0 = 1 and sin 0 = 0: with them
+// as literals the compiler drops only the exact identities (x * 1, x - 0), the
+// same bits as the general expression.
+__device__ __forceinline__ float4 to_end(float4 pi, const float* tc, const EndTrig& et, const ImuEnd& im, bool imu) {
+  if (imu) return to_end_t(pi, tc, et, im);
+  return to_end_t(pi, tc, et, ImuEnd{1.f, 1.f, 1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 1.f, 0.f, 1.f, 0.f});
 }
 
 // AccumulateRotation :1015-1032
@@ -1654,7 +1662,8 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     const EndTrig et = end_trig(tcur);
     // updateImuRollPitchYawStartSinCos (:1761) and the imu*Last terms of TransformToEnd
     ImuEnd im{1.f, 1.f, 1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 1.f, 0.f, 1.f, 0.f};  // cos 0 / sin 0
-    if (bb.imu)
+    const bool hasImu = bb.imu != nullptr;
+    if (hasImu)
       im = ImuEnd{lego_cosf(iq.rollStart), lego_cosf(iq.pitchStart), lego_cosf(iq.yawStart),
                   lego_sinf(iq.rollStart), lego_sinf(iq.pitchStart), lego_sinf(iq.yawStart),
                   lego_cosf(iq.yawCur), lego_sinf(iq.yawCur), lego_cosf(iq.pitchCur),
@@ -1692,7 +1701,7 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
       const int n = F.nLF + F.nLS, per = (n + ob.G - 1) / ob.G;
       const int a = min(n, ob.wg * per), e = min(n, a + per);
       for (int i = a + t0; i < e; i += tstep) {
-        const float4 p = to_end(i < F.nLF ? F.lflat[i] : F.lsharp[i - F.nLF], tcur, et, im);
+        const float4 p = to_end(i < F.nLF ? F.lflat[i] : F.lsharp[i - F.nLF], tcur, et, im, hasImu);
         x_publish(xh + 3 * i, xtag | __float_as_uint(p.x));
         x_publish(xh + 3 * i + 1, xtag | __float_as_uint(p.y));
         x_publish(xh + 3 * i + 2, xtag | __float_as_uint(p.z));
@@ -1733,7 +1742,7 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
           if (i < n) {
             const bool corner = i >= nS;
             if (rebuild) nbr_keys(i, nS, n, wp, wn, kp, kn);
-            p = init ? r : to_end(r, tcur, et, im);
+            p = init ? r : to_end(r, tcur, et, im, hasImu);
             if (corner) {
               gCn[i - nS] = p;
               if (lead) cEnd[i - nS] = p;
@@ -1806,7 +1815,7 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
             float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
             int kp = 0, kn = 0;
             if (miss) {
-              p = to_end(i < nS ? F.lflat[i] : F.lsharp[i - nS], tcur, et, im);
+              p = to_end(i < nS ? F.lflat[i] : F.lsharp[i - nS], tcur, et, im, hasImu);
               put(i, p);
               nbr_keys(i, nS, n, w_at(max(i - 1, 0)), w_at(min(i + 1, n - 1)), kp, kn);
             }
