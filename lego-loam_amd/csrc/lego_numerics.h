@@ -204,6 +204,28 @@ LEGO_HD double reduce_large(uint32_t xi, int* np) {
   return x * 0x1.921FB54442D18p-62;
 }
 
+// |y| >= 120 and non-finite y (sin, cos): out of line.  The Payne-Hanek
+// reduction's table and 64-bit products are code every inlined sinf / cosf
+// would carry through the kernels' hot loops, where the angles are small.
+struct SinCos {
+  float s, c;
+};
+LEGO_HD __attribute__((noinline)) SinCos lego_sincosf_huge(float y) {
+  SinCos r;
+  if (abstop12(y) < abstop12(__builtin_inff())) {
+    uint32_t xi = f2u(y);
+    int sign = xi >> 31, n;
+    const double x = reduce_large(xi, &n);
+    double s = sincos_sign((n + sign) & 3);
+    const SinCosTab p = sincos_tab(((n + sign) & 2) ? 1 : 0);
+    r.s = sinf_poly(x * s, x * x, p, n);
+    r.c = sinf_poly(x * s, x * x, p, n ^ 1);
+  } else {
+    r.s = r.c = (y - y) / (y - y);
+  }
+  return r;
+}
+
 LEGO_HD float lego_sinf(float y) {
   double x = y;
   int n;
@@ -217,15 +239,8 @@ LEGO_HD float lego_sinf(float y) {
     double s = sincos_sign(n & 3);
     const SinCosTab p = sincos_tab((n & 2) ? 1 : 0);
     return sinf_poly(x * s, x * x, p, n);
-  } else if (abstop12(y) < abstop12(__builtin_inff())) {
-    uint32_t xi = f2u(y);
-    int sign = xi >> 31;
-    x = reduce_large(xi, &n);
-    double s = sincos_sign((n + sign) & 3);
-    const SinCosTab p = sincos_tab(((n + sign) & 2) ? 1 : 0);
-    return sinf_poly(x * s, x * x, p, n);
   }
-  return (y - y) / (y - y);
+  return lego_sincosf_huge(y).s;
 }
 
 LEGO_HD float lego_cosf(float y) {
@@ -241,15 +256,8 @@ LEGO_HD float lego_cosf(float y) {
     double s = sincos_sign(n & 3);
     const SinCosTab p = sincos_tab((n & 2) ? 1 : 0);
     return sinf_poly(x * s, x * x, p, n ^ 1);
-  } else if (abstop12(y) < abstop12(__builtin_inff())) {
-    uint32_t xi = f2u(y);
-    int sign = xi >> 31;
-    x = reduce_large(xi, &n);
-    double s = sincos_sign((n + sign) & 3);
-    const SinCosTab p = sincos_tab(((n + sign) & 2) ? 1 : 0);
-    return sinf_poly(x * s, x * x, p, n ^ 1);
   }
-  return (y - y) / (y - y);
+  return lego_sincosf_huge(y).c;
 }
 
 // sinf and cosf of one argument (glibc's sincosf structure): the range
@@ -274,16 +282,10 @@ LEGO_HD void lego_sincosf(float y, float* sp, float* cp) {
     const SinCosTab p = sincos_tab((n & 2) ? 1 : 0);
     *sp = sinf_poly(x * s, x * x, p, n);
     *cp = sinf_poly(x * s, x * x, p, n ^ 1);
-  } else if (abstop12(y) < abstop12(__builtin_inff())) {
-    const uint32_t xi = f2u(y);
-    const int sign = xi >> 31;
-    x = reduce_large(xi, &n);
-    const double s = sincos_sign((n + sign) & 3);
-    const SinCosTab p = sincos_tab(((n + sign) & 2) ? 1 : 0);
-    *sp = sinf_poly(x * s, x * x, p, n);
-    *cp = sinf_poly(x * s, x * x, p, n ^ 1);
   } else {
-    *sp = *cp = (y - y) / (y - y);
+    const SinCos r = lego_sincosf_huge(y);
+    *sp = r.s;
+    *cp = r.c;
   }
 }
 
