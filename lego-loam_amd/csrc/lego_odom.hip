@@ -1479,10 +1479,14 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
           a2 = b7 * cf.x - srx * cf.y - b3 * cf.z;
         }
         const float bb = (float)(-0.05 * (double)cf.w);
+        // a product of two floats is exact in double, so one fma rounds the
+        // sum exactly as the separate multiply and add do
         const double d0 = a0, d1 = a1, d2 = a2, db = bb;
-        acc[0] += d0 * d0; acc[1] += d0 * d1; acc[2] += d0 * d2;
-        acc[3] += d1 * d1; acc[4] += d1 * d2; acc[5] += d2 * d2;
-        acc[6] += d0 * db; acc[7] += d1 * db; acc[8] += d2 * db;
+        acc[0] = __builtin_fma(d0, d0, acc[0]); acc[1] = __builtin_fma(d0, d1, acc[1]);
+        acc[2] = __builtin_fma(d0, d2, acc[2]); acc[3] = __builtin_fma(d1, d1, acc[3]);
+        acc[4] = __builtin_fma(d1, d2, acc[4]); acc[5] = __builtin_fma(d2, d2, acc[5]);
+        acc[6] = __builtin_fma(d0, db, acc[6]); acc[7] = __builtin_fma(d1, db, acc[7]);
+        acc[8] = __builtin_fma(d2, db, acc[8]);
         mloc++;
       }
     }
