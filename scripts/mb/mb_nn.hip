@@ -195,10 +195,10 @@ __global__ void __launch_bounds__(512) knn(const float4* lastS, int nLS, const f
   for (int i = tid; i < nLS; i += 512) L.lastS[i] = lastS[i];
   for (int i = tid; i < nLC; i += 512) L.lastC[i] = lastC[i];
   __syncthreads();
-  nn_build2(lds_build_args(L, st, c), nullptr);
+  nn_build2(lds_build_args(L, st, c, 0), nullptr);  // the grids (this benchmark times their searches)
   for (int side = 0; side < 2; ++side) {
     const bool surf = side == 0;
-    const NNView<uint16_t> v = view_lds(surf, L, st, c);
+    const NNView<uint16_t> v = view_lds(surf, L, st, c, 0);
     const float4* qp = surf ? qS : qC;
     const int nQ = surf ? nQS : nQC, lastN = surf ? nLS : nLC, jend = min(nQ, lastN);
     for (int q = w; q < nQ && w < nwk; q += nwk) {
