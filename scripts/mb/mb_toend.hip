@@ -35,12 +35,12 @@ __global__ void __launch_bounds__(512) kend(const float4* lf, const float4* ls, 
         const int i = i0 + lane;
         float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
         if (i < nS) {
-          p = (MODE & 1) ? to_end(lf[i], tcur, et, im) : lf[i];
+          p = (MODE & 1) ? to_end(lf[i], tcur, et, im, false) : lf[i];
           if (MODE & 2) { gS[i] = p; sE[i] = p; }
           lastS[i] = p;
         } else if (i < n) {
           const int j = i - nS;
-          p = (MODE & 1) ? to_end(ls[j], tcur, et, im) : ls[j];
+          p = (MODE & 1) ? to_end(ls[j], tcur, et, im, false) : ls[j];
           if (MODE & 2) { gC[j] = p; cE[j] = p; }
           lastC[j] = p;
         }
