@@ -11,13 +11,16 @@
 //     one wave (kGL = 64 lanes) per query:
 //       - the exact nearest neighbour in the last cloud (replaces KdTreeFLANN,
 //         :1054, :1165; ties -> lower index, FLANN's tie order is traversal
-//         dependent): a 0.5 m hash grid with provable coverage, else an
-//         exhaustive pass over the cloud;
+//         dependent): an exhaustive pass over the LDS cloud when a stream has
+//         enough workgroups for about one query per wave (OdomBufs::gridless)
+//         or the cloud is small, else a 0.5 m hash grid with provable
+//         coverage, falling back to the exhaustive pass;
 //       - the scan-line neighbours (:1062-1099, :1173-1220, incl. the
 //         loop-bound quirk): the reference's sequential loops visit an index
 //         window bounded by ring breaks; the window is read off per-ring
 //         first/last tables, keeping the (distance, visit order) tie rule;
-//     then publishes (i1, i2, i3) and reads the other slices' granules;
+//     then publishes (i1, i2, i3) as one packed granule per query and reads
+//     the other slices' granules;
 //   one lane per query: line / plane residual, weight and Jacobian row
 //     (:1106-1151, :1228-1321);
 //   reduction of AtA, AtB with double accumulation (DPP row sums, one barrier);
