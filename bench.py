@@ -418,7 +418,8 @@ def main():
     ap.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
     ap.add_argument("--odom-profile", action="store_true", help="in-kernel phase stamps (diagnostic)")
     ap.add_argument("--mapping-steps", type=int, default=15, help="C5 scan-to-map steps (aux; 0 = skip)")
-    ap.add_argument("--fleet-streams", type=int, default=64, help="streams of the fleet aux line (0 = skip)")
+    ap.add_argument("--fleet-streams", type=int, default=256,
+                    help="streams of the fleet aux line (0 = skip); 256 = one odometry workgroup per stream and CU")
     ap.add_argument("--loop-scans", type=int, default=340, help="loop-closure aux stream length (0 = skip)")
     ap.add_argument("--dense-scans", type=int, default=200, help="C3 HDL-64E scans of the aux line (0 = skip)")
     args = ap.parse_args()
@@ -568,7 +569,8 @@ def main():
                              f"{args.sensor} stream, seed {seed}) through oracle ip+fa incl. LM, 1 thread"}
             # min(streams, cores) threads, the streams being the fleet line's
             thr = max(1, min(max(args.fleet_streams, 1), host_info()["affinity"]))
-            cpu_all = cpu_all_cores(L, args.sensor, thr, 60, args.cpu_budget)
+            # each thread repeats its own stream; the streams' synthesis is kept to ~3.8 k scans
+            cpu_all = cpu_all_cores(L, args.sensor, thr, max(10, 3840 // thr), args.cpu_budget)
         if args.odom_profile:
             prof = (C.c_uint64 * 32)()
             lib.lego_odom_profile(gpu.h, -1, prof)

@@ -21,7 +21,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/pr
   -- python3 "$R/bench.py" --no-cpu --fleet-streams 0 --dense-scans 0 --loop-scans 0 --steps 1 --warmup 1 \
   --mapping-steps 5 > "$O/prof_c5.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_fleet" -o run \
-  -- python3 "$R/scripts/fleet_probe.py" --streams 64 --steps 3 > "$O/prof_fleet.log" 2>&1
+  -- python3 "$R/scripts/fleet_probe.py" --streams 256 --steps 3 > "$O/prof_fleet.log" 2>&1
 timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_gather" -o run \
   -- "$R/build/mb_gather" > "$O/pmc_gather.log" 2>&1
 echo done
