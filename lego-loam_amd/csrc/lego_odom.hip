@@ -4,7 +4,7 @@
 // scan k-1's result through transformCur and the TransformToEnd'ed "last"
 // clouds, featureAssociation.cpp:1759-1815), so the per-scan chain never
 // returns to the host.  One launch runs G workgroups of 512 threads per
-// stream (48 for VLP-16, odom_workgroups); each runs the whole serial chain
+// stream (24 for VLP-16, odom_workgroups); each runs the whole serial chain
 // redundantly and they split only the correspondence searches, exchanging the
 // results through tagged granules ("exchange" below).  Per LM iteration:
 //   every 5th iteration: each workgroup searches its slice of the queries,
@@ -1951,16 +1951,20 @@ void launch_pack_recs(const BatchBufs& bb, const OdomBufs& ob, int B, PackedRec*
   k_pack_recs<<<(B + 1 + 63) / 64, 64, 0, s>>>(bb, ob, B, out);
 }
 
-// LDS-resident sensors: one wave per query of the largest NN round (the flat
-// features, 24 per ring) — 48 workgroups for VLP-16.  Larger sensors keep
+// LDS-resident sensors: one wave per query of the corner NN rounds (the sharp
+// features, 12 per ring; three of a scan's four rounds) — 24 workgroups for
+// VLP-16, whose single surf round then takes two queries per wave (measured
+// on C2 with the gridless search: 16 → 13.2 k, 20 → 13.7 k, 24–32 → 14.05 k,
+// 40–64 → 13.85–13.95 k scans/s; fewer workgroups also poll fewer
+// granules per round).  Larger sensors keep
 // their clouds and indexes in HBM, and each workgroup builds its own index
 // copy per scan: four queries per wave balance that redundant build against
 // the search split (HDL-64E: 48 workgroups; measured 1.4 k scans/s at 192,
 // 2.7 k at 48, 2.6 k at 24).  Capped at the CU count.
 int odom_workgroups(int N, int cusAvailable) {
   const bool resident = N * kFlatPerRing <= kLdsQ && N * kSharpPerRing <= kLdsQ / 2;
-  const int perWg = kOdomWaves * (resident ? 1 : 4);
-  const int g = (N * kFlatPerRing + perWg - 1) / perWg;
+  const int g = resident ? (N * kSharpPerRing + kOdomWaves - 1) / kOdomWaves
+                         : (N * kFlatPerRing + 4 * kOdomWaves - 1) / (4 * kOdomWaves);
   return g < cusAvailable ? g : cusAvailable;
 }
 

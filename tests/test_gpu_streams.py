@@ -102,7 +102,7 @@ def test_vlp16_grid_and_gridless_odometry(L, gridless):
     """Both closest-point searches of the LDS-resident odometry against the
     oracle: the hashed 0.5 m grids (what a fleet with few workgroups per stream
     runs) and the gridless mode (exhaustive pass over the LDS cloud, key tables
-    only; what a single stream's 48 workgroups run).  LEGO_ODOM_GRIDLESS
+    only; what a single stream's 24 workgroups run).  LEGO_ODOM_GRIDLESS
     overrides the host's choice (OdomBufs::gridless)."""
     import os
 
