@@ -23,7 +23,7 @@ shutil.copy(src / "prof_stats" / "run_kernel_stats.csv", prof / f"{rnd}_kernel_s
 subprocess.run([sys.executable, str(REPO / "scripts" / "pmc_summary.py"), str(src), str(prof / f"{rnd}_pmc_summary.json"),
                 "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes over bench.py --no-cpu "
                 "--mapping-steps 0 --fleet-streams 0 --dense-scans 0 --loop-scans 0 --steps 2 --warmup 1 "
-                "(3 launches per kernel, 100 VLP-16 scans each; k_odom = 48 workgroups, plain launch)", commit],
+                "(3 launches per kernel, 100 VLP-16 scans each; k_odom = 24 workgroups, plain launch)", commit],
                check=True)
 for sub, name in (("prof_fleet", "fleet_kernel_stats.csv"), ("prof_c5", "c5_kernel_stats.csv")):
     f = src / sub / "run_kernel_stats.csv"
