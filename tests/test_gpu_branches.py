@@ -19,7 +19,11 @@ branch was taken (include/lego_loam.h LEGO_REC_*):
   walk their six sectors at once and re-walk a sector whose predecessor's
   boundary suppression reached a position it picked): lego_extract_profile's
   counters prove both the parallel walks and re-walks ran, and the four
-  feature clouds must equal the oracle's byte for byte."""
+  feature clouds must equal the oracle's byte for byte;
+* starved scans mid-stream (a sensor blocked but for a narrow sector: scans
+  with no features at all, or a few): the LM gate on the last clouds' sizes
+  and the few-rows guards, in a single-stream context and in a fleet (hashed
+  grids over near-empty clouds), every pose equal to the oracle's."""
 import numpy as np
 import pytest
 
@@ -134,3 +138,67 @@ def test_speculative_picking_rewalks_match_oracle(L):
     rings, rewalks, parallel = xp[4], xp[5], xp[6]
     print(f"rings {rings}, picked in parallel {parallel}, sector re-walks {rewalks}")
     assert rings >= 10 * 16 and parallel > 0 and rewalks > 0
+
+
+def wedge(pts, a0_deg, width_deg):
+    """The points of a scan whose azimuth lies in [a0, a0 + width) degrees, in
+    their firing order (a sensor blocked but for a narrow sector)."""
+    az = np.degrees(np.arctan2(pts["y"].astype(np.float64), pts["x"].astype(np.float64))) % 360.0
+    keep = (az >= a0_deg) & (az < a0_deg + width_deg)
+    assert keep.any()
+    return pts[keep]
+
+
+def _sparse_stream(L):
+    """A VLP-16 stream with starved scans mid-stream: the next scans' LM finds
+    fewer than 10 corner or 100 surf points in the last clouds and skips the
+    update (featureAssociation.cpp:1668 gate), the first scans after the
+    blockage run their LM against the starved clouds (few rows: the < 10
+    rows guard, :1677 / :1690), and the stream then recovers."""
+    sc = L.synth_cfg("VLP-16", 5)
+    scans = [L.synth_scan(sc, k) for k in range(14)]
+    for k, w in ((4, 6.0), (5, 2.0), (8, 20.0), (11, 1.0)):
+        p, s = scans[k]
+        scans[k] = (wedge(p, 30.0 * k, w), s)
+    return scans
+
+
+def test_starved_scans_mid_stream(L):
+    scans = _sparse_stream(L)
+    ref = _oracle(L, scans)
+    small = [len(o["less_sharp"]) < 10 or len(o["less_flat"]) < 100 for o in ref]
+    assert any(small) and not all(small), [(len(o["less_sharp"]), len(o["less_flat"])) for o in ref]
+    cfg = L.sensor_cfg("VLP-16", L.hip_lib())
+    cap = max(len(p) for p, _ in scans) + 16
+    gpu = L.Lego(cfg, max_points=cap, max_batch=7)  # a batch boundary right after the first blockage
+    recs = list(gpu.odom_batch(*_pack(scans[:7]))) + list(gpu.odom_batch(*_pack(scans[7:])))
+    gpu.close()
+    _check_recs(recs, ref, "starved scans")
+
+
+def test_starved_scans_in_a_fleet(L):
+    """The same stream beside a normal one in a fleet context (a few odometry
+    workgroups per stream: the hashed grids over near-empty clouds): every
+    record equals the stream's own context byte for byte."""
+    starved = _sparse_stream(L)
+    sc = L.synth_cfg("VLP-16", 6)
+    normal = [L.synth_scan(sc, k) for k in range(len(starved))]
+    cfg = L.sensor_cfg("VLP-16", L.hip_lib())
+    cap = max(len(p) for p, _ in starved + normal) + 16
+    K = len(starved) // 2
+    ref = []
+    for scans in (starved, normal):
+        g = L.Lego(cfg, max_points=cap, max_batch=K)
+        raw = bytes(g.odom_batch(*_pack(scans[:K]))) + bytes(g.odom_batch(*_pack(scans[K:])))
+        g.close()
+        ref.append([raw[64 * k:64 * k + 60] for k in range(2 * K)])
+    fl = L.Lego(cfg, max_points=cap, max_batch=K, streams=2)
+    got = [[], []]
+    for h in (slice(0, K), slice(K, 2 * K)):
+        raw = bytes(fl.odom_batch(*_pack(starved[h] + normal[h])))
+        for s in range(2):
+            got[s] += [raw[64 * (s * K + k):64 * (s * K + k) + 60] for k in range(K)]
+    fl.close()
+    assert got == ref
+    recs = [L.PoseRec.from_buffer_copy(r + bytes(4)) for r in got[0]]
+    _check_recs(recs, _oracle(L, starved), "starved scans in a fleet")
