@@ -3,7 +3,7 @@
 set -uo pipefail
 R="${GRAFT_REPO_ROOT:-$(pwd)}"
 cd "$R"
-for g in 24 48 96 160; do
+for g in ${GS:-24 48 96 160}; do
   LEGO_ODOM_WORKGROUPS=$g timeout -k 10 120 python -c "
 import sys; sys.path.insert(0, '.')
 import bench
