@@ -793,6 +793,63 @@ __device__ __forceinline__ bool nn_lines(const NNView<Idx>& v, int ci, int jend,
 }
 
 
+// Corner query against a small cloud (<= kBruteSmall points, ordered keys):
+// the closest point and the scan-line neighbour from the same four points per
+// lane, loaded once (nn_brute + nn_lines without reloading the window).  The
+// candidates, their classes and visit ranks are nn_lines' exactly, and the
+// lexicographic minima do not depend on which lane visits what.  Returns i1;
+// *o2 the neighbour, *ok false when the key tables cannot bound the loops
+// (the caller then runs them literally).
+template <class Idx>
+__device__ __forceinline__ int nn_corner_small(const NNView<Idx>& v, int jend, float4 sel, float bound,
+                                               float nn_sq, int g, int* o2, bool* ok) {
+  float4 p[4];
+  float bd = bound;
+  int bi = INT_MAX;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int j = g + k * kGL;
+    p[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (j < v.n) {
+      p[k] = v.pts[j];
+      const float d2 = flann_d2(sel, p[k]);
+      if (d2 < bd) { bd = d2; bi = j; }
+    }
+  }
+  group_lex_min(bd, bi);
+  *o2 = -1;
+  *ok = true;
+  if (bi == INT_MAX || !(bd < bound)) return -1;
+  const int ci = bi;
+  const int kc = ci / kGL;  // wave-uniform
+  const float wc = kc == 0 ? p[0].w : (kc == 1 ? p[1].w : (kc == 2 ? p[2].w : p[3].w));
+  const int cScan = (int)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(wc), ci % kGL));
+  const int F = (cScan + 3 <= v.NK) ? v.sufFirst[cScan + 3] : INT_MAX;
+  const int B = (cScan - 3 >= 0) ? v.preLast[cScan - 3] : -1;
+  if (F <= ci || B >= ci) {
+    *ok = false;
+    return ci;
+  }
+  const int fwdEnd = min(F, jend);
+  float m2 = nn_sq;
+  int r2 = INT_MAX, i2 = -1;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int j = g + k * kGL;
+    const bool fwd = j > ci && j < fwdEnd, bwd = j > B && j < ci;
+    const int kj = (int)p[k].w;
+    if ((fwd && kj > cScan) || (bwd && kj < cScan)) {
+      const float d = line_d2(p[k], sel);
+      const int rank = fwd ? j - ci : (jend - ci) + (ci - j);
+      const bool u = d < nn_sq && (d < m2 || (d == m2 && rank < r2));
+      m2 = u ? d : m2; r2 = u ? rank : r2; i2 = u ? j : i2;
+    }
+  }
+  group_lex_min3(m2, r2, i2);
+  *o2 = i2;
+  return ci;
+}
+
 // The reference's sequential loops, kGL indices per step (fallback).  Every
 // lane keeps a lexicographic (distance, visit rank) minimum over the indices
 // it visits and one group reduction combines them.
@@ -1356,6 +1413,18 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
         const float cz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cv), 2));
         const float4 sel = to_start_t(pq, s, tc, cx, sx, cy, sy, cz, sz);
         sub(P_G0_TOSTART);
+        // a corner query against a small cloud: one pass over registers
+        // (+0.35% on C2, A/B)
+        if (!surf && !stale && !nn.irregular && nn.n <= kBruteSmall) {
+          bool ok;
+          i3 = -1;
+          i1 = nn_corner_small(nn, jend, sel, c.nn_sq, c.nn_sq, g, &i2, &ok);
+          if (i1 >= lastN) i1 = -1;
+          if (i1 >= 0 && !ok) scanline_group(last, jend, i1, sel, surf, c.nn_sq, g, &i2, &i3);
+          if (i1 < 0) i2 = -1;
+          sub(P_G0_SCAN);
+          return;
+        }
         i1 = stale ? nn_brute(snap, snapN, sel, c.nn_sq, g) : nn_i1(nn, sel, c.nn_sq, g, S.prof);
         if (i1 >= lastN) i1 = -1;  // an index past a stale snapshot's cloud
         sub(P_G0_NN);
