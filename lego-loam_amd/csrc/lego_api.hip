@@ -1135,14 +1135,10 @@ static int mo_alloc(lego_ctx* x, int nc, int ns) {
   }
   const int vcap = std::max(std::max(nc, ns), 2 * P);
   if (vcap > m.vg.cap) {  // buffers are never freed before the context: grow by reallocating
-    VgScratch& v = m.vg;
-    v.cap = vcap;
-    MA(v.keys, vcap); MA(v.keys2, vcap); MA(v.vals, vcap); MA(v.vals2, vcap);
-    MA(v.heads, vcap); MA(v.scan, vcap); MA(v.mm, 8); MA(v.overflow, 4);
-    v.tmpBytes = voxel_scratch_tmp_bytes(vcap);
-    unsigned char* t = nullptr;
-    MA(t, v.tmpBytes);
-    v.tmp = t;
+    auto ctx_alloc = [](void* c, void** p, size_t bytes) {
+      return static_cast<lego_ctx*>(c)->alloc(reinterpret_cast<unsigned char**>(p), bytes) == hipSuccess ? 0 : -1;
+    };
+    if (vg_scratch_alloc(m.vg, vcap, x, ctx_alloc)) return fail("VoxelGrid scratch");
   }
   if (nc > m.mapCornerCap) {
     m.mapCornerCap = nc;

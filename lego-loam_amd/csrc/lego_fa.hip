@@ -19,6 +19,7 @@
 
 #include "lego_device.h"
 #include "lego_introsort.h"
+#include "lego_vgsort.h"
 #include "lego_kernels.h"
 
 namespace lego {
@@ -223,7 +224,9 @@ struct ExtractLds {
   uint16_t* perm;
   SmoothEntry* srt;
   SmoothEntry* orig;
-  unsigned long long* vox;
+  uint32_t* vkey;     // VoxelGrid: voxel index per less-flat point (sorted in place)
+  uint16_t* vpr;      // VoxelGrid: partition partners
+  uint32_t* vlists;   // VoxelGrid: the two segment lists
   int* misc;
   float* red;
 };
@@ -242,10 +245,16 @@ __host__ __device__ inline int next_pow2(int x) {
 //   picking  A: pick lists [0, 1 KB), the initial  B: curv, perm, gfl
 //               picked copy, picked, label, col
 //   less-flat                                      B: lf (its tail)
-//   VoxelGrid   the keys from offset 0 over A and B's head, lf in B's tail
+//   VoxelGrid   keys, partners and segment lists from offset 0 over A and
+//               B's head; lf in B's tail (the payload, sorted with the keys)
 // col, picked and label are loaded once the sorts are done.
 // A sector holds n <= (H + 32) / 6 + 2 entries plus the fallback sort's
 // stack (kIntroStack words) behind it.
+// the VoxelGrid's keys (4 B), partners (2 B) and two segment lists
+__host__ __device__ inline size_t vg_extract_lists_off(size_t W) { return (6 * W + 3) & ~(size_t)3; }
+__host__ __device__ inline size_t vg_extract_bytes(size_t W) {
+  return vg_extract_lists_off(W) + 8 * (size_t)vg_list_cap((int)W);
+}
 __host__ __device__ inline int extract_sector_cap(int H) { return next_pow2((H + 32) / 6 + 2 + (kIntroStack + 1) / 2); }
 constexpr int kSortWaves = 3;  // waves sorting sectors at once (the scratch holds their sectors)
 struct ExtractLayout {
@@ -260,7 +269,7 @@ __host__ __device__ inline ExtractLayout extract_layout(int H) {
   if (sec > a) a = sec;
   e.lfOff = (5 * W + 1) & ~(size_t)1;          // over perm / gfl, dead once the walks are done
   e.B = (e.lfOff + 2 * W + 15) & ~(size_t)15;
-  const size_t vox = (size_t)next_pow2((int)W) * 8;  // keys from A's start up to lf
+  const size_t vox = vg_extract_bytes(W);  // keys from A's start up to lf
   if (vox > a + e.lfOff) a = vox - e.lfOff;
   e.A = (a + 15) & ~(size_t)15;
   return e;
@@ -276,7 +285,9 @@ __device__ __forceinline__ ExtractLds carve(unsigned char* base, int H) {
   ExtractLds L;
   unsigned char* A = base;
   unsigned char* B = base + e.A;
-  L.vox = (unsigned long long*)A;
+  L.vkey = (uint32_t*)A;
+  L.vpr = (uint16_t*)(A + 4 * W);
+  L.vlists = (uint32_t*)(A + vg_extract_lists_off(W));
   L.srt = (SmoothEntry*)A;
   L.orig = nullptr;
   L.picked = A + 1024 + W;  // [1024, 1024 + W): the initial picked copy of the speculative walks
@@ -333,65 +344,6 @@ __device__ __forceinline__ void wave_bitonic_entries(SmoothEntry* a, int m) {
     }
   }
 }
-__device__ __forceinline__ void bitonic_u64(unsigned long long* a, int m) {
-  for (int k = 2; k <= m; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int t = threadIdx.x; t < m / 2; t += blockDim.x) {
-        const int i = (t / j) * 2 * j + (t % j);
-        const int l = i + j;
-        const bool up = (i & k) == 0;
-        const unsigned long long x = a[i], y = a[l];
-        if ((x > y) == up) { a[i] = y; a[l] = x; }
-      }
-      __syncthreads();
-    }
-  }
-}
-
-// The same network with the block barriers only where a pass crosses waves:
-// wave w owns the aligned chunk [w*C, (w+1)*C), C = m / waves, and every pass
-// with j < C pairs elements inside one chunk, so the wave that owns the chunk
-// runs it alone behind a wave-level LDS fence.  Only the passes with j >= C
-// (log2(waves) per merge stage above C) sit between two __syncthreads: for
-// m = 2048 on 4 waves that is 3 block passes instead of 66.  Same compare-
-// exchange sequence per element pair as bitonic_u64, so the result is the
-// same sorted array (the keys are unique).
-__device__ __forceinline__ void bitonic_u64_chunked(unsigned long long* a, int m) {
-  const int nw = blockDim.x >> 6, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int C = m / nw;
-  if (C < 128) {
-    bitonic_u64(a, m);
-    return;
-  }
-  unsigned long long* w = a + wave * C;
-  const int base = wave * C;
-  for (int k = 2; k <= m; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      if (j >= C) {
-        __syncthreads();
-        for (int t = threadIdx.x; t < m / 2; t += blockDim.x) {
-          const int i = (t / j) * 2 * j + (t % j);
-          const int l = i + j;
-          const bool up = (i & k) == 0;
-          const unsigned long long x = a[i], y = a[l];
-          if ((x > y) == up) { a[i] = y; a[l] = x; }
-        }
-        __syncthreads();
-      } else {
-        for (int t = lane; t < C / 2; t += 64) {
-          const int i = (t / j) * 2 * j + (t % j);
-          const int l = i + j;
-          const bool up = ((base + i) & k) == 0;
-          const unsigned long long x = w[i], y = w[l];
-          if ((x > y) == up) { w[i] = y; w[l] = x; }
-        }
-        wave_sync_lds();
-      }
-    }
-  }
-  __syncthreads();
-}
-
 // Ordered block compaction helper: returns this thread's exclusive rank among
 // flagged threads of the block and the block total (256 threads = 4 waves).
 __device__ __forceinline__ int block_rank(bool f, int* woff, int* total) {
@@ -927,38 +879,34 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
     for (int t = tid; t < K; t += blockDim.x) olf[t] = bb.dsk[R.base + R.lo + L.lf[t]];
     nlf = K;
   } else if (K > 0) {
-    const int m = next_pow2(K);
     const int d0 = L.misc[M_D0], d1 = L.misc[M_D1];
     const float fb0 = (float)L.misc[M_MB0], fb1 = (float)L.misc[M_MB1], fb2 = (float)L.misc[M_MB2];
-    for (int t = tid, i = 0; t < m; t += blockDim.x, ++i) {
-      unsigned long long key = ~0ull;
-      if (t < K) {
-        float4 p;
-        if (i < kLfRegs) {  // a register, selected without a dynamic index
+    for (int t = tid, i = 0; t < K; t += blockDim.x, ++i) {
+      float4 p;
+      if (i < kLfRegs) {  // a register, selected without a dynamic index
 #pragma unroll
-          for (int u = 0; u < kLfRegs; ++u)
-            if (u == i) p = lp[u];
-        } else {
-          p = bb.dsk[R.base + R.lo + L.lf[t]];
-        }
-        const int i0 = (int)(floorf(p.x * inv) - fb0);
-        const int i1 = (int)(floorf(p.y * inv) - fb1);
-        const int i2 = (int)(floorf(p.z * inv) - fb2);
-        const int idx = i0 + i1 * d0 + i2 * d0 * d1;
-        key = ((unsigned long long)(unsigned)idx << 32) | (unsigned)t;
+        for (int u = 0; u < kLfRegs; ++u)
+          if (u == i) p = lp[u];
+      } else {
+        p = bb.dsk[R.base + R.lo + L.lf[t]];
       }
-      L.vox[t] = key;
+      const int i0 = (int)(floorf(p.x * inv) - fb0);
+      const int i1 = (int)(floorf(p.y * inv) - fb1);
+      const int i2 = (int)(floorf(p.z * inv) - fb2);
+      L.vkey[t] = (uint32_t)(i0 + i1 * d0 + i2 * d0 * d1);
     }
     __syncthreads();
-    bitonic_u64_chunked(L.vox, m);
+    // PCL's std::sort of (idx, point) by idx: its unstable order of a voxel's
+    // points is the summation order (lego_vgsort.h); lf moves with the keys
+    vg_block_sort(L.vkey, L.lf, L.vpr, L.vlists, (int*)(L.red + 32), K);
     int outc = 0;
     for (int t0 = 0; t0 < K; t0 += blockDim.x) {
       const int t = t0 + tid;
-      const bool head = t < K && (t == 0 || (L.vox[t] >> 32) != (L.vox[t - 1] >> 32));
+      const bool head = t < K && (t == 0 || L.vkey[t] != L.vkey[t - 1]);
       int tot;
       const int r = block_rank(head, L.misc + M_WOFF, &tot);
       if (head) {
-        const unsigned key = (unsigned)(L.vox[t] >> 32);
+        const uint32_t key = L.vkey[t];
         // the voxel's points in sorted order (PCL's accumulation order),
         // four loads in flight per round instead of one per add
         float cx = 0, cy = 0, cz = 0, ci = 0;
@@ -969,8 +917,8 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
           bool in[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            in[i] = u + i < K && (unsigned)(L.vox[u + i] >> 32) == key;
-            if (in[i]) q[i] = bb.dsk[R.base + R.lo + L.lf[(unsigned)(L.vox[u + i] & 0xffffffffu)]];
+            in[i] = u + i < K && L.vkey[u + i] == key;
+            if (in[i]) q[i] = bb.dsk[R.base + R.lo + L.lf[u + i]];
           }
 #pragma unroll
           for (int i = 0; i < 4; ++i)

@@ -27,22 +27,37 @@ struct MoCounts {
   int _pad;
 };
 
-// VoxelGrid / index-build scratch for clouds of up to cap points.
+// VoxelGrid / index-build scratch for clouds of up to cap points (lego_vg.hip).
 struct VgScratch {
-  unsigned* keys;
-  unsigned* keys2;
-  int* vals;
-  int* vals2;
-  int* heads;
-  int* scan;
-  int* mm;        // [6] ordered-int min / max
-  int* overflow;  // [1]
-  void* tmp;
-  size_t tmpBytes;
-  int cap;
+  unsigned* keys;   // [cap] voxel index per point, sorted in place
+  int* vals;        // [cap] point index, moved with the keys
+  int* pl;          // [cap] a round's swapped left stops, by partner rank
+  int* pr;          // [cap] a round's swapped right stops, by rank
+  int2* big;        // [2][capBig] segments partitioned by the current / next round
+  int* cut;         // [capBig] the round's cut per segment
+  int* kcnt;        // [capBig] the round's swap count per segment
+  int* tileOff;     // [capBig + 1] first tile of each segment
+  int* tileL;       // [capTiles] left stops per tile
+  int* tileR;       // [capTiles] right stops per tile
+  int4* loc;        // [capLoc] segments sorted in one workgroup (s, e, depth budget)
+  int* scanTiles;   // [capScanTiles] tile sums of the scans
+  int* ctl;         // [16] counters (lego_vg.hip C_*)
+  int* mm;          // [6] ordered-int min / max
+  int* overflow;    // [1]
+  int cap, capBig, capTiles, capLoc, capScanTiles;
 };
 
-// 1 m hashed cells over a map cloud: points sorted by bucket (w = index).
+// 1 m cells of the mapping NN index, hashed into T buckets
+__device__ __forceinline__ unsigned mo_cell_hash(int ix, int iy, int iz) {
+  unsigned long long k = ((unsigned long long)(unsigned)(ix + (1 << 20)) << 42) |
+                         ((unsigned long long)(unsigned)(iy + (1 << 20)) << 21) |
+                         (unsigned long long)(unsigned)(iz + (1 << 20));
+  k ^= k >> 33; k *= 0xff51afd7ed558ccdULL; k ^= k >> 33;
+  return (unsigned)k;
+}
+__device__ __forceinline__ int cell1(float v) { return (int)floorf(v); }  // 1 m cells
+
+// 1 m hashed cells over a map cloud: points grouped by bucket (w = index).
 struct MoIndex {
   int* begin;
   int* end;
@@ -132,7 +147,9 @@ struct LcDev {
   int cap;
 };
 
-size_t voxel_scratch_tmp_bytes(int cap);
+// allocates every VgScratch buffer for clouds of up to cap points through
+// alloc (0 = success)
+int vg_scratch_alloc(VgScratch& v, int cap, void* ctx, int (*alloc)(void* ctx, void** p, size_t bytes));
 int voxel_grid_device(const float4* in, int n, const int* nDev, float leaf, float4* out, int* nOut,
                       const VgScratch& v, hipStream_t s);
 int mo_set_map_device(MoDev& m, int nCornerMap, int nSurfMap, hipStream_t s);

@@ -3,15 +3,15 @@
 // Per mapping step (mapOptmization.cpp:1487-1522 with the loop closure off):
 //   k_mo_associate   1 thread: laserOdometryHandler's quaternion -> RPY
 //                    (:629-641), transformAssociateToMap (:376-461)
-//   VoxelGrid        PCL's filter (voxel_grid.hpp) as device passes: min/max,
-//                    voxel index per point, stable radix sort (hipCUB) of
-//                    (index, point), segment heads + scan, one lane per voxel
-//                    summing its points in input order — the map (once per
-//                    installed map) and the scan's corner / surf / outlier /
-//                    surf+outlier clouds (:1067-1091)
-//   NN index         1 m cells hashed into buckets, sorted by bucket (radix
-//                    sort), begin/end per bucket; replaces KdTreeFLANN on the
-//                    map (:1335-1336).  Every use is thresholded (5th nearest
+//   VoxelGrid        PCL's filter (voxel_grid.hpp, lego_vg.hip): min/max,
+//                    voxel index per point, std::sort's permutation of
+//                    (index, point) reproduced (lego_vgsort.h), one lane per
+//                    voxel summing its points in that order — the map (once
+//                    per installed map) and the scan's corner / surf /
+//                    outlier / surf+outlier clouds (:1067-1091)
+//   NN index         1 m cells hashed into buckets by a counting sort,
+//                    begin/end per bucket (lego_vg.hip); replaces KdTreeFLANN
+//                    on the map (:1335-1336).  Every use is thresholded (5th nearest
 //                    within 1 m, :1101, :1183), so the 27 cells around a query
 //                    hold every candidate; ties resolve to the lower index.
 //   per LM iteration (<= 10, :1337-1345):
@@ -29,8 +29,6 @@
 // per map: the filter of an unchanged cloud is the same cloud every step.  With
 // lego_mo_opts.fixed_map_per_step it is filtered and indexed on every step, the
 // work the reference does on its surrounding map (like-for-like timing).
-#include <hipcub/hipcub.hpp>
-
 #include <algorithm>
 #include <cfloat>
 #include <climits>
@@ -44,219 +42,12 @@ namespace lego {
 constexpr unsigned kInvalidKey = 0xffffffffu;
 constexpr int kMoSolveThreads = 1024;
 
-// ---------------------------------------------------------------- VoxelGrid
-__device__ __forceinline__ int ord_of(float f) {  // order-preserving float -> int
-  const int o = __float_as_int(f);
-  return o >= 0 ? o : o ^ 0x7fffffff;
-}
-__device__ __forceinline__ float of_ord(int o) { return __int_as_float(o >= 0 ? o : o ^ 0x7fffffff); }
-__device__ __forceinline__ bool finite3(float4 p) {
-  return __builtin_isfinite(p.x) && __builtin_isfinite(p.y) && __builtin_isfinite(p.z);
-}
-
-__global__ void k_vg_init(VgScratch v) {
-  if (threadIdx.x < 3) { v.mm[threadIdx.x] = INT_MAX; v.mm[3 + threadIdx.x] = INT_MIN; }
-  if (threadIdx.x == 0) *v.overflow = 0;
-}
-
-// n: element count (host bound); nDev: actual count on the device, or null
-__global__ void k_vg_minmax(const float4* in, int n, const int* nDev, VgScratch v) {
-  const int nn = nDev ? min(n, *nDev) : n;
-  int mn[3] = {INT_MAX, INT_MAX, INT_MAX}, mx[3] = {INT_MIN, INT_MIN, INT_MIN};
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nn; i += gridDim.x * blockDim.x) {
-    const float4 p = in[i];
-    if (!finite3(p)) continue;
-    const int o[3] = {ord_of(p.x), ord_of(p.y), ord_of(p.z)};
-#pragma unroll
-    for (int k = 0; k < 3; ++k) { mn[k] = min(mn[k], o[k]); mx[k] = max(mx[k], o[k]); }
-  }
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    for (int off = 32; off > 0; off >>= 1) {
-      mn[k] = min(mn[k], __shfl_xor(mn[k], off, 64));
-      mx[k] = max(mx[k], __shfl_xor(mx[k], off, 64));
-    }
-  }
-  // the block's waves through LDS, then one atomic per block and component
-  // (a few hundred blocks: per-wave atomics on the same six words serialise)
-  __shared__ int red[6][16];
-  const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  if ((threadIdx.x & 63) == 0)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) { red[k][wave] = mn[k]; red[3 + k][wave] = mx[k]; }
-  __syncthreads();
-  if (threadIdx.x < 6) {
-    const int k = threadIdx.x;
-    int r = red[k][0];
-    for (int w = 1; w < nw; ++w) r = k < 3 ? min(r, red[k][w]) : max(r, red[k][w]);
-    if (k < 3) atomicMin(&v.mm[k], r);
-    else atomicMax(&v.mm[k], r);
-  }
-}
-
-struct VgGeom {
-  float inv;
-  int minb[3], divb0, divb1;
-  bool overflow;
-};
-// pcl::VoxelGrid::applyFilter: leaf_size -> inverse, integer-overflow guard,
-// min/max voxel, division multipliers (float arithmetic as PCL's Eigen arrays).
-__device__ __forceinline__ VgGeom vg_geom(const VgScratch& v, float leaf) {
-  VgGeom g;
-  g.inv = 1.0f / leaf;
-  float minp[3], maxp[3];
-  for (int k = 0; k < 3; ++k) { minp[k] = of_ord(v.mm[k]); maxp[k] = of_ord(v.mm[3 + k]); }
-  const long long dx = (long long)((maxp[0] - minp[0]) * g.inv) + 1;
-  const long long dy = (long long)((maxp[1] - minp[1]) * g.inv) + 1;
-  const long long dz = (long long)((maxp[2] - minp[2]) * g.inv) + 1;
-  g.overflow = dx * dy * dz > (long long)INT_MAX;
-  int maxb[3];
-  for (int k = 0; k < 3; ++k) {
-    g.minb[k] = (int)floorf(minp[k] * g.inv);
-    maxb[k] = (int)floorf(maxp[k] * g.inv);
-  }
-  g.divb0 = maxb[0] - g.minb[0] + 1;
-  g.divb1 = maxb[1] - g.minb[1] + 1;
-  return g;
-}
-
-__global__ void k_vg_keys(const float4* in, int n, const int* nDev, float leaf, VgScratch v) {
-  const int nn = nDev ? min(n, *nDev) : n;
-  const VgGeom g = vg_geom(v, leaf);
-  if (blockIdx.x == 0 && threadIdx.x == 0 && g.overflow) *v.overflow = 1;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    unsigned key = kInvalidKey;
-    if (i < nn) {
-      const float4 p = in[i];
-      if (finite3(p)) {
-        const int i0 = (int)(floorf(p.x * g.inv) - (float)g.minb[0]);
-        const int i1 = (int)(floorf(p.y * g.inv) - (float)g.minb[1]);
-        const int i2 = (int)(floorf(p.z * g.inv) - (float)g.minb[2]);
-        key = (unsigned)(i0 + i1 * g.divb0 + i2 * g.divb0 * g.divb1);
-      }
-    }
-    v.keys[i] = key;
-    v.vals[i] = i;
-  }
-}
-
-__global__ void k_vg_heads(int n, VgScratch v) {
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
-    const unsigned k = v.keys2[t];
-    v.heads[t] = (k != kInvalidKey && (t == 0 || v.keys2[t - 1] != k)) ? 1 : 0;
-  }
-}
-
-// One lane per voxel: the centroid of its points summed in sorted (= input,
-// the sort is stable) order, written at the voxel's rank.  Overflow: copy.
-__global__ void k_vg_emit(const float4* in, int n, const int* nDev, VgScratch v, float4* out, int* nOut) {
-  const int nn = nDev ? min(n, *nDev) : n;
-  if (*v.overflow) {
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nn; i += gridDim.x * blockDim.x) out[i] = in[i];
-    if (blockIdx.x == 0 && threadIdx.x == 0) *nOut = nn;
-    return;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) *nOut = n > 0 ? v.scan[n - 1] + v.heads[n - 1] : 0;
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
-    if (!v.heads[t]) continue;
-    const unsigned k = v.keys2[t];
-    float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
-    int j = t;
-    for (; j < n && v.keys2[j] == k; ++j) {
-      const float4 p = in[v.vals2[j]];
-      c0 += p.x; c1 += p.y; c2 += p.z; c3 += p.w;
-    }
-    const float cnt = (float)(j - t);
-    out[v.scan[t]] = make_float4(c0 / cnt, c1 / cnt, c2 / cnt, c3 / cnt);
-  }
-}
-
 static int grid_for(int n, int bs = 256) {
   int g = (n + bs - 1) / bs;
   return g < 1 ? 1 : (g > 4096 ? 4096 : g);
 }
 
-// in[0 .. min(n, *nDev)) -> out[0 .. *nOut), all on stream s.  n is a host
-// upper bound (the capacity the scratch was sized for).
-int voxel_grid_device(const float4* in, int n, const int* nDev, float leaf, float4* out, int* nOut,
-                      const VgScratch& v, hipStream_t s) {
-  if (n <= 0) {
-    if (hipMemsetAsync(nOut, 0, sizeof(int), s) != hipSuccess) return -1;
-    return 0;
-  }
-  if (n > v.cap) return -1;
-  k_vg_init<<<1, 64, 0, s>>>(v);
-  k_vg_minmax<<<std::min(grid_for(n), 512), 256, 0, s>>>(in, n, nDev, v);
-  k_vg_keys<<<grid_for(n), 256, 0, s>>>(in, n, nDev, leaf, v);
-  size_t tb = v.tmpBytes;
-  if (hipcub::DeviceRadixSort::SortPairs(v.tmp, tb, v.keys, v.keys2, v.vals, v.vals2, n, 0, 32, s) != hipSuccess)
-    return -1;
-  k_vg_heads<<<grid_for(n), 256, 0, s>>>(n, v);
-  tb = v.tmpBytes;
-  if (hipcub::DeviceScan::ExclusiveSum(v.tmp, tb, v.heads, v.scan, n, s) != hipSuccess) return -1;
-  k_vg_emit<<<grid_for(n), 256, 0, s>>>(in, n, nDev, v, out, nOut);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-size_t voxel_scratch_tmp_bytes(int cap) {
-  size_t a = 0, b = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (unsigned*)nullptr, (unsigned*)nullptr, (int*)nullptr,
-                                           (int*)nullptr, cap, 0, 32);
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (int*)nullptr, (int*)nullptr, cap);
-  return a > b ? a : b;
-}
-
-// ---------------------------------------------------------------- NN index
-__device__ __forceinline__ unsigned mo_cell_hash(int ix, int iy, int iz) {
-  unsigned long long k = ((unsigned long long)(unsigned)(ix + (1 << 20)) << 42) |
-                         ((unsigned long long)(unsigned)(iy + (1 << 20)) << 21) |
-                         (unsigned long long)(unsigned)(iz + (1 << 20));
-  k ^= k >> 33; k *= 0xff51afd7ed558ccdULL; k ^= k >> 33;
-  return (unsigned)k;
-}
-__device__ __forceinline__ int cell1(float v) { return (int)floorf(v); }  // 1 m cells
-
-__global__ void k_idx_keys(const float4* pts, const int* nDev, int n, int T, VgScratch v) {
-  const int nn = min(n, *nDev);
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    unsigned key = kInvalidKey;
-    if (i < nn) {
-      const float4 p = pts[i];
-      key = mo_cell_hash(cell1(p.x), cell1(p.y), cell1(p.z)) & (unsigned)(T - 1);
-    }
-    v.keys[i] = key;
-    v.vals[i] = i;
-  }
-}
-// bucket begin/end (end == begin == 0 for an empty bucket) and the points in
-// bucket order carrying their index in w
-__global__ void k_idx_fill(const float4* pts, int n, VgScratch v, MoIndex ix) {
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
-    const unsigned k = v.keys2[t];
-    if (k == kInvalidKey) continue;
-    const int i = v.vals2[t];
-    const float4 p = pts[i];
-    ix.sorted[t] = make_float4(p.x, p.y, p.z, __int_as_float(i));
-    if (t == 0 || v.keys2[t - 1] != k) ix.begin[k] = t;
-    if (t == n - 1 || v.keys2[t + 1] != k) ix.end[k] = t + 1;
-  }
-}
-
-int index_build_device(const float4* pts, int n, const int* nDev, MoIndex& ix, const VgScratch& v, hipStream_t s) {
-  if (n > v.cap || n > ix.cap) return -1;
-  int T = 64;
-  while (T < n) T <<= 1;
-  ix.T = T;
-  if (hipMemsetAsync(ix.begin, 0, sizeof(int) * T, s) != hipSuccess) return -1;
-  if (hipMemsetAsync(ix.end, 0, sizeof(int) * T, s) != hipSuccess) return -1;
-  if (n <= 0) return 0;
-  k_idx_keys<<<grid_for(n), 256, 0, s>>>(pts, nDev, n, T, v);
-  size_t tb = v.tmpBytes;
-  if (hipcub::DeviceRadixSort::SortPairs(v.tmp, tb, v.keys, v.keys2, v.vals, v.vals2, n, 0, 32, s) != hipSuccess)
-    return -1;
-  k_idx_fill<<<grid_for(n), 256, 0, s>>>(pts, n, v, ix);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
+// VoxelGrid and the NN index build: lego_vg.hip.
 
 // The 5 nearest map points with squared distance < 1 (FLANN L2_Simple order),
 // sorted by (distance, index), found by a 32-lane group: lane l < 27 scans cell

@@ -468,13 +468,19 @@ def fa_to_dict(o: FaOut) -> dict:
 class Oracle:
     """TEST INFRASTRUCTURE: stateful oracle pipeline (one stream)."""
 
-    def __init__(self, cfg: SensorCfg, pcl_sort: bool = False):
+    VG_FA = 1  # featureAssociation's per-ring VoxelGrid in PCL's std::sort order
+    VG_MO = 2  # mapOptimization's VoxelGrids in PCL's std::sort order
+    DEFAULT_OPTS = VG_FA | VG_MO  # LEGO_ORACLE_DEFAULT_OPTS: the reference's order everywhere
+
+    def __init__(self, cfg: SensorCfg, vg_opts: int | None = None):
+        """vg_opts: None keeps the default (the reference's VoxelGrid order,
+        which the product reproduces); 0 sums every voxel in input order."""
         self.lib = oracle_lib()
         self.cfg = cfg
         self.h = C.c_void_p()
         check(self.lib.lego_oracle_create(C.byref(cfg), C.byref(self.h)), "oracle_create")
-        if pcl_sort:
-            self.lib.lego_oracle_set_options(self.h, 1)
+        if vg_opts is not None:
+            check(self.lib.lego_oracle_set_options(self.h, int(vg_opts)), "oracle_set_options")
         self._ip = IpOut()
         self._fa = FaOut()
 

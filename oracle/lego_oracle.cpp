@@ -86,7 +86,8 @@ using Pt = lego_point_xyzi;
 // pcl::VoxelGrid<PointXYZI>::applyFilter (PCL 1.8, downsample_all_data_=true,
 // min_points_per_voxel_=0).  In-voxel summation order: PCL std::sorts the
 // (idx, point) pairs by idx only, so equal-idx order is libstdc++ introsort's
-// (pcl_sort=1 reproduces it); the product fixes it to input order (pcl_sort=0).
+// (pcl_sort=1 reproduces it, the product's order: lego_vgsort.h); pcl_sort=0
+// sums in input order (std::stable_sort), kept for comparison.
 void voxel_grid(const std::vector<Pt>& in, float leaf, bool pcl_sort, std::vector<Pt>& out) {
   out.clear();
   if (in.empty()) return;
@@ -1361,6 +1362,8 @@ extern "C" int lego_oracle_create(const lego_sensor_cfg* cfg, lego_oracle** out)
   o->mo.reset(new oracle::MapOptimization(*cfg));
   o->fa->log = &o->log;
   o->mo->log = &o->log;
+  o->fa->pcl_sort = (LEGO_ORACLE_DEFAULT_OPTS & LEGO_ORACLE_VG_FA) != 0;
+  o->mo->pcl_sort = (LEGO_ORACLE_DEFAULT_OPTS & LEGO_ORACLE_VG_MO) != 0;
   *out = o;
   return LEGO_OK;
 }
@@ -1372,8 +1375,8 @@ extern "C" int lego_oracle_destroy(lego_oracle* o) {
 
 extern "C" int lego_oracle_set_options(lego_oracle* o, uint32_t opts) {
   if (!o) return LEGO_E_ARG;
-  o->fa->pcl_sort = (opts & 1u) != 0;
-  o->mo->pcl_sort = (opts & 1u) != 0;
+  o->fa->pcl_sort = (opts & LEGO_ORACLE_VG_FA) != 0;
+  o->mo->pcl_sort = (opts & LEGO_ORACLE_VG_MO) != 0;
   return LEGO_OK;
 }
 

@@ -20,8 +20,15 @@ typedef struct lego_oracle lego_oracle;
 int lego_oracle_sensor_preset(const char* name, lego_sensor_cfg* out);
 int lego_oracle_create(const lego_sensor_cfg* cfg, lego_oracle** out);
 int lego_oracle_destroy(lego_oracle* o);
-/* Options: bit 0 = PCL VoxelGrid in-voxel order via std::sort (unstable, the
- * exact reference behaviour) instead of input order (the product's order). */
+/* Options: the VoxelGrid in-voxel summation order.  Bit 0: featureAssociation's
+ * per-ring VoxelGrid (featureAssociation.cpp:778-780), bit 1: mapOptimization's
+ * VoxelGrids (mapOptmization.cpp:1058-1091, 1363).  A set bit sums each voxel
+ * in PCL's order (std::sort of (idx, point) by idx, unstable: the reference's
+ * behaviour), a clear bit in input order (std::stable_sort).  The default
+ * (LEGO_ORACLE_DEFAULT_OPTS) is the product's: both bits set. */
+#define LEGO_ORACLE_VG_FA 1u
+#define LEGO_ORACLE_VG_MO 2u
+#define LEGO_ORACLE_DEFAULT_OPTS (LEGO_ORACLE_VG_FA | LEGO_ORACLE_VG_MO)
 int lego_oracle_set_options(lego_oracle* o, uint32_t opts);
 int lego_oracle_ip_process(lego_oracle* o, const lego_point_xyzir* pts, int32_t n,
                            double stamp, uint32_t flags, lego_ip_out* out);

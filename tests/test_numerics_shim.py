@@ -33,6 +33,16 @@ def test_introsort_port_matches_std_sort(tmp_path):
     assert r.returncode == 0, r.stdout
 
 
+def test_vgsort_partition_rules_match_std_sort(tmp_path):
+    """lego_vgsort.h's parallel partition rules (prefix-count pairing, cut,
+    level order, stable blocks, heap-sort fallback) give std::sort's order of
+    equal VoxelGrid keys — the order PCL sums a voxel's points in."""
+    exe = _build(tmp_path, "vgsort_check", REPO / "tests/native/vgsort_check.cpp")
+    r = subprocess.run([str(exe), "6000"], capture_output=True, text=True, timeout=600)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout
+
+
 def test_eigen3_register_form_matches_generic(tmp_path):
     """The device solver's register-resident 3x3 Jacobi (cv_eigen_sym3) must
     equal the OpenCV JacobiImpl_ restatement (cv_eigen_sym<3>) bit for bit."""
