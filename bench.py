@@ -463,6 +463,11 @@ def main():
     if args.odom_profile:
         lib.lego_odom_profile(gpu.h, 1, None)
     recs = (L.PoseRec * B)()
+    # N > 1 hand-off transport: the C-ABI's own collective (lego_comm_gather_handoff_ex,
+    # RCCL send/recv over xGMI, packets kept in rank 0's HBM) when every rank has
+    # its GPU; the one-GPU rehearsal (gloo, shared device) gathers over torch.
+    native = dist is not None and backend == "nccl"
+    comm = ms.native_comm(L, dist, local) if native else None
 
     # Steps are pipelined two deep (lego_odom_batch_submit / _wait): step i+1's
     # projection + extraction run while step i's odometry chain does.
@@ -474,8 +479,14 @@ def main():
         cp = (L.PoseRec * B)()
         C.memmove(cp, recs, C.sizeof(recs))
         # N > 1: the step's hand-off packet (pose records + the published
-        # corner / surf / outlier clouds) packed into HBM before the slot is reused
-        pkt = gpu.handoff_tensor(dev) if dist else None
+        # corner / surf / outlier clouds) to rank 0 before the slot is reused:
+        # gathered right here by the native collective, or packed into HBM for
+        # the torch gather
+        pkt = None
+        if native:
+            pkt = ms.native_gather_handoff(L, comm, gpu, 0, device=True)
+        elif dist:
+            pkt = gpu.handoff_tensor(dev)
         return i, gpu.stage_times(), cp, pkt
 
     def submit(i):
@@ -510,8 +521,10 @@ def main():
             for k, v in st.items():
                 stage_acc[k] = stage_acc.get(k, 0.0) + v
             alg_bytes += odom_alg_bytes(rc)
-            if dist:  # hand-off of the step to the serial consumer on rank 0 (RCCL over xGMI)
-                gathered = ms.gather_packets(pkt if backend == "nccl" else pkt.cpu(), dist, to_host=False)
+            if native:  # gathered in retire(): rank 0's device copies of every rank's packet
+                gathered = pkt
+            elif dist:  # hand-off of the step to the serial consumer on rank 0 (torch gather, rehearsal)
+                gathered = ms.gather_packets(pkt.cpu(), dist, to_host=False)
 
     for i in range(args.steps):
         account(submit(args.warmup + i))
@@ -533,12 +546,27 @@ def main():
     if rank == 0:
         handoff = mapping_handoff(gpu, B)
         if gathered is not None:  # the last step's packets as rank 0 received them
-            hdrs = [L.handoff_header(g.cpu().numpy()) for g in gathered]
+            if native:
+                L.check(lib.lego_comm_wait(comm), "lego_comm_wait", lib)
+                hdrs = []
+                for ptr, nbytes in gathered:
+                    h = L.HandoffHdr()
+                    if ptr and nbytes >= C.sizeof(h):
+                        L.hip_memcpy_d2h(C.addressof(h), ptr, C.sizeof(h))
+                    hdrs.append(h)
+                sizes = [int(nb) for _, nb in gathered]
+                transport = ("lego_comm_gather_handoff_ex (C-ABI; RCCL ncclGather of sizes + ncclSend/ncclRecv "
+                             "of packets, LEGO_COMM_DEVICE_RESULT), every step in the timed region")
+            else:
+                hdrs = [L.handoff_header(g.cpu().numpy()) for g in gathered]
+                sizes = [int(g.numel()) for g in gathered]
+                transport = f"torch.distributed gather ({backend}) of lego_handoff_pack_into packets, in the timed region"
             handoff["gathered_to_rank0"] = {
                 "ranks": len(hdrs), "scans_per_rank": [h.nscans for h in hdrs],
                 "published_per_rank": [h.npub for h in hdrs], "bytes_per_rank": [h.bytes for h in hdrs],
-                "valid": all(h.magic == L.HANDOFF_MAGIC and h.nscans == B for h in hdrs),
-                "transport": f"torch.distributed gather ({backend}) of lego_handoff_pack_into packets, in the timed region"}
+                "valid": len(hdrs) == world and all(h.magic == L.HANDOFF_MAGIC and h.nscans == B and h.bytes == n
+                                                    for h, n in zip(hdrs, sizes)),
+                "transport": transport}
         # the batch runs as chunks (lego_api.hip run_batch): k_odom launches per step
         launches = {k[2:]: v / args.steps for k, v in stage_acc.items() if k.startswith("n:")}
         stage_acc = {k: v for k, v in stage_acc.items() if not k.startswith("n:")}
@@ -629,7 +657,8 @@ def main():
                                     "gathered to rank 0 every step"),
                        "scans_per_step": B, "stream_len": args.stream_len,
                        "parallelism": f"stream-per-gpu x{world}",
-                       "gather": "per step: pose records + published clouds to rank 0" if world > 1 else None},
+                       "gather": ((("lego_comm (C-ABI RCCL send/recv)" if native else f"torch.distributed ({backend})")
+                                   + ": per step, pose records + published clouds to rank 0") if world > 1 else None)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "traffic_over_alg": (traffic / (alg_bytes / args.steps * 1.0 / n_odom)
@@ -642,6 +671,8 @@ def main():
             "aux": aux,
         }
         print(json.dumps(line))
+    if comm is not None:
+        lib.lego_comm_destroy(comm)
     gpu.close()
     if dist:
         dist.destroy_process_group()

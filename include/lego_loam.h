@@ -438,11 +438,29 @@ int lego_comm_create(const uint8_t id[128], int32_t nranks, int32_t rank, int32_
 int lego_comm_destroy(lego_comm* comm);
 /* Collective over all ranks: every rank packs its context's last batch
  * (lego_handoff_pack) and root receives every rank's packet (ncclGather of
- * the sizes, then ncclSend / ncclRecv of the packets in one group). */
+ * the sizes, then ncclSend / ncclRecv of the packets in one group).  Returns
+ * once the packets are in root's host memory (lego_comm_handoff).
+ * = lego_comm_gather_handoff_ex(comm, ctx, root, 0). */
 int lego_comm_gather_handoff(lego_comm* comm, lego_ctx* ctx, int32_t root);
+/* flags: LEGO_COMM_DEVICE_RESULT keeps the gathered packets in root's device
+ * memory (lego_comm_handoff_device) and returns once the send / receive is
+ * enqueued on the communicator's stream: root waits only for the 8-byte
+ * sizes, no packet crosses PCIe and no rank waits for the transfer (the next
+ * call, lego_comm_wait or a device synchronisation does).  A rank whose pack
+ * fails still takes part with an empty packet (the others do not hang) and
+ * returns the pack's status; an RCCL or device error after the communicator
+ * was used aborts it (ncclCommAbort) and every later call returns
+ * LEGO_E_STATE. */
+#define LEGO_COMM_DEVICE_RESULT 1u
+int lego_comm_gather_handoff_ex(lego_comm* comm, lego_ctx* ctx, int32_t root, uint32_t flags);
+/* Blocks until the last gather on the communicator has completed. */
+int lego_comm_wait(lego_comm* comm);
 /* On root after lego_comm_gather_handoff: rank r's packet in host memory,
  * valid until the next gather on the communicator. */
 int lego_comm_handoff(lego_comm* comm, int32_t rank, const void** packet, uint64_t* bytes);
+/* On root after either gather: rank r's packet in device memory (complete
+ * once lego_comm_wait returns), valid until the next gather. */
+int lego_comm_handoff_device(lego_comm* comm, int32_t rank, const void** dpacket, uint64_t* bytes);
 
 /* Last device error string (static storage). */
 const char* lego_last_error(void);

@@ -730,6 +730,8 @@ static int submit_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t*
     return LEGO_E_STATE;
   }
   const int h = x->nextSlot, base = h * x->maxBatch;
+  // the waited batch in this slot is about to be overwritten: no hand-off of it after this
+  if (x->lastBatch && x->lastBase == base) x->lastBatch = false;
   BatchBufs bb = bb_slice(x->bb, x->dc, base, B);
   int st = stage_inputs(x, pts, offsets, B, on_device, bb);
   if (st != LEGO_OK) return st;
@@ -1027,6 +1029,7 @@ int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
   }
   x->lastB = 1;
   x->lastBase = 0;
+  x->lastBatch = false;  // slot 0's buffers now hold this scan, not a waited batch
   x->lastIpDevice = false;
   return fetch_fa(x, 0, out);
 }
@@ -1643,6 +1646,7 @@ static int handoff_pack(lego_ctx* x, uint8_t* dst, uint64_t cap, const void** pa
   }
   const int slot = x->lastBase / x->maxBatch;
   const PackedRec* pk = x->h_pack + (size_t)slot * (x->maxBatch + 1);
+  const std::vector<double>& stamps = x->slotStamps[slot];  // the waited batch's, whatever was submitted since
   const size_t head = sizeof(lego_handoff_hdr) + sizeof(lego_handoff_scan) * (size_t)B;
   x->h_handoffHead.assign(head, 0);
   lego_handoff_hdr* h = reinterpret_cast<lego_handoff_hdr*>(x->h_handoffHead.data());
@@ -1651,7 +1655,7 @@ static int handoff_pack(lego_ctx* x, uint8_t* dst, uint64_t cap, const void** pa
   for (int k = 0; k < B; ++k) {
     const PackedRec& p = pk[k];
     lego_pose_rec& r = e[k].rec;
-    r.stamp = k < (int)x->stamps.size() ? x->stamps[k] : 0.0;
+    r.stamp = k < (int)stamps.size() ? stamps[k] : 0.0;
     for (int i = 0; i < 6; ++i) { r.transform_sum[i] = p.sum[i]; e[k].transform_cur[i] = p.cur[i]; }
     r.n_segmented = p.ns;
     r.n_sharp = p.cnt[0]; r.n_less_sharp = p.cnt[1]; r.n_flat = p.cnt[2]; r.n_less_flat = p.cnt[3];

@@ -8,7 +8,15 @@
 // group of ncclSend (every other rank) / ncclRecv (root, one per peer), so
 // each peer's packet travels on its own link.  Root's own packet is a
 // device-to-device copy.  The received packets are copied to pinned host
-// memory for the host-side consumers (lego_handoff_unpack -> lego_mo_process).
+// memory for the host-side consumers (lego_handoff_unpack -> lego_mo_process),
+// or, with LEGO_COMM_DEVICE_RESULT, stay in HBM and nothing waits for the
+// transfer (the next call does: the sender's packet buffer is reused then).
+//
+// Failure policy: a rank whose pack fails sends an empty packet, so the
+// others never wait for it; an RCCL or device error once the communicator is
+// in use closes any open group and aborts the communicator (ncclCommAbort),
+// and the communicator is dead from then on.  Only root sizes buffers after
+// the size exchange; it aborts if that fails.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -32,7 +40,8 @@ struct lego_comm {
   uint8_t* hRecv = nullptr;    // pinned copy of dRecv
   size_t hCap = 0;
   std::vector<uint64_t> sizes, offs;
-  bool haveResult = false;
+  bool haveResult = false, haveHost = false;
+  bool dead = false;
   ~lego_comm() {
     if (device >= 0) (void)hipSetDevice(device);
     if (s) (void)hipStreamSynchronize(s);
@@ -113,57 +122,113 @@ int lego_comm_destroy(lego_comm* c) {
   return LEGO_OK;
 }
 
-int lego_comm_gather_handoff(lego_comm* c, lego_ctx* ctx, int32_t root) {
-  if (!c || !ctx || root < 0 || root >= c->nranks) return LEGO_E_ARG;
-  c->haveResult = false;
+static int comm_abort(lego_comm* c, bool inGroup, const char* what, const char* why) {
+  if (inGroup) (void)ncclGroupEnd();
+  lego_set_error("lego_comm: %s: %s (communicator aborted)", what, why);
+  if (c->nc) (void)ncclCommAbort(c->nc);
+  c->nc = nullptr;
+  c->dead = true;
+  c->haveResult = c->haveHost = false;
+  return LEGO_E_DEVICE;
+}
+#define COMM_TRY_HIP(call, inGroup)                                          \
+  do {                                                                      \
+    hipError_t e_ = (call);                                                 \
+    if (e_ != hipSuccess) return comm_abort(c, inGroup, #call, hipGetErrorString(e_)); \
+  } while (0)
+#define COMM_TRY_NCCL(call, inGroup)                                         \
+  do {                                                                      \
+    ncclResult_t r_ = (call);                                               \
+    if (r_ != ncclSuccess) return comm_abort(c, inGroup, #call, ncclGetErrorString(r_)); \
+  } while (0)
+
+int lego_comm_gather_handoff_ex(lego_comm* c, lego_ctx* ctx, int32_t root, uint32_t flags) {
+  if (!c || !ctx || root < 0 || root >= c->nranks || (flags & ~LEGO_COMM_DEVICE_RESULT)) return LEGO_E_ARG;
+  if (c->dead) {
+    lego_set_error("lego_comm: the communicator was aborted by an earlier error");
+    return LEGO_E_STATE;
+  }
+  c->haveResult = c->haveHost = false;
+  COMM_HIP(hipSetDevice(c->device));
+  // the previous gather's send reads ctx's packet buffer, which the pack reuses
+  COMM_TRY_HIP(hipStreamSynchronize(c->s), false);
   const void* pkt = nullptr;
   uint64_t bytes = 0;
-  const int st = lego_handoff_pack(ctx, &pkt, &bytes);  // complete on return
-  if (st != LEGO_OK) return st;
-  COMM_HIP(hipSetDevice(c->device));
-  COMM_HIP(hipMemcpyAsync(c->dSize, &bytes, sizeof(bytes), hipMemcpyHostToDevice, c->s));
-  COMM_NCCL(ncclGather(c->dSize, c->dSizes, 1, ncclUint64, root, c->nc, c->s));
+  const int packSt = lego_handoff_pack(ctx, &pkt, &bytes);  // complete on return
+  if (packSt != LEGO_OK) { pkt = nullptr; bytes = 0; }     // take part with an empty packet
+  COMM_TRY_HIP(hipMemcpyAsync(c->dSize, &bytes, sizeof(bytes), hipMemcpyHostToDevice, c->s), false);
+  COMM_TRY_NCCL(ncclGather(c->dSize, c->dSizes, 1, ncclUint64, root, c->nc, c->s), false);
   const bool isRoot = c->rank == root;
   if (isRoot) {
-    COMM_HIP(hipMemcpyAsync(c->sizes.data(), c->dSizes, sizeof(uint64_t) * c->nranks, hipMemcpyDeviceToHost, c->s));
-    COMM_HIP(hipStreamSynchronize(c->s));
+    COMM_TRY_HIP(hipMemcpyAsync(c->sizes.data(), c->dSizes, sizeof(uint64_t) * c->nranks, hipMemcpyDeviceToHost, c->s),
+                 false);
+    COMM_TRY_HIP(hipStreamSynchronize(c->s), false);
     for (int r = 0; r < c->nranks; ++r) c->offs[r + 1] = c->offs[r] + ((c->sizes[r] + 255) & ~(uint64_t)255);
     const size_t need = c->offs[c->nranks];
     if (need > c->recvCap) {
-      if (c->dRecv) COMM_HIP(hipFree(c->dRecv));
+      if (c->dRecv) COMM_TRY_HIP(hipFree(c->dRecv), false);
       c->dRecv = nullptr;
       c->recvCap = 0;
-      COMM_HIP(hipMalloc(&c->dRecv, need));
+      COMM_TRY_HIP(hipMalloc(&c->dRecv, need), false);
       c->recvCap = need;
     }
-    if (need > c->hCap) {
-      if (c->hRecv) COMM_HIP(hipHostFree(c->hRecv));
-      c->hRecv = nullptr;
-      c->hCap = 0;
-      COMM_HIP(hipHostMalloc(&c->hRecv, need, hipHostMallocDefault));
-      c->hCap = need;
-    }
-    COMM_HIP(hipMemcpyAsync(c->dRecv + c->offs[root], pkt, bytes, hipMemcpyDeviceToDevice, c->s));
+    if (bytes) COMM_TRY_HIP(hipMemcpyAsync(c->dRecv + c->offs[root], pkt, bytes, hipMemcpyDeviceToDevice, c->s), false);
   }
-  COMM_NCCL(ncclGroupStart());
+  COMM_TRY_NCCL(ncclGroupStart(), false);
   if (isRoot) {
     for (int r = 0; r < c->nranks; ++r)
       if (r != root && c->sizes[r])
-        COMM_NCCL(ncclRecv(c->dRecv + c->offs[r], c->sizes[r], ncclUint8, r, c->nc, c->s));
+        COMM_TRY_NCCL(ncclRecv(c->dRecv + c->offs[r], c->sizes[r], ncclUint8, r, c->nc, c->s), true);
   } else if (bytes) {
-    COMM_NCCL(ncclSend(pkt, bytes, ncclUint8, root, c->nc, c->s));
+    COMM_TRY_NCCL(ncclSend(pkt, bytes, ncclUint8, root, c->nc, c->s), true);
   }
-  COMM_NCCL(ncclGroupEnd());
-  if (isRoot) COMM_HIP(hipMemcpyAsync(c->hRecv, c->dRecv, c->offs[c->nranks], hipMemcpyDeviceToHost, c->s));
-  COMM_HIP(hipStreamSynchronize(c->s));
+  COMM_TRY_NCCL(ncclGroupEnd(), false);
+  if (!(flags & LEGO_COMM_DEVICE_RESULT)) {
+    if (isRoot) {
+      const size_t need = c->offs[c->nranks];
+      if (need > c->hCap) {
+        if (c->hRecv) COMM_TRY_HIP(hipHostFree(c->hRecv), false);
+        c->hRecv = nullptr;
+        c->hCap = 0;
+        COMM_TRY_HIP(hipHostMalloc(&c->hRecv, need, hipHostMallocDefault), false);
+        c->hCap = need;
+      }
+      COMM_TRY_HIP(hipMemcpyAsync(c->hRecv, c->dRecv, need, hipMemcpyDeviceToHost, c->s), false);
+    }
+    COMM_TRY_HIP(hipStreamSynchronize(c->s), false);
+    c->haveHost = isRoot;
+  }
   c->haveResult = isRoot;
+  return packSt;
+}
+
+int lego_comm_gather_handoff(lego_comm* c, lego_ctx* ctx, int32_t root) {
+  return lego_comm_gather_handoff_ex(c, ctx, root, 0);
+}
+
+int lego_comm_wait(lego_comm* c) {
+  if (!c) return LEGO_E_ARG;
+  if (c->dead) return LEGO_E_STATE;
+  COMM_HIP(hipSetDevice(c->device));
+  COMM_TRY_HIP(hipStreamSynchronize(c->s), false);
+  return LEGO_OK;
+}
+
+int lego_comm_handoff_device(lego_comm* c, int32_t rank, const void** dpacket, uint64_t* bytes) {
+  if (!c || !dpacket || !bytes || rank < 0 || rank >= c->nranks) return LEGO_E_ARG;
+  if (!c->haveResult) {
+    lego_set_error("lego_comm_handoff_device: no gathered result on this rank (root, after a gather)");
+    return LEGO_E_STATE;
+  }
+  *dpacket = c->dRecv + c->offs[rank];
+  *bytes = c->sizes[rank];
   return LEGO_OK;
 }
 
 int lego_comm_handoff(lego_comm* c, int32_t rank, const void** packet, uint64_t* bytes) {
   if (!c || !packet || !bytes || rank < 0 || rank >= c->nranks) return LEGO_E_ARG;
-  if (!c->haveResult) {
-    lego_set_error("lego_comm_handoff: no gathered result on this rank (root, after lego_comm_gather_handoff)");
+  if (!c->haveHost) {
+    lego_set_error("lego_comm_handoff: no host result on this rank (root, after lego_comm_gather_handoff)");
     return LEGO_E_STATE;
   }
   *packet = c->hRecv + c->offs[rank];

@@ -274,7 +274,8 @@ HIP_EXPORTS = ["lego_sensor_preset", "lego_create", "lego_fleet_create", "lego_d
                "lego_fusion_odometry", "lego_fusion_aft_mapped",
                "lego_mo_set_map", "lego_mo_configure", "lego_mo_process", "lego_mo_loop_closure", "lego_last_error", "lego_stage_times",
                "lego_odom_profile", "lego_extract_profile", "lego_handoff_pack", "lego_handoff_pack_into", "lego_handoff_unpack", "lego_comm_unique_id",
-               "lego_comm_create", "lego_comm_destroy", "lego_comm_gather_handoff", "lego_comm_handoff"]
+               "lego_comm_create", "lego_comm_destroy", "lego_comm_gather_handoff", "lego_comm_handoff",
+               "lego_comm_gather_handoff_ex", "lego_comm_wait", "lego_comm_handoff_device"]
 
 
 def hip_lib() -> C.CDLL:
@@ -319,6 +320,9 @@ def hip_lib() -> C.CDLL:
     lib.lego_comm_destroy.argtypes = [C.c_void_p]
     lib.lego_comm_gather_handoff.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
     lib.lego_comm_handoff.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]
+    lib.lego_comm_gather_handoff_ex.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_uint32]
+    lib.lego_comm_wait.argtypes = [C.c_void_p]
+    lib.lego_comm_handoff_device.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]
     lib.lego_last_error.restype = C.c_char_p
     lib.lego_odom_profile.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
     lib.lego_extract_profile.argtypes = [C.c_void_p, C.c_void_p]
@@ -334,7 +338,15 @@ def hip_memcpy_d2h(dst: int, src: int, n: int) -> int:
     """hipMemcpy device -> host through the HIP runtime already loaded."""
     global _hiprt
     if _hiprt is None:
-        _hiprt = C.CDLL("libamdhip64.so.7")
+        hip_lib()  # the runtime liblego_hip.so links is then loaded: take that one
+        for name in ("libamdhip64.so", "libamdhip64.so.7", "libamdhip64.so.6"):
+            try:
+                _hiprt = C.CDLL(name)
+                break
+            except OSError:
+                continue
+        if _hiprt is None:
+            raise OSError("no HIP runtime (libamdhip64.so) to copy the packet with")
         _hiprt.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
     return _hiprt.hipMemcpy(C.c_void_p(dst), C.c_void_p(src), n, 2)  # hipMemcpyDeviceToHost
 

@@ -7,8 +7,8 @@ serial consumer (the reference's mapOptimization / transformFusion nodes):
 the fixed 64-B `lego_pose_rec`s of every step (`gather_pose_records`, the
 bench's per-step gather) and the batch's hand-off packet with the published
 corner / surf / outlier clouds (`gather_packets` over torch.distributed, or
-`native_gather_handoff`, the C-ABI's RCCL collective, lego_comm.hip), which
-rank 0 maps with `Lego.mo_handoff`.  On ROCm the "nccl" backend is RCCL over
+`native_gather_handoff`, the C-ABI's RCCL collective, lego_comm.hip — what
+bench.py's N > 1 path times), which rank 0 maps with `Lego.mo_handoff`.  On ROCm the "nccl" backend is RCCL over
 xGMI; the CPU tests drive the same code over gloo.
 """
 from __future__ import annotations
@@ -110,12 +110,31 @@ def native_comm(L, dist, device: int):
     return comm
 
 
-def native_gather_handoff(L, comm, ctx, root: int = 0):
-    """lego_comm_gather_handoff: every rank's last batch packet to root over
-    RCCL.  Returns the host packets on root (list per rank), None elsewhere."""
+LEGO_COMM_DEVICE_RESULT = 1
+
+
+def native_gather_handoff(L, comm, ctx, root: int = 0, device: bool = False):
+    """lego_comm_gather_handoff(_ex): every rank's last batch packet to root
+    over RCCL.  Returns on root the host packets (list per rank) or, with
+    device=True (LEGO_COMM_DEVICE_RESULT: no D2H copy, no wait for the
+    transfer), the (device pointer, bytes) of each rank's packet, complete once
+    lego_comm_wait or a device synchronisation returns; None elsewhere."""
     import ctypes as C
 
     lib = L.hip_lib()
+    if device:
+        L.check(lib.lego_comm_gather_handoff_ex(comm, ctx.h, root, LEGO_COMM_DEVICE_RESULT),
+                "lego_comm_gather_handoff_ex", lib)
+        out = []
+        for r in range(10 ** 6):
+            ptr, n = C.c_void_p(), C.c_uint64()
+            st = lib.lego_comm_handoff_device(comm, r, C.byref(ptr), C.byref(n))
+            if st == L.LEGO_E_STATE:
+                return None  # not root
+            if st != L.LEGO_OK:
+                break  # past the last rank
+            out.append((ptr.value, n.value))
+        return out
     L.check(lib.lego_comm_gather_handoff(comm, ctx.h, root), "lego_comm_gather_handoff", lib)
     out = []
     r = 0

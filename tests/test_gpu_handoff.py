@@ -174,3 +174,93 @@ def test_world2_packets_mapped_on_rank0(L, tmp_path):
     out = tmp_path / "rank0.txt"
     mp.spawn(_worker, args=(2, _free_port(), str(out)), nprocs=2, join=True)
     assert out.read_text() == "ok"
+
+
+def test_native_rccl_gather_device_result_world1(L):
+    """LEGO_COMM_DEVICE_RESULT: the packet stays in HBM, the call does not wait
+    for the transfer; after lego_comm_wait its bytes equal the host path's."""
+    import ctypes as C
+
+    lib = L.hip_lib()
+    uid = (C.c_uint8 * 128)()
+    L.check(lib.lego_comm_unique_id(uid), "lego_comm_unique_id", lib)
+    comm = C.c_void_p()
+    L.check(lib.lego_comm_create(uid, 1, 0, 0, C.byref(comm)), "lego_comm_create", lib)
+    scans = _scans(L, 2)
+    g = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=40000, max_batch=K // 2)
+    for part in (scans[:K // 2], scans[K // 2:]):
+        g.odom_batch(*_pack(part))
+        got = ms.native_gather_handoff(L, comm, g, 0, device=True)
+        assert len(got) == 1
+        L.check(lib.lego_comm_wait(comm), "lego_comm_wait", lib)
+        ptr, n = got[0]
+        host = np.zeros(n, np.uint8)
+        assert L.hip_memcpy_d2h(host.ctypes.data, ptr, n) == 0
+        assert np.array_equal(host, g.handoff_packet())
+        # the host result is only produced by the host-result call
+        p, b = C.c_void_p(), C.c_uint64()
+        assert lib.lego_comm_handoff(comm, 0, C.byref(p), C.byref(b)) == L.LEGO_E_STATE
+    g.close()
+    lib.lego_comm_destroy(comm)
+
+
+def _native_worker(rank, world, port, out):
+    """One process per GPU: the C-ABI collective (RCCL send/recv between the
+    GPUs) gathers every rank's packets to rank 0, host and device results."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(rank)
+    sys.path.insert(0, str(REPO / "tests"))
+    from conftest import _load_ffi
+
+    L = _load_ffi()
+    lib = L.hip_lib()
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        comm = ms.native_comm(L, dist, rank)
+        scans = _scans(L, ms.stream_seed(rank))
+        g = L.Lego(L.sensor_cfg("VLP-16", lib), device=rank, max_points=40000, max_batch=K // 2)
+        host_steps, dev_steps = [], []
+        for part in (scans[:K // 2], scans[K // 2:]):
+            g.odom_batch(*_pack(part))
+            own = g.handoff_packet()
+            host_steps.append(ms.native_gather_handoff(L, comm, g, 0))
+            dev = ms.native_gather_handoff(L, comm, g, 0, device=True)
+            L.check(lib.lego_comm_wait(comm), "lego_comm_wait", lib)
+            if rank == 0:
+                copies = []
+                for ptr, n in dev:
+                    h = np.zeros(n, np.uint8)
+                    assert L.hip_memcpy_d2h(h.ctypes.data, ptr, n) == 0
+                    copies.append(h)
+                dev_steps.append(copies)
+                assert np.array_equal(host_steps[-1][0], own)
+        g.close()
+        lib.lego_comm_destroy(comm)
+        if rank == 0:
+            for r in range(world):
+                for hs, ds in zip(host_steps, dev_steps):
+                    assert np.array_equal(hs[r], ds[r]), f"rank {r}: device result differs from host result"
+                _map_packets(L, [step[r] for step in host_steps],
+                             _oracle_mapping(L, _scans(L, ms.stream_seed(r))), f"rank {r} stream")
+            Path(out).write_text("ok")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_native_rccl_gather_all_gpus(L, tmp_path):
+    """lego_comm_gather_handoff(_ex) with one rank per visible GPU (world =
+    torch.cuda.device_count(), up to 8): the ncclSend / ncclRecv branch.  Rank
+    0 maps every stream from the gathered packets bit-exactly like the
+    oracle.  Needs two GPUs or more (skipped on a one-GPU box)."""
+    import torch
+    import torch.multiprocessing as mp
+
+    world = min(torch.cuda.device_count(), 8)
+    if world < 2:
+        pytest.skip("one GPU: RCCL needs a device per rank")
+    out = tmp_path / "rank0.txt"
+    mp.spawn(_native_worker, args=(world, _free_port(), str(out)), nprocs=world, join=True)
+    assert out.read_text() == "ok"
