@@ -462,6 +462,21 @@ int lego_comm_handoff(lego_comm* comm, int32_t rank, const void** packet, uint64
  * once lego_comm_wait returns), valid until the next gather. */
 int lego_comm_handoff_device(lego_comm* comm, int32_t rank, const void** dpacket, uint64_t* bytes);
 
+/* pcl::VoxelGrid<PointXYZI> (leaf size `leaf`, downsample_all_data, no
+ * field filter) of a host cloud on the context's device: the filter every
+ * mapping VoxelGrid call runs (mapOptmization.cpp:1058-1091), including PCL's
+ * std::sort order of each voxel's points.  out holds up to n points; *n_out
+ * the voxels written.  Non-finite points are skipped, as PCL does for a cloud
+ * that is not dense. */
+int lego_voxel_grid(lego_ctx* ctx, const lego_point_xyzi* in, int32_t n, float leaf, lego_point_xyzi* out,
+                    int32_t* n_out);
+/* Counters of the last lego_voxel_grid: [0] finite points sorted, [1] voxels,
+ * [2] partition rounds launched, [3] segments sorted in one workgroup,
+ * [4] of them still above the workgroup size after the rounds, [5] heap-sorted
+ * segments (depth budget spent), [6] non-finite points, [7] device time in
+ * microseconds.  Diagnostics for tests and benchmarks. */
+int lego_voxel_grid_stats(lego_ctx* ctx, int32_t stats[8]);
+
 /* Last device error string (static storage). */
 const char* lego_last_error(void);
 

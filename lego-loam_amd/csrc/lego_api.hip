@@ -146,6 +146,12 @@ struct lego_ctx {
   // scan-to-map (lego_mo_*): buffers allocated by the first lego_mo_set_map
   MoDev mo{};
   bool moAlloc = false, moFixed = false;
+  // lego_voxel_grid: its own scratch and device cloud buffers, grown on demand
+  VgScratch vgApi{};
+  float4 *vgIn = nullptr, *vgOut = nullptr;
+  int* vgN = nullptr;
+  int vgCap = 0;
+  int vgStats[8] = {};
   lego_mo_opts moOpts{};
   double moTimeLast = -1;
   double moTimeOdom = 0;  // timeLaserOdometry: the last hand-off's stamp (laserOdometryHandler :630)
@@ -1214,6 +1220,62 @@ int lego_mo_set_map(lego_ctx* x, const lego_point_xyzi* corner, int32_t n_corner
   }
   HIPCHK(hipStreamSynchronize(x->stream));
   x->moFixed = true;
+  return LEGO_OK;
+}
+
+int lego_voxel_grid(lego_ctx* x, const lego_point_xyzi* in, int32_t n, float leaf, lego_point_xyzi* out,
+                    int32_t* n_out) {
+  if (!x || !n_out || n < 0 || (n > 0 && (!in || !out)) || !(leaf > 0.f)) return LEGO_E_ARG;
+  HIPCHK(hipSetDevice(x->device));
+  if (n > x->vgCap) {
+    auto ctx_alloc = [](void* c, void** p, size_t bytes) {
+      return static_cast<lego_ctx*>(c)->alloc(reinterpret_cast<unsigned char**>(p), bytes) == hipSuccess ? 0 : -1;
+    };
+    if (vg_scratch_alloc(x->vgApi, n, x, ctx_alloc)) {
+      set_err("hipMalloc failed for the VoxelGrid scratch");
+      return LEGO_E_DEVICE;
+    }
+    if (x->alloc(&x->vgIn, n) != hipSuccess || x->alloc(&x->vgOut, n) != hipSuccess ||
+        (!x->vgN && x->alloc(&x->vgN, 1) != hipSuccess)) {
+      set_err("hipMalloc failed for the VoxelGrid clouds");
+      return LEGO_E_DEVICE;
+    }
+    x->vgCap = n;
+  }
+  if (n == 0) {
+    *n_out = 0;
+    std::fill(x->vgStats, x->vgStats + 8, 0);
+    return LEGO_OK;
+  }
+  hipEvent_t e0, e1;
+  HIPCHK(hipEventCreate(&e0));
+  HIPCHK(hipEventCreate(&e1));
+  HIPCHK(hipMemcpyAsync(x->vgIn, in, sizeof(float4) * n, hipMemcpyHostToDevice, x->stream));
+  HIPCHK(hipEventRecord(e0, x->stream));
+  const int rc = voxel_grid_device(x->vgIn, n, nullptr, leaf, x->vgOut, x->vgN, x->vgApi, x->stream);
+  HIPCHK(hipEventRecord(e1, x->stream));
+  int nOut = 0, ctl[16];
+  HIPCHK(hipMemcpyAsync(&nOut, x->vgN, sizeof(int), hipMemcpyDeviceToHost, x->stream));
+  HIPCHK(hipStreamSynchronize(x->stream));
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (rc != 0 || vg_read_ctl(x->vgApi, ctl, x->stream) != 0) {
+    set_err("VoxelGrid launch failed");
+    return LEGO_E_DEVICE;
+  }
+  HIPCHK(hipMemcpy(out, x->vgOut, sizeof(float4) * nOut, hipMemcpyDeviceToHost));
+  *n_out = nOut;
+  // ctl: C_M 0, C_NLOC 4, C_NONFIN 5, C_NOUT 6, C_SLOW 7, C_HEAP 8 (lego_vg.hip)
+  const int st[8] = {ctl[0], ctl[6], vg_rounds_for(n), ctl[4], ctl[7], ctl[8], ctl[5], (int)(ms * 1000.f)};
+  std::copy(st, st + 8, x->vgStats);
+  return LEGO_OK;
+}
+
+int lego_voxel_grid_stats(lego_ctx* x, int32_t stats[8]) {
+  if (!x || !stats) return LEGO_E_ARG;
+  std::copy(x->vgStats, x->vgStats + 8, stats);
   return LEGO_OK;
 }
 

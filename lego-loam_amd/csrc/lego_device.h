@@ -18,7 +18,7 @@
 namespace lego {
 
 constexpr int kMaxRings = 128;        // rowmask = 2 x u64
-constexpr int kMaxHorizon = 4096;     // col fits u16; ring window fits LDS
+constexpr int kMaxHorizon = 2048;     // col fits u16; a ring's less-flat VoxelGrid sort holds <= 2048 keys (lego_vgsort.h)
 constexpr int kSharpPerRing = 12;     // 2 per sector (featureAssociation.cpp:709)
 constexpr int kLessSharpPerRing = 120;// 20 per sector (:713)
 constexpr int kFlatPerRing = 24;      // 4 per sector (:746-748)

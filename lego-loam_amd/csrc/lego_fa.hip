@@ -224,9 +224,6 @@ struct ExtractLds {
   uint16_t* perm;
   SmoothEntry* srt;
   SmoothEntry* orig;
-  uint32_t* vkey;     // VoxelGrid: voxel index per less-flat point (sorted in place)
-  uint16_t* vpr;      // VoxelGrid: partition partners
-  uint32_t* vlists;   // VoxelGrid: the two segment lists
   int* misc;
   float* red;
 };
@@ -245,16 +242,11 @@ __host__ __device__ inline int next_pow2(int x) {
 //   picking  A: pick lists [0, 1 KB), the initial  B: curv, perm, gfl
 //               picked copy, picked, label, col
 //   less-flat                                      B: lf (its tail)
-//   VoxelGrid   keys, partners and segment lists from offset 0 over A and
-//               B's head; lf in B's tail (the payload, sorted with the keys)
+//   less-flat   lf in B's tail (its points go to the ring's slot; the
+//               VoxelGrid is k_lf_voxel's)
 // col, picked and label are loaded once the sorts are done.
 // A sector holds n <= (H + 32) / 6 + 2 entries plus the fallback sort's
 // stack (kIntroStack words) behind it.
-// the VoxelGrid's keys (4 B), partners (2 B) and two segment lists
-__host__ __device__ inline size_t vg_extract_lists_off(size_t W) { return (6 * W + 3) & ~(size_t)3; }
-__host__ __device__ inline size_t vg_extract_bytes(size_t W) {
-  return vg_extract_lists_off(W) + 8 * (size_t)vg_list_cap((int)W);
-}
 __host__ __device__ inline int extract_sector_cap(int H) { return next_pow2((H + 32) / 6 + 2 + (kIntroStack + 1) / 2); }
 constexpr int kSortWaves = 3;  // waves sorting sectors at once (the scratch holds their sectors)
 struct ExtractLayout {
@@ -269,8 +261,6 @@ __host__ __device__ inline ExtractLayout extract_layout(int H) {
   if (sec > a) a = sec;
   e.lfOff = (5 * W + 1) & ~(size_t)1;          // over perm / gfl, dead once the walks are done
   e.B = (e.lfOff + 2 * W + 15) & ~(size_t)15;
-  const size_t vox = vg_extract_bytes(W);  // keys from A's start up to lf
-  if (vox > a + e.lfOff) a = vox - e.lfOff;
   e.A = (a + 15) & ~(size_t)15;
   return e;
 }
@@ -285,9 +275,6 @@ __device__ __forceinline__ ExtractLds carve(unsigned char* base, int H) {
   ExtractLds L;
   unsigned char* A = base;
   unsigned char* B = base + e.A;
-  L.vkey = (uint32_t*)A;
-  L.vpr = (uint16_t*)(A + 4 * W);
-  L.vlists = (uint32_t*)(A + vg_extract_lists_off(W));
   L.srt = (SmoothEntry*)A;
   L.orig = nullptr;
   L.picked = A + 1024 + W;  // [1024, 1024 + W): the initial picked copy of the speculative walks
@@ -815,126 +802,15 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
     if (tid == 0) L.misc[M_LF] = total;
     __syncthreads();
   }
-  if (tid == 0) L.misc[M_P0] = (R.Wn > 0 && L.picked[0]) ? 1 : 0;  // the carry's, before the keys overwrite picked
+  if (tid == 0) L.misc[M_P0] = (R.Wn > 0 && L.picked[0]) ? 1 : 0;  // the carry's
   stamp(2);  // picked-point copies + the ordered less-flat set
-  // ---- per-ring VoxelGrid 0.2 m on the less-flat set (:778-782)
+  // ---- the less-flat set's points, in order, to the ring's slot: the
+  // VoxelGrid (:778-782) runs in k_lf_voxel over every ring of the batch
   const int K = L.misc[M_LF];
-  const float inv = 1.0f / 0.2f;
-  float mn[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
-  float mx[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
-  // the less-flat points, gathered once: the thread's first kLfRegs in
-  // registers for the keys below, the rest (rings wider than
-  // kLfRegs * 256 points) gathered again there
-  constexpr int kLfRegs = 4;
-  float4 lp[kLfRegs];
-#pragma unroll
-  for (int i = 0; i < kLfRegs; ++i) {
-    const int t = tid + i * (int)blockDim.x;
-    lp[i] = t < K ? bb.dsk[R.base + R.lo + L.lf[t]] : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-#pragma unroll
-  for (int i = 0; i < kLfRegs; ++i) {
-    if (tid + i * (int)blockDim.x < K) {
-      const float4 p = lp[i];
-      mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
-      mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
-    }
-  }
-  for (int t = tid + kLfRegs * (int)blockDim.x; t < K; t += blockDim.x) {
-    const float4 p = bb.dsk[R.base + R.lo + L.lf[t]];
-    mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
-    mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
-  }
-  for (int q = 0; q < 3; ++q) {
-    for (int o = 32; o > 0; o >>= 1) {
-      mn[q] = fminf(mn[q], __shfl_xor(mn[q], o, 64));
-      mx[q] = fmaxf(mx[q], __shfl_xor(mx[q], o, 64));
-    }
-  }
-  if (lane == 0)
-    for (int q = 0; q < 3; ++q) { L.red[wave * 6 + q] = mn[q]; L.red[wave * 6 + 3 + q] = mx[q]; }
+  for (int t = tid; t < K; t += blockDim.x) olf[t] = bb.dsk[R.base + R.lo + L.lf[t]];
+  const int nlf = K;
   __syncthreads();
-  if (tid == 0 && K > 0) {
-    for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
-      for (int q = 0; q < 3; ++q) {
-        L.red[q] = fminf(L.red[q], L.red[w * 6 + q]);
-        L.red[3 + q] = fmaxf(L.red[3 + q], L.red[w * 6 + 3 + q]);
-      }
-    const long long dx = (long long)((L.red[3] - L.red[0]) * inv) + 1;
-    const long long dy = (long long)((L.red[4] - L.red[1]) * inv) + 1;
-    const long long dz = (long long)((L.red[5] - L.red[2]) * inv) + 1;
-    L.misc[M_OVF] = (dx * dy * dz > (long long)INT_MAX) ? 1 : 0;
-    int mb[3], xb[3];
-    for (int q = 0; q < 3; ++q) {
-      mb[q] = (int)floorf(L.red[q] * inv);
-      xb[q] = (int)floorf(L.red[3 + q] * inv);
-    }
-    L.misc[M_MB0] = mb[0]; L.misc[M_MB1] = mb[1]; L.misc[M_MB2] = mb[2];
-    L.misc[M_D0] = xb[0] - mb[0] + 1;
-    L.misc[M_D1] = xb[1] - mb[1] + 1;
-  }
-  __syncthreads();
-  int nlf = 0;
-  if (K > 0 && L.misc[M_OVF]) {
-    for (int t = tid; t < K; t += blockDim.x) olf[t] = bb.dsk[R.base + R.lo + L.lf[t]];
-    nlf = K;
-  } else if (K > 0) {
-    const int d0 = L.misc[M_D0], d1 = L.misc[M_D1];
-    const float fb0 = (float)L.misc[M_MB0], fb1 = (float)L.misc[M_MB1], fb2 = (float)L.misc[M_MB2];
-    for (int t = tid, i = 0; t < K; t += blockDim.x, ++i) {
-      float4 p;
-      if (i < kLfRegs) {  // a register, selected without a dynamic index
-#pragma unroll
-        for (int u = 0; u < kLfRegs; ++u)
-          if (u == i) p = lp[u];
-      } else {
-        p = bb.dsk[R.base + R.lo + L.lf[t]];
-      }
-      const int i0 = (int)(floorf(p.x * inv) - fb0);
-      const int i1 = (int)(floorf(p.y * inv) - fb1);
-      const int i2 = (int)(floorf(p.z * inv) - fb2);
-      L.vkey[t] = (uint32_t)(i0 + i1 * d0 + i2 * d0 * d1);
-    }
-    __syncthreads();
-    // PCL's std::sort of (idx, point) by idx: its unstable order of a voxel's
-    // points is the summation order (lego_vgsort.h); lf moves with the keys
-    vg_block_sort(L.vkey, L.lf, L.vpr, L.vlists, (int*)(L.red + 32), K);
-    int outc = 0;
-    for (int t0 = 0; t0 < K; t0 += blockDim.x) {
-      const int t = t0 + tid;
-      const bool head = t < K && (t == 0 || L.vkey[t] != L.vkey[t - 1]);
-      int tot;
-      const int r = block_rank(head, L.misc + M_WOFF, &tot);
-      if (head) {
-        const uint32_t key = L.vkey[t];
-        // the voxel's points in sorted order (PCL's accumulation order),
-        // four loads in flight per round instead of one per add
-        float cx = 0, cy = 0, cz = 0, ci = 0;
-        int u = t, n = 0;
-        bool more = true;
-        while (more) {
-          float4 q[4];
-          bool in[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            in[i] = u + i < K && L.vkey[u + i] == key;
-            if (in[i]) q[i] = bb.dsk[R.base + R.lo + L.lf[u + i]];
-          }
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (in[i]) { cx += q[i].x; cy += q[i].y; cz += q[i].z; ci += q[i].w; ++n; }
-          more = in[3];
-          u += 4;
-        }
-        const float cnt = (float)n;
-        olf[outc + r] = make_float4(cx / cnt, cy / cnt, cz / cnt, ci / cnt);
-      }
-      outc += tot;
-    }
-    nlf = outc;
-  }
-  __syncthreads();
-  stamp(3);  // the VoxelGrid (bounds, keys, sort, centroids)
+  stamp(3);  // the less-flat points to the ring's slot
   if (xp && tid == 0) {
     atomicAdd(xp + 4, 1ull);
     atomicAdd(xp + 8, ~0ull);  // leaves the in-flight count
@@ -958,7 +834,103 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
   __syncthreads();
 }
 
-__global__ void __launch_bounds__(kExtractThreads, 6) k_extract(BatchBufs bb, DevCfg c) {  // six waves per SIMD: six workgroups per CU
+// ---------------------------------------------------------------- less-flat VoxelGrid
+// pcl::VoxelGrid<PointType> downSizeFilter, leaf 0.2 (featureAssociation.cpp:
+// 778-782) on each ring's less-flat set, one (scan, ring) workgroup: the
+// points from the ring's slot into LDS, getMinMax3D, the voxel index per
+// point, PCL's std::sort of (idx, point) by idx (lego_vgsort.h: libstdc++'s
+// order of each voxel's points, which is the summation order), one lane per
+// voxel summing its points in that order, the centroids back to the slot.
+// The slot's count goes from the less-flat set's size to the voxels'.
+__host__ __device__ inline size_t lfvox_lds_bytes(int H) {
+  return (size_t)H * 16 + (((size_t)H * 6 + 15) & ~(size_t)15) + vg_sort_scratch_bytes(H, kExtractThreads) + 64;
+}
+__global__ void __launch_bounds__(kExtractThreads) k_lf_voxel(BatchBufs bb, DevCfg c) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  const int ring = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int H = c.H;
+  float4* pts = (float4*)lds_raw;
+  uint32_t* key = (uint32_t*)(lds_raw + (size_t)H * 16);
+  uint16_t* val = (uint16_t*)(lds_raw + (size_t)H * 20);
+  unsigned char* sc = lds_raw + (size_t)H * 16 + (((size_t)H * 6 + 15) & ~(size_t)15);
+  int* misc = (int*)(sc + vg_sort_scratch_bytes(H, kExtractThreads));  // [16]
+  float* red = (float*)(misc + 8);                                      // not overlapping misc[0..7]
+  __shared__ float mm[4][6];
+  int* cnt = bb.r_cnt + ((size_t)b * c.N + ring) * 4;
+  float4* slot = bb.r_lflat + (size_t)b * c.P + (size_t)ring * H;
+  const int K = cnt[3];
+  (void)red;
+  if (K <= 0) return;
+  const float inv = 1.0f / 0.2f;
+  float mn[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
+  float mx[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+  for (int t = tid; t < K; t += blockDim.x) {
+    const float4 p = slot[t];
+    pts[t] = p;
+    mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+    mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+  }
+  for (int q = 0; q < 3; ++q) {
+    for (int o = 32; o > 0; o >>= 1) {
+      mn[q] = fminf(mn[q], __shfl_xor(mn[q], o, 64));
+      mx[q] = fmaxf(mx[q], __shfl_xor(mx[q], o, 64));
+    }
+  }
+  if (lane == 0)
+    for (int q = 0; q < 3; ++q) { mm[wave][q] = mn[q]; mm[wave][3 + q] = mx[q]; }
+  __syncthreads();
+  float lo[3], hi[3];
+  for (int q = 0; q < 3; ++q) {
+    lo[q] = mm[0][q];
+    hi[q] = mm[0][3 + q];
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) { lo[q] = fminf(lo[q], mm[w][q]); hi[q] = fmaxf(hi[q], mm[w][3 + q]); }
+  }
+  const long long dx = (long long)((hi[0] - lo[0]) * inv) + 1;
+  const long long dy = (long long)((hi[1] - lo[1]) * inv) + 1;
+  const long long dz = (long long)((hi[2] - lo[2]) * inv) + 1;
+  if (dx * dy * dz > (long long)INT_MAX) return;  // PCL keeps the cloud (it is in the slot already)
+  int mb[3], xb[3];
+  for (int q = 0; q < 3; ++q) {
+    mb[q] = (int)floorf(lo[q] * inv);
+    xb[q] = (int)floorf(hi[q] * inv);
+  }
+  const int d0 = xb[0] - mb[0] + 1, d1 = xb[1] - mb[1] + 1;
+  for (int t = tid; t < K; t += blockDim.x) {
+    const float4 p = pts[t];
+    const int i0 = (int)(floorf(p.x * inv) - (float)mb[0]);
+    const int i1 = (int)(floorf(p.y * inv) - (float)mb[1]);
+    const int i2 = (int)(floorf(p.z * inv) - (float)mb[2]);
+    key[t] = (uint32_t)(i0 + i1 * d0 + i2 * d0 * d1);
+    val[t] = (uint16_t)t;
+  }
+  __syncthreads();
+  vg_block_sort(vg_sort_carve(key, val, sc, K, (int)blockDim.x), K);
+  int outc = 0;
+  for (int t0 = 0; t0 < K; t0 += blockDim.x) {
+    const int t = t0 + tid;
+    const bool head = t < K && (t == 0 || key[t] != key[t - 1]);
+    int tot;
+    const int r = block_rank(head, misc, &tot);
+    if (head) {
+      const uint32_t k = key[t];
+      float cx = 0, cy = 0, cz = 0, ci = 0;
+      int u = t;
+      for (; u < K && key[u] == k; ++u) {
+        const float4 q = pts[val[u]];
+        cx += q.x; cy += q.y; cz += q.z; ci += q.w;
+      }
+      const float n = (float)(u - t);
+      slot[outc + r] = make_float4(cx / n, cy / n, cz / n, ci / n);
+    }
+    outc += tot;
+  }
+  if (tid == 0) cnt[3] = outc;
+}
+
+#ifndef EXTRACT_MINWAVES
+#define EXTRACT_MINWAVES 6
+#endif
+__global__ void __launch_bounds__(kExtractThreads, EXTRACT_MINWAVES) k_extract(BatchBufs bb, DevCfg c) {  // six waves per SIMD: six workgroups per CU
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   const ExtractLds L = carve(lds_raw, c.H);
   const int ring = blockIdx.x, b = blockIdx.y;
@@ -1069,6 +1041,8 @@ void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_ca
   k_extract<<<dim3(c.N, B), kExtractThreads, lds, s>>>(bb, c);
   tm->mark("fa.fixup", s);
   k_fa_fixup<<<S, kExtractThreads, lds, s>>>(bb, c, B / S, d_carry);
+  tm->mark("fa.voxel", s);
+  k_lf_voxel<<<dim3(c.N, B), kExtractThreads, lfvox_lds_bytes(c.H), s>>>(bb, c);
   tm->mark("fa.compact", s);
   k_fa_compact<<<dim3(c.N, B), 256, 0, s>>>(bb, c);
 }

@@ -152,6 +152,11 @@ struct LcDev {
 int vg_scratch_alloc(VgScratch& v, int cap, void* ctx, int (*alloc)(void* ctx, void** p, size_t bytes));
 int voxel_grid_device(const float4* in, int n, const int* nDev, float leaf, float4* out, int* nOut,
                       const VgScratch& v, hipStream_t s);
+// partition rounds voxel_grid_device launches for a cloud of n points
+// (LEGO_VG_ROUNDS overrides: diagnostic)
+int vg_rounds_for(int n);
+// the VgScratch counters of the last voxel_grid_device on s (16 ints, synchronous)
+int vg_read_ctl(const VgScratch& v, int* ctl16, hipStream_t s);
 int mo_set_map_device(MoDev& m, int nCornerMap, int nSurfMap, hipStream_t s);
 int index_build_device(const float4* pts, int n, const int* nDev, MoIndex& ix, const VgScratch& v, hipStream_t s);
 // One performLoopClosure over the keyframe store (tnow = timeLaserOdometry).

@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <climits>
+#include <cstdlib>
 
 #include "lego_device.h"
 #include "lego_kernels.h"
@@ -36,7 +37,7 @@ namespace lego {
 constexpr unsigned kInvalidKey = 0xffffffffu;
 constexpr int kScanThreads = 256, kScanPer = 16, kScanTile = kScanThreads * kScanPer;
 constexpr int kVgTileThreads = 256, kVgTilePer = 16, kVgTile = kVgTileThreads * kVgTilePer;
-constexpr int kVgLocal = 8192, kVgLocalThreads = 512;
+constexpr int kVgLocal = 4096, kVgLocalThreads = 512;  // vg_sort_max(512) = 4096
 constexpr int kVgRoundsMax = 16;
 constexpr int kVgPlanThreads = 1024;
 
@@ -250,7 +251,7 @@ __device__ void vg_plan_big(const VgScratch& v, const int2* big, int nb, int* tm
 
 // Removes non-finite points (stable), then the first level: the whole array as
 // one big segment (partitioned by the rounds) or one local segment.
-__global__ void __launch_bounds__(kVgPlanThreads) k_vg_plan0(int n, const int* nDev, VgScratch v) {
+__global__ void __launch_bounds__(kVgPlanThreads) k_vg_plan0(int n, const int* nDev, VgScratch v, int rounds) {
   __shared__ int tmp[20];
   const int nn = nDev ? min(n, *nDev) : n;
   int m = nn;
@@ -279,7 +280,7 @@ __global__ void __launch_bounds__(kVgPlanThreads) k_vg_plan0(int n, const int* n
     if (threadIdx.x == 0) { v.ctl[C_NB] = 0; v.ctl[C_NT] = 0; v.tileOff[0] = 0; }
     return;
   }
-  if (m <= kVgLocal) {
+  if (m <= kVgLocal || rounds == 0) {  // one workgroup (above kVgLocal: its global-memory partition)
     if (threadIdx.x == 0) {
       v.loc[0] = make_int4(0, m, 2 * lg2i(m), 0);
       v.ctl[C_NLOC] = 1;
@@ -511,32 +512,27 @@ __device__ int vg_block_partition_global(const VgScratch& v, int s, int e, int* 
   return cut;
 }
 
-struct VgLocalLds {
-  uint32_t* key;
-  uint16_t* lv;  // the element's position in the segment before the sort
-  uint16_t* pr;
-  uint32_t* lists;
-  int* ctl;
-};
 __host__ __device__ inline size_t vg_local_lds_bytes() {
-  return (size_t)kVgLocal * 8 + 8 * (size_t)vg_list_cap(kVgLocal) + 64;
+  return (size_t)kVgLocal * 6 + vg_sort_scratch_bytes(kVgLocal, kVgLocalThreads);
 }
 
 // [s, s + m), m <= kVgLocal, through LDS: keys and local positions sorted,
-// then the keys and the gathered point indices written back.
-__device__ void vg_local_sort(const VgScratch& v, const VgLocalLds& L, int s, int m, int depth) {
+// then the keys and the gathered point indices written back.  lv: the
+// element's position in the segment before the sort.
+__device__ void vg_local_sort(const VgScratch& v, uint32_t* key, uint16_t* lv, unsigned char* sc, int s, int m,
+                              int depth) {
   for (int i = threadIdx.x; i < m; i += blockDim.x) {
-    L.key[i] = v.keys[s + i];
-    L.lv[i] = (uint16_t)i;
+    key[i] = v.keys[s + i];
+    lv[i] = (uint16_t)i;
   }
   __syncthreads();
-  vg_block_sort(L.key, L.lv, L.pr, L.lists, L.ctl, m, depth);
+  vg_block_sort(vg_sort_carve(key, lv, sc, m, (int)blockDim.x), m, depth, v.ctl + C_HEAP);
   for (int i = threadIdx.x; i < m; i += blockDim.x) {
-    v.keys[s + i] = L.key[i];
-    L.key[i] = (uint32_t)v.vals[s + L.lv[i]];
+    v.keys[s + i] = key[i];
+    key[i] = (uint32_t)v.vals[s + lv[i]];
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < m; i += blockDim.x) v.vals[s + i] = (int)L.key[i];
+  for (int i = threadIdx.x; i < m; i += blockDim.x) v.vals[s + i] = (int)key[i];
   __threadfence_block();
   __syncthreads();
 }
@@ -550,17 +546,14 @@ __global__ void __launch_bounds__(kVgLocalThreads) k_vg_local(VgScratch v) {
   __shared__ int rows[32];
   __shared__ int4 stk[64];
   __shared__ int sp;
-  VgLocalLds L;
-  L.key = (uint32_t*)lds_raw;
-  L.lv = (uint16_t*)(lds_raw + (size_t)kVgLocal * 4);
-  L.pr = (uint16_t*)(lds_raw + (size_t)kVgLocal * 6);
-  L.lists = (uint32_t*)(lds_raw + (size_t)kVgLocal * 8);
-  L.ctl = (int*)(lds_raw + (size_t)kVgLocal * 8 + 8 * (size_t)vg_list_cap(kVgLocal));
+  uint32_t* key = (uint32_t*)lds_raw;
+  uint16_t* lv = (uint16_t*)(lds_raw + (size_t)kVgLocal * 4);
+  unsigned char* sc = lds_raw + (size_t)kVgLocal * 6;
   const int nloc = v.ctl[C_NLOC];
   for (int t = blockIdx.x; t < nloc; t += gridDim.x) {
     const int4 g = v.loc[t];
     if (g.y - g.x <= kVgLocal) {
-      vg_local_sort(v, L, g.x, g.y - g.x, g.z);
+      vg_local_sort(v, key, lv, sc, g.x, g.y - g.x, g.z);
       continue;
     }
     if (threadIdx.x == 0) { stk[0] = g; sp = 1; atomicAdd(&v.ctl[C_SLOW], 1); }
@@ -571,7 +564,7 @@ __global__ void __launch_bounds__(kVgLocalThreads) k_vg_local(VgScratch v) {
       if (threadIdx.x == 0) --sp;
       const int m = c.y - c.x;
       if (m <= kVgLocal) {
-        vg_local_sort(v, L, c.x, m, c.z);
+        vg_local_sort(v, key, lv, sc, c.x, m, c.z);
       } else if (c.z == 0) {  // depth budget spent: std::__partial_sort
         if (threadIdx.x == 0) { VgHeap<int>{v.keys, v.vals}.sort(c.x, c.y); atomicAdd(&v.ctl[C_HEAP], 1); }
         __threadfence_block();
@@ -588,25 +581,29 @@ __global__ void __launch_bounds__(kVgLocalThreads) k_vg_local(VgScratch v) {
   }
 }
 
-__global__ void __launch_bounds__(kScanThreads) k_vg_head_tiles(VgScratch v) {
-  __shared__ int tmp[20];
+// voxel heads per tile of kHeadTile sorted positions (one position per thread)
+constexpr int kHeadTile = 256;
+__device__ __forceinline__ bool vg_head(const VgScratch& v, int t, int m) {
+  return t < m && (t == 0 || v.keys[t] != v.keys[t - 1]);
+}
+__global__ void __launch_bounds__(kHeadTile) k_vg_head_tiles(VgScratch v) {
   const int m = v.ctl[C_M];
-  const int base = blockIdx.x * kScanTile + threadIdx.x * kScanPer;
-  int h = 0;
-#pragma unroll
-  for (int j = 0; j < kScanPer; ++j) {
-    const int t = base + j;
-    h += (t < m && (t == 0 || v.keys[t] != v.keys[t - 1])) ? 1 : 0;
+  const int t = blockIdx.x * kHeadTile + threadIdx.x;
+  const unsigned long long b = __ballot(vg_head(v, t, m));
+  __shared__ int w[kHeadTile / 64];
+  if ((threadIdx.x & 63) == 0) w[threadIdx.x >> 6] = (int)__popcll(b);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int a = 0;
+    for (int i = 0; i < kHeadTile / 64; ++i) a += w[i];
+    v.scanTiles[blockIdx.x] = a;
   }
-  const int tot = block_sum(h, tmp);
-  if (threadIdx.x == 0) v.scanTiles[blockIdx.x] = tot;
 }
 
 // One lane per voxel: the centroid of its points summed in sorted order
 // (PCL's), written at the voxel's rank.  Overflow: copy.
-__global__ void __launch_bounds__(kScanThreads) k_vg_emit(const float4* in, int n, const int* nDev, VgScratch v,
-                                                          float4* out, int* nOut) {
-  __shared__ int tmp[20];
+__global__ void __launch_bounds__(kHeadTile) k_vg_emit(const float4* in, int n, const int* nDev, VgScratch v,
+                                                       float4* out, int* nOut) {
   const int nn = nDev ? min(n, *nDev) : n;
   if (*v.overflow) {
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nn; i += gridDim.x * blockDim.x) out[i] = in[i];
@@ -615,34 +612,30 @@ __global__ void __launch_bounds__(kScanThreads) k_vg_emit(const float4* in, int 
   }
   const int m = v.ctl[C_M];
   if (blockIdx.x == 0 && threadIdx.x == 0) *nOut = v.ctl[C_NOUT];
-  const int base = blockIdx.x * kScanTile + threadIdx.x * kScanPer;
-  unsigned hm = 0;
-  int h = 0;
-#pragma unroll
-  for (int j = 0; j < kScanPer; ++j) {
-    const int t = base + j;
-    const bool hd = t < m && (t == 0 || v.keys[t] != v.keys[t - 1]);
-    hm |= (hd ? 1u : 0u) << j;
-    h += hd;
+  const int t = blockIdx.x * kHeadTile + threadIdx.x;
+  const bool hd = vg_head(v, t, m);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const unsigned long long b = __ballot(hd);
+  __shared__ int w[kHeadTile / 64];
+  if (lane == 0) w[wave] = (int)__popcll(b);
+  __syncthreads();
+  if (!hd) return;
+  int r = v.scanTiles[blockIdx.x] + (int)__popcll(b & ((1ull << lane) - 1));
+  for (int i = 0; i < wave; ++i) r += w[i];
+  const unsigned k = v.keys[t];
+  float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
+  int u = t;
+  for (; u < m && v.keys[u] == k; ++u) {
+    const float4 p = in[v.vals[u]];
+    c0 += p.x; c1 += p.y; c2 += p.z; c3 += p.w;
   }
-  int tot;
-  int r = v.scanTiles[blockIdx.x] + block_excl_scan(h, tmp, &tot);
-  for (int j = 0; j < kScanPer; ++j) {
-    if (!((hm >> j) & 1u)) continue;
-    const int t = base + j;
-    const unsigned k = v.keys[t];
-    float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
-    int u = t;
-    for (; u < m && v.keys[u] == k; ++u) {
-      const float4 p = in[v.vals[u]];
-      c0 += p.x; c1 += p.y; c2 += p.z; c3 += p.w;
-    }
-    const float cnt = (float)(u - t);
-    out[r++] = make_float4(c0 / cnt, c1 / cnt, c2 / cnt, c3 / cnt);
-  }
+  const float cnt = (float)(u - t);
+  out[r] = make_float4(c0 / cnt, c1 / cnt, c2 / cnt, c3 / cnt);
 }
 
 int vg_rounds_for(int n) {
+  static const int forced = std::getenv("LEGO_VG_ROUNDS") ? std::atoi(std::getenv("LEGO_VG_ROUNDS")) : -1;
+  if (forced >= 0) return std::min(forced, kVgRoundsMax);
   if (n <= kVgLocal) return 0;
   int r = 1;
   while (((long long)kVgLocal << r) < n) ++r;
@@ -661,8 +654,8 @@ int voxel_grid_device(const float4* in, int n, const int* nDev, float leaf, floa
   k_vg_init<<<1, 64, 0, s>>>(v);
   k_vg_minmax<<<std::min(grid_for(n), 512), 256, 0, s>>>(in, n, nDev, v);
   k_vg_keys<<<grid_for(n), 256, 0, s>>>(in, n, nDev, leaf, v);
-  k_vg_plan0<<<1, kVgPlanThreads, 0, s>>>(n, nDev, v);
   const int R = vg_rounds_for(n);
+  k_vg_plan0<<<1, kVgPlanThreads, 0, s>>>(n, nDev, v, R);
   const int gt = tiles_for(n, kVgTile) + v.capBig;  // >= the tiles of any round
   for (int r = 0; r < R; ++r) {
     k_vg_count<<<gt, kVgTileThreads, 0, s>>>(v, r);
@@ -672,11 +665,16 @@ int voxel_grid_device(const float4* in, int n, const int* nDev, float leaf, floa
   }
   const int gl = n <= kVgLocal ? 1 : std::min(v.capLoc, 1024);
   k_vg_local<<<gl, kVgLocalThreads, vg_local_lds_bytes(), s>>>(v);
-  const int ht = tiles_for(n, kScanTile);
-  k_vg_head_tiles<<<ht, kScanThreads, 0, s>>>(v);
+  const int ht = tiles_for(n, kHeadTile);
+  k_vg_head_tiles<<<ht, kHeadTile, 0, s>>>(v);
   k_scan_top<<<1, 1024, 0, s>>>(v.scanTiles, ht, nullptr, v.ctl + C_NOUT);
-  k_vg_emit<<<ht, kScanThreads, 0, s>>>(in, n, nDev, v, out, nOut);
+  k_vg_emit<<<ht, kHeadTile, 0, s>>>(in, n, nDev, v, out, nOut);
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int vg_read_ctl(const VgScratch& v, int* ctl16, hipStream_t s) {
+  if (hipMemcpyAsync(ctl16, v.ctl, sizeof(int) * 16, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
+  return hipStreamSynchronize(s) == hipSuccess ? 0 : -1;
 }
 
 int vg_scratch_alloc(VgScratch& v, int cap, void* ctx, int (*alloc)(void* ctx, void** p, size_t bytes)) {
@@ -684,7 +682,7 @@ int vg_scratch_alloc(VgScratch& v, int cap, void* ctx, int (*alloc)(void* ctx, v
   v.capBig = cap / kVgLocal + 2;
   v.capTiles = tiles_for(cap, kVgTile) + v.capBig + 1;
   v.capLoc = 2 * (kVgRoundsMax + 1) * v.capBig + 4;
-  v.capScanTiles = tiles_for(2 * cap + 64, kScanTile) + 1;
+  v.capScanTiles = std::max(tiles_for(2 * cap + 64, kScanTile), tiles_for(cap, kHeadTile)) + 1;
   struct A { void** p; size_t b; } as[] = {
       {(void**)&v.keys, sizeof(unsigned) * (size_t)cap}, {(void**)&v.vals, sizeof(int) * (size_t)cap},
       {(void**)&v.pl, sizeof(int) * (size_t)cap},        {(void**)&v.pr, sizeof(int) * (size_t)cap},

@@ -129,126 +129,393 @@ struct VgHeap {
   }
 };
 
-// One wave partitions [s, e) (e - s > 16) as std::__unguarded_partition_pivot
-// and returns the cut.  pr[s .. e) is the wave's scratch for the partners.
-template <typename V, typename P>
-__device__ __forceinline__ int vg_wave_partition(uint32_t* key, V* val, P* pr, int s, int e) {
-  const int lane = threadIdx.x & 63;
-  if (lane == 0) vg_median_to_first(key, val, s, s + 1, s + (e - s) / 2, e - 1);
-  vg_wave_sync();
-  const uint32_t p = key[s];
-  const int b = s + 1;
-  const int nch = (e - b + 63) >> 6;
-  int totL = 0;
-  for (int k = 0; k < nch; ++k) {
-    const int i = b + (k << 6) + lane;
-    totL += (int)__popcll(__ballot(i < e && !(key[i] < p)));
-  }
-  const unsigned long long above = lane == 63 ? 0ull : (~0ull << (lane + 1));
-  int cLa = 0, cR = 0, cut = e;
-  for (int k = nch - 1; k >= 0; --k) {
-    const int c0 = b + (k << 6);
-    const int i = c0 + lane;
-    const bool in = i < e;
-    const uint32_t kv = in ? key[i] : 0u;
-    const bool lf = in && !(kv < p), rf = in && !(p < kv);
-    const unsigned long long ml = __ballot(lf), mr = __ballot(rf);
-    const int Lab = cLa + (int)__popcll(ml & above);  // left stops after i
-    const int Rab = cR + (int)__popcll(mr & above);   // right stops after i
-    // right stop of rank Rab + 1 (from the right): swapped iff at least that
-    // many left stops precede it; left stop of rank totL - Lab: swapped iff at
-    // least that many right stops follow it
-    const bool rsw = rf && totL - Lab - (lf ? 1 : 0) >= Rab + 1;
-    const bool lsw = lf && Rab >= totL - Lab;
-    if (rsw) pr[s + Rab] = (P)i;
-    const unsigned long long mc = __ballot((lf && !lsw) || rsw);
-    if (mc) cut = c0 + (int)__ffsll((long long)mc) - 1;
-    vg_wave_sync();
-    if (lsw) {
-      const int j = (int)pr[s + (totL - Lab) - 1];
-      const V vv = val[i];
-      key[i] = key[j]; val[i] = val[j];
-      key[j] = kv; val[j] = vv;
-    }
-    cR += (int)__popcll(mr);
-    cLa += (int)__popcll(ml);
-  }
-  vg_wave_sync();
-  return cut;
-}
-
-// Stable sort of up to two blocks of <= 16 (lanes 0-15: [s0, s0 + m0), lanes
-// 16-31: [s1, s1 + m1); m = 0 for none), i.e. the final insertion sort's
-// effect on them.
-template <typename V>
-__device__ __forceinline__ void vg_wave_leaf_sort(uint32_t* key, V* val, int s0, int m0, int s1, int m1) {
-  const int lane = threadIdx.x & 63;
-  const int g = lane >> 4, l = lane & 15;
-  const int s = g == 0 ? s0 : s1, m = g == 0 ? m0 : (g == 1 ? m1 : 0);
-  const bool act = l < m;
-  const uint32_t kv = act ? key[s + l] : 0u;
-  const V vv = act ? val[s + l] : (V)0;
-  int rank = 0;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const uint32_t kj = __shfl(kv, (lane & ~15) + j, 64);
-    if (j < m) rank += (kj < kv || (kj == kv && j < l)) ? 1 : 0;
-  }
-  vg_wave_sync();
-  if (act && m > 1) {
-    key[s + rank] = kv;
-    val[s + rank] = vv;
-  }
-  vg_wave_sync();
-}
-
 constexpr int kVgLeaf = 16;  // _S_threshold
 
-__host__ __device__ inline int vg_list_cap(int n) { return n / (kVgLeaf + 1) + 1; }
+// One segment of the current level: [s, e); A / B = left / right stops up to
+// and including e - 1 (block-wide inclusive counts); ck = the left stops up
+// to s (low half) | the swaps (high half: atomicMax of the swapped left
+// stops' ranks), then the children's first table slot | which children are
+// segments of the next level (bits 16, 17); cut (atomicMin).  16 B: two
+// 8-byte loads.
+struct alignas(16) VgSeg {
+  uint16_t s, e, A, B;
+  uint32_t ck, cut;
+};
 
-// std::sort of key[0, n) / val[0, n) by key, all threads of the block; depth:
-// the introsort loop's budget (2 lg n for a whole array, less for a segment
-// of one; -1 = 2 lg n).  pr: n entries of scratch; lists: 2 * vg_list_cap(n)
-// words; ctl: 3 ints.  n < 65536.  Ends with a block barrier.
-template <typename V, typename P>
-__device__ void vg_block_sort(uint32_t* key, V* val, P* pr, uint32_t* lists, int* ctl, int n, int depth = -1) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
-  if (n <= kVgLeaf) {
-    if (wave == 0 && n > 1) vg_wave_leaf_sort(key, val, 0, n, 0, 0);
+__host__ __device__ inline int vg_list_cap(int n) { return n / (kVgLeaf + 1) + 1; }
+constexpr int kVgRowsMax = 8;  // rows of 64 positions per wave
+// the largest sort a block of T threads handles
+__host__ __device__ inline int vg_sort_max(int T) { return (T / 64) * 64 * kVgRowsMax; }
+
+// The LDS a block sort of up to n keys uses besides key / val: segment id and
+// partner per position, two segment tables, the leaf-start bits, counters.
+template <typename V>
+struct VgSortLds {
+  uint32_t* key;   // [n]
+  V* val;          // [n]
+  uint16_t* sid;   // [n] the position's segment at this level, 0xffff in a leaf
+  uint16_t* pr;    // [n] partners: right stops from a segment's start, left stops from its middle
+  VgSeg* tab;      // [2 * vg_list_cap(n)]
+  uint32_t* head;  // [(n + 31) / 32 + 1] leaf starts
+  int* ctl;        // [2 + 2 * 16] segments of the current / next level, the waves' stop counts
+};
+__host__ __device__ inline size_t vg_sort_scratch_bytes(int n, int T) {
+  (void)T;
+  const size_t a = (4 * (size_t)n + 15) & ~(size_t)15;                    // sid, pr
+  const size_t b = 2 * (size_t)vg_list_cap(n) * sizeof(VgSeg);            // tab
+  const size_t c = (4 * (size_t)((n + 31) / 32 + 1) + 15) & ~(size_t)15;  // head
+  return a + b + c + 4 * (2 + 2 * 16);
+}
+// carves the scratch (16-B aligned base) for a sort of up to n keys
+template <typename V>
+__device__ __forceinline__ VgSortLds<V> vg_sort_carve(uint32_t* key, V* val, unsigned char* base, int n, int T) {
+  (void)T;
+  VgSortLds<V> S;
+  S.key = key;
+  S.val = val;
+  S.sid = (uint16_t*)base;
+  S.pr = S.sid + n;
+  unsigned char* p = base + ((4 * (size_t)n + 15) & ~(size_t)15);
+  S.tab = (VgSeg*)p;
+  p += 2 * (size_t)vg_list_cap(n) * sizeof(VgSeg);
+  S.head = (uint32_t*)p;
+  p += (4 * (size_t)((n + 31) / 32 + 1) + 15) & ~(size_t)15;
+  S.ctl = (int*)p;
+  return S;
+}
+
+#ifndef VG_STAMP
+#define VG_STAMP(k)
+#endif
+
+// std::sort of key[0, n) / val[0, n) by key, all threads of the block.
+// depth: the introsort loop's budget (2 lg n for a whole array, less for a
+// segment of one; -1 = 2 lg n).  n <= vg_sort_max(blockDim.x), blockDim.x <=
+// 1024; S carved for at least n.  heapStat: a counter bumped per heap-sorted
+// piece, or null.  Ends with a block barrier.
+//
+// Level by level, every segment (> 16 keys) of the level at once.  Wave w
+// owns the positions [w * P, (w + 1) * P) (P a multiple of 64, <= 8 rows of
+// 64), so its running stop counts are wave-uniform; each pass gathers its
+// rows' operands together (a few LDS round trips per pass, not per row) and
+// skips rows with no position in a segment.  Passes: the median of three, one
+// thread per segment; the stop flags and each wave's totals; the block-wide
+// counts at each segment's ends; each stop's ranks from them and its own
+// counts, the swapped right stops scattered by rank to the head of the
+// segment's partner scratch and the swapped left stops to its middle, the
+// cut's candidates and the swap count (one LDS atomic per segment run of a
+// row); the pairs swapped; the children (> 16 keys) numbered; the positions'
+// new segments.  Pieces of <= 16 keys become leaves; at the end every
+// position ranks itself within its leaf (stably: the final insertion sort's
+// effect) and moves there.
+template <typename V>
+__device__ void vg_block_sort(const VgSortLds<V>& S, int n, int depth = -1, int* heapStat = nullptr) {
+  constexpr int RM = kVgRowsMax;
+  const int tid = threadIdx.x, T = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = T >> 6;
+  const int cap = vg_list_cap(n);
+  const int D = depth >= 0 ? depth : (n > 1 ? 2 * (31 - __builtin_clz((unsigned)n)) : 0);
+  const int P = (((n + nw - 1) / nw) + 63) & ~63;  // positions per wave
+  const int w0 = wave * P;
+  const unsigned long long below = (1ull << lane) - 1;
+  int* wt = S.ctl + 2;  // [nw][2] the waves' stop totals
+  if (n <= 1) {
     __syncthreads();
     return;
   }
-  const int cap = vg_list_cap(n);
-  const int D = depth >= 0 ? depth : 2 * (31 - __builtin_clz((unsigned)n));
+  for (int i = tid; i < n; i += T) S.sid[i] = n > kVgLeaf ? 0 : 0xffff;
+  for (int w = tid; w < (n + 31) / 32 + 1; w += T) S.head[w] = (w == 0 && n <= kVgLeaf) ? 1u : 0u;
   if (tid == 0) {
-    lists[0] = (uint32_t)n << 16;  // [0, n)
-    ctl[0] = 1; ctl[1] = 0; ctl[2] = 0;
+    S.ctl[0] = n > kVgLeaf ? 1 : 0;
+    S.tab[0] = VgSeg{0, (uint16_t)n, 0, 0, 0u, (uint32_t)n};
   }
+  uint32_t rowact = 0;  // rows of this wave holding positions of a segment (wave-uniform)
+  if (n > kVgLeaf)
+#pragma unroll
+    for (int j = 0; j < RM; ++j)
+      if (w0 + (j << 6) < n && (j << 6) < P) rowact |= 1u << j;
   __syncthreads();
+  constexpr int BR = 4;  // rows whose operands are gathered together (registers)
   for (int r = 0;; ++r) {
-    const int ncur = ctl[r % 3];
-    if (ncur == 0) break;
-    const uint32_t* cur = lists + (r & 1) * cap;
-    uint32_t* nxt = lists + ((r + 1) & 1) * cap;
-    if (tid == 0) ctl[(r + 2) % 3] = 0;  // read in round r - 1 (before its barrier), appended in round r + 1
-    for (int t = wave; t < ncur; t += nw) {
-      const uint32_t sg = cur[t];
-      const int s = (int)(sg & 0xffffu), e = (int)(sg >> 16);
-      if (D - r == 0) {  // depth budget spent: __partial_sort
-        if (lane == 0) VgHeap<V>{key, val}.sort(s, e);
-        vg_wave_sync();
-        continue;
+    const int nseg = S.ctl[r & 1];
+    if (nseg == 0) break;
+    VgSeg* cur = S.tab + (r & 1) * cap;
+    VgSeg* nxt = S.tab + ((r + 1) & 1) * cap;
+    if (D - r == 0) {  // depth budget spent: std::__partial_sort of every piece
+      for (int j = tid; j < nseg; j += T) {
+        const int s = cur[j].s, e = cur[j].e;
+        VgHeap<V>{S.key, S.val}.sort(s, e);
+        for (int q = s; q < e; ++q) atomicOr(&S.head[q >> 5], 1u << (q & 31));
+        if (heapStat) atomicAdd(heapStat, 1);
       }
-      const int cut = vg_wave_partition(key, val, pr, s, e);
-      const int m0 = cut - s, m1 = e - cut;
-      if (lane == 0) {
-        if (m0 > kVgLeaf) nxt[atomicAdd(&ctl[(r + 1) % 3], 1)] = (uint32_t)s | ((uint32_t)cut << 16);
-        if (m1 > kVgLeaf) nxt[atomicAdd(&ctl[(r + 1) % 3], 1)] = (uint32_t)cut | ((uint32_t)e << 16);
+      __syncthreads();
+      break;
+    }
+    for (int j = tid; j < nseg; j += T) {
+      const int s = cur[j].s, e = cur[j].e;
+      vg_median_to_first(S.key, S.val, s, s + 1, s + (e - s) / 2, e - 1);
+      cur[j].cut = (uint32_t)e;
+      cur[j].ck = 0u;
+    }
+    if (tid == 0) S.ctl[(r + 1) & 1] = 0;  // last read at round r - 1's top
+    __syncthreads();
+    VG_STAMP(0);
+    // stop flags (a bit per row) and the wave's totals
+    uint32_t fl = 0, fr = 0;
+    int totLw = 0, totRw = 0;
+    for (int j0 = 0; j0 < RM; j0 += BR) {
+      if (!((rowact >> j0) & ((1u << BR) - 1))) continue;
+      int id[BR], ss[BR];
+      uint32_t kp[BR], ki[BR];
+#pragma unroll
+      for (int u = 0; u < BR; ++u) {
+        const int i = w0 + ((j0 + u) << 6) + lane;
+        id[u] = ((rowact >> (j0 + u)) & 1u) && i < n ? (int)S.sid[i] : 0xffff;
       }
-      vg_wave_leaf_sort(key, val, s, m0 > kVgLeaf ? 0 : m0, cut, m1 > kVgLeaf ? 0 : m1);
+#pragma unroll
+      for (int u = 0; u < BR; ++u) ss[u] = id[u] != 0xffff ? (int)cur[id[u]].s : 0;
+#pragma unroll
+      for (int u = 0; u < BR; ++u) {
+        const int i = w0 + ((j0 + u) << 6) + lane;
+        const bool in = id[u] != 0xffff && i > ss[u];
+        kp[u] = in ? S.key[ss[u]] : 0u;
+        ki[u] = in ? S.key[i] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < BR; ++u) {
+        const int i = w0 + ((j0 + u) << 6) + lane;
+        const bool in = id[u] != 0xffff && i > ss[u];
+        const bool lf = in && !(ki[u] < kp[u]), rf = in && !(kp[u] < ki[u]);
+        fl |= (lf ? 1u : 0u) << (j0 + u);
+        fr |= (rf ? 1u : 0u) << (j0 + u);
+        totLw += (int)__popcll(__ballot(lf));
+        totRw += (int)__popcll(__ballot(rf));
+      }
+    }
+    if (lane == 0) { wt[2 * wave] = totLw; wt[2 * wave + 1] = totRw; }
+    __syncthreads();
+    VG_STAMP(1);
+    int baseL = 0, baseR = 0;
+    for (int w = 0; w < wave; ++w) { baseL += wt[2 * w]; baseR += wt[2 * w + 1]; }
+    {  // the block-wide inclusive counts at every segment's start and last position
+      int aL = baseL, aR = baseR;
+      for (int j0 = 0; j0 < RM; j0 += BR) {
+        int id[BR], ss[BR], ee[BR], SL[BR], SR[BR];
+#pragma unroll
+        for (int u = 0; u < BR; ++u) {
+          const int j = j0 + u;
+          const bool lf = (fl >> j) & 1u, rf = (fr >> j) & 1u;
+          const unsigned long long ml = __ballot(lf), mr = __ballot(rf);
+          SL[u] = aL + (int)__popcll(ml & below) + (lf ? 1 : 0);
+          SR[u] = aR + (int)__popcll(mr & below) + (rf ? 1 : 0);
+          aL += (int)__popcll(ml);
+          aR += (int)__popcll(mr);
+        }
+        if (!((rowact >> j0) & ((1u << BR) - 1))) continue;
+#pragma unroll
+        for (int u = 0; u < BR; ++u) {
+          const int i = w0 + ((j0 + u) << 6) + lane;
+          id[u] = ((rowact >> (j0 + u)) & 1u) && i < n ? (int)S.sid[i] : 0xffff;
+        }
+#pragma unroll
+        for (int u = 0; u < BR; ++u) {
+          ss[u] = id[u] != 0xffff ? (int)cur[id[u]].s : -1;
+          ee[u] = id[u] != 0xffff ? (int)cur[id[u]].e : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < BR; ++u) {
+          const int i = w0 + ((j0 + u) << 6) + lane;
+          if (id[u] == 0xffff) continue;
+          if (i == ss[u]) *(uint16_t*)&cur[id[u]].ck = (uint16_t)SL[u];
+          if (i == ee[u] - 1) { cur[id[u]].A = (uint16_t)SL[u]; cur[id[u]].B = (uint16_t)SR[u]; }
+        }
+      }
     }
     __syncthreads();
+    VG_STAMP(2);
+    {  // ranks, the pairing rule, partners, the cut's candidates, the swap count
+      int aL = baseL, aR = baseR;
+      for (int j0 = 0; j0 < RM; j0 += BR) {
+        int SL[BR], SR[BR];
+#pragma unroll
+        for (int u = 0; u < BR; ++u) {
+          const int j = j0 + u;
+          const bool lf = (fl >> j) & 1u, rf = (fr >> j) & 1u;
+          const unsigned long long ml = __ballot(lf), mr = __ballot(rf);
+          SL[u] = aL + (int)__popcll(ml & below) + (lf ? 1 : 0);
+          SR[u] = aR + (int)__popcll(mr & below) + (rf ? 1 : 0);
+          aL += (int)__popcll(ml);
+          aR += (int)__popcll(mr);
+        }
+        if (!((rowact >> j0) & ((1u << BR) - 1))) continue;
+        int id[BR];
+        uint4 g[BR];  // s | e << 16, A | B << 16, ck, cut
+#pragma unroll
+        for (int u = 0; u < BR; ++u) {
+          const int i = w0 + ((j0 + u) << 6) + lane;
+          id[u] = (((fl | fr) >> (j0 + u)) & 1u) ? (int)S.sid[i] : 0xffff;
+        }
+#pragma unroll
+        for (int u = 0; u < BR; ++u) g[u] = id[u] != 0xffff ? *(const uint4*)&cur[id[u]] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < BR; ++u) {
+          const int j = j0 + u;
+          if (!((rowact >> j) & 1u)) continue;
+          const bool lf = (fl >> j) & 1u, rf = (fr >> j) & 1u;
+          const int i = w0 + (j << 6) + lane;
+          const int s = (int)(g[u].x & 0xffffu), e = (int)(g[u].x >> 16);
+          const int A = (int)(g[u].y & 0xffffu), B = (int)(g[u].y >> 16), Cc = (int)(g[u].z & 0xffffu);
+          const int totL = A - Cc, Lab = A - SL[u], Rab = B - SR[u];  // left stops, stops after i
+          // right stop of rank Rab + 1 (from the right): swapped iff at least
+          // that many left stops precede it; left stop of rank totL - Lab:
+          // swapped iff at least that many right stops follow it
+          const bool rsw = rf && totL - Lab - (lf ? 1 : 0) >= Rab + 1;
+          const bool lsw = lf && Rab >= totL - Lab;
+          if (rsw) S.pr[s + Rab] = (uint16_t)i;
+          if (lsw) S.pr[s + ((e - s + 1) >> 1) + (totL - Lab) - 1] = (uint16_t)i;
+          const bool cand = (lf && !lsw) || rsw;
+          // one atomic per segment run of the row: its lowest candidate, its
+          // highest swapped left stop (ranks grow with the position)
+          const unsigned long long mc = __ballot(cand), mw = __ballot(lsw);
+          const int rb = i - lane;
+          if (cand && !(mc & below & ~((1ull << max(0, s - rb)) - 1))) atomicMin(&cur[id[u]].cut, (uint32_t)i);
+          if (lsw) {
+            const int hiL = min(64, e - rb);
+            const unsigned long long abv = (hiL >= 64 ? ~0ull : ((1ull << hiL) - 1)) & ~below & ~(1ull << lane);
+            if (!(mw & abv)) atomicMax(&cur[id[u]].ck, (uint32_t)Cc | ((uint32_t)(totL - Lab) << 16));
+          }
+        }
+      }
+    }
+    __syncthreads();
+    VG_STAMP(3);
+    for (int j0 = 0; j0 < RM; j0 += BR) {  // pair q of a segment, at the position s + q
+      if (!((rowact >> j0) & ((1u << BR) - 1))) continue;
+      int id[BR], pa[BR], pb[BR];
+      uint4 g[BR];
+#pragma unroll
+      for (int u = 0; u < BR; ++u) {
+        const int x = w0 + ((j0 + u) << 6) + lane;
+        id[u] = ((rowact >> (j0 + u)) & 1u) && x < n ? (int)S.sid[x] : 0xffff;
+      }
+#pragma unroll
+      for (int u = 0; u < BR; ++u) g[u] = id[u] != 0xffff ? *(const uint4*)&cur[id[u]] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int u = 0; u < BR; ++u) {
+        const int x = w0 + ((j0 + u) << 6) + lane;
+        const int s = (int)(g[u].x & 0xffffu), e = (int)(g[u].x >> 16), q = x - s;
+        const bool sw = id[u] != 0xffff && q < (int)(g[u].z >> 16);
+        pa[u] = sw ? (int)S.pr[s + ((e - s + 1) >> 1) + q] : -1;
+        pb[u] = sw ? (int)S.pr[x] : -1;
+      }
+#pragma unroll
+      for (int u = 0; u < BR; ++u)
+        if (pa[u] >= 0) vg_swap(S.key, S.val, pa[u], pb[u]);
+    }
+    __syncthreads();
+    VG_STAMP(4);
+    for (int j = tid; j < nseg; j += T) {  // the children
+      const int s = cur[j].s, e = cur[j].e, cut = (int)cur[j].cut;
+      const int aL = cut - s > kVgLeaf ? 1 : 0, aR = e - cut > kVgLeaf ? 1 : 0;
+      const int base = (aL + aR) ? atomicAdd(&S.ctl[(r + 1) & 1], aL + aR) : 0;
+      if (aL) nxt[base] = VgSeg{(uint16_t)s, (uint16_t)cut, 0, 0, 0u, 0u};
+      else atomicOr(&S.head[s >> 5], 1u << (s & 31));
+      if (aR) nxt[base + aL] = VgSeg{(uint16_t)cut, (uint16_t)e, 0, 0, 0u, 0u};
+      else atomicOr(&S.head[cut >> 5], 1u << (cut & 31));
+      cur[j].ck = (uint32_t)base | ((uint32_t)(aL | (aR << 1)) << 16);
+    }
+    __syncthreads();
+    VG_STAMP(5);
+    {
+      uint32_t act = 0;
+      for (int j0 = 0; j0 < RM; j0 += BR) {
+        if (!((rowact >> j0) & ((1u << BR) - 1))) continue;
+        int id[BR];
+        uint4 g[BR];
+#pragma unroll
+        for (int u = 0; u < BR; ++u) {
+          const int i = w0 + ((j0 + u) << 6) + lane;
+          id[u] = ((rowact >> (j0 + u)) & 1u) && i < n ? (int)S.sid[i] : 0xffff;
+        }
+#pragma unroll
+        for (int u = 0; u < BR; ++u) g[u] = id[u] != 0xffff ? *(const uint4*)&cur[id[u]] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < BR; ++u) {
+          const int i = w0 + ((j0 + u) << 6) + lane;
+          int nid = 0xffff;
+          if (id[u] != 0xffff) {
+            const int ch = (int)(g[u].z >> 16), base = (int)(g[u].z & 0xffffu);
+            if (i < (int)g[u].w) { if (ch & 1) nid = base; }
+            else if (ch & 2) nid = base + (ch & 1);
+            S.sid[i] = (uint16_t)nid;
+          }
+          if ((rowact >> (j0 + u)) & 1u)
+            if (__ballot(nid != 0xffff)) act |= 1u << (j0 + u);
+        }
+      }
+      rowact = act;
+    }
+    __syncthreads();
+    VG_STAMP(6);
   }
+  VG_STAMP(7);
+  // leaves: every position ranks itself within its leaf (<= 16 keys, its
+  // start the highest leaf-start bit at or below it, its end the next one)
+  for (int i = tid; i < n; i += T) {
+    const int wi = i >> 5, bi = i & 31;
+    const uint32_t hw = S.head[wi];
+    const uint32_t msk = bi == 31 ? ~0u : ((2u << bi) - 1);
+    const uint32_t lo = hw & msk, hi = hw & ~msk;
+    int ls, le;
+    if (lo) ls = (wi << 5) + 31 - __builtin_clz(lo);
+    else ls = ((wi - 1) << 5) + 31 - __builtin_clz(S.head[wi - 1]);  // a leaf start lies within 16 below
+    if (hi) le = (wi << 5) + __builtin_ctz(hi);
+    else {
+      const uint32_t h2 = S.head[wi + 1];
+      le = h2 ? ((wi + 1) << 5) + __builtin_ctz(h2) : n;
+    }
+    le = min(le, n);
+    const uint32_t k = S.key[i];
+    int rank = 0;
+    for (int u0 = 0; u0 < le - ls; u0 += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int q = ls + u0 + u;
+        const uint32_t kq = S.key[min(q, n - 1)];
+        if (q < le) rank += (kq < k || (kq == k && q < i)) ? 1 : 0;
+      }
+    }
+    S.sid[i] = (uint16_t)(ls + rank);
+  }
+  __syncthreads();
+  // the moves, in batches of whole leaves (a batch ends at a leaf start):
+  // each batch's keys / vals / places to registers, then to their places
+  constexpr int MB = 4;
+  for (int b = 0; b < n;) {
+    int bn = b + T * MB;
+    if (bn >= n) {
+      bn = n;
+    } else {
+      int w = bn >> 5;
+      uint32_t m = S.head[w] & ~((1u << (bn & 31)) - 1);
+      while (!m && ((w + 1) << 5) < n) m = S.head[++w];
+      bn = m ? min(n, (w << 5) + __builtin_ctz(m)) : n;
+    }
+    uint32_t kk[MB + 1], vd[MB + 1];
+#pragma unroll
+    for (int j = 0; j <= MB; ++j) {
+      const int i = b + j * T + tid;
+      const bool in = i < bn && (j < MB || i >= b + T * MB);
+      kk[j] = in ? S.key[i] : 0u;
+      vd[j] = in ? ((uint32_t)S.val[i] | ((uint32_t)S.sid[i] << 16)) : 0xffffffffu;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j <= MB; ++j)
+      if (vd[j] != 0xffffffffu) { S.key[vd[j] >> 16] = kk[j]; S.val[vd[j] >> 16] = (V)(vd[j] & 0xffffu); }
+    __syncthreads();
+    b = bn;
+  }
+  VG_STAMP(8);
 }
 
 }  // namespace lego

@@ -275,7 +275,8 @@ HIP_EXPORTS = ["lego_sensor_preset", "lego_create", "lego_fleet_create", "lego_d
                "lego_mo_set_map", "lego_mo_configure", "lego_mo_process", "lego_mo_loop_closure", "lego_last_error", "lego_stage_times",
                "lego_odom_profile", "lego_extract_profile", "lego_handoff_pack", "lego_handoff_pack_into", "lego_handoff_unpack", "lego_comm_unique_id",
                "lego_comm_create", "lego_comm_destroy", "lego_comm_gather_handoff", "lego_comm_handoff",
-               "lego_comm_gather_handoff_ex", "lego_comm_wait", "lego_comm_handoff_device"]
+               "lego_comm_gather_handoff_ex", "lego_comm_wait", "lego_comm_handoff_device",
+               "lego_voxel_grid", "lego_voxel_grid_stats"]
 
 
 def hip_lib() -> C.CDLL:
@@ -323,6 +324,9 @@ def hip_lib() -> C.CDLL:
     lib.lego_comm_gather_handoff_ex.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_uint32]
     lib.lego_comm_wait.argtypes = [C.c_void_p]
     lib.lego_comm_handoff_device.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]
+    lib.lego_voxel_grid.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_float, C.c_void_p,
+                                    C.POINTER(C.c_int32)]
+    lib.lego_voxel_grid_stats.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
     lib.lego_last_error.restype = C.c_char_p
     lib.lego_odom_profile.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
     lib.lego_extract_profile.argtypes = [C.c_void_p, C.c_void_p]
@@ -706,6 +710,20 @@ class Lego:
         check(self.lib.lego_batch_fetch(self.h, k, C.byref(self._ip), C.byref(self._fa)),
               "lego_batch_fetch", self.lib)
         return ip_to_dict(self._ip, self.cfg, images), fa_to_dict(self._fa)
+
+    def voxel_grid(self, pts: np.ndarray, leaf: float) -> tuple[np.ndarray, dict]:
+        """lego_voxel_grid of an XYZI cloud on the device: (filtered cloud,
+        lego_voxel_grid_stats as a dict)."""
+        pts = np.ascontiguousarray(pts, dtype=XYZI_DTYPE)
+        out = np.zeros(max(len(pts), 1), XYZI_DTYPE)
+        n = C.c_int32()
+        check(self.lib.lego_voxel_grid(self.h, pts.ctypes.data, len(pts), leaf, out.ctypes.data, C.byref(n)),
+              "lego_voxel_grid", self.lib)
+        st = (C.c_int32 * 8)()
+        check(self.lib.lego_voxel_grid_stats(self.h, st), "lego_voxel_grid_stats", self.lib)
+        keys = ("sorted", "voxels", "rounds", "local_segments", "slow_segments", "heap_segments", "nonfinite",
+                "device_us")
+        return out[:n.value].copy(), dict(zip(keys, list(st)))
 
     def handoff_packet(self) -> np.ndarray:
         """lego_handoff_pack of the last waited batch, copied to the host

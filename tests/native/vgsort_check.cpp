@@ -17,6 +17,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 struct Idx {
@@ -117,6 +118,13 @@ static std::vector<unsigned> killer(int n) {
 }
 
 int main(int argc, char** argv) {
+  if (argc == 4 && std::string(argv[1]) == "killer") {  // keys for tests/golden/make_vg_killer.py
+    std::vector<unsigned> k = killer(atoi(argv[2]));
+    const unsigned div = (unsigned)atoi(argv[3]);
+    for (auto& x : k) x /= div;
+    fwrite(k.data(), sizeof(unsigned), k.size(), stdout);
+    return 0;
+  }
   const int trials = argc > 1 ? atoi(argv[1]) : 6000;
   long bad = 0, total = 0;
   auto check = [&](const std::vector<unsigned>& keys) {
