@@ -837,36 +837,34 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
 // ---------------------------------------------------------------- less-flat VoxelGrid
 // pcl::VoxelGrid<PointType> downSizeFilter, leaf 0.2 (featureAssociation.cpp:
 // 778-782) on each ring's less-flat set, one (scan, ring) workgroup: the
-// points from the ring's slot into LDS, getMinMax3D, the voxel index per
-// point, PCL's std::sort of (idx, point) by idx (lego_vgsort.h: libstdc++'s
-// order of each voxel's points, which is the summation order), one lane per
-// voxel summing its points in that order, the centroids back to the slot.
-// The slot's count goes from the less-flat set's size to the voxels'.
+// points from the ring's slot (L2-resident: k_extract just wrote them),
+// getMinMax3D, the voxel index per point, PCL's std::sort of (idx, point) by
+// idx (lego_vgsort.h: libstdc++'s order of each voxel's points, which is the
+// summation order), one lane per voxel summing its points in that order into
+// registers, then the centroids over the slot.  The slot's count goes from
+// the less-flat set's size to the voxels'.
+constexpr int kLfvMaxPer = 8;  // voxels per thread (H <= kLfvMaxPer * kExtractThreads)
 __host__ __device__ inline size_t lfvox_lds_bytes(int H) {
-  return (size_t)H * 16 + (((size_t)H * 6 + 15) & ~(size_t)15) + vg_sort_scratch_bytes(H, kExtractThreads) + 64;
+  return (((size_t)H * 6 + 15) & ~(size_t)15) + vg_sort_scratch_bytes(H, kExtractThreads) + 64;
 }
-__global__ void __launch_bounds__(kExtractThreads) k_lf_voxel(BatchBufs bb, DevCfg c) {
+__global__ void __launch_bounds__(kExtractThreads, 5) k_lf_voxel(BatchBufs bb, DevCfg c) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   const int ring = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int H = c.H;
-  float4* pts = (float4*)lds_raw;
-  uint32_t* key = (uint32_t*)(lds_raw + (size_t)H * 16);
-  uint16_t* val = (uint16_t*)(lds_raw + (size_t)H * 20);
-  unsigned char* sc = lds_raw + (size_t)H * 16 + (((size_t)H * 6 + 15) & ~(size_t)15);
+  uint32_t* key = (uint32_t*)lds_raw;
+  uint16_t* val = (uint16_t*)(lds_raw + (size_t)H * 4);
+  unsigned char* sc = lds_raw + (((size_t)H * 6 + 15) & ~(size_t)15);
   int* misc = (int*)(sc + vg_sort_scratch_bytes(H, kExtractThreads));  // [16]
-  float* red = (float*)(misc + 8);                                      // not overlapping misc[0..7]
   __shared__ float mm[4][6];
   int* cnt = bb.r_cnt + ((size_t)b * c.N + ring) * 4;
   float4* slot = bb.r_lflat + (size_t)b * c.P + (size_t)ring * H;
   const int K = cnt[3];
-  (void)red;
   if (K <= 0) return;
   const float inv = 1.0f / 0.2f;
   float mn[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
   float mx[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
   for (int t = tid; t < K; t += blockDim.x) {
     const float4 p = slot[t];
-    pts[t] = p;
     mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
     mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
   }
@@ -896,7 +894,7 @@ __global__ void __launch_bounds__(kExtractThreads) k_lf_voxel(BatchBufs bb, DevC
   }
   const int d0 = xb[0] - mb[0] + 1, d1 = xb[1] - mb[1] + 1;
   for (int t = tid; t < K; t += blockDim.x) {
-    const float4 p = pts[t];
+    const float4 p = slot[t];
     const int i0 = (int)(floorf(p.x * inv) - (float)mb[0]);
     const int i1 = (int)(floorf(p.y * inv) - (float)mb[1]);
     const int i2 = (int)(floorf(p.z * inv) - (float)mb[2]);
@@ -905,9 +903,15 @@ __global__ void __launch_bounds__(kExtractThreads) k_lf_voxel(BatchBufs bb, DevC
   }
   __syncthreads();
   vg_block_sort(vg_sort_carve(key, val, sc, K, (int)blockDim.x), K);
+  // centroids into registers (every read of the slot done), then over the slot
+  float4 cen[kLfvMaxPer];
+  int at[kLfvMaxPer];
   int outc = 0;
-  for (int t0 = 0; t0 < K; t0 += blockDim.x) {
-    const int t = t0 + tid;
+#pragma unroll
+  for (int j = 0; j < kLfvMaxPer; ++j) {
+    at[j] = -1;
+    const int t = j * (int)blockDim.x + tid;
+    if (j * (int)blockDim.x >= K) continue;  // uniform
     const bool head = t < K && (t == 0 || key[t] != key[t - 1]);
     int tot;
     const int r = block_rank(head, misc, &tot);
@@ -916,14 +920,19 @@ __global__ void __launch_bounds__(kExtractThreads) k_lf_voxel(BatchBufs bb, DevC
       float cx = 0, cy = 0, cz = 0, ci = 0;
       int u = t;
       for (; u < K && key[u] == k; ++u) {
-        const float4 q = pts[val[u]];
+        const float4 q = slot[val[u]];
         cx += q.x; cy += q.y; cz += q.z; ci += q.w;
       }
       const float n = (float)(u - t);
-      slot[outc + r] = make_float4(cx / n, cy / n, cz / n, ci / n);
+      cen[j] = make_float4(cx / n, cy / n, cz / n, ci / n);
+      at[j] = outc + r;
     }
     outc += tot;
   }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kLfvMaxPer; ++j)
+    if (at[j] >= 0) slot[at[j]] = cen[j];
   if (tid == 0) cnt[3] = outc;
 }
 

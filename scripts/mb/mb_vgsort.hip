@@ -34,6 +34,7 @@ __device__ unsigned long long g_wst[16], g_wcnt[16];
       atomicAdd(&g_wcnt[k], 1ull);                                               \
     }                                                                            \
   } while (0)
+#define VG_CLOCK() clock64()
 #include "lego_vgsort.h"
 
 using namespace lego;
@@ -234,8 +235,8 @@ int main(int argc, char** argv) {
       unsigned long long ws[16], wc[16];
       hipMemcpyFromSymbol(ws, HIP_SYMBOL(g_wst), sizeof(ws));
       hipMemcpyFromSymbol(wc, HIP_SYMBOL(g_wcnt), sizeof(wc));
-      printf("  wave work (kcycles, calls): heap %.1f/%llu  part<=64 %.1f/%llu  part<=256 %.1f/%llu  part>256 %.1f/%llu\n",
-             ws[9] / 1e3, wc[9], ws[10] / 1e3, wc[10], ws[11] / 1e3, wc[11], ws[12] / 1e3, wc[12]);
+      printf("  wave sort (kcycles, calls): median %.1f/%llu flags %.1f/%llu pairing %.1f/%llu scatter %.1f/%llu swaps %.1f/%llu final %.1f/%llu\n",
+             ws[9] / 1e3, wc[9], ws[10] / 1e3, wc[10], ws[11] / 1e3, wc[11], ws[12] / 1e3, wc[12], ws[13] / 1e3, wc[13], ws[14] / 1e3, wc[14]);
       printf("  ring 0 phases (kcycles): median %.1f flags %.1f counts %.1f ranks %.1f swaps %.1f children %.1f sid %.1f | loop-exit %.1f leaves %.1f  levels %llu\n",
              z[0] / 1e3, z[1] / 1e3, z[2] / 1e3, z[3] / 1e3, z[4] / 1e3, z[5] / 1e3, z[6] / 1e3, z[7] / 1e3, z[8] / 1e3, zl);
     }
