@@ -154,6 +154,7 @@ struct lego_ctx {
   int vgStats[8] = {};
   lego_mo_opts moOpts{};
   double moTimeLast = -1;
+  bool moStoreFull = false;  // sticky KF_OVF seen: no step runs until lego_reset
   double moTimeOdom = 0;  // timeLaserOdometry: the last hand-off's stamp (laserOdometryHandler :630)
   LcDev lc{};             // loop closure buffers (first lego_mo_loop_closure)
   // loop-closure mode (lego_mo_opts.loop_closure_enable): the pose graph, the
@@ -264,6 +265,7 @@ static int ctx_reset(lego_ctx* x) {
     HIPCHK(hipStreamSynchronize(x->stream));
   }
   x->moTimeLast = -1;
+  x->moStoreFull = false;
   x->moTimeOdom = 0;
   x->pg.clear();
   x->recent.clear();
@@ -1428,11 +1430,40 @@ static int lc_put_key(lego_ctx* x, int i, const float (&t)[6]) {
   MoKeyframes& kf = x->mo.kf;
   const std::array<float, 6> p6 = {t[3], t[4], t[5], t[0], t[1], t[2]};
   const float4 p3 = make_float4(t[3], t[4], t[5], (float)i);
-  x->kfPose[i] = p6;
+  if (i < (int)x->kfPose.size()) x->kfPose[i] = p6;  // the loop-closure mode's host mirror
   HIPCHK(hipMemcpyAsync(kf.pose6 + 6 * i, p6.data(), sizeof(float) * 6, hipMemcpyHostToDevice, x->stream));
   HIPCHK(hipMemcpyAsync(kf.pos3 + i, &p3, sizeof(float4), hipMemcpyHostToDevice, x->stream));
   HIPCHK(hipStreamSynchronize(x->stream));
   return LEGO_OK;
+}
+
+// Key K - 1 (just saved by k_kf_save from the chain's transform) takes iSAM2's
+// latest estimate t as the reference stores it (:1412-1432): the key pose,
+// and past the first key transformAftMapped = transformTobeMapped = t.
+// Device writes only where t differs from what the device holds.
+static int kf_put_estimate(lego_ctx* x, MoState& hs, int K, const float (&t)[6]) {
+  const float* chain = K == 1 ? hs.transformTobeMapped : hs.transformAftMapped;
+  if (std::memcmp(chain, t, sizeof(t)) == 0) return LEGO_OK;
+  const int st = lc_put_key(x, K - 1, t);
+  if (st != LEGO_OK) return st;
+  if (K > 1) {
+    for (int i = 0; i < 6; ++i) hs.transformAftMapped[i] = hs.transformTobeMapped[i] = t[i];
+    MoDev& m = x->mo;
+    HIPCHK(hipMemcpyAsync((char*)m.st + offsetof(MoState, transformAftMapped), t, sizeof(t), hipMemcpyHostToDevice,
+                          x->stream));
+    HIPCHK(hipMemcpyAsync((char*)m.st + offsetof(MoState, transformTobeMapped), t, sizeof(t), hipMemcpyHostToDevice,
+                          x->stream));
+    HIPCHK(hipStreamSynchronize(x->stream));  // t may be a stack array
+  }
+  return LEGO_OK;
+}
+
+// the chain's transform of the key just saved, round-tripped (no loop factor:
+// iSAM2's estimate is the chain itself)
+static void kf_chain_estimate(const MoState& hs, int K, float (&t)[6]) {
+  float c[6];
+  for (int i = 0; i < 6; ++i) c[i] = K == 1 ? hs.transformTobeMapped[i] : hs.transformAftMapped[i];
+  transform_roundtrip(c, t);
 }
 
 // saveKeyFramesAndFactor's graph part and correctPoses (:1372-1438, 1456-1478)
@@ -1462,24 +1493,16 @@ static int lc_after_step(lego_ctx* x, MoState& hs, int saved, int K) {
                         var);
       x->pg.insert(pose_from_transform(aft));
     }
-    if (x->pg.loops > 0) {  // otherwise the estimate is the chain the device already stored
+    float t[6];  // latestEstimate
+    if (x->pg.loops > 0) {
       x->pg.optimize();
-      float t[6];
       transform_from_pose(x->pg.est[K - 1], t);
-      int st = lc_put_key(x, K - 1, t);
-      if (st != LEGO_OK) return st;
-      if (K > 1) {  // transformAftMapped = transformTobeMapped = transformLast = latestEstimate
-        for (int i = 0; i < 6; ++i) hs.transformAftMapped[i] = hs.transformTobeMapped[i] = t[i];
-        HIPCHK(hipMemcpyAsync((char*)m.st + offsetof(MoState, transformAftMapped), t, sizeof(t),
-                              hipMemcpyHostToDevice, x->stream));
-        HIPCHK(hipMemcpyAsync((char*)m.st + offsetof(MoState, transformTobeMapped), t, sizeof(t),
-                              hipMemcpyHostToDevice, x->stream));
-        HIPCHK(hipStreamSynchronize(x->stream));  // t is a stack array
-        std::memcpy(x->transformLast, t, sizeof(t));
-      }
-    } else if (K > 1) {
-      for (int i = 0; i < 6; ++i) x->transformLast[i] = hs.transformAftMapped[i];
+    } else {
+      kf_chain_estimate(hs, K, t);
     }
+    const int st = kf_put_estimate(x, hs, K, t);
+    if (st != LEGO_OK) return st;
+    if (K > 1) std::memcpy(x->transformLast, t, sizeof(t));  // transformLast = latestEstimate
   }
   if (x->aLoopIsClosed) {  // correctPoses: the estimate of the last save, every key
     x->recent.clear();
@@ -1512,6 +1535,11 @@ int lego_mo_process(lego_ctx* x, const lego_fa_out* in, lego_mo_out* out) {
   }
   x->moTimeLast = in->stamp;
   MoDev& m = x->mo;
+  if (x->moStoreFull) {  // both map modes: nothing of the step runs (lego_mo.h MO_E_STORE_FULL)
+    set_err("scan-to-map: the keyframe store is full (%d keyframes / %d arena points); lego_reset to go on",
+            m.kf.kcap, m.kf.acap);
+    return LEGO_E_CAPACITY;
+  }
   const int N = x->dc.N, P = x->dc.P;
   if (in->n_corner_last < 0 || in->n_corner_last > N * kLessSharpPerRing || in->n_surf_last < 0 ||
       in->n_surf_last > P || in->n_outlier_last < 0 || in->n_outlier_last > P) {
@@ -1546,6 +1574,7 @@ int lego_mo_process(lego_ctx* x, const lego_fa_out* in, lego_mo_out* out) {
   switch (rs) {
     case MO_OK: break;
     case MO_E_STORE_FULL:  // sticky: the stream's keyframe history is incomplete from here on
+      x->moStoreFull = true;
       set_err("scan-to-map: the keyframe store is full (%d keyframes / %d arena points); lego_reset to go on",
               m.kf.kcap, m.kf.acap);
       return LEGO_E_CAPACITY;
@@ -1567,12 +1596,18 @@ int lego_mo_process(lego_ctx* x, const lego_fa_out* in, lego_mo_out* out) {
   if (!x->moFixed) HIPCHK(hipMemcpyAsync(meta, m.kf.meta, sizeof(meta), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   if (meta[KF_OVF]) {  // saveKeyFramesAndFactor of this very step found the store full (k_kf_save)
+    x->moStoreFull = true;
     set_err("scan-to-map: the keyframe store is full (%d keyframes / %d arena points): this step's keyframe "
             "was not saved; lego_reset to go on", m.kf.kcap, m.kf.acap);
     return LEGO_E_CAPACITY;
   }
   if (lcMode) {
     const int st = lc_after_step(x, hs, meta[KF_SAVED], meta[KF_K]);
+    if (st != LEGO_OK) return st;
+  } else if (!x->moFixed && meta[KF_SAVED]) {  // the key pose as iSAM2's estimate of the chain
+    float t[6];
+    kf_chain_estimate(hs, meta[KF_K], t);
+    const int st = kf_put_estimate(x, hs, meta[KF_K], t);
     if (st != LEGO_OK) return st;
   }
   if (hs.optimized) x->moImu.front = moFront;  // transformUpdate ran (:1345)

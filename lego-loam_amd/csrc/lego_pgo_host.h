@@ -102,6 +102,13 @@ inline void transform_from_pose(const Pose3d& p, float (&t)[6]) {
   t[5] = (float)p.t[0];
 }
 
+// A transform through gtsam::Pose3 and back: what the reference stores as
+// every key pose and, past the first key, as transformAftMapped /
+// TobeMapped / Last (mapOptmization.cpp:1412-1432 read latestEstimate's
+// rotation().pitch() / yaw() / roll()).  Wraps a yaw past +-pi, re-branches
+// |pitch| > pi/2, and may move a last bit.
+inline void transform_roundtrip(const float (&in)[6], float (&out)[6]) { transform_from_pose(pose_from_transform(in), out); }
+
 // a^-1 b
 inline Pose3d pose_between(const Pose3d& a, const Pose3d& b) {
   Pose3d r;

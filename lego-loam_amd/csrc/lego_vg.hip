@@ -12,10 +12,10 @@
 //                      its order of equal keys is the summation order, so the
 //                      permutation is reproduced exactly (lego_vgsort.h):
 //     per round        k_vg_count / k_vg_decide / k_vg_swap partition every
-//                      segment larger than kVgLocal across many workgroups
+//                      segment larger than kVgSplit across many workgroups
 //                      (tiles of kVgTile keys), k_vg_plan turns the cuts into
 //                      the next level's segments
-//     k_vg_local       each remaining segment in one workgroup's LDS
+//     k_vg_local_small / k_vg_local  each remaining segment in one workgroup's LDS
 //   k_vg_head_tiles, k_scan_top, k_vg_emit
 //                      voxel heads, their ranks, one lane per voxel summing its
 //                      points in sorted order (PCL's centroid)
@@ -37,7 +37,12 @@ namespace lego {
 constexpr unsigned kInvalidKey = 0xffffffffu;
 constexpr int kScanThreads = 256, kScanPer = 16, kScanTile = kScanThreads * kScanPer;
 constexpr int kVgTileThreads = 256, kVgTilePer = 16, kVgTile = kVgTileThreads * kVgTilePer;
-constexpr int kVgLocal = 4096, kVgLocalThreads = 512;  // vg_sort_max(512) = 4096
+// The rounds split segments down to kVgSplit keys; those sort in small
+// workgroups (many per CU, so the sorts' latency overlaps).  Segments the
+// rounds leave larger (their last round, or rounds forced off) go to the big
+// local kernel: LDS up to kVgLocal, a global-memory partition above.
+constexpr int kVgSplit = 1024, kVgSplitThreads = 256;    // vg_sort_max(256) = 2048 >= kVgSplit
+constexpr int kVgLocal = 4096, kVgLocalThreads = 1024;  // vg_sort_max(1024) = 8192 >= kVgLocal
 constexpr int kVgRoundsMax = 16;
 constexpr int kVgPlanThreads = 1024;
 
@@ -280,7 +285,7 @@ __global__ void __launch_bounds__(kVgPlanThreads) k_vg_plan0(int n, const int* n
     if (threadIdx.x == 0) { v.ctl[C_NB] = 0; v.ctl[C_NT] = 0; v.tileOff[0] = 0; }
     return;
   }
-  if (m <= kVgLocal || rounds == 0) {  // one workgroup (above kVgLocal: its global-memory partition)
+  if (m <= kVgSplit || rounds == 0) {  // one workgroup (above kVgLocal: its global-memory partition)
     if (threadIdx.x == 0) {
       v.loc[0] = make_int4(0, m, 2 * lg2i(m), 0);
       v.ctl[C_NLOC] = 1;
@@ -294,7 +299,7 @@ __global__ void __launch_bounds__(kVgPlanThreads) k_vg_plan0(int n, const int* n
 }
 
 // After round r - 1 (big list in big[(r-1)&1]): the cuts make the children;
-// children larger than kVgLocal form the next round's big list (unless
+// children larger than kVgSplit form the next round's big list (unless
 // flush), the others (and, when flushing, all) go to the local list with
 // their depth budget 2 lg m - r.
 __global__ void __launch_bounds__(kVgPlanThreads) k_vg_plan(VgScratch v, int r, int flush) {
@@ -315,7 +320,7 @@ __global__ void __launch_bounds__(kVgPlanThreads) k_vg_plan(VgScratch v, int r, 
       ch[1] = make_int2(cut, e);
       for (int q = 0; q < 2; ++q) {
         const int sz = ch[q].y - ch[q].x;
-        if (!flush && sz > kVgLocal) {
+        if (!flush && sz > kVgSplit) {
           ++nbig;
         } else if (sz > 1) {
           const int at = atomicAdd(&v.ctl[C_NLOC], 1);
@@ -327,7 +332,7 @@ __global__ void __launch_bounds__(kVgPlanThreads) k_vg_plan(VgScratch v, int r, 
     int at = carry + block_excl_scan(nbig, tmp, &t);
     if (b < nbp)
       for (int q = 0; q < 2; ++q)
-        if (!flush && ch[q].y - ch[q].x > kVgLocal) next[at++] = ch[q];
+        if (!flush && ch[q].y - ch[q].x > kVgSplit) next[at++] = ch[q];
     carry += t;
   }
   __syncthreads();  // the cut / kcnt slots are reused below
@@ -512,8 +517,9 @@ __device__ int vg_block_partition_global(const VgScratch& v, int s, int e, int* 
   return cut;
 }
 
+template <int CAP, int T>
 __host__ __device__ inline size_t vg_local_lds_bytes() {
-  return (size_t)kVgLocal * 6 + vg_sort_scratch_bytes(kVgLocal, kVgLocalThreads);
+  return (size_t)CAP * 6 + vg_sort_scratch_bytes(CAP, T);
 }
 
 // [s, s + m), m <= kVgLocal, through LDS: keys and local positions sorted,
@@ -537,9 +543,23 @@ __device__ void vg_local_sort(const VgScratch& v, uint32_t* key, uint16_t* lv, u
   __syncthreads();
 }
 
-// Every local segment (grid-stride over the list): LDS sort, or for a segment
-// still above kVgLocal the block partition in global memory, depth first with
-// an LDS stack, its pieces sorted in LDS.
+// The local segments (grid-stride over the list) of up to kVgSplit keys:
+// LDS sorts in small workgroups.
+__global__ void __launch_bounds__(kVgSplitThreads) k_vg_local_small(VgScratch v) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  uint32_t* key = (uint32_t*)lds_raw;
+  uint16_t* lv = (uint16_t*)(lds_raw + (size_t)kVgSplit * 4);
+  unsigned char* sc = lds_raw + (size_t)kVgSplit * 6;
+  const int nloc = v.ctl[C_NLOC];
+  for (int t = blockIdx.x; t < nloc; t += gridDim.x) {
+    const int4 g = v.loc[t];
+    if (g.y - g.x <= kVgSplit) vg_local_sort(v, key, lv, sc, g.x, g.y - g.x, g.z);
+  }
+}
+
+// The larger local segments: LDS sort up to kVgLocal, above it the block
+// partition in global memory, depth first with an LDS stack, its pieces
+// sorted in LDS.
 __global__ void __launch_bounds__(kVgLocalThreads) k_vg_local(VgScratch v) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   __shared__ int tmp[20];
@@ -552,6 +572,7 @@ __global__ void __launch_bounds__(kVgLocalThreads) k_vg_local(VgScratch v) {
   const int nloc = v.ctl[C_NLOC];
   for (int t = blockIdx.x; t < nloc; t += gridDim.x) {
     const int4 g = v.loc[t];
+    if (g.y - g.x <= kVgSplit) continue;  // k_vg_local_small's
     if (g.y - g.x <= kVgLocal) {
       vg_local_sort(v, key, lv, sc, g.x, g.y - g.x, g.z);
       continue;
@@ -636,9 +657,9 @@ __global__ void __launch_bounds__(kHeadTile) k_vg_emit(const float4* in, int n, 
 int vg_rounds_for(int n) {
   static const int forced = std::getenv("LEGO_VG_ROUNDS") ? std::atoi(std::getenv("LEGO_VG_ROUNDS")) : -1;
   if (forced >= 0) return std::min(forced, kVgRoundsMax);
-  if (n <= kVgLocal) return 0;
+  if (n <= kVgSplit) return 0;
   int r = 1;
-  while (((long long)kVgLocal << r) < n) ++r;
+  while (((long long)kVgSplit << r) < n) ++r;
   return std::min(r + 1, kVgRoundsMax);
 }
 
@@ -663,8 +684,10 @@ int voxel_grid_device(const float4* in, int n, const int* nDev, float leaf, floa
     k_vg_swap<<<gt, kVgTileThreads, 0, s>>>(v, r);
     k_vg_plan<<<1, kVgPlanThreads, 0, s>>>(v, r + 1, r + 1 == R ? 1 : 0);
   }
-  const int gl = n <= kVgLocal ? 1 : std::min(v.capLoc, 1024);
-  k_vg_local<<<gl, kVgLocalThreads, vg_local_lds_bytes(), s>>>(v);
+  const int gl = n <= kVgSplit ? 1 : std::min(v.capLoc, 2048);
+  k_vg_local_small<<<gl, kVgSplitThreads, vg_local_lds_bytes<kVgSplit, kVgSplitThreads>(), s>>>(v);
+  if (n > kVgSplit)
+    k_vg_local<<<std::min(v.capLoc, 256), kVgLocalThreads, vg_local_lds_bytes<kVgLocal, kVgLocalThreads>(), s>>>(v);
   const int ht = tiles_for(n, kHeadTile);
   k_vg_head_tiles<<<ht, kHeadTile, 0, s>>>(v);
   k_scan_top<<<1, 1024, 0, s>>>(v.scanTiles, ht, nullptr, v.ctl + C_NOUT);
@@ -679,7 +702,7 @@ int vg_read_ctl(const VgScratch& v, int* ctl16, hipStream_t s) {
 
 int vg_scratch_alloc(VgScratch& v, int cap, void* ctx, int (*alloc)(void* ctx, void** p, size_t bytes)) {
   v.cap = cap;
-  v.capBig = cap / kVgLocal + 2;
+  v.capBig = cap / kVgSplit + 2;
   v.capTiles = tiles_for(cap, kVgTile) + v.capBig + 1;
   v.capLoc = 2 * (kVgRoundsMax + 1) * v.capBig + 4;
   v.capScanTiles = std::max(tiles_for(2 * cap + 64, kScanTile), tiles_for(cap, kHeadTile)) + 1;
