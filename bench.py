@@ -70,6 +70,22 @@ def odom_alg_bytes(recs) -> float:
     return tot
 
 
+def pipeline_alg_bytes(cfg, npts, rec) -> float:
+    """SURVEY.md §8d's whole-pipeline algorithmic bytes of one scan, from its
+    actual counts: projection 16N + 16P + 4P, ground 12(g+1)H + 9P, CCL 9P,
+    compaction 21P + 25Ns, curvature / occlusion 13Ns, sort / extract
+    10Ns + 16F, deskew and TransformToEnd 32Ns, and the odometry as k_odom's
+    compulsory bytes (odom_alg_bytes: 16F + 32 last).  Outliers (a few
+    hundred points) are left out."""
+    P = cfg.n_scan * cfg.horizon_scan
+    H, g = cfg.horizon_scan, cfg.ground_scan_ind
+    ns = rec.n_segmented
+    f = rec.n_sharp + rec.n_less_sharp + rec.n_flat + rec.n_less_flat
+    last = rec.n_less_sharp + rec.n_less_flat
+    return (16 * npts + 20 * P + 12 * (g + 1) * H + 9 * P + 9 * P + 21 * P + 25 * ns + 13 * ns + 10 * ns
+            + 16 * f + 32 * ns + 16 * f + 32 * last)
+
+
 def cpu_baseline(L, sensor, seed, nscans, budget_s):
     """The oracle (C++ restatement, 1 thread) over the same stream, repeated
     until ~budget_s of CPU work."""
@@ -263,14 +279,15 @@ def mapping_bench(L, steps: int, cpu: bool):
                              "peak_gbs": HBM_PEAK_GBS, "frac": alg / (med * 1e-3) / 1e9 / HBM_PEAK_GBS,
                              "note": "SURVEY §8d C5 bytes (2*16*M_raw + 2*16*M_ds + 112*Q*iters) / median step"}})
     if cpu:
-        n = 3
+        n = 5
         cdts, couts = run(L.Oracle(L.sensor_cfg(sensor)), None, n)
         res["cpu_ms_per_step"] = statistics.median(cdts)
         res["cpu_iterations"] = [o["iterations"] for o in couts]
         res["cpu_sample"] = (f"first {n} mapping steps of the same consecutive scans through the oracle (1 thread; "
                              "map VoxelGrid + kd-tree build every step, as the reference)")
         res["same_iterations_as_gpu"] = res["cpu_iterations"] == its[:n]
-        res["cpu_vs_gpu_steps"] = "the oracle's steps 1..3 against the GPU's iterations of steps 1..3 (GPU timing: 2..)"
+        res["cpu_vs_gpu_steps"] = (f"the oracle's steps 1..{n} (median of {n}) against the GPU's iterations of "
+                                   f"steps 1..{n} (GPU timing: 2..)")
     return res
 
 
@@ -306,10 +323,13 @@ def loop_bench(L, nscans: int, calls: int, cpu: bool):
             ora.ip(pts, stamp)
             ora.fa()
             ora.mo()
-        t0 = time.perf_counter()
-        ora.loop_closure()
-        res["cpu_ms_per_call"] = (time.perf_counter() - t0) * 1e3
-        res["cpu_sample"] = "1 call of the oracle (1 thread; kd-tree ICP as PCL)"
+        cd = []
+        for _ in range(calls):
+            t0 = time.perf_counter()
+            ora.loop_closure()
+            cd.append((time.perf_counter() - t0) * 1e3)
+        res["cpu_ms_per_call"] = statistics.median(cd)
+        res["cpu_sample"] = f"median of {calls} calls of the oracle (1 thread; kd-tree ICP as PCL)"
     return res
 
 
@@ -342,8 +362,15 @@ def dense_bench(L, nscans: int, batch: int, device: int, cpu: bool = False, budg
     dt = time.perf_counter() - t0
     g.close()
     n = (nb - 1) * batch
+    j = nb - 1  # recs: the last batch's records
+    per_scan = statistics.mean(pipeline_alg_bytes(cfg, int(off[j * batch + k + 1] - off[j * batch + k]), recs[k])
+                               for k in range(batch))
     res = {"workload": f"C3: HDL-64E 64x2048 synthetic stream (seed 2), {batch} scans per call, two in flight",
-           "scans": n, "scans_per_s": n / dt, "ms_per_scan": dt / n * 1e3, "points_per_scan": int(maxn)}
+           "scans": n, "scans_per_s": n / dt, "ms_per_scan": dt / n * 1e3, "points_per_scan": int(maxn),
+           "roofline": {"bound": "hbm", "alg_bytes_per_scan": per_scan, "achieved_gbs": per_scan * n / dt / 1e9,
+                        "peak_gbs": HBM_PEAK_GBS, "frac": per_scan * n / dt / 1e9 / HBM_PEAK_GBS,
+                        "note": "SURVEY §8d whole-pipeline bytes per scan (pipeline_alg_bytes, the last batch's "
+                                "counts) x scans/s"}}
     if cpu:  # the oracle on one core over the same stream (scans synthesised beforehand) until ~budget_s
         sc = L.synth_cfg("HDL-64E", 2)
         scans = [L.synth_scan(sc, k) for k in range(min(nscans, 40))]
@@ -365,20 +392,26 @@ def fleet_bench(L, streams: int, k: int, steps: int, device: int):
     """Auxiliary (not the headline metric): `streams` independent VLP-16
     streams in one fleet context (lego_fleet_create) on one GPU, k scans per
     stream per call, the stream-major batch resident in HBM.  Whole-GPU
-    scans/s over `steps` calls (host wall clock, like the headline).  Four
-    distinct synthetic streams are reused round-robin."""
+    scans/s over `steps` calls (host wall clock, like the headline).  Every
+    stream is its own synthetic drive (seed 10 + s), synthesised on the host's
+    cores beforehand."""
     import torch
+    from concurrent.futures import ThreadPoolExecutor
 
     cfg = L.sensor_cfg("VLP-16", L.hip_lib())
     nwin = steps + 1
-    src = []
-    for d in range(min(4, streams)):
+
+    def synth(d):  # the synthesis library runs outside the GIL
         sc = L.synth_cfg("VLP-16", 10 + d)
-        src.append([L.synth_scan(sc, j)[0] for j in range(k * nwin)])
+        return [L.synth_scan(sc, j)[0] for j in range(k * nwin)]
+
+    with ThreadPoolExecutor(max_workers=max(1, min(16, host_info()["affinity"]))) as ex:
+        src = list(ex.map(synth, range(streams)))
     maxn = max(len(p) for s in src for p in s)
-    wins = []
+    wins, npts = [], []
     for w in range(nwin):
-        scans = [src[s % len(src)][w * k + j] for s in range(streams) for j in range(k)]
+        scans = [src[s][w * k + j] for s in range(streams) for j in range(k)]
+        npts.append([len(p) for p in scans])
         off = np.zeros(len(scans) + 1, np.int64)
         off[1:] = np.cumsum([len(p) for p in scans])
         st = np.concatenate([np.arange(w * k, (w + 1) * k) * 0.1] * streams)
@@ -399,10 +432,18 @@ def fleet_bench(L, streams: int, k: int, steps: int, device: int):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     fl.close()
-    return {"workload": f"fleet: {streams} independent VLP-16 streams x {k} scans per call on one GPU "
-                        "(lego_fleet_create, two calls in flight), full per-scan pipeline incl. LM odometry",
+    # recs hold the last call's records (window nwin - 1), stream-major like its points
+    per_scan = statistics.mean(pipeline_alg_bytes(cfg, npts[-1][i], recs[i]) for i in range(streams * k))
+    sps = streams * k * steps / dt
+    return {"workload": f"fleet: {streams} independent VLP-16 streams (seeds 10..{9 + streams}) x {k} scans per "
+                        "call on one GPU (lego_fleet_create, two calls in flight), full per-scan pipeline incl. LM "
+                        "odometry",
             "streams": streams, "scans_per_stream_per_call": k, "calls": steps,
-            "scans_per_s": streams * k * steps / dt, "ms_per_call": dt / steps * 1e3}
+            "scans_per_s": sps, "ms_per_call": dt / steps * 1e3,
+            "roofline": {"bound": "hbm", "alg_bytes_per_scan": per_scan, "achieved_gbs": per_scan * sps / 1e9,
+                         "peak_gbs": HBM_PEAK_GBS, "frac": per_scan * sps / 1e9 / HBM_PEAK_GBS,
+                         "note": "SURVEY §8d whole-pipeline bytes per scan (pipeline_alg_bytes, the last call's "
+                                 "counts) x scans/s"}}
 
 
 def main():
@@ -413,6 +454,9 @@ def main():
     ap.add_argument("--batch", type=int, default=100, help="scans per step")
     ap.add_argument("--stream-len", type=int, default=600, help="synthetic stream length (C2: 600)")
     ap.add_argument("--sensor", default="VLP-16")
+    ap.add_argument("--seed", type=int, default=None, help="stream seed at N=1 (default 1: C2; C3 is 2)")
+    ap.add_argument("--no-handoff", action="store_true",
+                    help="skip the untimed mapping hand-off fetches (profiling runs: only the timed work)")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of oracle work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--stages", action="store_true", help="print per-stage times to stderr")
@@ -447,7 +491,8 @@ def main():
     lib = L.hip_lib()
     cfg = L.sensor_cfg(args.sensor, lib)
     # N=1: the C2 stream (seed 1).  N>1: C4, stream `rank` (seed 10 + rank).
-    seed = 1 if world == 1 else ms.stream_seed(ms.streams_of_rank(world, world, rank)[0])
+    seed = (args.seed if args.seed is not None else 1) if world == 1 else ms.stream_seed(
+        ms.streams_of_rank(world, world, rank)[0])
     pts, off, stamps, maxn = make_stream(L, args.sensor, seed, args.stream_len)
     B = args.batch
     nb = args.stream_len // B
@@ -513,11 +558,15 @@ def main():
     alg_bytes = 0.0
 
     gpu_recs = {}  # batch index within the stream -> its pose records (each pass starts from reset)
+    pipe_bytes = 0.0
 
     def account(done):
-        nonlocal alg_bytes, gathered
+        nonlocal alg_bytes, gathered, pipe_bytes
         for i, st, rc, pkt in done:
             gpu_recs[i % nb] = rc
+            j = i % nb
+            pipe_bytes += sum(pipeline_alg_bytes(cfg, int(off[j * B + k + 1] - off[j * B + k]), rc[k])
+                              for k in range(B))
             for k, v in st.items():
                 stage_acc[k] = stage_acc.get(k, 0.0) + v
             alg_bytes += odom_alg_bytes(rc)
@@ -544,7 +593,7 @@ def main():
 
     handoff = None
     if rank == 0:
-        handoff = mapping_handoff(gpu, B)
+        handoff = mapping_handoff(gpu, B) if not args.no_handoff else {}
         if gathered is not None:  # the last step's packets as rank 0 received them
             if native:
                 L.check(lib.lego_comm_wait(comm), "lego_comm_wait", lib)
@@ -577,7 +626,8 @@ def main():
         # rocprofv3 passes over this command, scripts/gpu_profile.sh) of the newest
         # committed summary, labelled with the commit it was measured at
         traffic, traffic_src = None, None
-        for pmc in (REPO / "profiles" / "r02_pmc_summary.json", REPO / "profiles" / "r01_pmc_summary.json"):
+        pmcs = sorted((REPO / "profiles").glob("r[0-9][0-9]_pmc_summary.json"), reverse=True)
+        for pmc in pmcs:
             if pmc.exists():
                 try:
                     js = json.loads(pmc.read_text())
@@ -655,7 +705,7 @@ def main():
                                     f"C4: one {args.sensor} stream per GPU (seeds 10..{9 + world}) @10Hz, full "
                                     f"per-scan pipeline incl. 2-step LM odometry, {B} scans/step, hand-off "
                                     "gathered to rank 0 every step"),
-                       "scans_per_step": B, "stream_len": args.stream_len,
+                       "scans_per_step": B, "stream_len": args.stream_len, "seed": seed,
                        "parallelism": f"stream-per-gpu x{world}",
                        "gather": ((("lego_comm (C-ABI RCCL send/recv)" if native else f"torch.distributed ({backend})")
                                    + ": per step, pose records + published clouds to rank 0") if world > 1 else None)},
@@ -664,7 +714,12 @@ def main():
                          "traffic_over_alg": (traffic / (alg_bytes / args.steps * 1.0 / n_odom)
                                               if traffic and alg_bytes else None),
                          "kernel": "k_odom", "launch_ms": odom_ms / n_odom, "launches_per_step": n_odom,
-                         "kernel_ms_per_step": odom_ms},
+                         "kernel_ms_per_step": odom_ms,
+                         "pipeline": {"alg_bytes_per_scan": pipe_bytes / (args.steps * B),
+                                      "achieved_gbs": pipe_bytes * world / dt / 1e9,
+                                      "frac": pipe_bytes * world / dt / 1e9 / HBM_PEAK_GBS,
+                                      "note": "SURVEY §8d whole-pipeline bytes of every timed scan (pipeline_alg_bytes) "
+                                              "over the timed region, all ranks"}},
             "cpu_baseline": cpu,
             "pose_delta_vs_oracle": pose_delta,
             "stages_ms_per_step": {k: v / args.steps for k, v in stage_acc.items()},
