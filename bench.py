@@ -340,7 +340,7 @@ def dense_bench(L, nscans: int, batch: int, device: int, cpu: bool = False, budg
     import torch
 
     cfg = L.sensor_cfg("HDL-64E", L.hip_lib())
-    nscans = max(nscans, 2 * batch)  # a warm-up batch and at least one timed one
+    nscans = max(nscans, 3 * batch)  # two warm-up batches and at least one timed one
     pts, off, stamps, maxn = make_stream(L, "HDL-64E", 2, nscans)
     nb = nscans // batch
     d_pts = torch.from_numpy(pts.view(np.uint8)).to(device)
@@ -349,19 +349,27 @@ def dense_bench(L, nscans: int, batch: int, device: int, cpu: bool = False, budg
     recs = (L.PoseRec * batch)()
     sub = lambda j: g.submit_device(d_pts.data_ptr(), d_off[j].data_ptr(), stamps[j * batch:(j + 1) * batch],  # noqa: E731
                                     batch)
-    sub(0)  # warm-up batch
-    g.wait(recs)
+    warm = 2  # as the headline loop: two warm-up batches, then the rest two deep
+    for j in range(warm):
+        sub(j)
+    for j in range(warm):
+        g.wait(recs)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for j in range(1, nb):
-        sub(j)
-        if j > 1:
+    inflight = 0
+    for j in range(warm, nb):
+        if inflight == 2:
             g.wait(recs)
-    g.wait(recs)
+            inflight -= 1
+        sub(j)
+        inflight += 1
+    while inflight:
+        g.wait(recs)
+        inflight -= 1
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     g.close()
-    n = (nb - 1) * batch
+    n = (nb - warm) * batch
     j = nb - 1  # recs: the last batch's records
     per_scan = statistics.mean(pipeline_alg_bytes(cfg, int(off[j * batch + k + 1] - off[j * batch + k]), recs[k])
                                for k in range(batch))
@@ -675,6 +683,16 @@ def main():
             for k, v in sorted(stage_acc.items(), key=lambda kv: -kv[1]):
                 print(f"  {k:14s} {v / args.steps:9.3f} ms/step  {100 * v / max(tot, 1e-9):5.1f}%",
                       file=sys.stderr)
+        # The headline context is done: close it before the aux lines.  A
+        # process's HIP streams share GPU_MAX_HW_QUEUES (4) hardware queues, and
+        # an idle context's two streams left open make a later context's
+        # extraction and odometry streams share a queue (C3 measured 4.0 k
+        # instead of 5.1 k scans/s that way, scripts/dense_probe3.py).
+        if comm is not None:
+            lib.lego_comm_destroy(comm)
+            comm = None
+        gpu.close()
+        gpu = None
         aux = {"mapping_handoff": handoff}
         if args.mapping_steps > 0 and world == 1:
             aux["scan_to_map_c5"] = mapping_bench(L, args.mapping_steps, not args.no_cpu)
@@ -728,7 +746,8 @@ def main():
         print(json.dumps(line))
     if comm is not None:
         lib.lego_comm_destroy(comm)
-    gpu.close()
+    if gpu is not None:
+        gpu.close()
     if dist:
         dist.destroy_process_group()
 
