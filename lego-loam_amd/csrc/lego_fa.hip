@@ -20,6 +20,7 @@
 #include "lego_device.h"
 #include "lego_introsort.h"
 #include "lego_vgsort.h"
+#include "lego_vgsort_wave.h"
 #include "lego_kernels.h"
 
 namespace lego {
@@ -843,13 +844,102 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
 // summation order), one lane per voxel summing its points in that order into
 // registers, then the centroids over the slot.  The slot's count goes from
 // the less-flat set's size to the voxels'.
+// the per-voxel centroid of PCL's VoxelGrid: the points of sorted positions
+// [t, u) (one voxel), summed in that order from the ring's slot
+__device__ __forceinline__ float4 lfv_centroid(const float4* slot, const uint16_t* val, const uint32_t* key, int t,
+                                               int K) {
+  const uint32_t k = key[t];
+  float cx = 0, cy = 0, cz = 0, ci = 0;
+  int u = t;
+  for (; u < K && key[u] == k; ++u) {
+    const float4 q = slot[val[u]];
+    cx += q.x; cy += q.y; cz += q.z; ci += q.w;
+  }
+  const float n = (float)(u - t);
+  return make_float4(cx / n, cy / n, cz / n, ci / n);
+}
+
+// A ring of up to kVgWaveMax less-flat points by ONE wave (lego_vgsort_wave.h:
+// the same permutation as the block sort, no workgroup barrier): the same
+// steps as lfv_block below, wave-wide.  lds: the wave's key / payload /
+// scratch words.
+constexpr int kLfvWaveRows = kVgWaveMax / 64;
+constexpr size_t kLfvWaveLds = (size_t)4 * kVgWaveMax * 10;  // four waves' key (4 B), payload (2 B), scratch (4 B)
+__device__ void lfv_wave(const BatchBufs& bb, const DevCfg& c, int ring, int b, unsigned char* lds) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (ring >= c.N) return;
+  int* cnt = bb.r_cnt + ((size_t)b * c.N + ring) * 4;
+  const int K = cnt[3];
+  if (K <= 0 || K > kVgWaveMax) return;  // wave-uniform
+  float4* slot = bb.r_lflat + (size_t)b * c.P + (size_t)ring * c.H;
+  uint32_t* key = (uint32_t*)lds + (size_t)wave * kVgWaveMax;
+  uint16_t* val = (uint16_t*)(lds + (size_t)16 * kVgWaveMax) + (size_t)wave * kVgWaveMax;
+  uint32_t* scw = (uint32_t*)(lds + (size_t)24 * kVgWaveMax) + (size_t)wave * kVgWaveMax;
+  const float inv = 1.0f / 0.2f;
+  float mn[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
+  float mx[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+  for (int t = lane; t < K; t += 64) {
+    const float4 p = slot[t];
+    mn[0] = fminf(mn[0], p.x); mn[1] = fminf(mn[1], p.y); mn[2] = fminf(mn[2], p.z);
+    mx[0] = fmaxf(mx[0], p.x); mx[1] = fmaxf(mx[1], p.y); mx[2] = fmaxf(mx[2], p.z);
+  }
+  for (int q = 0; q < 3; ++q) {
+    for (int o = 32; o > 0; o >>= 1) {
+      mn[q] = fminf(mn[q], __shfl_xor(mn[q], o, 64));
+      mx[q] = fmaxf(mx[q], __shfl_xor(mx[q], o, 64));
+    }
+  }
+  const long long dx = (long long)((mx[0] - mn[0]) * inv) + 1;
+  const long long dy = (long long)((mx[1] - mn[1]) * inv) + 1;
+  const long long dz = (long long)((mx[2] - mn[2]) * inv) + 1;
+  if (dx * dy * dz > (long long)INT_MAX) return;  // PCL keeps the cloud (it is in the slot already)
+  int mb[3], xb[3];
+  for (int q = 0; q < 3; ++q) {
+    mb[q] = (int)floorf(mn[q] * inv);
+    xb[q] = (int)floorf(mx[q] * inv);
+  }
+  const int d0 = xb[0] - mb[0] + 1, d1 = xb[1] - mb[1] + 1;
+  for (int t = lane; t < K; t += 64) {
+    const float4 p = slot[t];
+    const int i0 = (int)(floorf(p.x * inv) - (float)mb[0]);
+    const int i1 = (int)(floorf(p.y * inv) - (float)mb[1]);
+    const int i2 = (int)(floorf(p.z * inv) - (float)mb[2]);
+    key[t] = (uint32_t)(i0 + i1 * d0 + i2 * d0 * d1);
+    val[t] = (uint16_t)t;
+  }
+  vg_wave_sync();
+  vg_wave_sort(key, val, scw, K);
+  // centroids into registers (every read of the slot done), then over the slot
+  float4 cen[kLfvWaveRows];
+  int at[kLfvWaveRows];
+  int outc = 0;
+  const unsigned long long below = (1ull << lane) - 1;
+#pragma unroll
+  for (int j = 0; j < kLfvWaveRows; ++j) {
+    at[j] = -1;
+    const int t = (j << 6) + lane;
+    const bool head = t < K && (t == 0 || key[t] != key[t - 1]);
+    const unsigned long long m = __ballot(head);
+    if (head) {
+      cen[j] = lfv_centroid(slot, val, key, t, K);
+      at[j] = outc + (int)__popcll(m & below);
+    }
+    outc += (int)__popcll(m);
+  }
+  vg_wave_sync();  // the wave's slot reads have returned
+#pragma unroll
+  for (int j = 0; j < kLfvWaveRows; ++j)
+    if (at[j] >= 0) slot[at[j]] = cen[j];
+  if (lane == 0) cnt[3] = outc;
+}
+
 constexpr int kLfvMaxPer = 8;  // voxels per thread (H <= kLfvMaxPer * kExtractThreads)
 __host__ __device__ inline size_t lfvox_lds_bytes(int H) {
   return (((size_t)H * 6 + 15) & ~(size_t)15) + vg_sort_scratch_bytes(H, kExtractThreads) + 64;
 }
-__global__ void __launch_bounds__(kExtractThreads, 5) k_lf_voxel(BatchBufs bb, DevCfg c) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-  const int ring = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+__device__ void lfv_block(const BatchBufs& bb, const DevCfg& c, int ring, int b, int waveMax,
+                          unsigned char* lds_raw) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int H = c.H;
   uint32_t* key = (uint32_t*)lds_raw;
   uint16_t* val = (uint16_t*)(lds_raw + (size_t)H * 4);
@@ -859,7 +949,7 @@ __global__ void __launch_bounds__(kExtractThreads, 5) k_lf_voxel(BatchBufs bb, D
   int* cnt = bb.r_cnt + ((size_t)b * c.N + ring) * 4;
   float4* slot = bb.r_lflat + (size_t)b * c.P + (size_t)ring * H;
   const int K = cnt[3];
-  if (K <= 0) return;
+  if (K <= waveMax) return;  // a wave's (or empty)
   const float inv = 1.0f / 0.2f;
   float mn[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
   float mx[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
@@ -916,15 +1006,7 @@ __global__ void __launch_bounds__(kExtractThreads, 5) k_lf_voxel(BatchBufs bb, D
     int tot;
     const int r = block_rank(head, misc, &tot);
     if (head) {
-      const uint32_t k = key[t];
-      float cx = 0, cy = 0, cz = 0, ci = 0;
-      int u = t;
-      for (; u < K && key[u] == k; ++u) {
-        const float4 q = slot[val[u]];
-        cx += q.x; cy += q.y; cz += q.z; ci += q.w;
-      }
-      const float n = (float)(u - t);
-      cen[j] = make_float4(cx / n, cy / n, cz / n, ci / n);
+      cen[j] = lfv_centroid(slot, val, key, t, K);
       at[j] = outc + r;
     }
     outc += tot;
@@ -934,6 +1016,18 @@ __global__ void __launch_bounds__(kExtractThreads, 5) k_lf_voxel(BatchBufs bb, D
   for (int j = 0; j < kLfvMaxPer; ++j)
     if (at[j] >= 0) slot[at[j]] = cen[j];
   if (tid == 0) cnt[3] = outc;
+}
+
+// The batch's per-ring VoxelGrids in one launch, so small and large rings
+// interleave: workgroups [0, g4) of each scan take four rings each, a ring of
+// up to kVgWaveMax points per wave (lfv_wave); workgroups [g4, g4 + N) one
+// larger ring each with the whole workgroup (lfv_block).  g4 = 0 (diagnostic
+// LEGO_LFV_WAVE=0): every ring by a workgroup.
+__global__ void __launch_bounds__(kExtractThreads, 4) k_lf_voxel(BatchBufs bb, DevCfg c, int g4) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  const int b = blockIdx.y;
+  if ((int)blockIdx.x < g4) lfv_wave(bb, c, (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6), b, lds_raw);
+  else lfv_block(bb, c, (int)blockIdx.x - g4, b, g4 > 0 ? kVgWaveMax : 0, lds_raw);
 }
 
 #ifndef EXTRACT_MINWAVES
@@ -1046,12 +1140,14 @@ void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_ca
   if (bb.imu) k_fa_imu_start<<<(B + 63) / 64, 64, 0, s>>>(bb, c);
   k_fa_point<<<gpts, 256, 0, s>>>(bb, c);
   tm->mark("fa.extract", s);
-  const size_t lds = extract_lds_bytes(c.H) + (std::getenv("LEGO_XLDS_PAD") ? (size_t)std::atoi(std::getenv("LEGO_XLDS_PAD")) : 0);
+  const size_t lds = extract_lds_bytes(c.H);
   k_extract<<<dim3(c.N, B), kExtractThreads, lds, s>>>(bb, c);
   tm->mark("fa.fixup", s);
   k_fa_fixup<<<S, kExtractThreads, lds, s>>>(bb, c, B / S, d_carry);
   tm->mark("fa.voxel", s);
-  k_lf_voxel<<<dim3(c.N, B), kExtractThreads, lfvox_lds_bytes(c.H), s>>>(bb, c);
+  static const bool waveOn = !std::getenv("LEGO_LFV_WAVE") || std::atoi(std::getenv("LEGO_LFV_WAVE")) != 0;
+  const int g4 = waveOn ? (c.N + 3) / 4 : 0;
+  k_lf_voxel<<<dim3(g4 + c.N, B), kExtractThreads, std::max(kLfvWaveLds, lfvox_lds_bytes(c.H)), s>>>(bb, c, g4);
   tm->mark("fa.compact", s);
   k_fa_compact<<<dim3(c.N, B), 256, 0, s>>>(bb, c);
 }

@@ -389,6 +389,8 @@ __device__ __forceinline__ double mo_wave_sum(double v) {
   return (mo_rdlane(v, 0) + mo_rdlane(v, 16)) + (mo_rdlane(v, 32) + mo_rdlane(v, 48));
 }
 
+__device__ void mo_solve_tail(MoState* st, const double* tot, int iterCount, float* ws, int* wsi);
+
 constexpr int kMoSums = 21 + 6 + 1;  // AtA upper triangle, AtB, row count
 
 __global__ void __launch_bounds__(kMoSolveThreads) k_mo_solve(MoState* st, const MoCounts* cnt, const float* rows,
@@ -430,6 +432,13 @@ __global__ void __launch_bounds__(kMoSolveThreads) k_mo_solve(MoState* st, const
     for (int w = 0; w < kMoSolveThreads / 64; ++w) sum += red[w][k];
     tot[k] = sum;
   }
+  mo_solve_tail(st, tot, iterCount, ws, wsi);
+}
+
+// LMOptimization (:1229-1327) from the reduced sums, one thread: the 6x6 QR
+// solve, the iteration-0 eigen analysis (degeneracy), the update and the
+// convergence test.  ws / wsi: LDS workspace of the eigen / inverse.
+__device__ void mo_solve_tail(MoState* st, const double* tot, int iterCount, float* ws, int* wsi) {
   const int M = (int)tot[27];
   st->rowsLast = M;
   st->iterations = iterCount + 1;
@@ -720,8 +729,7 @@ int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, h
   for (int it = 0; it < 10; ++it) {
     if (qcap > 0)
       k_mo_rows<<<grid_for(qcap, kMoRowsThreads / kKnnLanes), kMoRowsThreads, 0, s>>>(
-          m.st, m.cnt, m.cornerDS, m.surfTotalDS, m.cornerIx, m.surfIx,
-                                                   m.cornerMapDS, m.surfMapDS, m.rows, qcap);
+          m.st, m.cnt, m.cornerDS, m.surfTotalDS, m.cornerIx, m.surfIx, m.cornerMapDS, m.surfMapDS, m.rows, qcap);
     k_mo_solve<<<1, kMoSolveThreads, 0, s>>>(m.st, m.cnt, m.rows, qcap, it);
   }
   k_mo_finish<<<1, 64, 0, s>>>(m.st, a.imuOn, a.imuRoll, a.imuPitch);

@@ -36,6 +36,7 @@ __device__ unsigned long long g_wst[16], g_wcnt[16];
   } while (0)
 #define VG_CLOCK() clock64()
 #include "lego_vgsort.h"
+#include "lego_vgsort_wave.h"
 
 using namespace lego;
 
@@ -95,6 +96,25 @@ __global__ void __launch_bounds__(256) k_vgsort(const uint32_t* keys, int n, uin
   for (int t = threadIdx.x; t < n; t += blockDim.x) {
     out[(size_t)blockIdx.x * n + t] = key[t];
     outv[(size_t)blockIdx.x * n + t] = val[t];
+  }
+}
+
+// one ring per wave (n <= kVgWaveMax): four rings per workgroup, no barrier
+__global__ void __launch_bounds__(256) k_vgsort_wave(const uint32_t* keys, int n, uint32_t* out, uint16_t* outv,
+                                                     int G) {
+  __shared__ uint32_t key[4][kVgWaveMax];
+  __shared__ uint16_t val[4][kVgWaveMax];
+  __shared__ uint32_t cw[4][kVgWaveMax];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int ring = blockIdx.x * 4 + wave;
+  if (ring >= G) return;
+  const uint32_t* k = keys + (size_t)ring * n;
+  for (int t = lane; t < n; t += 64) { key[wave][t] = k[t]; val[wave][t] = (uint16_t)t; }
+  vg_wave_sync();
+  vg_wave_sort(key[wave], val[wave], cw[wave], n);
+  for (int t = lane; t < n; t += 64) {
+    out[(size_t)ring * n + t] = key[wave][t];
+    outv[(size_t)ring * n + t] = val[wave][t];
   }
 }
 
@@ -163,8 +183,76 @@ static int run_file(const char* path, int reps) {
   return 0;
 }
 
+static int run_wave(int n, int G) {
+  for (int shape = 0; shape < 4; ++shape) {
+    std::vector<uint32_t> h((size_t)G * n);
+    for (int g = 0; g < G; ++g) {
+      uint64_t s = 88172645463325252ull + g;
+      for (int i = 0; i < n; ++i) {
+        s ^= s << 13; s ^= s >> 7; s ^= s << 17;
+        uint32_t key;
+        if (shape == 3) {  // a whole ring (the main mode's shape 0)
+          const double th = 2 * M_PI * i / n + 0.001 * g;
+          const double r = 12 + 3 * std::sin(3 * th + g) + 0.05 * (double)(s % 100) / 100;
+          const float x = (float)(r * std::cos(th)), y = (float)(r * std::sin(th)), z = -1.2f;
+          key = (uint32_t)((int)(std::floor(x * 5.0f) + 80) + (int)(std::floor(y * 5.0f) + 80) * 161 +
+                           (int)(std::floor(z * 5.0f) + 7) * 161 * 161);
+        } else if (shape == 0) {  // a ring's arc, 0.2 m voxels, a few points per voxel
+          const double th = 0.6 * M_PI * i / n + 0.01 * g;
+          const double r = 8 + 2 * std::sin(3 * th + g) + 0.05 * (double)(s % 100) / 100;
+          const float x = (float)(r * std::cos(th)), y = (float)(r * std::sin(th));
+          key = (uint32_t)((int)(std::floor(x * 5.0f) + 80) + (int)(std::floor(y * 5.0f) + 80) * 161);
+        } else if (shape == 1) {
+          key = (uint32_t)(s % (uint64_t)(n / 2 + 1));
+        } else {
+          key = (uint32_t)(s % 100000u);
+        }
+        h[(size_t)g * n + i] = key;
+      }
+    }
+    uint32_t *dk, *dout;
+    uint16_t* dv;
+    hipMalloc(&dk, h.size() * 4);
+    hipMalloc(&dout, h.size() * 4);
+    hipMalloc(&dv, h.size() * 2);
+    hipMemcpy(dk, h.data(), h.size() * 4, hipMemcpyHostToDevice);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    auto timeit = [&](const char* name, auto&& launch) {
+      launch();
+      hipDeviceSynchronize();
+      hipEventRecord(e0);
+      for (int r = 0; r < 5; ++r) launch();
+      hipEventRecord(e1);
+      hipEventSynchronize(e1);
+      float ms;
+      hipEventElapsedTime(&ms, e0, e1);
+      printf("  %-22s %9.2f us/launch  %7.4f us/ring\n", name, 1000 * ms / 5, 1000 * ms / 5 / G);
+    };
+    printf("%s keys, n=%d, %d rings\n", shape == 0 ? "arc" : (shape == 1 ? "dup" : (shape == 2 ? "random" : "ring")), n,
+           G);
+    timeit("block (ring per WG)", [&] { k_vgsort<<<G, 256>>>(dk, n, dout, dv); });
+    timeit("wave (ring per wave)", [&] { k_vgsort_wave<<<(G + 3) / 4, 256>>>(dk, n, dout, dv, G); });
+    std::vector<uint16_t> hv(h.size());
+    hipMemcpy(hv.data(), dv, hv.size() * 2, hipMemcpyDeviceToHost);
+    long bad = 0;
+    for (int g = 0; g < G; ++g) {
+      std::vector<Idx> a(n);
+      for (int i = 0; i < n; ++i) a[i] = {h[(size_t)g * n + i], (uint32_t)i};
+      std::sort(a.begin(), a.end());
+      for (int i = 0; i < n; ++i)
+        if (a[i].t != hv[(size_t)g * n + i]) { ++bad; break; }
+    }
+    printf("  wave sort vs std::sort: %ld of %d rings differ\n", bad, G);
+    hipFree(dk); hipFree(dout); hipFree(dv);
+  }
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc > 2 && std::string(argv[1]) == "file") return run_file(argv[2], argc > 3 ? atoi(argv[3]) : 3);
+  if (argc > 3 && std::string(argv[1]) == "wave") return run_wave(atoi(argv[2]), atoi(argv[3]));
   const int n = argc > 1 ? atoi(argv[1]) : 1800;
   const int G = argc > 2 ? atoi(argv[2]) : 1536;
   const int shapes = argc > 3 ? atoi(argv[3]) : 2;
