@@ -476,6 +476,16 @@ int lego_voxel_grid(lego_ctx* ctx, const lego_point_xyzi* in, int32_t n, float l
  * segments (depth budget spent), [6] non-finite points, [7] device time in
  * microseconds.  Diagnostics for tests and benchmarks. */
 int lego_voxel_grid_stats(lego_ctx* ctx, int32_t stats[8]);
+/* The permutation libstdc++'s std::sort gives (key, index) pairs compared by
+ * key alone — the sort pcl::VoxelGrid::applyFilter runs on (voxel idx, point)
+ * (voxel_grid.hpp; featureAssociation.cpp:778-782, mapOptmization.cpp:1058-1091),
+ * whose order of equal keys is the VoxelGrid's summation order — computed on
+ * the device: perm[i] = the input index at sorted position i.  wave = 0: the
+ * workgroup sort the VoxelGrids use (n <= 8192); wave = 1: the one-wave sort
+ * of the per-ring less-flat VoxelGrid (n <= 512).  heap_pieces (may be NULL):
+ * how many pieces the depth budget sent to std::__partial_sort. */
+int lego_sort_permutation(lego_ctx* ctx, const uint32_t* keys, int32_t n, int32_t wave, int32_t* perm,
+                          int32_t* heap_pieces);
 
 /* Last device error string (static storage). */
 const char* lego_last_error(void);

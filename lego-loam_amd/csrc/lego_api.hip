@@ -1225,6 +1225,36 @@ int lego_mo_set_map(lego_ctx* x, const lego_point_xyzi* corner, int32_t n_corner
   return LEGO_OK;
 }
 
+int lego_sort_permutation(lego_ctx* x, const uint32_t* keys, int32_t n, int32_t wave, int32_t* perm,
+                          int32_t* heap_pieces) {
+  if (!x || n < 0 || (n > 0 && (!keys || !perm)) || (wave != 0 && wave != 1)) return LEGO_E_ARG;
+  if (n > (wave ? 512 : 8192)) {
+    set_err("lego_sort_permutation: n = %d above the %s sort's %d", n, wave ? "wave" : "block", wave ? 512 : 8192);
+    return LEGO_E_CAPACITY;
+  }
+  HIPCHK(hipSetDevice(x->device));
+  uint32_t* dk = nullptr;
+  int* dp = nullptr;
+  HIPCHK(hipMallocAsync((void**)&dk, sizeof(uint32_t) * (size_t)(n + 1) + sizeof(int) * (size_t)(n + 2), x->stream));
+  dp = (int*)(dk + n + 1);
+  HIPCHK(hipMemsetAsync(dp, 0, sizeof(int), x->stream));
+  if (n) HIPCHK(hipMemcpyAsync(dk, keys, sizeof(uint32_t) * n, hipMemcpyHostToDevice, x->stream));
+  const int rc = sort_perm_device(dk, n, wave, dp + 1, dp, x->stream);
+  int h = 0;
+  if (rc == 0) {
+    if (n) HIPCHK(hipMemcpyAsync(perm, dp + 1, sizeof(int) * n, hipMemcpyDeviceToHost, x->stream));
+    HIPCHK(hipMemcpyAsync(&h, dp, sizeof(int), hipMemcpyDeviceToHost, x->stream));
+  }
+  HIPCHK(hipFreeAsync(dk, x->stream));
+  HIPCHK(hipStreamSynchronize(x->stream));
+  if (rc) {
+    set_err("lego_sort_permutation: launch failed");
+    return LEGO_E_DEVICE;
+  }
+  if (heap_pieces) *heap_pieces = h;
+  return LEGO_OK;
+}
+
 int lego_voxel_grid(lego_ctx* x, const lego_point_xyzi* in, int32_t n, float leaf, lego_point_xyzi* out,
                     int32_t* n_out) {
   if (!x || !n_out || n < 0 || (n > 0 && (!in || !out)) || !(leaf > 0.f)) return LEGO_E_ARG;

@@ -908,7 +908,7 @@ __device__ void lfv_wave(const BatchBufs& bb, const DevCfg& c, int ring, int b, 
     val[t] = (uint16_t)t;
   }
   vg_wave_sync();
-  vg_wave_sort(key, val, scw, K);
+  vg_wave_sort(key, val, scw, K);  // a whole array: budget 2 lg K
   // centroids into registers (every read of the slot done), then over the slot
   float4 cen[kLfvWaveRows];
   int at[kLfvWaveRows];

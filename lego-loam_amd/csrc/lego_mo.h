@@ -158,6 +158,10 @@ int vg_rounds_for(int n);
 // the VgScratch counters of the last voxel_grid_device on s (16 ints, synchronous)
 int vg_read_ctl(const VgScratch& v, int* ctl16, hipStream_t s);
 int mo_set_map_device(MoDev& m, int nCornerMap, int nSurfMap, hipStream_t s);
+// libstdc++'s std::sort permutation of (key, index) by key on the device
+// (lego_vg.hip): wave = 0 the block sort (n <= 8192), 1 one wave's (n <= 512);
+// heap: the heap-sorted pieces are counted into it.
+int sort_perm_device(const uint32_t* keys, int n, int wave, int* perm, int* heap, hipStream_t s);
 int index_build_device(const float4* pts, int n, const int* nDev, MoIndex& ix, const VgScratch& v, hipStream_t s);
 // One performLoopClosure over the keyframe store (tnow = timeLaserOdometry).
 // Returns MO_OK (hostState holds the result), MO_E_LAUNCH, or MO_E_MAP_CAP when

@@ -31,6 +31,7 @@
 #include "lego_kernels.h"
 #include "lego_mo.h"
 #include "lego_vgsort.h"
+#include "lego_vgsort_wave.h"
 
 namespace lego {
 
@@ -720,6 +721,38 @@ int vg_scratch_alloc(VgScratch& v, int cap, void* ctx, int (*alloc)(void* ctx, v
   for (auto& a : as)
     if (alloc(ctx, a.p, a.b)) return -1;
   return 0;
+}
+
+// ---------------------------------------------------------------- sort permutation
+// libstdc++'s std::sort permutation of (key, index) pairs compared by key
+// (the VoxelGrid's sort) for one array: wave = 0 the block sort (one
+// 1024-thread workgroup, n <= kSortPermBlockMax), wave = 1 one wave's sort
+// (n <= kVgWaveMax).  perm[i] = the index of the pair at sorted position i.
+constexpr int kSortPermBlockMax = 8192;  // vg_sort_max(1024)
+__global__ void __launch_bounds__(1024) k_sort_perm(const uint32_t* keys, int n, int wave, int* perm, int* heap) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  uint32_t* key = (uint32_t*)lds_raw;
+  uint16_t* val = (uint16_t*)(lds_raw + (size_t)4 * kSortPermBlockMax);
+  unsigned char* sc = lds_raw + (size_t)6 * kSortPermBlockMax;
+  if (wave) {
+    if (threadIdx.x >= 64) return;
+    for (int i = threadIdx.x; i < n; i += 64) { key[i] = keys[i]; val[i] = (uint16_t)i; }
+    vg_wave_sync();
+    vg_wave_sort(key, val, (uint32_t*)sc, n, -1, heap);
+    for (int i = threadIdx.x; i < n; i += 64) perm[i] = val[i];
+    return;
+  }
+  for (int i = threadIdx.x; i < n; i += blockDim.x) { key[i] = keys[i]; val[i] = (uint16_t)i; }
+  __syncthreads();
+  vg_block_sort(vg_sort_carve(key, val, sc, n, (int)blockDim.x), n, -1, heap);
+  for (int i = threadIdx.x; i < n; i += blockDim.x) perm[i] = val[i];
+}
+size_t sort_perm_lds_bytes() { return (size_t)6 * kSortPermBlockMax + vg_sort_scratch_bytes(kSortPermBlockMax, 1024); }
+int sort_perm_device(const uint32_t* keys, int n, int wave, int* perm, int* heap, hipStream_t s) {
+  if (n < 0 || n > (wave ? kVgWaveMax : kSortPermBlockMax)) return -1;
+  if (n == 0) return 0;
+  k_sort_perm<<<1, 1024, sort_perm_lds_bytes(), s>>>(keys, n, wave, perm, heap);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 // ---------------------------------------------------------------- NN index

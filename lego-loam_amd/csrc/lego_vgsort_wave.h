@@ -339,10 +339,12 @@ __device__ void vg_wave_sortR(uint32_t* key, V* val, uint32_t* c, int s, int m, 
 
 // std::sort of key[0, n) / val[0, n), n <= kVgWaveMax, by the calling wave
 // alone; c: an LDS scratch word per key.  Ends with the wave in sync.
+// depth: the introsort loop's budget (2 lg n for a whole array, less for a
+// segment of one; -1 = 2 lg n); heapStat: bumped per heap-sorted piece.
 template <typename V>
-__device__ void vg_wave_sort(uint32_t* key, V* val, uint32_t* c, int n, int* heapStat = nullptr) {
+__device__ void vg_wave_sort(uint32_t* key, V* val, uint32_t* c, int n, int depth = -1, int* heapStat = nullptr) {
   if (n <= 1) return;
-  const int D = 2 * (31 - __builtin_clz((unsigned)n));
+  const int D = depth >= 0 ? depth : 2 * (31 - __builtin_clz((unsigned)n));
   if (n <= 64) vg_wave_sort64(key, val, 0, n, D, heapStat);
   else vg_wave_sortR(key, val, c, 0, n, D, heapStat);
 }

@@ -242,6 +242,7 @@ def oracle_lib() -> C.CDLL:
     lib = _load(ORACLE_LIB, "oracle")
     lib.lego_oracle_sensor_preset.argtypes = [C.c_char_p, C.POINTER(SensorCfg)]
     lib.lego_oracle_create.argtypes = [C.POINTER(SensorCfg), C.POINTER(C.c_void_p)]
+    lib.lego_oracle_sort_permutation.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
     lib.lego_oracle_destroy.argtypes = [C.c_void_p]
     lib.lego_oracle_set_options.argtypes = [C.c_void_p, C.c_uint32]
     lib.lego_oracle_ip_process.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_double,
@@ -276,7 +277,7 @@ HIP_EXPORTS = ["lego_sensor_preset", "lego_create", "lego_fleet_create", "lego_d
                "lego_odom_profile", "lego_extract_profile", "lego_handoff_pack", "lego_handoff_pack_into", "lego_handoff_unpack", "lego_comm_unique_id",
                "lego_comm_create", "lego_comm_destroy", "lego_comm_gather_handoff", "lego_comm_handoff",
                "lego_comm_gather_handoff_ex", "lego_comm_wait", "lego_comm_handoff_device",
-               "lego_voxel_grid", "lego_voxel_grid_stats"]
+               "lego_voxel_grid", "lego_voxel_grid_stats", "lego_sort_permutation"]
 
 
 def hip_lib() -> C.CDLL:
@@ -327,6 +328,8 @@ def hip_lib() -> C.CDLL:
     lib.lego_voxel_grid.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_float, C.c_void_p,
                                     C.POINTER(C.c_int32)]
     lib.lego_voxel_grid_stats.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
+    lib.lego_sort_permutation.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p,
+                                          C.POINTER(C.c_int32)]
     lib.lego_last_error.restype = C.c_char_p
     lib.lego_odom_profile.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
     lib.lego_extract_profile.argtypes = [C.c_void_p, C.c_void_p]
@@ -724,6 +727,16 @@ class Lego:
         keys = ("sorted", "voxels", "rounds", "local_segments", "slow_segments", "heap_segments", "nonfinite",
                 "device_us")
         return out[:n.value].copy(), dict(zip(keys, list(st)))
+
+    def sort_permutation(self, keys: np.ndarray, wave: bool = False) -> tuple[np.ndarray, int]:
+        """lego_sort_permutation: std::sort's permutation of (key, index) by key
+        on the device (block or one-wave sort) and the heap-sorted piece count."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint32)
+        perm = np.zeros(max(len(keys), 1), np.int32)
+        heap = C.c_int32()
+        check(self.lib.lego_sort_permutation(self.h, keys.ctypes.data, len(keys), int(wave), perm.ctypes.data,
+                                             C.byref(heap)), "lego_sort_permutation", self.lib)
+        return perm[:len(keys)].copy(), heap.value
 
     def handoff_packet(self) -> np.ndarray:
         """lego_handoff_pack of the last waited batch, copied to the host

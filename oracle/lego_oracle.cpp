@@ -1480,6 +1480,20 @@ extern "C" int lego_oracle_voxel_grid(const lego_point_xyzi* in, int32_t n, floa
   return LEGO_OK;
 }
 
+extern "C" int lego_oracle_sort_permutation(const uint32_t* keys, int32_t n, int32_t* perm) {
+  if (n < 0 || (n && (!keys || !perm))) return LEGO_E_ARG;
+  struct KI {  // voxel_grid.hpp's cloud_point_index_idx: compared by idx alone
+    uint32_t idx;
+    int32_t i;
+    bool operator<(const KI& o) const { return idx < o.idx; }
+  };
+  std::vector<KI> a((size_t)n);
+  for (int32_t i = 0; i < n; ++i) a[(size_t)i] = {keys[i], i};
+  std::sort(a.begin(), a.end());
+  for (int32_t i = 0; i < n; ++i) perm[i] = a[(size_t)i].i;
+  return LEGO_OK;
+}
+
 extern "C" float lego_oracle_atan2f(float y, float x) { return lego_atan2f(y, x); }
 extern "C" float lego_oracle_sinf(float x) { return lego_sinf(x); }
 extern "C" float lego_oracle_cosf(float x) { return lego_cosf(x); }

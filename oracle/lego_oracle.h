@@ -58,6 +58,9 @@ int lego_oracle_systems(lego_oracle* o, int32_t kind, float* out, int32_t cap, i
 /* Stand-alone pieces for known-answer tests. */
 int lego_oracle_voxel_grid(const lego_point_xyzi* in, int32_t n, float leaf,
                            int32_t pcl_sort, lego_point_xyzi* out, int32_t* n_out);
+/* libstdc++'s std::sort of (key, index) pairs by key (PCL VoxelGrid's
+ * sort): perm[i] = the index at sorted position i. */
+int lego_oracle_sort_permutation(const uint32_t* keys, int32_t n, int32_t* perm);
 float lego_oracle_atan2f(float y, float x);
 float lego_oracle_sinf(float x);
 float lego_oracle_cosf(float x);

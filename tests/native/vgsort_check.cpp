@@ -125,6 +125,23 @@ int main(int argc, char** argv) {
     fwrite(k.data(), sizeof(unsigned), k.size(), stdout);
     return 0;
   }
+  if (argc == 3 && std::string(argv[1]) == "heaps") {  // heap-sorted pieces std::sort takes on these keys
+    std::vector<unsigned> k;
+    unsigned x;
+    FILE* f = fopen(argv[2], "rb");
+    if (!f) return 2;
+    while (fread(&x, sizeof x, 1, f) == 1) k.push_back(x);
+    fclose(f);
+    std::vector<Idx> a(k.size()), b;
+    for (size_t i = 0; i < k.size(); ++i) a[i] = {k[i], (unsigned)i};
+    b = a;
+    std::sort(a.begin(), a.end(), std::less<Idx>());
+    emulate(b);
+    for (size_t i = 0; i < a.size(); ++i)
+      if (a[i].cpi != b[i].cpi) return 3;
+    printf("%d\n", heap_segments);
+    return 0;
+  }
   const int trials = argc > 1 ? atoi(argv[1]) : 6000;
   long bad = 0, total = 0;
   auto check = [&](const std::vector<unsigned>& keys) {

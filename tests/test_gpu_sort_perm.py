@@ -1,0 +1,82 @@
+"""lego_sort_permutation — the device's libstdc++ std::sort permutation of
+(key, index) pairs compared by key (PCL VoxelGrid's sort; lego_vgsort.h's
+workgroup sort and lego_vgsort_wave.h's one-wave sort of the per-ring
+less-flat VoxelGrid) — against the oracle's real std::sort
+(lego_oracle_sort_permutation): the same permutation on random keys with ties,
+sorted / reversed / constant / organ-pipe arrays, every size around the
+16-key insertion-sort threshold and the one-wave sort's 64-key and 512-key
+bounds, and McIlroy-adversary keys (tests/golden/vg_killer.npz, made by
+tests/golden/make_vg_killer.py against libstdc++) that drive std::sort into
+its heap-sort fallback — the device must take that fallback too."""
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+REPO = Path(__file__).resolve().parent.parent
+
+
+def ref_perm(L, keys):
+    keys = np.ascontiguousarray(keys, dtype=np.uint32)
+    perm = np.zeros(max(len(keys), 1), np.int32)
+    assert L.oracle_lib().lego_oracle_sort_permutation(keys.ctypes.data, len(keys), perm.ctypes.data) == 0
+    return perm[:len(keys)]
+
+
+@pytest.fixture(scope="module")
+def gpu(L):
+    g = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=1000, max_batch=1)
+    yield g
+    g.close()
+
+
+def shapes(n, rng):
+    yield "random_ties", rng.integers(0, max(1, n // 3), n)
+    yield "random", rng.integers(0, 1 << 30, n)
+    yield "sorted", np.arange(n)
+    yield "reversed", np.arange(n)[::-1].copy()
+    yield "constant", np.full(n, 7)
+    yield "organ_pipe", np.concatenate([np.arange(n // 2), np.arange(n - n // 2)[::-1]])
+    yield "two_runs", np.concatenate([np.sort(rng.integers(0, 1000, n // 2)), np.sort(rng.integers(0, 1000, n - n // 2))])
+
+
+SIZES = [0, 1, 2, 15, 16, 17, 33, 63, 64, 65, 100, 127, 128, 129, 255, 256, 300, 511, 512]
+
+
+@pytest.mark.parametrize("wave", [True, False])
+@pytest.mark.parametrize("n", SIZES)
+def test_permutation_matches_std_sort(L, gpu, n, wave):
+    rng = np.random.default_rng(1000 + n)
+    for name, keys in shapes(n, rng):
+        got, _ = gpu.sort_permutation(keys, wave=wave)
+        np.testing.assert_array_equal(got, ref_perm(L, keys), err_msg=f"{name} n={n} wave={wave}")
+
+
+@pytest.mark.parametrize("n", [600, 1000, 1800, 4096, 8192])
+def test_block_sort_larger_arrays(L, gpu, n):
+    rng = np.random.default_rng(n)
+    for name, keys in shapes(n, rng):
+        got, _ = gpu.sort_permutation(keys, wave=False)
+        np.testing.assert_array_equal(got, ref_perm(L, keys), err_msg=f"{name} n={n}")
+
+
+@pytest.mark.parametrize("case", ["n64_div1", "n200_div1", "n500_div3", "n512_div1", "n3000_div2"])
+def test_adversarial_keys_take_the_heap_fallback(L, gpu, case):
+    """the same permutation, and exactly as many heap-sorted pieces as
+    std::sort takes (heaps_<case>: counted by tests/native/vgsort_check.cpp's
+    restatement, itself checked equal to std::sort on those keys)"""
+    z = np.load(REPO / "tests/golden/vg_killer.npz")
+    keys, heaps = z[case], int(z["heaps_" + case][0])
+    for wave in ([True, False] if len(keys) <= 512 else [False]):
+        got, heap = gpu.sort_permutation(keys, wave=wave)
+        np.testing.assert_array_equal(got, ref_perm(L, keys), err_msg=f"{case} wave={wave}")
+        assert heap == heaps, f"{case} wave={wave}: {heap} heap-sorted pieces, std::sort takes {heaps}"
+    assert any(int(z["heaps_" + c][0]) > 0 for c in ("n64_div1", "n200_div1", "n512_div1"))
+
+
+def test_size_limits(L, gpu):
+    with pytest.raises(Exception):
+        gpu.sort_permutation(np.zeros(513, np.uint32), wave=True)
+    with pytest.raises(Exception):
+        gpu.sort_permutation(np.zeros(8193, np.uint32), wave=False)
