@@ -133,7 +133,7 @@ struct lego_ctx {
   size_t rawCap = 0;
   Pc2Desc* d_desc = nullptr;
   std::vector<Pc2Desc> h_desc;
-  PackedRec* d_pack = nullptr;  // [maxBatch + 1]
+  PackedRec* d_pack = nullptr;  // h_pack's device address: k_pack_recs writes the records there
   PackedRec* h_pack = nullptr;  // pinned
   int64_t* h_offp = nullptr;    // pinned [maxBatch + 1]: device offsets read back for validation
   OdomState* h_resetSt = nullptr;   // pinned [S]: construction state (ctx_reset)
@@ -408,8 +408,10 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
   A(bb.f_cnt, B * 4);
   A(bb.imuScan, B);
   A(x->d_desc, B);
-  A(x->d_pack, 2 * (B1 + 1));
-  if (hipHostMalloc(&x->h_pack, sizeof(PackedRec) * 2 * (B1 + 1), hipHostMallocDefault) != hipSuccess) {
+  if (hipHostMalloc(&x->h_pack, sizeof(PackedRec) * 2 * (B1 + 1), hipHostMallocMapped | hipHostMallocCoherent) !=
+          hipSuccess ||
+      hipHostGetDevicePointer((void**)&x->d_pack, x->h_pack, 0) != hipSuccess) {
+    if (x->h_pack) (void)hipHostFree(x->h_pack);
     x->h_pack = nullptr;
     set_err("hipHostMalloc failed for the record buffer");
     return fail(LEGO_E_DEVICE);
@@ -758,18 +760,15 @@ static int submit_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t*
   tm.end(x->stream);
   HIPCHK(hipEventRecord(x->faDone[h], x->stream));
   HIPCHK(hipStreamWaitEvent(x->ostream, x->faDone[h], 0));
-  HIPCHK(hipMemsetAsync(x->ob.xerr, 0, sizeof(unsigned), x->ostream));
-  const OdomBufs ob = ob_slice(x->ob, x->dc, base, 0, S);
+  const OdomBufs ob = ob_slice(x->ob, x->dc, base, 0, S);  // launch_odom zeroes *ob.xerr
   if (launch_odom(bb, ob, x->dc, B / S, x->ostream, &otm, x->profOn ? x->d_prof : nullptr) != 0) {
     set_err("odometry launch failed (%d workgroups)", x->ob.G);
     return LEGO_E_DEVICE;
   }
   otm.end(x->ostream);
-  // the batch's records, non-dense flags and the error word in one copy
-  PackedRec* dp = x->d_pack + (size_t)h * (x->maxBatch + 1);
-  launch_pack_recs(bb, ob, B, dp, x->ostream);
-  HIPCHK(hipMemcpyAsync(x->h_pack + (size_t)h * (x->maxBatch + 1), dp, sizeof(PackedRec) * (B + 1),
-                        hipMemcpyDeviceToHost, x->ostream));
+  // the batch's records, non-dense flags and the error word, written by the
+  // kernel straight into the pinned (coherent, mapped) host slot
+  launch_pack_recs(bb, ob, B, x->d_pack + (size_t)h * (x->maxBatch + 1), x->ostream);
   HIPCHK(hipEventRecord(x->recsDone[h], x->ostream));
   HIPCHK(hipGetLastError());
   x->slotB[h] = B;

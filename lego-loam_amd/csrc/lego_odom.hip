@@ -2043,17 +2043,31 @@ int odom_workgroups(int N, int cusAvailable) {
   return g < cusAvailable ? g : cusAvailable;
 }
 
+// The launch's preparation in one kernel (it was two memsets and a copy, each
+// a dependent operation on the odometry stream between two k_odom launches):
+// the error word, the exchange slots of the rounds this launch can use, and
+// the read-only input state (OdomBufs::stIn) from the state the previous
+// launch left.
+__global__ void k_odom_prep(unsigned* xerr, uint4* xg, size_t xgVec, const uint4* st, uint4* stIn, int stVec) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x, T = (size_t)gridDim.x * blockDim.x;
+  if (t == 0) *xerr = 0u;
+  for (size_t i = t; i < xgVec; i += T) xg[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (size_t i = t; i < (size_t)stVec; i += T) stIn[i] = st[i];
+}
+
 int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int K, hipStream_t s, StageTimer* tm,
                 unsigned long long* prof) {
   tm->mark("odom.lm", s);
   // zero the exchange slots of the rounds this launch can use (10 per scan)
   const size_t slot = (size_t)ob.capQ * sizeof(unsigned long long);
-  const size_t bytes = ob.S == 1 ? std::min<size_t>(ob.roundsCap, (size_t)10 * K) * slot
-                                 : (size_t)ob.S * ob.roundsCap * slot;
-  if (ob.G > 1 && hipMemsetAsync(ob.xg, 0, bytes, s) != hipSuccess) return -1;
-  // the read-only input state of this launch (see OdomBufs::stIn)
-  if (hipMemcpyAsync(ob.stIn, ob.st, sizeof(OdomState) * ob.S, hipMemcpyDeviceToDevice, s) != hipSuccess)
-    return -1;
+  const size_t bytes = ob.G <= 1 ? 0
+                       : ob.S == 1 ? std::min<size_t>(ob.roundsCap, (size_t)10 * K) * slot
+                                   : (size_t)ob.S * ob.roundsCap * slot;
+  static_assert(sizeof(OdomState) % 16 == 0, "OdomState copies as 16-byte words");
+  const int stVec = (int)(sizeof(OdomState) * ob.S / 16);
+  const size_t xgVec = bytes / 16;  // capQ is even: whole 16-byte words
+  const int grid = (int)std::max<size_t>(1, std::min<size_t>(512, (std::max<size_t>(xgVec, stVec) + 255) / 256));
+  k_odom_prep<<<grid, 256, 0, s>>>(ob.xerr, (uint4*)ob.xg, xgVec, (const uint4*)ob.st, (uint4*)ob.stIn, stVec);
   if (ob.late >= 0 && hipMemsetAsync(ob.xerr + 1, 0, sizeof(unsigned), s) != hipSuccess) return -1;
   if (ob.wg >= 0 && ob.G > 1 &&  // the diagnostic silent workgroup's copy (single-stream contexts)
       hipMemsetAsync((unsigned char*)ob.xblock + 16, 0, ob.xbytes - 16, s) != hipSuccess)

@@ -233,7 +233,8 @@ static int run_wave(int n, int G) {
     printf("%s keys, n=%d, %d rings\n", shape == 0 ? "arc" : (shape == 1 ? "dup" : (shape == 2 ? "random" : "ring")), n,
            G);
     timeit("block (ring per WG)", [&] { k_vgsort<<<G, 256>>>(dk, n, dout, dv); });
-    timeit("wave (ring per wave)", [&] { k_vgsort_wave<<<(G + 3) / 4, 256>>>(dk, n, dout, dv, G); });
+    timeit("block, 128 threads", [&] { k_vgsort<<<G, 128>>>(dk, n, dout, dv); });
+    if (n <= kVgWaveMax) timeit("wave (ring per wave)", [&] { k_vgsort_wave<<<(G + 3) / 4, 256>>>(dk, n, dout, dv, G); });
     std::vector<uint16_t> hv(h.size());
     hipMemcpy(hv.data(), dv, hv.size() * 2, hipMemcpyDeviceToHost);
     long bad = 0;
