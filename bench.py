@@ -520,7 +520,13 @@ def main():
     # RCCL send/recv over xGMI, packets kept in rank 0's HBM) when every rank has
     # its GPU; the one-GPU rehearsal (gloo, shared device) gathers over torch.
     native = dist is not None and backend == "nccl"
-    comm = ms.native_comm(L, dist, local) if native else None
+    native_error = None  # a native-collective failure on every rank falls back to the torch gather, and says so
+    comm = None
+    if native:
+        try:
+            comm = ms.native_comm(L, dist, local)
+        except Exception as e:  # noqa: BLE001
+            native, native_error = False, f"lego_comm_create: {e}"
 
     # Steps are pipelined two deep (lego_odom_batch_submit / _wait): step i+1's
     # projection + extraction run while step i's odometry chain does.
@@ -535,10 +541,14 @@ def main():
         # corner / surf / outlier clouds) to rank 0 before the slot is reused:
         # gathered right here by the native collective, or packed into HBM for
         # the torch gather
+        nonlocal native, native_error
         pkt = None
         if native:
-            pkt = ms.native_gather_handoff(L, comm, gpu, 0, device=True)
-        elif dist:
+            try:
+                pkt = ms.native_gather_handoff(L, comm, gpu, 0, device=True)
+            except Exception as e:  # noqa: BLE001
+                native, native_error = False, f"lego_comm_gather_handoff_ex: {e}"
+        if dist and not native:
             pkt = gpu.handoff_tensor(dev)
         return i, gpu.stage_times(), cp, pkt
 
@@ -726,7 +736,8 @@ def main():
                        "scans_per_step": B, "stream_len": args.stream_len, "seed": seed,
                        "parallelism": f"stream-per-gpu x{world}",
                        "gather": ((("lego_comm (C-ABI RCCL send/recv)" if native else f"torch.distributed ({backend})")
-                                   + ": per step, pose records + published clouds to rank 0") if world > 1 else None)},
+                                   + ": per step, pose records + published clouds to rank 0") if world > 1 else None),
+                       "gather_native_error": native_error},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "traffic_over_alg": (traffic / (alg_bytes / args.steps * 1.0 / n_odom)
