@@ -992,7 +992,7 @@ __device__ void lfv_block(const BatchBufs& bb, const DevCfg& c, int ring, int b,
     val[t] = (uint16_t)t;
   }
   __syncthreads();
-  vg_block_sort(vg_sort_carve(key, val, sc, K, (int)blockDim.x), K);
+  vg_block_sort(vg_sort_carve(key, val, sc, K, (int)blockDim.x), K, -1, nullptr, true);
   // centroids into registers (every read of the slot done), then over the slot
   float4 cen[kLfvMaxPer];
   int at[kLfvMaxPer];

@@ -533,7 +533,7 @@ __device__ void vg_local_sort(const VgScratch& v, uint32_t* key, uint16_t* lv, u
     lv[i] = (uint16_t)i;
   }
   __syncthreads();
-  vg_block_sort(vg_sort_carve(key, lv, sc, m, (int)blockDim.x), m, depth, v.ctl + C_HEAP);
+  vg_block_sort(vg_sort_carve(key, lv, sc, m, (int)blockDim.x), m, depth, v.ctl + C_HEAP, true);
   for (int i = threadIdx.x; i < m; i += blockDim.x) {
     v.keys[s + i] = key[i];
     key[i] = (uint32_t)v.vals[s + lv[i]];

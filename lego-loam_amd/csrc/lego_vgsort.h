@@ -131,6 +131,9 @@ struct VgHeap {
 
 constexpr int kVgLeaf = 16;  // _S_threshold
 
+// bits 0..b of a word
+__device__ __forceinline__ uint32_t bi_mask_le(int b) { return b == 31 ? ~0u : ((2u << b) - 1); }
+
 // One segment of the current level: [s, e); A / B = left / right stops up to
 // and including e - 1 (block-wide inclusive counts); ck = the left stops up
 // to s (low half) | the swaps (high half: atomicMax of the swapped left
@@ -208,8 +211,20 @@ __device__ __forceinline__ VgSortLds<V> vg_sort_carve(uint32_t* key, V* val, uns
 // new segments.  Pieces of <= 16 keys become leaves; at the end every
 // position ranks itself within its leaf (stably: the final insertion sort's
 // effect) and moves there.
+//
+// sumOrder: the caller only sums each key's payloads in the sorted order (a
+// VoxelGrid centroid, summed from 0).  A heap-sorted piece whose keys each
+// occur at most twice in it, and whose smallest key, if twice, does not also
+// end the pieces before it, then yields the same sums from a stable order: a
+// key's one or two points in the piece are its voxel's first addends, and
+// 0 + a + b == 0 + b + a (IEEE addition commutes).  Such a piece is ranked in
+// parallel like a leaf instead of heap-sorted by one lane; any other piece is
+// still heap-sorted exactly.  Off, the permutation itself is std::sort's
+// (lego_sort_permutation).
+constexpr int kVgMoveRows = 4;  // the moves' batch: rows of blockDim.x positions
 template <typename V>
-__device__ void vg_block_sort(const VgSortLds<V>& S, int n, int depth = -1, int* heapStat = nullptr) {
+__device__ void vg_block_sort(const VgSortLds<V>& S, int n, int depth = -1, int* heapStat = nullptr,
+                              bool sumOrder = false) {
   constexpr int RM = kVgRowsMax;
   const int tid = threadIdx.x, T = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = T >> 6;
   const int cap = vg_list_cap(n);
@@ -243,8 +258,13 @@ __device__ void vg_block_sort(const VgSortLds<V>& S, int n, int depth = -1, int*
     if (D - r == 0) {  // depth budget spent: std::__partial_sort of every piece
       for (int j = tid; j < nseg; j += T) {
         const int s = cur[j].s, e = cur[j].e;
-        VgHeap<V>{S.key, S.val}.sort(s, e);
-        for (int q = s; q < e; ++q) atomicOr(&S.head[q >> 5], 1u << (q & 31));
+        if (sumOrder && e - s <= T * kVgMoveRows) {  // a leaf of > 16 keys; pr[s]: a key occurs 3+ times
+          atomicOr(&S.head[s >> 5], 1u << (s & 31));
+          S.pr[s] = 0;
+        } else {
+          VgHeap<V>{S.key, S.val}.sort(s, e);
+          for (int q = s; q < e; ++q) atomicOr(&S.head[q >> 5], 1u << (q & 31));
+        }
         if (heapStat) atomicAdd(heapStat, 1);
       }
       __syncthreads();
@@ -458,59 +478,95 @@ __device__ void vg_block_sort(const VgSortLds<V>& S, int n, int depth = -1, int*
     VG_STAMP(6);
   }
   VG_STAMP(7);
-  // leaves: every position ranks itself within its leaf (<= 16 keys, its
-  // start the highest leaf-start bit at or below it, its end the next one)
+  // leaves: every position ranks itself within its leaf (its start the
+  // highest leaf-start bit at or below it, its end the next one; <= 16 keys,
+  // or a heap piece of up to T * kVgMoveRows with sumOrder)
   for (int i = tid; i < n; i += T) {
     const int wi = i >> 5, bi = i & 31;
     const uint32_t hw = S.head[wi];
     const uint32_t msk = bi == 31 ? ~0u : ((2u << bi) - 1);
-    const uint32_t lo = hw & msk, hi = hw & ~msk;
-    int ls, le;
-    if (lo) ls = (wi << 5) + 31 - __builtin_clz(lo);
-    else ls = ((wi - 1) << 5) + 31 - __builtin_clz(S.head[wi - 1]);  // a leaf start lies within 16 below
-    if (hi) le = (wi << 5) + __builtin_ctz(hi);
-    else {
-      const uint32_t h2 = S.head[wi + 1];
-      le = h2 ? ((wi + 1) << 5) + __builtin_ctz(h2) : n;
-    }
-    le = min(le, n);
+    uint32_t lo = hw & msk, hi = hw & ~msk;
+    int wl = wi, wh = wi;
+    while (!lo) lo = S.head[--wl];  // position 0 is always a leaf start
+    while (!hi && ((wh + 1) << 5) < n) hi = S.head[++wh];
+    const int ls = (wl << 5) + 31 - __builtin_clz(lo);
+    const int le = hi ? min(n, (wh << 5) + __builtin_ctz(hi)) : n;
     const uint32_t k = S.key[i];
-    int rank = 0;
+    int lt = 0, eqb = 0, eq = 0;
     for (int u0 = 0; u0 < le - ls; u0 += 8) {
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int q = ls + u0 + u;
         const uint32_t kq = S.key[min(q, n - 1)];
-        if (q < le) rank += (kq < k || (kq == k && q < i)) ? 1 : 0;
+        if (q < le) {
+          lt += kq < k ? 1 : 0;
+          eqb += (kq == k && q < i) ? 1 : 0;
+          eq += kq == k ? 1 : 0;
+        }
       }
     }
-    S.sid[i] = (uint16_t)(ls + rank);
+    if (sumOrder && le - ls > kVgLeaf) {
+      // a key 3+ times, or the piece's smallest key twice when the pieces
+      // before it end with that key too (its sum then starts before the
+      // piece and the two addends no longer come first): exact heap sort.
+      // Every key before the piece is <= every key in it, so only the
+      // preceding leaf can hold it.
+      bool exact = eq >= 3;
+      if (!exact && eq == 2 && lt == 0 && eqb == 0 && ls > 0) {
+        int w = (ls - 1) >> 5;
+        uint32_t m = S.head[w] & bi_mask_le((ls - 1) & 31);
+        while (!m) m = S.head[--w];
+        const int pls = (w << 5) + 31 - __builtin_clz(m);
+        for (int q = pls; q < ls && !exact; ++q) exact = S.key[q] == k;
+      }
+      if (exact) S.pr[ls] = 1;
+    }
+    S.sid[i] = (uint16_t)(ls + lt + eqb);
   }
   __syncthreads();
-  // the moves, in batches of whole leaves (a batch ends at a leaf start):
-  // each batch's keys / vals / places to registers, then to their places
-  constexpr int MB = 4;
+  if (sumOrder) {  // heap pieces holding a key 3+ times: std::__partial_sort after all
+    for (int i = tid; i < n; i += T) {
+      if (!((S.head[i >> 5] >> (i & 31)) & 1u)) continue;
+      int w = i >> 5;
+      uint32_t hi = S.head[w] & ~(bi_mask_le(i & 31));
+      while (!hi && ((w + 1) << 5) < n) hi = S.head[++w];
+      const int le = hi ? min(n, (w << 5) + __builtin_ctz(hi)) : n;
+      if (le - i <= kVgLeaf || !S.pr[i]) continue;
+      VgHeap<V>{S.key, S.val}.sort(i, le);
+      for (int q = i; q < le; ++q) S.sid[q] = (uint16_t)q;
+    }
+    __syncthreads();
+  }
+  // the moves, in batches of whole leaves (a batch ends at the highest leaf
+  // start within kVgMoveRows rows; every leaf fits in them): each batch's
+  // keys / vals / places to registers, then to their places
+  constexpr int MB = kVgMoveRows;
   for (int b = 0; b < n;) {
     int bn = b + T * MB;
     if (bn >= n) {
       bn = n;
     } else {
       int w = bn >> 5;
-      uint32_t m = S.head[w] & ~((1u << (bn & 31)) - 1);
-      while (!m && ((w + 1) << 5) < n) m = S.head[++w];
-      bn = m ? min(n, (w << 5) + __builtin_ctz(m)) : n;
+      const int wb = b >> 5;
+      uint32_t m = S.head[w] & bi_mask_le(bn & 31);
+      if (w == wb) m &= ~bi_mask_le(b & 31);
+      while (!m) {
+        m = S.head[--w];
+        if (w == wb) m &= ~bi_mask_le(b & 31);
+      }
+      bn = (w << 5) + 31 - __builtin_clz(m);
     }
-    uint32_t kk[MB + 1], vd[MB + 1];
+    uint32_t kk[MB], vd[MB];
 #pragma unroll
-    for (int j = 0; j <= MB; ++j) {
+    for (int j = 0; j < MB; ++j) {
       const int i = b + j * T + tid;
-      const bool in = i < bn && (j < MB || i >= b + T * MB);
+      const bool in = i < bn;
       kk[j] = in ? S.key[i] : 0u;
       vd[j] = in ? ((uint32_t)S.val[i] | ((uint32_t)S.sid[i] << 16)) : 0xffffffffu;
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j <= MB; ++j)
+    for (int j = 0; j < MB; ++j)
       if (vd[j] != 0xffffffffu) { S.key[vd[j] >> 16] = kk[j]; S.val[vd[j] >> 16] = (V)(vd[j] & 0xffffu); }
     __syncthreads();
     b = bn;

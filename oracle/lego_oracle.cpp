@@ -125,6 +125,14 @@ void voxel_grid(const std::vector<Pt>& in, float leaf, bool pcl_sort, std::vecto
     int i2 = (int)(std::floor(p.z * inv) - (float)minb[2]);
     iv.push_back({i0 + i1 * divb0 + i2 * divb0 * divb1, (unsigned)i});
   }
+  if (const char* dump = std::getenv("LEGO_ORACLE_VG_DUMP")) {  // diagnostic: the sort's keys, per call
+    if (FILE* f = std::fopen(dump, "ab")) {
+      const int32_t m = (int32_t)iv.size();
+      std::fwrite(&m, 4, 1, f);
+      for (const Idx& e : iv) std::fwrite(&e.idx, 4, 1, f);
+      std::fclose(f);
+    }
+  }
   if (pcl_sort) std::sort(iv.begin(), iv.end(), std::less<Idx>());
   else std::stable_sort(iv.begin(), iv.end(), std::less<Idx>());
   size_t idx = 0;

@@ -87,7 +87,14 @@ def test_scan_shaped_clouds_match_pcl_order(L, gpu):
         _same(got, oracle_vg(L, p, leaf), f"leaf {leaf}")
 
 
-@pytest.mark.parametrize("case", ["n8000_div3", "n30000_div3", "n20000_div1"])
+# Which sort path the heap-sorted pieces take (lego_vgsort.h, sumOrder): the
+# div3 cases hold keys three times inside their pieces (exact heap sort by one
+# lane); n20000_div1's one piece of 19,944 keys exceeds a workgroup's LDS
+# (exact heap sort in global memory); n3000_div2 (one piece of 2,956 keys,
+# each twice), n512_div1 and n200_div1 (distinct keys) are ranked in parallel,
+# which gives the same centroids (two addends commute).
+@pytest.mark.parametrize("case", ["n8000_div3", "n30000_div3", "n20000_div1", "n3000_div2", "n512_div1",
+                                  "n200_div1"])
 def test_adversarial_keys_heap_fallback(L, gpu, case):
     z = np.load(REPO / "tests/golden/vg_killer.npz")
     keys = z[case]
