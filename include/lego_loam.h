@@ -482,8 +482,13 @@ int lego_voxel_grid_stats(lego_ctx* ctx, int32_t stats[8]);
  * whose order of equal keys is the VoxelGrid's summation order — computed on
  * the device: perm[i] = the input index at sorted position i.  wave = 0: the
  * workgroup sort the VoxelGrids use (n <= 8192); wave = 1: the one-wave sort
- * of the per-ring less-flat VoxelGrid (n <= 512).  heap_pieces (may be NULL):
- * how many pieces the depth budget sent to std::__partial_sort. */
+ * of the per-ring less-flat VoxelGrid (n <= 512).  wave = 2 / 3: the workgroup
+ * sort as the VoxelGrids run it, with 256 threads (n <= 2048) / 1024 threads
+ * (n <= 8192): heap-sorted pieces whose voxel sums do not depend on their
+ * order (each key at most twice, the smallest not continuing the preceding
+ * piece) come back in stable order instead of std::sort's, every other
+ * position as std::sort leaves it.  heap_pieces (may be NULL): how many pieces
+ * the depth budget sent to std::__partial_sort. */
 int lego_sort_permutation(lego_ctx* ctx, const uint32_t* keys, int32_t n, int32_t wave, int32_t* perm,
                           int32_t* heap_pieces);
 

@@ -1226,9 +1226,10 @@ int lego_mo_set_map(lego_ctx* x, const lego_point_xyzi* corner, int32_t n_corner
 
 int lego_sort_permutation(lego_ctx* x, const uint32_t* keys, int32_t n, int32_t wave, int32_t* perm,
                           int32_t* heap_pieces) {
-  if (!x || n < 0 || (n > 0 && (!keys || !perm)) || (wave != 0 && wave != 1)) return LEGO_E_ARG;
-  if (n > (wave ? 512 : 8192)) {
-    set_err("lego_sort_permutation: n = %d above the %s sort's %d", n, wave ? "wave" : "block", wave ? 512 : 8192);
+  if (!x || n < 0 || (n > 0 && (!keys || !perm)) || wave < 0 || wave > 3) return LEGO_E_ARG;
+  const int cap = wave == 1 ? 512 : wave == 2 ? 2048 : 8192;
+  if (n > cap) {
+    set_err("lego_sort_permutation: n = %d above the mode-%d sort's %d", n, wave, cap);
     return LEGO_E_CAPACITY;
   }
   HIPCHK(hipSetDevice(x->device));

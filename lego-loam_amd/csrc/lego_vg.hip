@@ -734,7 +734,7 @@ __global__ void __launch_bounds__(1024) k_sort_perm(const uint32_t* keys, int n,
   uint32_t* key = (uint32_t*)lds_raw;
   uint16_t* val = (uint16_t*)(lds_raw + (size_t)4 * kSortPermBlockMax);
   unsigned char* sc = lds_raw + (size_t)6 * kSortPermBlockMax;
-  if (wave) {
+  if (wave == 1) {
     if (threadIdx.x >= 64) return;
     for (int i = threadIdx.x; i < n; i += 64) { key[i] = keys[i]; val[i] = (uint16_t)i; }
     vg_wave_sync();
@@ -744,14 +744,18 @@ __global__ void __launch_bounds__(1024) k_sort_perm(const uint32_t* keys, int n,
   }
   for (int i = threadIdx.x; i < n; i += blockDim.x) { key[i] = keys[i]; val[i] = (uint16_t)i; }
   __syncthreads();
-  vg_block_sort(vg_sort_carve(key, val, sc, n, (int)blockDim.x), n, -1, heap);
+  vg_block_sort(vg_sort_carve(key, val, sc, n, (int)blockDim.x), n, -1, heap, wave >= 2);
   for (int i = threadIdx.x; i < n; i += blockDim.x) perm[i] = val[i];
 }
 size_t sort_perm_lds_bytes() { return (size_t)6 * kSortPermBlockMax + vg_sort_scratch_bytes(kSortPermBlockMax, 1024); }
+// wave = 2 / 3: the block sort as the VoxelGrids run it (sumOrder: heap pieces
+// whose centroids do not depend on their order ranked stably) with 256 threads
+// (k_lf_voxel's large rings, n <= 2048) / 1024 threads (n <= 8192).
 int sort_perm_device(const uint32_t* keys, int n, int wave, int* perm, int* heap, hipStream_t s) {
-  if (n < 0 || n > (wave ? kVgWaveMax : kSortPermBlockMax)) return -1;
+  const int cap = wave == 1 ? kVgWaveMax : wave == 2 ? vg_sort_max(256) : kSortPermBlockMax;
+  if (n < 0 || n > cap || wave < 0 || wave > 3) return -1;
   if (n == 0) return 0;
-  k_sort_perm<<<1, 1024, sort_perm_lds_bytes(), s>>>(keys, n, wave, perm, heap);
+  k_sort_perm<<<1, wave == 2 ? 256 : 1024, sort_perm_lds_bytes(), s>>>(keys, n, wave == 1 ? 1 : wave, perm, heap);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -80,3 +80,61 @@ def test_size_limits(L, gpu):
         gpu.sort_permutation(np.zeros(513, np.uint32), wave=True)
     with pytest.raises(Exception):
         gpu.sort_permutation(np.zeros(8193, np.uint32), wave=False)
+
+
+def voxel_sums(keys, perm, vals):
+    """each key's values summed from 0 in the order perm leaves them (float32,
+    one addend at a time: k_vg_emit / lfv_centroid)"""
+    out, cur, acc = [], None, np.float32(0)
+    for i in perm:
+        if keys[i] != cur:
+            if cur is not None:
+                out.append(acc)
+            cur, acc = keys[i], np.float32(0)
+        acc = np.float32(acc + vals[i])
+    if cur is not None:
+        out.append(acc)
+    return np.array(out, np.float32)
+
+
+def sum_order_cases():
+    z = np.load(REPO / "tests/golden/c2_ring_keys.npz")
+    for k in z.files:
+        yield f"c2_{k}", z[k]
+    zk = np.load(REPO / "tests/golden/vg_killer.npz")
+    for k in ("n200_div1", "n512_div1", "n3000_div2", "n8000_div3", "n500_div3"):
+        yield k, zk[k]
+    rng = np.random.default_rng(5)
+    for n in (700, 1800, 5000):
+        for name, keys in shapes(n, rng):
+            yield f"{name}_{n}", keys
+
+
+@pytest.mark.parametrize("mode", [2, 3])
+def test_sum_order_sort_gives_std_sort_sums(L, gpu, mode):
+    """The VoxelGrids' form of the block sort (lego_vgsort.h sumOrder; mode 2 =
+    256 threads as k_lf_voxel's large rings, 3 = 1024 as the mapping clouds):
+    a permutation, sorted by key, every position outside the stably ranked
+    heap pieces as std::sort leaves it, and every key's float32 sum from 0 in
+    its order bit-equal to the sum in std::sort's order (random values).  The
+    C2 rings are scan 465's (tests/golden/make_ring_keys.py); ring6 holds heap
+    pieces of both kinds."""
+    cap = 2048 if mode == 2 else 8192
+    rng = np.random.default_rng(11)
+    ranked = 0
+    for name, keys in sum_order_cases():
+        keys = np.ascontiguousarray(keys, dtype=np.uint32)
+        if len(keys) > cap:
+            continue
+        got, heaps = gpu.sort_permutation(keys, wave=mode)
+        ref = ref_perm(L, keys)
+        assert np.array_equal(np.sort(got), np.arange(len(keys))), name
+        assert np.all(np.diff(keys[got].astype(np.int64)) >= 0), name
+        vals = rng.uniform(-10, 10, len(keys)).astype(np.float32)
+        np.testing.assert_array_equal(voxel_sums(keys, got, vals).view(np.uint32),
+                                      voxel_sums(keys, ref, vals).view(np.uint32), err_msg=name)
+        _, heaps_exact = gpu.sort_permutation(keys, wave=False) if len(keys) <= 8192 else (None, heaps)
+        assert heaps == heaps_exact, name
+        ranked += int(not np.array_equal(got, ref))
+    print(f"mode {mode}: {ranked} arrays with stably ranked heap pieces")
+    assert ranked > 0
