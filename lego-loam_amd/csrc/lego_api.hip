@@ -184,6 +184,8 @@ struct lego_ctx {
     if (device >= 0) (void)hipSetDevice(device);
     if (stream) (void)hipStreamSynchronize(stream);  // batches still in flight
     if (ostream) (void)hipStreamSynchronize(ostream);
+    for (int i = 1; i < 3; ++i)  // the mapping VoxelGrids' forks
+      if (mo.fork[i]) (void)hipStreamSynchronize(mo.fork[i]);
     if (d_raw) (void)hipFree(d_raw);
     if (d_handoff) (void)hipFree(d_handoff);
     if (h_pack) (void)hipHostFree(h_pack);
@@ -196,6 +198,10 @@ struct lego_ctx {
       if (faDone[i]) (void)hipEventDestroy(faDone[i]);
       if (recsDone[i]) (void)hipEventDestroy(recsDone[i]);
     }
+    for (int i = 1; i < 3; ++i)
+      if (mo.fork[i]) (void)hipStreamDestroy(mo.fork[i]);
+    for (auto e : mo.ev)
+      if (e) (void)hipEventDestroy(e);
     if (hstream) (void)hipStreamSynchronize(hstream);
     if (hstream) (void)hipStreamDestroy(hstream);
     if (ostream) (void)hipStreamDestroy(ostream);
@@ -1141,15 +1147,25 @@ static int mo_alloc(lego_ctx* x, int nc, int ns) {
     MA(m.rows, (size_t)m.rowCap * 8);
     HIPCHK(hipMemsetAsync(m.st, 0, sizeof(MoState), x->stream));
     HIPCHK(hipMemsetAsync(m.cnt, 0, sizeof(MoCounts), x->stream));
+    // the VoxelGrids' fork streams (lego_mo.h): created with the mapping
+    // buffers, so contexts that never map keep two streams
+    m.fork[0] = x->ostream;
+    for (int i = 1; i < 3; ++i)
+      if (hipStreamCreateWithFlags(&m.fork[i], hipStreamNonBlocking) != hipSuccess) return fail("fork stream");
+    for (auto& e : m.ev)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail("fork event");
     x->moAlloc = true;
   }
+  auto ctx_alloc = [](void* c, void** p, size_t bytes) {
+    return static_cast<lego_ctx*>(c)->alloc(reinterpret_cast<unsigned char**>(p), bytes) == hipSuccess ? 0 : -1;
+  };
+  // buffers are never freed before the context: grow by reallocating
   const int vcap = std::max(std::max(nc, ns), 2 * P);
-  if (vcap > m.vg.cap) {  // buffers are never freed before the context: grow by reallocating
-    auto ctx_alloc = [](void* c, void** p, size_t bytes) {
-      return static_cast<lego_ctx*>(c)->alloc(reinterpret_cast<unsigned char**>(p), bytes) == hipSuccess ? 0 : -1;
-    };
-    if (vg_scratch_alloc(m.vg, vcap, x, ctx_alloc)) return fail("VoxelGrid scratch");
-  }
+  if (vcap > m.vg.cap && vg_scratch_alloc(m.vg, vcap, x, ctx_alloc)) return fail("VoxelGrid scratch");
+  const int v2cap = std::max(nc, N * kLessSharpPerRing);
+  if (v2cap > m.vgMap2.cap && vg_scratch_alloc(m.vgMap2, v2cap, x, ctx_alloc)) return fail("VoxelGrid scratch");
+  if (2 * P > m.vgScan1.cap && vg_scratch_alloc(m.vgScan1, 2 * P, x, ctx_alloc)) return fail("VoxelGrid scratch");
+  if (P > m.vgScan2.cap && vg_scratch_alloc(m.vgScan2, P, x, ctx_alloc)) return fail("VoxelGrid scratch");
   if (nc > m.mapCornerCap) {
     m.mapCornerCap = nc;
     MA(m.cornerMap, nc); MA(m.cornerMapDS, nc);

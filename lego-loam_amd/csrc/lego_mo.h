@@ -110,6 +110,15 @@ struct MoDev {
   MoKeyframes kf;
   float4 *cornerFromMap, *surfFromMap;  // [fromMapCap]
   int fromMapCap;
+  // Fork-join of a step's independent VoxelGrids (each is latency-bound and
+  // fills a small part of the GPU): fork[0] (the context's odometry stream)
+  // takes the map's corner cloud and its index, then the scan's corner cloud;
+  // fork[1] the scan's surf cloud, then surf + outlier; fork[2] the outlier
+  // cloud; the step's stream the map's surf cloud and index.  Each fork has
+  // its own VoxelGrid scratch.
+  hipStream_t fork[3];
+  hipEvent_t ev[6];
+  VgScratch vgMap2, vgScan1, vgScan2;
 };
 
 struct MoStepArgs {

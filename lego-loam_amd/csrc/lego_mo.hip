@@ -668,13 +668,50 @@ __global__ void k_kf_copy(MoKeyframes kf, const float4* cornerDS, const float4* 
   }
 }
 
-// The surrounding map's VoxelGrids (:1058-1064) and NN indexes.
+enum { EV_MAP_FORK, EV_MAP_CORNER, EV_SCAN_FORK, EV_SCAN_CORNER, EV_OUTLIER, EV_SCAN_DONE };
+
+static bool fork_wait(MoDev& m, int ev, hipStream_t from, hipStream_t to) {
+  return hipEventRecord(m.ev[ev], from) == hipSuccess && hipStreamWaitEvent(to, m.ev[ev], 0) == hipSuccess;
+}
+
+// The map's VoxelGrids (corner 0.2 m, surf 0.4 m, :1058-1064) and NN indexes
+// (:1333-1334): the corner cloud on fork[0], the surf cloud on s, joined on s.
+static int map_filter(MoDev& m, const float4* corner, int nC, const float4* surf, int nS, hipStream_t s) {
+  const hipStream_t f = m.fork[0];
+  if (!fork_wait(m, EV_MAP_FORK, s, f)) return -1;
+  if (voxel_grid_device(corner, nC, nullptr, 0.2f, m.cornerMapDS, &m.cnt->cornerMapDS, m.vgMap2, f)) return -1;
+  if (index_build_device(m.cornerMapDS, nC, &m.cnt->cornerMapDS, m.cornerIx, m.vgMap2, f)) return -1;
+  if (voxel_grid_device(surf, nS, nullptr, 0.4f, m.surfMapDS, &m.cnt->surfMapDS, m.vg, s)) return -1;
+  if (index_build_device(m.surfMapDS, nS, &m.cnt->surfMapDS, m.surfIx, m.vg, s)) return -1;
+  return fork_wait(m, EV_MAP_CORNER, f, s) ? 0 : -1;
+}
+
+// downsampleCurrentScan (:1067-1091) forked off s: the outlier cloud on
+// fork[2]; the surf cloud on fork[1], then (after the outlier cloud) the
+// concatenation and its VoxelGrid; the corner cloud on fork[0].  join_scan
+// makes s wait for them.
+static int scan_filter_fork(MoDev& m, const MoStepArgs& a, hipStream_t s) {
+  if (hipEventRecord(m.ev[EV_SCAN_FORK], s) != hipSuccess) return -1;
+  for (int i = 0; i < 3; ++i)
+    if (hipStreamWaitEvent(m.fork[i], m.ev[EV_SCAN_FORK], 0) != hipSuccess) return -1;
+  const hipStream_t f0 = m.fork[0], f1 = m.fork[1], f2 = m.fork[2];
+  if (voxel_grid_device(m.outlierLast, a.nOutlier, nullptr, 0.4f, m.outlierDS, &m.cnt->outlierDS, m.vgScan2, f2))
+    return -1;
+  if (voxel_grid_device(m.surfLast, a.nSurf, nullptr, 0.4f, m.surfDS, &m.cnt->surfDS, m.vgScan1, f1)) return -1;
+  if (!fork_wait(m, EV_OUTLIER, f2, f1)) return -1;
+  k_mo_concat<<<grid_for(a.nSurf + a.nOutlier), 256, 0, f1>>>(m.surfDS, m.outlierDS, m.cnt, m.surfTotal);
+  if (voxel_grid_device(m.surfTotal, a.nSurf + a.nOutlier, &m.cnt->surfTotal, 0.4f, m.surfTotalDS,
+                        &m.cnt->surfTotalDS, m.vgScan1, f1))
+    return -1;
+  if (voxel_grid_device(m.cornerLast, a.nCorner, nullptr, 0.2f, m.cornerDS, &m.cnt->cornerDS, m.vgMap2, f0)) return -1;
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+static int join_scan(MoDev& m, hipStream_t s) {
+  return fork_wait(m, EV_SCAN_CORNER, m.fork[0], s) && fork_wait(m, EV_SCAN_DONE, m.fork[1], s) ? 0 : -1;
+}
+
 static int kf_map_filter(MoDev& m, int nCM, int nSM, hipStream_t s) {
-  if (voxel_grid_device(m.cornerFromMap, nCM, nullptr, 0.2f, m.cornerMapDS, &m.cnt->cornerMapDS, m.vg, s)) return -1;
-  if (voxel_grid_device(m.surfFromMap, nSM, nullptr, 0.4f, m.surfMapDS, &m.cnt->surfMapDS, m.vg, s)) return -1;
-  if (index_build_device(m.cornerMapDS, nCM, &m.cnt->cornerMapDS, m.cornerIx, m.vg, s)) return -1;
-  if (index_build_device(m.surfMapDS, nSM, &m.cnt->surfMapDS, m.surfIx, m.vg, s)) return -1;
-  return 0;
+  return map_filter(m, m.cornerFromMap, nCM, m.surfFromMap, nSM, s);
 }
 
 // The surrounding map of the keyframe store, filtered and indexed.
@@ -705,6 +742,10 @@ static int kf_map_recent(MoDev& m, const MoStepArgs& a, hipStream_t s) {
 int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, hipStream_t s) {
   k_mo_associate<<<1, 64, 0, s>>>(m.st, a.quat[0], a.quat[1], a.quat[2], a.quat[3], a.pos[0], a.pos[1], a.pos[2]);
   if (hipGetLastError() != hipSuccess) return -1;
+  // the scan's VoxelGrids first with a fixed map (no early return below);
+  // after the keyframe map's plan otherwise (its capacity checks return
+  // before anything of the step's clouds ran)
+  if (fixedMap && scan_filter_fork(m, a, s)) return -1;
   if (!fixedMap && a.nPlan >= 0) {  // extractSurroundingKeyFrames, loop-closure branch :961-999
     const int st = kf_map_recent(m, a, s);
     if (st) return st;
@@ -715,13 +756,8 @@ int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, h
     if (mo_set_map_device(m, m.nCornerMap, m.nSurfMap, s)) return -1;
   }
   // downsampleCurrentScan :1067-1091
-  if (voxel_grid_device(m.cornerLast, a.nCorner, nullptr, 0.2f, m.cornerDS, &m.cnt->cornerDS, m.vg, s)) return -1;
-  if (voxel_grid_device(m.surfLast, a.nSurf, nullptr, 0.4f, m.surfDS, &m.cnt->surfDS, m.vg, s)) return -1;
-  if (voxel_grid_device(m.outlierLast, a.nOutlier, nullptr, 0.4f, m.outlierDS, &m.cnt->outlierDS, m.vg, s)) return -1;
-  k_mo_concat<<<grid_for(a.nSurf + a.nOutlier), 256, 0, s>>>(m.surfDS, m.outlierDS, m.cnt, m.surfTotal);
-  if (voxel_grid_device(m.surfTotal, a.nSurf + a.nOutlier, &m.cnt->surfTotal, 0.4f, m.surfTotalDS,
-                        &m.cnt->surfTotalDS, m.vg, s))
-    return -1;
+  if (!fixedMap && scan_filter_fork(m, a, s)) return -1;
+  if (join_scan(m, s)) return -1;
   k_mo_guard<<<1, 64, 0, s>>>(m.st, m.cnt);
   // scan2MapOptimization :1329-1350 — the iterations exit on the device once converged
   const int qcap = a.nCorner + a.nSurf + a.nOutlier;
@@ -743,11 +779,7 @@ int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, h
 // Installs a fixed map: voxel filter (corner 0.2 m, surf 0.4 m, :1062-1064) and
 // NN index, once.
 int mo_set_map_device(MoDev& m, int nCornerMap, int nSurfMap, hipStream_t s) {
-  if (voxel_grid_device(m.cornerMap, nCornerMap, nullptr, 0.2f, m.cornerMapDS, &m.cnt->cornerMapDS, m.vg, s)) return -1;
-  if (voxel_grid_device(m.surfMap, nSurfMap, nullptr, 0.4f, m.surfMapDS, &m.cnt->surfMapDS, m.vg, s)) return -1;
-  if (index_build_device(m.cornerMapDS, nCornerMap, &m.cnt->cornerMapDS, m.cornerIx, m.vg, s)) return -1;
-  if (index_build_device(m.surfMapDS, nSurfMap, &m.cnt->surfMapDS, m.surfIx, m.vg, s)) return -1;
-  return 0;
+  return map_filter(m, m.cornerMap, nCornerMap, m.surfMap, nSurfMap, s);
 }
 
 }  // namespace lego
