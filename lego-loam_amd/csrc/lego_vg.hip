@@ -43,7 +43,7 @@ constexpr int kVgTileThreads = 256, kVgTilePer = 16, kVgTile = kVgTileThreads * 
 // rounds leave larger (their last round, or rounds forced off) go to the big
 // local kernel: LDS up to kVgLocal, a global-memory partition above.
 constexpr int kVgSplit = 1024, kVgSplitThreads = 256;    // vg_sort_max(256) = 2048 >= kVgSplit
-constexpr int kVgLocal = 4096, kVgLocalThreads = 1024;  // vg_sort_max(1024) = 8192 >= kVgLocal
+constexpr int kVgLocal = 8192, kVgLocalThreads = 1024;  // vg_sort_max(1024) = 8192 >= kVgLocal (98 KB of LDS)
 constexpr int kVgRoundsMax = 16;
 constexpr int kVgPlanThreads = 1024;
 
@@ -661,7 +661,9 @@ int vg_rounds_for(int n) {
   if (n <= kVgSplit) return 0;
   int r = 1;
   while (((long long)kVgSplit << r) < n) ++r;
-  return std::min(r + 1, kVgRoundsMax);
+  // one more round above 256 k keys: the C5 map's leftovers then fit one
+  // workgroup's LDS (kVgLocal) instead of its global-memory partition
+  return std::min(r + 1 + (n > (1 << 18) ? 1 : 0), kVgRoundsMax);
 }
 
 // in[0 .. min(n, *nDev)) -> out[0 .. *nOut), all on stream s.  n is a host
