@@ -184,8 +184,7 @@ struct lego_ctx {
     if (device >= 0) (void)hipSetDevice(device);
     if (stream) (void)hipStreamSynchronize(stream);  // batches still in flight
     if (ostream) (void)hipStreamSynchronize(ostream);
-    for (int i = 1; i < 3; ++i)  // the mapping VoxelGrids' forks
-      if (mo.fork[i]) (void)hipStreamSynchronize(mo.fork[i]);
+    if (mo.fork[1]) (void)hipStreamSynchronize(mo.fork[1]);  // the mapping VoxelGrids' fork
     if (d_raw) (void)hipFree(d_raw);
     if (d_handoff) (void)hipFree(d_handoff);
     if (h_pack) (void)hipHostFree(h_pack);
@@ -198,8 +197,7 @@ struct lego_ctx {
       if (faDone[i]) (void)hipEventDestroy(faDone[i]);
       if (recsDone[i]) (void)hipEventDestroy(recsDone[i]);
     }
-    for (int i = 1; i < 3; ++i)
-      if (mo.fork[i]) (void)hipStreamDestroy(mo.fork[i]);
+    if (mo.fork[1]) (void)hipStreamDestroy(mo.fork[1]);
     for (auto e : mo.ev)
       if (e) (void)hipEventDestroy(e);
     if (hstream) (void)hipStreamSynchronize(hstream);
@@ -1150,8 +1148,7 @@ static int mo_alloc(lego_ctx* x, int nc, int ns) {
     // the VoxelGrids' fork streams (lego_mo.h): created with the mapping
     // buffers, so contexts that never map keep two streams
     m.fork[0] = x->ostream;
-    for (int i = 1; i < 3; ++i)
-      if (hipStreamCreateWithFlags(&m.fork[i], hipStreamNonBlocking) != hipSuccess) return fail("fork stream");
+    if (hipStreamCreateWithFlags(&m.fork[1], hipStreamNonBlocking) != hipSuccess) return fail("fork stream");
     for (auto& e : m.ev)
       if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail("fork event");
     x->moAlloc = true;

@@ -112,11 +112,11 @@ struct MoDev {
   int fromMapCap;
   // Fork-join of a step's independent VoxelGrids (each is latency-bound and
   // fills a small part of the GPU): fork[0] (the context's odometry stream)
-  // takes the map's corner cloud and its index, then the scan's corner cloud;
-  // fork[1] the scan's surf cloud, then surf + outlier; fork[2] the outlier
-  // cloud; the step's stream the map's surf cloud and index.  Each fork has
-  // its own VoxelGrid scratch.
-  hipStream_t fork[3];
+  // takes the scan's outlier cloud, the map's corner cloud and its index, then
+  // the scan's corner cloud; fork[1] the scan's surf cloud, then surf +
+  // outlier; the step's stream the map's surf cloud and index.  Each chain
+  // has its own VoxelGrid scratch.
+  hipStream_t fork[2];
   hipEvent_t ev[6];
   VgScratch vgMap2, vgScan1, vgScan2;
 };

@@ -37,6 +37,9 @@
 #include "lego_kernels.h"
 #include "lego_mo.h"
 
+#include <chrono>
+#include <cstdio>
+
 namespace lego {
 
 constexpr unsigned kInvalidKey = 0xffffffffu;
@@ -677,28 +680,38 @@ static bool fork_wait(MoDev& m, int ev, hipStream_t from, hipStream_t to) {
 // The map's VoxelGrids (corner 0.2 m, surf 0.4 m, :1058-1064) and NN indexes
 // (:1333-1334): the corner cloud on fork[0], the surf cloud on s, joined on s.
 static int map_filter(MoDev& m, const float4* corner, int nC, const float4* surf, int nS, hipStream_t s) {
+  // enqueued longest first: the host's launches take longer than the GPU's
+  // short kernels, so the order of enqueueing is the order the chains start
   const hipStream_t f = m.fork[0];
-  if (!fork_wait(m, EV_MAP_FORK, s, f)) return -1;
-  if (voxel_grid_device(corner, nC, nullptr, 0.2f, m.cornerMapDS, &m.cnt->cornerMapDS, m.vgMap2, f)) return -1;
-  if (index_build_device(m.cornerMapDS, nC, &m.cnt->cornerMapDS, m.cornerIx, m.vgMap2, f)) return -1;
+  if (hipEventRecord(m.ev[EV_MAP_FORK], s) != hipSuccess) return -1;
   if (voxel_grid_device(surf, nS, nullptr, 0.4f, m.surfMapDS, &m.cnt->surfMapDS, m.vg, s)) return -1;
   if (index_build_device(m.surfMapDS, nS, &m.cnt->surfMapDS, m.surfIx, m.vg, s)) return -1;
+  if (hipStreamWaitEvent(f, m.ev[EV_MAP_FORK], 0) != hipSuccess) return -1;
+  if (voxel_grid_device(corner, nC, nullptr, 0.2f, m.cornerMapDS, &m.cnt->cornerMapDS, m.vgMap2, f)) return -1;
+  if (index_build_device(m.cornerMapDS, nC, &m.cnt->cornerMapDS, m.cornerIx, m.vgMap2, f)) return -1;
   return fork_wait(m, EV_MAP_CORNER, f, s) ? 0 : -1;
 }
 
-// downsampleCurrentScan (:1067-1091) forked off s: the outlier cloud on
-// fork[2]; the surf cloud on fork[1], then (after the outlier cloud) the
-// concatenation and its VoxelGrid; the corner cloud on fork[0].  join_scan
-// makes s wait for them.
-static int scan_filter_fork(MoDev& m, const MoStepArgs& a, hipStream_t s) {
-  if (hipEventRecord(m.ev[EV_SCAN_FORK], s) != hipSuccess) return -1;
-  for (int i = 0; i < 3; ++i)
-    if (hipStreamWaitEvent(m.fork[i], m.ev[EV_SCAN_FORK], 0) != hipSuccess) return -1;
-  const hipStream_t f0 = m.fork[0], f1 = m.fork[1], f2 = m.fork[2];
-  if (voxel_grid_device(m.outlierLast, a.nOutlier, nullptr, 0.4f, m.outlierDS, &m.cnt->outlierDS, m.vgScan2, f2))
+// downsampleCurrentScan (:1067-1091) forked off s at EV_SCAN_FORK, in two
+// parts around the map's work so that every chain starts early: the outlier
+// cloud on fork[0] and the surf cloud on fork[1] first; after the map's
+// launches the concatenation and its VoxelGrid on fork[1] (after the outlier
+// cloud) and the corner cloud on fork[0].  join_scan makes s wait for them.
+// (Two forks: with the step's stream that is three hardware queues, as many
+// as a process gets besides the runtime's own; a third fork shared one.)
+static int scan_filter_begin(MoDev& m, const MoStepArgs& a) {
+  const hipStream_t f0 = m.fork[0], f1 = m.fork[1];
+  if (hipStreamWaitEvent(f0, m.ev[EV_SCAN_FORK], 0) != hipSuccess) return -1;
+  if (hipStreamWaitEvent(f1, m.ev[EV_SCAN_FORK], 0) != hipSuccess) return -1;
+  if (voxel_grid_device(m.outlierLast, a.nOutlier, nullptr, 0.4f, m.outlierDS, &m.cnt->outlierDS, m.vgScan2, f0))
     return -1;
+  if (hipEventRecord(m.ev[EV_OUTLIER], f0) != hipSuccess) return -1;
   if (voxel_grid_device(m.surfLast, a.nSurf, nullptr, 0.4f, m.surfDS, &m.cnt->surfDS, m.vgScan1, f1)) return -1;
-  if (!fork_wait(m, EV_OUTLIER, f2, f1)) return -1;
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+static int scan_filter_end(MoDev& m, const MoStepArgs& a) {
+  const hipStream_t f0 = m.fork[0], f1 = m.fork[1];
+  if (hipStreamWaitEvent(f1, m.ev[EV_OUTLIER], 0) != hipSuccess) return -1;
   k_mo_concat<<<grid_for(a.nSurf + a.nOutlier), 256, 0, f1>>>(m.surfDS, m.outlierDS, m.cnt, m.surfTotal);
   if (voxel_grid_device(m.surfTotal, a.nSurf + a.nOutlier, &m.cnt->surfTotal, 0.4f, m.surfTotalDS,
                         &m.cnt->surfTotalDS, m.vgScan1, f1))
@@ -739,13 +752,27 @@ static int kf_map_recent(MoDev& m, const MoStepArgs& a, hipStream_t s) {
   return kf_map_filter(m, a.nCM, a.nSM, s);
 }
 
+// LEGO_MO_HOSTPROF (diagnostic): the host's enqueue time of the step's parts
+// to stderr (map, scan VoxelGrids, LM).
+static const bool g_hostprof = std::getenv("LEGO_MO_HOSTPROF") != nullptr;
+#define MO_HOSTPROF(k)                                                                                  \
+  if (g_hostprof) {                                                                                     \
+    hp[k] = std::chrono::steady_clock::now();                                                           \
+    if (k == 3)                                                                                         \
+      std::fprintf(stderr, "mo enqueue us: map %.0f scan %.0f lm %.0f\n",                              \
+                   std::chrono::duration<double, std::micro>(hp[1] - hp[0]).count(),                    \
+                   std::chrono::duration<double, std::micro>(hp[2] - hp[1]).count(),                    \
+                   std::chrono::duration<double, std::micro>(hp[3] - hp[2]).count());                   \
+  }
+
 int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, hipStream_t s) {
+  std::chrono::steady_clock::time_point hp[4];
   k_mo_associate<<<1, 64, 0, s>>>(m.st, a.quat[0], a.quat[1], a.quat[2], a.quat[3], a.pos[0], a.pos[1], a.pos[2]);
   if (hipGetLastError() != hipSuccess) return -1;
-  // the scan's VoxelGrids first with a fixed map (no early return below);
-  // after the keyframe map's plan otherwise (its capacity checks return
-  // before anything of the step's clouds ran)
-  if (fixedMap && scan_filter_fork(m, a, s)) return -1;
+  MO_HOSTPROF(0);
+  // the scan's VoxelGrids fork here: they need only the uploaded clouds
+  if (hipEventRecord(m.ev[EV_SCAN_FORK], s) != hipSuccess) return -1;
+  if (scan_filter_begin(m, a)) return -1;
   if (!fixedMap && a.nPlan >= 0) {  // extractSurroundingKeyFrames, loop-closure branch :961-999
     const int st = kf_map_recent(m, a, s);
     if (st) return st;
@@ -756,8 +783,10 @@ int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, h
     if (mo_set_map_device(m, m.nCornerMap, m.nSurfMap, s)) return -1;
   }
   // downsampleCurrentScan :1067-1091
-  if (!fixedMap && scan_filter_fork(m, a, s)) return -1;
+  MO_HOSTPROF(1);
+  if (scan_filter_end(m, a)) return -1;
   if (join_scan(m, s)) return -1;
+  MO_HOSTPROF(2);
   k_mo_guard<<<1, 64, 0, s>>>(m.st, m.cnt);
   // scan2MapOptimization :1329-1350 — the iterations exit on the device once converged
   const int qcap = a.nCorner + a.nSurf + a.nOutlier;
@@ -769,6 +798,7 @@ int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, h
     k_mo_solve<<<1, kMoSolveThreads, 0, s>>>(m.st, m.cnt, m.rows, qcap, it);
   }
   k_mo_finish<<<1, 64, 0, s>>>(m.st, a.imuOn, a.imuRoll, a.imuPitch);
+  MO_HOSTPROF(3);
   if (!fixedMap) {  // saveKeyFramesAndFactor :1353-1454
     k_kf_save<<<1, 64, 0, s>>>(m.kf, m.st, m.cnt, a.stamp);
     k_kf_copy<<<grid_for(qcap), 256, 0, s>>>(m.kf, m.cornerDS, m.surfDS, m.outlierDS);
