@@ -1143,6 +1143,8 @@ static int mo_alloc(lego_ctx* x, int nc, int ns) {
     MA(m.surfTotal, 2 * P); MA(m.surfTotalDS, 2 * P);
     m.rowCap = N * kLessSharpPerRing + 2 * P;
     MA(m.rows, (size_t)m.rowCap * 8);
+    m.partCap = 4096;  // k_mo_rows' grid cap (grid_for)
+    MA(m.part, (size_t)m.partCap * 28);
     HIPCHK(hipMemsetAsync(m.st, 0, sizeof(MoState), x->stream));
     HIPCHK(hipMemsetAsync(m.cnt, 0, sizeof(MoCounts), x->stream));
     // the VoxelGrids' fork streams (lego_mo.h): created with the mapping

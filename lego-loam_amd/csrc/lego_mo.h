@@ -106,6 +106,8 @@ struct MoDev {
   int scanCap;
   float* rows;  // [rowCap x 8]
   int rowCap;
+  double* part;  // [partCap x 28] the rows' AtA / AtB sums per k_mo_rows workgroup
+  int partCap;
   // keyframe-built map (when no fixed map is installed)
   MoKeyframes kf;
   float4 *cornerFromMap, *surfFromMap;  // [fromMapCap]

@@ -43,7 +43,7 @@
 namespace lego {
 
 constexpr unsigned kInvalidKey = 0xffffffffu;
-constexpr int kMoSolveThreads = 1024;
+constexpr int kMoSolveThreads = 256;
 
 static int grid_for(int n, int bs = 256) {
   int g = (n + bs - 1) / bs;
@@ -263,9 +263,9 @@ __device__ __forceinline__ float4 associate_to_map(float4 pi, const MoState* st)
 // One 32-lane group per query: corner queries [0, nCornerDS), then
 // surf+outlier queries.  Row r = {arx, ary, arz, cf.x, cf.y, cf.z, B, valid},
 // written by the group's lane 0 (the fit runs on every lane of the group).
-__device__ __forceinline__ void mo_row(MoState* st, int nC, const float4* cornerDS, const float4* surfTotalDS,
+__device__ __forceinline__ bool mo_row(MoState* st, int nC, const float4* cornerDS, const float4* surfTotalDS,
                                        const MoIndex& cornerIx, const MoIndex& surfIx, const float4* cornerMap,
-                                       const float4* surfMap, float* rows, int q) {
+                                       const float4* surfMap, float* rows, int q, float (&ra)[7]) {
   const bool lead = (threadIdx.x & (kKnnLanes - 1)) == 0;
   float* row = rows + (size_t)q * 8;
   if (lead) row[7] = 0.f;
@@ -274,7 +274,7 @@ __device__ __forceinline__ void mo_row(MoState* st, int nC, const float4* corner
   const float4 sel = associate_to_map(po, st);
   int ind[5];
   float sq[5];
-  if (knn5_group(corner ? cornerIx : surfIx, sel, ind, sq) < 5) return;
+  if (knn5_group(corner ? cornerIx : surfIx, sel, ind, sq) < 5) return false;
   float4 cf;
   if (corner) {  // cornerOptimization :1093-1174
     float cx = 0, cy = 0, cz = 0;
@@ -294,7 +294,7 @@ __device__ __forceinline__ void mo_row(MoState* st, int nC, const float4* corner
     const float A1[3][3] = {{a11, a12, a13}, {a12, a22, a23}, {a13, a23, a33}};
     float D1[3], V1[3][3];
     cv_eigen_sym3(A1, D1, V1);
-    if (!(D1[0] > 3 * D1[1])) return;
+    if (!(D1[0] > 3 * D1[1])) return false;
     const float x0 = sel.x, y0 = sel.y, z0 = sel.z;
     const float x1 = (float)(cx + 0.1 * (double)V1[0][0]);
     const float y1 = (float)(cy + 0.1 * (double)V1[0][1]);
@@ -312,7 +312,7 @@ __device__ __forceinline__ void mo_row(MoState* st, int nC, const float4* corner
     const float lc = -((x1 - x2) * m22 + (y1 - y2) * m33) / a012 / l12;
     const float ld2 = a012 / l12;
     const float s = (float)(1 - 0.9 * (double)lfabsf(ld2));
-    if (!((double)s > 0.1)) return;
+    if (!((double)s > 0.1)) return false;
     cf = make_float4(s * la, s * lb, s * lc, s * ld2);
   } else {  // surfOptimization :1176-1227
     float A0[5][3];
@@ -329,12 +329,12 @@ __device__ __forceinline__ void mo_row(MoState* st, int nC, const float4* corner
     pa /= ps; pb /= ps; pc /= ps; pd /= ps;
     for (int j = 0; j < 5; j++) {
       const float4 m = surfMap[ind[j]];
-      if ((double)lfabsf(pa * m.x + pb * m.y + pc * m.z + pd) > 0.2) return;
+      if ((double)lfabsf(pa * m.x + pb * m.y + pc * m.z + pd) > 0.2) return false;
     }
     const float pd2 = pa * sel.x + pb * sel.y + pc * sel.z + pd;
     const float s = (float)(1 - 0.9 * (double)lfabsf(pd2) /
                                     (double)__builtin_sqrtf(__builtin_sqrtf(sel.x * sel.x + sel.y * sel.y + sel.z * sel.z)));
-    if (!((double)s > 0.1)) return;
+    if (!((double)s > 0.1)) return false;
     cf = make_float4(s * pa, s * pb, s * pc, s * pd2);
   }
   // LMOptimization's Jacobian row (:1244-1270)
@@ -349,24 +349,57 @@ __device__ __forceinline__ void mo_row(MoState* st, int nC, const float4* corner
   const float arz = ((crz * srx * sry - cry * srz) * po.x + (-cry * crz - srx * sry * srz) * po.y) * cf.x +
                     (crx * crz * po.x - crx * srz * po.y) * cf.y +
                     ((sry * srz + cry * crz * srx) * po.x + (crz * sry - cry * srx * srz) * po.y) * cf.z;
-  if (!lead) return;
-  row[0] = arx; row[1] = ary; row[2] = arz;
-  row[3] = cf.x; row[4] = cf.y; row[5] = cf.z;
-  row[6] = -cf.w;
-  row[7] = 1.f;
+  ra[0] = arx; ra[1] = ary; ra[2] = arz;
+  ra[3] = cf.x; ra[4] = cf.y; ra[5] = cf.z;
+  ra[6] = -cf.w;
+  if (lead) {
+    row[0] = arx; row[1] = ary; row[2] = arz;
+    row[3] = cf.x; row[4] = cf.y; row[5] = cf.z;
+    row[6] = -cf.w;
+    row[7] = 1.f;
+  }
+  return true;
 }
 
 constexpr int kMoRowsThreads = 256;
+constexpr int kMoSums = 21 + 6 + 1;  // AtA upper triangle, AtB, row count
+// One 32-lane group per query; each workgroup also sums its rows' AtA / AtB
+// terms in double (products of floats are exact in double) into part[block],
+// so k_mo_solve reduces one partial per workgroup instead of every row.
 __global__ void __launch_bounds__(kMoRowsThreads) k_mo_rows(MoState* st, const MoCounts* cnt, const float4* cornerDS,
                                                            const float4* surfTotalDS, MoIndex cornerIx,
                                                            MoIndex surfIx, const float4* cornerMap,
-                                                           const float4* surfMap, float* rows, int qcap) {
+                                                           const float4* surfMap, float* rows, int qcap,
+                                                           double* part) {
   if (!st->optimized || st->converged) return;
   const int nC = cnt->cornerDS, nQ = min(nC + cnt->surfTotalDS, qcap);
   constexpr int kGroups = kMoRowsThreads / kKnnLanes;
+  __shared__ double red[kGroups][kMoSums];
+  const int g = (int)threadIdx.x / kKnnLanes;
+  const bool lead = (threadIdx.x & (kKnnLanes - 1)) == 0;
+  if (lead)
+    for (int k = 0; k < kMoSums; ++k) red[g][k] = 0.0;
   for (int q0 = blockIdx.x * kGroups; q0 < nQ; q0 += gridDim.x * kGroups) {  // group-uniform
-    const int q = q0 + (int)threadIdx.x / kKnnLanes;
-    if (q < nQ) mo_row(st, nC, cornerDS, surfTotalDS, cornerIx, surfIx, cornerMap, surfMap, rows, q);
+    const int q = q0 + g;
+    float ra[7];
+    const bool ok = q < nQ && mo_row(st, nC, cornerDS, surfTotalDS, cornerIx, surfIx, cornerMap, surfMap, rows, q, ra);
+    if (lead && ok) {
+      int o = 0;
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = i; j < 6; ++j) red[g][o++] += (double)ra[i] * (double)ra[j];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) red[g][21 + i] += (double)ra[i] * (double)ra[6];
+      red[g][27] += 1.0;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < kMoSums) {
+    double sum = 0.0;
+#pragma unroll
+    for (int w = 0; w < kGroups; ++w) sum += red[w][threadIdx.x];
+    part[(size_t)blockIdx.x * kMoSums + threadIdx.x] = sum;
   }
 }
 
@@ -392,35 +425,23 @@ __device__ __forceinline__ double mo_wave_sum(double v) {
   return (mo_rdlane(v, 0) + mo_rdlane(v, 16)) + (mo_rdlane(v, 32) + mo_rdlane(v, 48));
 }
 
-__device__ void mo_solve_tail(MoState* st, const double* tot, int iterCount, float* ws, int* wsi);
+__device__ __forceinline__ void mo_solve_tail(MoState* st, const double* tot, int iterCount, float* ws, int* wsi);
 
-constexpr int kMoSums = 21 + 6 + 1;  // AtA upper triangle, AtB, row count
-
-__global__ void __launch_bounds__(kMoSolveThreads) k_mo_solve(MoState* st, const MoCounts* cnt, const float* rows,
-                                                             int qcap, int iterCount) {
+// nb: the partials k_mo_rows wrote (its grid)
+__global__ void __launch_bounds__(kMoSolveThreads) k_mo_solve(MoState* st, const double* part, int nb,
+                                                             int iterCount) {
   if (!st->optimized || st->converged) return;
   __shared__ double red[kMoSolveThreads / 64][kMoSums];
   __shared__ float ws[6 * 6 * 6 + 16];  // eigen / inverse workspace (thread 0)
   __shared__ int wsi[16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int Q = min(cnt->cornerDS + cnt->surfTotalDS, qcap);
   double acc[kMoSums];
 #pragma unroll
   for (int k = 0; k < kMoSums; ++k) acc[k] = 0.0;
-  for (int r = tid; r < Q; r += kMoSolveThreads) {
-    const float* row = rows + (size_t)r * 8;
-    if (row[7] == 0.f) continue;
-    double a[7];
+  for (int b = tid; b < nb; b += kMoSolveThreads) {
+    const double* pb = part + (size_t)b * kMoSums;
 #pragma unroll
-    for (int k = 0; k < 7; ++k) a[k] = row[k];
-    int o = 0;
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-#pragma unroll
-      for (int j = i; j < 6; ++j) acc[o++] += a[i] * a[j];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) acc[21 + i] += a[i] * a[6];
-    acc[27] += 1.0;
+    for (int k = 0; k < kMoSums; ++k) acc[k] += pb[k];
   }
 #pragma unroll
   for (int k = 0; k < kMoSums; ++k) {
@@ -430,8 +451,10 @@ __global__ void __launch_bounds__(kMoSolveThreads) k_mo_solve(MoState* st, const
   __syncthreads();
   if (tid != 0) return;
   double tot[kMoSums];
+#pragma unroll
   for (int k = 0; k < kMoSums; ++k) {
     double sum = 0;
+#pragma unroll
     for (int w = 0; w < kMoSolveThreads / 64; ++w) sum += red[w][k];
     tot[k] = sum;
   }
@@ -441,18 +464,23 @@ __global__ void __launch_bounds__(kMoSolveThreads) k_mo_solve(MoState* st, const
 // LMOptimization (:1229-1327) from the reduced sums, one thread: the 6x6 QR
 // solve, the iteration-0 eigen analysis (degeneracy), the update and the
 // convergence test.  ws / wsi: LDS workspace of the eigen / inverse.
-__device__ void mo_solve_tail(MoState* st, const double* tot, int iterCount, float* ws, int* wsi) {
+__device__ __forceinline__ void mo_solve_tail(MoState* st, const double* tot, int iterCount, float* ws, int* wsi) {
   const int M = (int)tot[27];
   st->rowsLast = M;
   st->iterations = iterCount + 1;
   if (M < 50) return;  // LMOptimization returns false: not converged
   float AtA[6][6], AtB[6];
   int o = 0;
+#pragma unroll
   for (int i = 0; i < 6; ++i)
+#pragma unroll
     for (int j = i; j < 6; ++j) { AtA[i][j] = AtA[j][i] = (float)tot[o++]; }
+#pragma unroll
   for (int i = 0; i < 6; ++i) AtB[i] = (float)tot[21 + i];
   float Aq[6][6], X[6];
+#pragma unroll
   for (int i = 0; i < 6; ++i)
+#pragma unroll
     for (int j = 0; j < 6; ++j) Aq[i][j] = AtA[i][j];
   cv_solve_qr<6, 6>(Aq, AtB, X);
   float (&P)[6][6] = *reinterpret_cast<float(*)[6][6]>(st->matP);
@@ -465,7 +493,9 @@ __device__ void mo_solve_tail(MoState* st, const double* tot, int iterCount, flo
     float (&E)[6] = *reinterpret_cast<float(*)[6]>(ws + 144);
     int (&indR)[6] = *reinterpret_cast<int(*)[6]>(wsi);
     int (&indC)[6] = *reinterpret_cast<int(*)[6]>(wsi + 6);
+#pragma unroll
     for (int i = 0; i < 6; ++i)
+#pragma unroll
       for (int j = 0; j < 6; ++j) Ae[i][j] = AtA[i][j];
     cv_eigen_sym_ws<6>(Ae, E, V, indR, indC);
     for (int i = 0; i < 6; ++i)
@@ -484,10 +514,12 @@ __device__ void mo_solve_tail(MoState* st, const double* tot, int iterCount, flo
   }
   if (st->isDegenerate) {
     float X2[6];
+#pragma unroll
     for (int i = 0; i < 6; ++i) X2[i] = X[i];
     cv_matvec<6>(P, X2, X);
   }
   float* t = st->transformTobeMapped;
+#pragma unroll
   for (int i = 0; i < 6; i++) t[i] += X[i];
   // pcl::rad2deg(float) = a * 57.29578f
   const double d0 = X[0] * 57.29578f, d1 = X[1] * 57.29578f, d2 = X[2] * 57.29578f;
@@ -791,11 +823,13 @@ int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, h
   // scan2MapOptimization :1329-1350 — the iterations exit on the device once converged
   const int qcap = a.nCorner + a.nSurf + a.nOutlier;
   if (qcap > m.rowCap) return -1;
+  const int nb = qcap > 0 ? grid_for(qcap, kMoRowsThreads / kKnnLanes) : 0;
+  if (nb > m.partCap) return -1;
   for (int it = 0; it < 10; ++it) {
     if (qcap > 0)
-      k_mo_rows<<<grid_for(qcap, kMoRowsThreads / kKnnLanes), kMoRowsThreads, 0, s>>>(
-          m.st, m.cnt, m.cornerDS, m.surfTotalDS, m.cornerIx, m.surfIx, m.cornerMapDS, m.surfMapDS, m.rows, qcap);
-    k_mo_solve<<<1, kMoSolveThreads, 0, s>>>(m.st, m.cnt, m.rows, qcap, it);
+      k_mo_rows<<<nb, kMoRowsThreads, 0, s>>>(m.st, m.cnt, m.cornerDS, m.surfTotalDS, m.cornerIx, m.surfIx,
+                                                m.cornerMapDS, m.surfMapDS, m.rows, qcap, m.part);
+    k_mo_solve<<<1, kMoSolveThreads, 0, s>>>(m.st, m.part, nb, it);
   }
   k_mo_finish<<<1, 64, 0, s>>>(m.st, a.imuOn, a.imuRoll, a.imuPitch);
   MO_HOSTPROF(3);
