@@ -361,7 +361,7 @@ __device__ __forceinline__ bool mo_row(MoState* st, int nC, const float4* corner
   return true;
 }
 
-constexpr int kMoRowsThreads = 256;
+constexpr int kMoRowsThreads = 256, kMoRowsGrid = 1536;
 constexpr int kMoSums = 21 + 6 + 1;  // AtA upper triangle, AtB, row count
 // One 32-lane group per query; each workgroup also sums its rows' AtA / AtB
 // terms in double (products of floats are exact in double) into part[block],
@@ -823,7 +823,10 @@ int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, h
   // scan2MapOptimization :1329-1350 — the iterations exit on the device once converged
   const int qcap = a.nCorner + a.nSurf + a.nOutlier;
   if (qcap > m.rowCap) return -1;
-  const int nb = qcap > 0 ? grid_for(qcap, kMoRowsThreads / kKnnLanes) : 0;
+  // qcap bounds the filtered query count from above (the raw clouds): 1536
+  // workgroups (six per CU) cover C5's ~12 k queries in one pass and keep
+  // thousands of empty workgroups off the dispatcher; larger clouds loop
+  const int nb = qcap > 0 ? std::min(grid_for(qcap, kMoRowsThreads / kKnnLanes), kMoRowsGrid) : 0;
   if (nb > m.partCap) return -1;
   for (int it = 0; it < 10; ++it) {
     if (qcap > 0)
