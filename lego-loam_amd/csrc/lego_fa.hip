@@ -934,6 +934,7 @@ __device__ void lfv_wave(const BatchBufs& bb, const DevCfg& c, int ring, int b, 
 }
 
 constexpr int kLfvMaxPer = 8;  // voxels per thread (H <= kLfvMaxPer * kExtractThreads)
+constexpr int kLfvBlockRings = 2;  // rings per large-ring workgroup (k_lf_voxel; 1 / 2 / 4 / 8: fleet 254 / 256 / 245 / 253 k)
 __host__ __device__ inline size_t lfvox_lds_bytes(int H) {
   return (((size_t)H * 6 + 15) & ~(size_t)15) + vg_sort_scratch_bytes(H, kExtractThreads) + 64;
 }
@@ -1020,14 +1021,21 @@ __device__ void lfv_block(const BatchBufs& bb, const DevCfg& c, int ring, int b,
 
 // The batch's per-ring VoxelGrids in one launch, so small and large rings
 // interleave: workgroups [0, g4) of each scan take four rings each, a ring of
-// up to kVgWaveMax points per wave (lfv_wave); workgroups [g4, g4 + N) one
-// larger ring each with the whole workgroup (lfv_block).  g4 = 0 (diagnostic
-// LEGO_LFV_WAVE=0): every ring by a workgroup.
-__global__ void __launch_bounds__(kExtractThreads, 4) k_lf_voxel(BatchBufs bb, DevCfg c, int g4) {
+// up to kVgWaveMax points per wave (lfv_wave); workgroups [g4, g4 + gb) the
+// larger rings with the whole workgroup (lfv_block), workgroup k the rings
+// k, k + gb, ... (gb < N: fewer workgroups that find no large ring).  g4 = 0
+// (diagnostic LEGO_LFV_WAVE=0): every ring by a workgroup.
+__global__ void __launch_bounds__(kExtractThreads, 4) k_lf_voxel(BatchBufs bb, DevCfg c, int g4, int gb) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   const int b = blockIdx.y;
-  if ((int)blockIdx.x < g4) lfv_wave(bb, c, (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6), b, lds_raw);
-  else lfv_block(bb, c, (int)blockIdx.x - g4, b, g4 > 0 ? kVgWaveMax : 0, lds_raw);
+  if ((int)blockIdx.x < g4) {
+    lfv_wave(bb, c, (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6), b, lds_raw);
+    return;
+  }
+  for (int ring = (int)blockIdx.x - g4; ring < c.N; ring += gb) {
+    lfv_block(bb, c, ring, b, g4 > 0 ? kVgWaveMax : 0, lds_raw);
+    __syncthreads();  // the next ring reuses the LDS
+  }
 }
 
 #ifndef EXTRACT_MINWAVES
@@ -1147,7 +1155,12 @@ void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_ca
   tm->mark("fa.voxel", s);
   static const bool waveOn = !std::getenv("LEGO_LFV_WAVE") || std::atoi(std::getenv("LEGO_LFV_WAVE")) != 0;
   const int g4 = waveOn ? (c.N + 3) / 4 : 0;
-  k_lf_voxel<<<dim3(g4 + c.N, B), kExtractThreads, std::max(kLfvWaveLds, lfvox_lds_bytes(c.H)), s>>>(bb, c, g4);
+  // rings per large-ring workgroup (LEGO_LFV_BLOCK_RINGS, A/B knob; 1 = one
+  // workgroup per ring)
+  static const int rpb = std::getenv("LEGO_LFV_BLOCK_RINGS") ? std::max(1, std::atoi(std::getenv("LEGO_LFV_BLOCK_RINGS")))
+                                                              : (waveOn ? kLfvBlockRings : 1);
+  const int gb = (c.N + rpb - 1) / rpb;
+  k_lf_voxel<<<dim3(g4 + gb, B), kExtractThreads, std::max(kLfvWaveLds, lfvox_lds_bytes(c.H)), s>>>(bb, c, g4, gb);
   tm->mark("fa.compact", s);
   k_fa_compact<<<dim3(c.N, B), 256, 0, s>>>(bb, c);
 }
