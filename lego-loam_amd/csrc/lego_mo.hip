@@ -265,7 +265,7 @@ __device__ __forceinline__ float4 associate_to_map(float4 pi, const MoState* st)
 // written by the group's lane 0 (the fit runs on every lane of the group).
 __device__ __forceinline__ bool mo_row(MoState* st, int nC, const float4* cornerDS, const float4* surfTotalDS,
                                        const MoIndex& cornerIx, const MoIndex& surfIx, const float4* cornerMap,
-                                       const float4* surfMap, float* rows, int q, float (&ra)[7]) {
+                                       const float4* surfMap, float* rows, int q, double* red) {
   const bool lead = (threadIdx.x & (kKnnLanes - 1)) == 0;
   float* row = rows + (size_t)q * 8;
   if (lead) row[7] = 0.f;
@@ -349,14 +349,21 @@ __device__ __forceinline__ bool mo_row(MoState* st, int nC, const float4* corner
   const float arz = ((crz * srx * sry - cry * srz) * po.x + (-cry * crz - srx * sry * srz) * po.y) * cf.x +
                     (crx * crz * po.x - crx * srz * po.y) * cf.y +
                     ((sry * srz + cry * crz * srx) * po.x + (crz * sry - cry * srx * srz) * po.y) * cf.z;
-  ra[0] = arx; ra[1] = ary; ra[2] = arz;
-  ra[3] = cf.x; ra[4] = cf.y; ra[5] = cf.z;
-  ra[6] = -cf.w;
   if (lead) {
     row[0] = arx; row[1] = ary; row[2] = arz;
     row[3] = cf.x; row[4] = cf.y; row[5] = cf.z;
     row[6] = -cf.w;
     row[7] = 1.f;
+    // the workgroup's AtA / AtB sums (products of floats are exact in double)
+    const float ra[7] = {arx, ary, arz, cf.x, cf.y, cf.z, -cf.w};
+    int o = 0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = i; j < 6; ++j) red[o++] += (double)ra[i] * (double)ra[j];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) red[21 + i] += (double)ra[i] * (double)ra[6];
+    red[27] += 1.0;
   }
   return true;
 }
@@ -381,18 +388,7 @@ __global__ void __launch_bounds__(kMoRowsThreads) k_mo_rows(MoState* st, const M
     for (int k = 0; k < kMoSums; ++k) red[g][k] = 0.0;
   for (int q0 = blockIdx.x * kGroups; q0 < nQ; q0 += gridDim.x * kGroups) {  // group-uniform
     const int q = q0 + g;
-    float ra[7];
-    const bool ok = q < nQ && mo_row(st, nC, cornerDS, surfTotalDS, cornerIx, surfIx, cornerMap, surfMap, rows, q, ra);
-    if (lead && ok) {
-      int o = 0;
-#pragma unroll
-      for (int i = 0; i < 6; ++i)
-#pragma unroll
-        for (int j = i; j < 6; ++j) red[g][o++] += (double)ra[i] * (double)ra[j];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) red[g][21 + i] += (double)ra[i] * (double)ra[6];
-      red[g][27] += 1.0;
-    }
+    if (q < nQ) mo_row(st, nC, cornerDS, surfTotalDS, cornerIx, surfIx, cornerMap, surfMap, rows, q, red[g]);
   }
   __syncthreads();
   if (threadIdx.x < kMoSums) {
