@@ -114,10 +114,10 @@ struct MoDev {
   int fromMapCap;
   // Fork-join of a step's independent VoxelGrids (each is latency-bound and
   // fills a small part of the GPU): fork[0] (the context's odometry stream)
-  // takes the scan's outlier cloud, the map's corner cloud and its index, then
-  // the scan's corner cloud; fork[1] the scan's surf cloud, then surf +
-  // outlier; the step's stream the map's surf cloud and index.  Each chain
-  // has its own VoxelGrid scratch.
+  // takes the scan's outlier cloud, then the map's corner cloud and its
+  // index; fork[1] the scan's surf cloud, then surf + outlier; the step's
+  // stream the map's surf cloud and index, then the scan's corner cloud.
+  // Each chain has its own VoxelGrid scratch.
   hipStream_t fork[2];
   hipEvent_t ev[6];
   VgScratch vgMap2, vgScan1, vgScan2;
