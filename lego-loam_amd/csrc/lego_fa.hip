@@ -821,7 +821,7 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
     cnt[0] = L.misc[M_NSH];
     cnt[1] = L.misc[M_NLS];
     cnt[2] = L.misc[M_NFL];
-    cnt[3] = nlf;
+    cnt[3] = nlf | (nlf << 16);  // high half: the less-flat count k_lf_voxel decides on (never overwritten)
   }
   if (ring == 0 && carry) {
     // wave 0 holds the picking flags; lane values of `flags` are merged below
@@ -869,7 +869,10 @@ __device__ void lfv_wave(const BatchBufs& bb, const DevCfg& c, int ring, int b, 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (ring >= c.N) return;
   int* cnt = bb.r_cnt + ((size_t)b * c.N + ring) * 4;
-  const int K = cnt[3];
+  // the count as k_extract wrote it (high half): a large ring's workgroup may
+  // already have replaced the low half with its voxel count, which must not
+  // make this wave filter the filtered ring again
+  const int K = cnt[3] >> 16;
   if (K <= 0 || K > kVgWaveMax) return;  // wave-uniform
   float4* slot = bb.r_lflat + (size_t)b * c.P + (size_t)ring * c.H;
   uint32_t* key = (uint32_t*)lds + (size_t)wave * kVgWaveMax;
@@ -930,7 +933,7 @@ __device__ void lfv_wave(const BatchBufs& bb, const DevCfg& c, int ring, int b, 
 #pragma unroll
   for (int j = 0; j < kLfvWaveRows; ++j)
     if (at[j] >= 0) slot[at[j]] = cen[j];
-  if (lane == 0) cnt[3] = outc;
+  if (lane == 0) cnt[3] = outc | (K << 16);
 }
 
 constexpr int kLfvMaxPer = 8;  // voxels per thread (H <= kLfvMaxPer * kExtractThreads)
@@ -949,7 +952,7 @@ __device__ void lfv_block(const BatchBufs& bb, const DevCfg& c, int ring, int b,
   __shared__ float mm[4][6];
   int* cnt = bb.r_cnt + ((size_t)b * c.N + ring) * 4;
   float4* slot = bb.r_lflat + (size_t)b * c.P + (size_t)ring * H;
-  const int K = cnt[3];
+  const int K = cnt[3] >> 16;  // as k_extract wrote it (lfv_wave)
   if (K <= waveMax) return;  // a wave's (or empty)
   const float inv = 1.0f / 0.2f;
   float mn[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
@@ -1016,7 +1019,7 @@ __device__ void lfv_block(const BatchBufs& bb, const DevCfg& c, int ring, int b,
 #pragma unroll
   for (int j = 0; j < kLfvMaxPer; ++j)
     if (at[j] >= 0) slot[at[j]] = cen[j];
-  if (tid == 0) cnt[3] = outc;
+  if (tid == 0) cnt[3] = outc | (K << 16);
 }
 
 // The batch's per-ring VoxelGrids in one launch, so small and large rings
@@ -1114,7 +1117,7 @@ __global__ void k_fa_compact(BatchBufs bb, DevCfg c) {
     int s[4] = {0, 0, 0, 0};
     for (int q = tid; q < r; q += 64)
 #pragma unroll
-      for (int f = 0; f < 4; ++f) s[f] += cnt[q * 4 + f];
+      for (int f = 0; f < 4; ++f) s[f] += cnt[q * 4 + f] & 0xffff;  // [3]: the VoxelGrid's count, low half
 #pragma unroll
     for (int f = 0; f < 4; ++f)
       for (int o = 32; o > 0; o >>= 1) s[f] += __shfl_xor(s[f], o, 64);
@@ -1122,7 +1125,7 @@ __global__ void k_fa_compact(BatchBufs bb, DevCfg c) {
 #pragma unroll
       for (int f = 0; f < 4; ++f) {
         off[f] = s[f];
-        if (r == c.N - 1) bb.f_cnt[b * 4 + f] = s[f] + cnt[r * 4 + f];
+        if (r == c.N - 1) bb.f_cnt[b * 4 + f] = s[f] + (cnt[r * 4 + f] & 0xffff);
       }
     }
   }
@@ -1134,7 +1137,7 @@ __global__ void k_fa_compact(BatchBufs bb, DevCfg c) {
     bb.f_lsharp[(size_t)b * c.N * kLessSharpPerRing + off[1] + t] = bb.r_lsharp[rb * kLessSharpPerRing + t];
   for (int t = tid; t < cnt[r * 4 + 2]; t += blockDim.x)
     bb.f_flat[(size_t)b * c.N * kFlatPerRing + off[2] + t] = bb.r_flat[rb * kFlatPerRing + t];
-  for (int t = tid; t < cnt[r * 4 + 3]; t += blockDim.x)
+  for (int t = tid; t < (cnt[r * 4 + 3] & 0xffff); t += blockDim.x)
     bb.f_lflat[(size_t)b * c.P + off[3] + t] = bb.r_lflat[(size_t)b * c.P + (size_t)r * c.H + t];
 }
 
