@@ -865,7 +865,7 @@ __device__ __forceinline__ float4 lfv_centroid(const float4* slot, const uint16_
 // scratch words.
 constexpr int kLfvWaveRows = kVgWaveMax / 64;
 constexpr size_t kLfvWaveLds = (size_t)4 * kVgWaveMax * 10;  // four waves' key (4 B), payload (2 B), scratch (4 B)
-__device__ void lfv_wave(const BatchBufs& bb, const DevCfg& c, int ring, int b, unsigned char* lds) {
+__device__ __forceinline__ void lfv_wave(const BatchBufs& bb, const DevCfg& c, int ring, int b, unsigned char* lds) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (ring >= c.N) return;
   int* cnt = bb.r_cnt + ((size_t)b * c.N + ring) * 4;
@@ -941,7 +941,7 @@ constexpr int kLfvBlockRings = 2;  // rings per large-ring workgroup (k_lf_voxel
 __host__ __device__ inline size_t lfvox_lds_bytes(int H) {
   return (((size_t)H * 6 + 15) & ~(size_t)15) + vg_sort_scratch_bytes(H, kExtractThreads) + 64;
 }
-__device__ void lfv_block(const BatchBufs& bb, const DevCfg& c, int ring, int b, int waveMax,
+__device__ __forceinline__ void lfv_block(const BatchBufs& bb, const DevCfg& c, int ring, int b, int waveMax,
                           unsigned char* lds_raw) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int H = c.H;
@@ -1028,7 +1028,10 @@ __device__ void lfv_block(const BatchBufs& bb, const DevCfg& c, int ring, int b,
 // larger rings with the whole workgroup (lfv_block), workgroup k the rings
 // k, k + gb, ... (gb < N: fewer workgroups that find no large ring).  g4 = 0
 // (diagnostic LEGO_LFV_WAVE=0): every ring by a workgroup.
-__global__ void __launch_bounds__(kExtractThreads, 4) k_lf_voxel(BatchBufs bb, DevCfg c, int g4, int gb) {
+#ifndef LFV_MINB
+#define LFV_MINB 4
+#endif
+__global__ void __launch_bounds__(kExtractThreads, LFV_MINB) k_lf_voxel(BatchBufs bb, DevCfg c, int g4, int gb) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   const int b = blockIdx.y;
   if ((int)blockIdx.x < g4) {
