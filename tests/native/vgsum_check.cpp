@@ -1,11 +1,13 @@
-// vg_sum_order_check.cpp — replays libstdc++'s introsort levels over key
+// vgsum_check.cpp — replays libstdc++'s introsort levels over key
 // arrays dumped by the oracle (LEGO_ORACLE_VG_DUMP: int32 count, then the
 // keys, per VoxelGrid call) and checks lego_vgsort.h's sumOrder rule: with the
 // heap pieces it ranks stably (each key at most twice in the piece, the
 // smallest not also in the preceding leaf) and the others heap-sorted, every
 // voxel's float sum from 0 of random values equals the sum in std::sort's
-// order.  g++ -O2 -std=c++17 scripts/vg_sum_order_check.cpp -o /tmp/vgsum
-// && /tmp/vgsum dump.bin   (V=1 lists the ranked pieces)
+// order.  tests/test_numerics_shim.py::test_vgsort_sum_order_rule runs it
+// over the C2 ring keys and adversary fixtures; by hand: g++ -O2 -std=c++17
+// tests/native/vgsum_check.cpp -o /tmp/vgsum && /tmp/vgsum dump.bin (V=1
+// lists the ranked pieces).  Exit status 1 when a voxel sum differs.
 #include <cstdio>
 #include <vector>
 #include <algorithm>
@@ -44,4 +46,5 @@ int main(int argc,char**argv){ FILE* f=fopen(argv[1],"rb"); int m; int call=0; i
    for(int i=0;i<m;){ int j=i; float s1=0,s2=0; while(j<m && ref[j].k==ref[i].k){ s1+=val[ref[j].v]; s2+=val[out[j].v]; if(out[j].k!=ref[j].k){bad++; break;} j++; } if(memcmp(&s1,&s2,4)) { bad++; printf("call %d voxel at %d differs\n",call,i);} i=j; }
  }
  printf("calls %d shortcuts %d flagged %d bad %d\n",call,shortcuts,flagged,bad);
+ return bad ? 1 : 0;
 }

@@ -43,6 +43,38 @@ def test_vgsort_partition_rules_match_std_sort(tmp_path):
     assert r.returncode == 0, r.stdout
 
 
+def test_vgsort_sum_order_rule(tmp_path):
+    """lego_vgsort.h's sumOrder: a heap-sorted piece ranked stably instead
+    (each key at most twice in it, its smallest not also in the preceding
+    leaf) must give every voxel the same float sum from 0 as std::sort's
+    order.  Replayed over C2 scan 465's ring keys, the adversary fixtures and
+    tied random keys, with both kinds of piece present."""
+    import numpy as np
+
+    exe = _build(tmp_path, "vgsum_check", REPO / "tests/native/vgsum_check.cpp")
+    arrays = list(np.load(REPO / "tests/golden/c2_ring_keys.npz").values())
+    z = np.load(REPO / "tests/golden/vg_killer.npz")
+    arrays += [z[k] for k in z.files if not k.startswith("heaps_")]
+    rng = np.random.default_rng(4)
+    for n in (300, 900, 2000, 5000):
+        for div in (1, 2, 3):  # ascending runs with ties: std::sort's degenerate splits
+            a = np.sort(rng.integers(0, n // div + 1, n))
+            b = np.sort(rng.integers(0, n // div + 1, n))
+            arrays.append(np.concatenate([a, b]))
+    dump = tmp_path / "keys.bin"
+    with open(dump, "wb") as f:
+        for k in arrays:
+            k = np.asarray(k, np.int64)
+            k = (k - k.min()).astype(np.uint32)
+            np.array([len(k)], np.int32).tofile(f)
+            k.tofile(f)
+    r = subprocess.run([str(exe), str(dump)], capture_output=True, text=True, timeout=600)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout
+    ranked, exact = (int(x) for x in r.stdout.split("shortcuts")[1].split("bad")[0].replace("flagged", "").split())
+    assert ranked > 0 and exact > 0, r.stdout
+
+
 def test_eigen3_register_form_matches_generic(tmp_path):
     """The device solver's register-resident 3x3 Jacobi (cv_eigen_sym3) must
     equal the OpenCV JacobiImpl_ restatement (cv_eigen_sym<3>) bit for bit."""
