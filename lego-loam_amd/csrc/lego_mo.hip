@@ -715,9 +715,9 @@ static int map_filter(MoDev& m, const float4* corner, int nC, const float4* surf
   if (voxel_grid_device(surf, nS, nullptr, 0.4f, m.surfMapDS, &m.cnt->surfMapDS, m.vg, s)) return -1;
   if (index_build_device(m.surfMapDS, nS, &m.cnt->surfMapDS, m.surfIx, m.vg, s)) return -1;
   if (hipStreamWaitEvent(f, m.ev[EV_MAP_FORK], 0) != hipSuccess) return -1;
-  if (voxel_grid_device(corner, nC, nullptr, 0.2f, m.cornerMapDS, &m.cnt->cornerMapDS, m.vgMap2, f)) return -1;
-  if (index_build_device(m.cornerMapDS, nC, &m.cnt->cornerMapDS, m.cornerIx, m.vgMap2, f)) return -1;
-  return fork_wait(m, EV_MAP_CORNER, f, s) ? 0 : -1;
+  const bool ok = voxel_grid_device(corner, nC, nullptr, 0.2f, m.cornerMapDS, &m.cnt->cornerMapDS, m.vgMap2, f) == 0 &&
+                  index_build_device(m.cornerMapDS, nC, &m.cnt->cornerMapDS, m.cornerIx, m.vgMap2, f) == 0;
+  return fork_wait(m, EV_MAP_CORNER, f, s) && ok ? 0 : -1;  // joined on failure too
 }
 
 // downsampleCurrentScan (:1067-1091) forked off s at EV_SCAN_FORK, in two
@@ -803,20 +803,26 @@ int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, h
   MO_HOSTPROF(0);
   // the scan's VoxelGrids fork here: they need only the uploaded clouds
   if (hipEventRecord(m.ev[EV_SCAN_FORK], s) != hipSuccess) return -1;
-  if (scan_filter_begin(m, a)) return -1;
+  // Any return from here on first joins the forks into s: the next step's
+  // uploads on s must not overwrite clouds a fork still reads.
+  auto fail = [&](int st) {
+    (void)join_scan(m, s);
+    return st;
+  };
+  if (scan_filter_begin(m, a)) return fail(-1);
   if (!fixedMap && a.nPlan >= 0) {  // extractSurroundingKeyFrames, loop-closure branch :961-999
     const int st = kf_map_recent(m, a, s);
-    if (st) return st;
+    if (st) return fail(st);
   } else if (!fixedMap) {  // extractSurroundingKeyFrames :1001-1065
     const int st = kf_map(m, radius, s);
-    if (st) return st;
+    if (st) return fail(st);
   } else if (m.mapPerStep) {  // the map VoxelGrids (:1058-1064) and kd-tree builds (:1333-1334) of every step
-    if (mo_set_map_device(m, m.nCornerMap, m.nSurfMap, s)) return -1;
+    if (mo_set_map_device(m, m.nCornerMap, m.nSurfMap, s)) return fail(-1);
   }
   MO_HOSTPROF(1);
-  if (scan_filter_end(m, a)) return -1;
+  if (scan_filter_end(m, a)) return fail(-1);
   // the scan's corner cloud on s, after the map's surf cloud (:1069-1073)
-  if (voxel_grid_device(m.cornerLast, a.nCorner, nullptr, 0.2f, m.cornerDS, &m.cnt->cornerDS, m.vg, s)) return -1;
+  if (voxel_grid_device(m.cornerLast, a.nCorner, nullptr, 0.2f, m.cornerDS, &m.cnt->cornerDS, m.vg, s)) return fail(-1);
   if (join_scan(m, s)) return -1;
   MO_HOSTPROF(2);
   k_mo_guard<<<1, 64, 0, s>>>(m.st, m.cnt);
