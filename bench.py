@@ -519,14 +519,25 @@ def main():
     # N > 1 hand-off transport: the C-ABI's own collective (lego_comm_gather_handoff_ex,
     # RCCL send/recv over xGMI, packets kept in rank 0's HBM) when every rank has
     # its GPU; the one-GPU rehearsal (gloo, shared device) gathers over torch.
-    native = dist is not None and backend == "nccl"
-    native_error = None  # a native-collective failure on every rank falls back to the torch gather, and says so
-    comm = None
-    if native:
-        try:
-            comm = ms.native_comm(L, dist, local)
-        except Exception as e:  # noqa: BLE001
-            native, native_error = False, f"lego_comm_create: {e}"
+    # The choice is collective (ms.HandoffTransport): the ranks agree over a gloo
+    # control group after the communicator's creation and after every native
+    # gather, and a failure on any rank moves EVERY rank to the torch gather at
+    # the same step (never RCCL on some ranks and torch on others: a hang).
+    comm, transport = None, None
+    if dist is not None:
+        ctrl = dist.new_group(backend="gloo") if backend != "gloo" else None
+        want_native = backend == "nccl"
+        create_error = None
+        if want_native:
+            try:
+                comm = ms.native_comm(L, dist, local)
+            except Exception as e:  # noqa: BLE001
+                create_error = f"lego_comm_create: {e}"
+        transport = ms.HandoffTransport(dist, ctrl, want_native and comm is not None, create_error)
+        if not transport.native and comm is not None:
+            lib.lego_comm_abort(comm)
+            lib.lego_comm_destroy(comm)
+            comm = None
 
     # Steps are pipelined two deep (lego_odom_batch_submit / _wait): step i+1's
     # projection + extraction run while step i's odometry chain does.
@@ -538,18 +549,17 @@ def main():
         cp = (L.PoseRec * B)()
         C.memmove(cp, recs, C.sizeof(recs))
         # N > 1: the step's hand-off packet (pose records + the published
-        # corner / surf / outlier clouds) to rank 0 before the slot is reused:
-        # gathered right here by the native collective, or packed into HBM for
-        # the torch gather
-        nonlocal native, native_error
+        # corner / surf / outlier clouds) gathered to rank 0 right here, before
+        # the slot is reused: by the native collective, or (every rank at once)
+        # by the torch gather of the packet packed into HBM
         pkt = None
-        if native:
-            try:
-                pkt = ms.native_gather_handoff(L, comm, gpu, 0, device=True)
-            except Exception as e:  # noqa: BLE001
-                native, native_error = False, f"lego_comm_gather_handoff_ex: {e}"
-        if dist and not native:
-            pkt = gpu.handoff_tensor(dev)
+        if transport is not None:
+            def fallback():
+                t = gpu.handoff_tensor(dev)
+                return ms.gather_packets(t if backend == "nccl" else t.cpu(), dist, to_host=False)
+
+            _, pkt = transport.step(lambda: ms.native_gather_handoff(L, comm, gpu, 0, device=True), fallback,
+                                    lambda: lib.lego_comm_abort(comm) if comm is not None else None)
         return i, gpu.stage_times(), cp, pkt
 
     def submit(i):
@@ -588,10 +598,8 @@ def main():
             for k, v in st.items():
                 stage_acc[k] = stage_acc.get(k, 0.0) + v
             alg_bytes += odom_alg_bytes(rc)
-            if native:  # gathered in retire(): rank 0's device copies of every rank's packet
+            if dist:  # gathered in retire(): rank 0's copies of every rank's packet
                 gathered = pkt
-            elif dist:  # hand-off of the step to the serial consumer on rank 0 (torch gather, rehearsal)
-                gathered = ms.gather_packets(pkt.cpu(), dist, to_host=False)
 
     for i in range(args.steps):
         account(submit(args.warmup + i))
@@ -613,7 +621,7 @@ def main():
     if rank == 0:
         handoff = mapping_handoff(gpu, B) if not args.no_handoff else {}
         if gathered is not None:  # the last step's packets as rank 0 received them
-            if native:
+            if transport.native:
                 L.check(lib.lego_comm_wait(comm), "lego_comm_wait", lib)
                 hdrs = []
                 for ptr, nbytes in gathered:
@@ -735,9 +743,12 @@ def main():
                                     "gathered to rank 0 every step"),
                        "scans_per_step": B, "stream_len": args.stream_len, "seed": seed,
                        "parallelism": f"stream-per-gpu x{world}",
-                       "gather": ((("lego_comm (C-ABI RCCL send/recv)" if native else f"torch.distributed ({backend})")
-                                   + ": per step, pose records + published clouds to rank 0") if world > 1 else None),
-                       "gather_native_error": native_error},
+                       "gather": ((("lego_comm (C-ABI RCCL send/recv)" if transport.native
+                                    else f"torch.distributed ({backend})")
+                                   + ": per step, pose records + published clouds to rank 0, one transport on every "
+                                     "rank (agreed over a gloo control group)") if transport else None),
+                       "gather_native_error": (transport.errors or None) if transport else None,
+                       "gather_fallback_from_step": transport.switched_at if transport else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "traffic_over_alg": (traffic / (alg_bytes / args.steps * 1.0 / n_odom)

@@ -436,6 +436,16 @@ typedef struct lego_comm lego_comm;
 int lego_comm_unique_id(uint8_t id[128]);
 int lego_comm_create(const uint8_t id[128], int32_t nranks, int32_t rank, int32_t device, lego_comm** out);
 int lego_comm_destroy(lego_comm* comm);
+/* Aborts the communicator (ncclCommAbort): every operation still queued on it
+ * is cancelled, so its stream drains, and every later call returns
+ * LEGO_E_STATE.  Call it on every rank once any rank reports a failed gather
+ * (the caller agrees on that over its own control channel): a failure on root
+ * after the size exchange (a receive buffer it cannot allocate, a copy error)
+ * aborts only root's communicator, and the other ranks' sends of that gather,
+ * queued with LEGO_COMM_DEVICE_RESULT, would otherwise never complete; their
+ * next lego_comm_wait or gather would block.  lego_comm_destroy after an abort
+ * does not block. */
+int lego_comm_abort(lego_comm* comm);
 /* Collective over all ranks: every rank packs its context's last batch
  * (lego_handoff_pack) and root receives every rank's packet (ncclGather of
  * the sizes, then ncclSend / ncclRecv of the packets in one group).  Returns
@@ -450,7 +460,12 @@ int lego_comm_gather_handoff(lego_comm* comm, lego_ctx* ctx, int32_t root);
  * fails still takes part with an empty packet (the others do not hang) and
  * returns the pack's status; an RCCL or device error after the communicator
  * was used aborts it (ncclCommAbort) and every later call returns
- * LEGO_E_STATE. */
+ * LEGO_E_STATE (the other ranks then call lego_comm_abort, above).
+ * The send reads the context's packet buffer (lego_handoff_pack's) while it
+ * is in flight: a lego_handoff_pack on the same context waits for that send
+ * before it rewrites or regrows the buffer (the gather records a fence on the
+ * context), so repacking in between is safe; lego_handoff_pack_into writes the
+ * caller's buffer and does not wait. */
 #define LEGO_COMM_DEVICE_RESULT 1u
 int lego_comm_gather_handoff_ex(lego_comm* comm, lego_ctx* ctx, int32_t root, uint32_t flags);
 /* Blocks until the last gather on the communicator has completed. */

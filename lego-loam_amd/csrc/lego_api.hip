@@ -115,6 +115,8 @@ struct lego_ctx {
   uint8_t* d_handoff = nullptr;  // lego_handoff_pack's packet (grown on demand)
   hipStream_t hstream = nullptr; // the hand-off packing (first use)
   size_t handoffCap = 0;
+  hipEvent_t handoffFence = nullptr;  // a lego_comm send of d_handoff in flight (lego_handoff_fence)
+  bool handoffFenced = false;
   std::vector<uint8_t> h_handoffHead;
   std::vector<lego_point_xyzi> h_info, h_gcloud, h_pure;
   std::vector<lego_point_xyzi> h_cornerLast, h_surfLast, h_outlLast;
@@ -152,6 +154,7 @@ struct lego_ctx {
   int* vgN = nullptr;
   int vgCap = 0;
   int vgStats[8] = {};
+  hipEvent_t vgEv[2] = {nullptr, nullptr};  // lego_voxel_grid's timing events (first use)
   lego_mo_opts moOpts{};
   double moTimeLast = -1;
   bool moStoreFull = false;  // sticky KF_OVF seen: no step runs until lego_reset
@@ -186,6 +189,10 @@ struct lego_ctx {
     if (ostream) (void)hipStreamSynchronize(ostream);
     if (mo.fork[1]) (void)hipStreamSynchronize(mo.fork[1]);  // the mapping VoxelGrids' fork
     if (d_raw) (void)hipFree(d_raw);
+    if (handoffFenced) (void)hipEventSynchronize(handoffFence);  // a send still reading d_handoff
+    if (handoffFence) (void)hipEventDestroy(handoffFence);
+    for (auto e : vgEv)
+      if (e) (void)hipEventDestroy(e);
     if (d_handoff) (void)hipFree(d_handoff);
     if (h_pack) (void)hipHostFree(h_pack);
     if (h_offp) (void)hipHostFree(h_offp);
@@ -1294,9 +1301,9 @@ int lego_voxel_grid(lego_ctx* x, const lego_point_xyzi* in, int32_t n, float lea
     std::fill(x->vgStats, x->vgStats + 8, 0);
     return LEGO_OK;
   }
-  hipEvent_t e0, e1;
-  HIPCHK(hipEventCreate(&e0));
-  HIPCHK(hipEventCreate(&e1));
+  for (auto& e : x->vgEv)
+    if (!e) HIPCHK(hipEventCreate(&e));  // once per context (destroyed with it)
+  hipEvent_t e0 = x->vgEv[0], e1 = x->vgEv[1];
   HIPCHK(hipMemcpyAsync(x->vgIn, in, sizeof(float4) * n, hipMemcpyHostToDevice, x->stream));
   HIPCHK(hipEventRecord(e0, x->stream));
   const int rc = voxel_grid_device(x->vgIn, n, nullptr, leaf, x->vgOut, x->vgN, x->vgApi, x->stream);
@@ -1306,8 +1313,6 @@ int lego_voxel_grid(lego_ctx* x, const lego_point_xyzi* in, int32_t n, float lea
   HIPCHK(hipStreamSynchronize(x->stream));
   float ms = 0.f;
   HIPCHK(hipEventElapsedTime(&ms, e0, e1));
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
   if (rc != 0 || vg_read_ctl(x->vgApi, ctl, x->stream) != 0) {
     set_err("VoxelGrid launch failed");
     return LEGO_E_DEVICE;
@@ -1826,6 +1831,10 @@ static int handoff_pack(lego_ctx* x, uint8_t* dst, uint64_t cap, const void** pa
     return LEGO_E_CAPACITY;
   }
   if (!dst) {
+    if (x->handoffFenced) {  // a lego_comm send still reads the buffer (lego_handoff_fence)
+      HIPCHK(hipEventSynchronize(x->handoffFence));
+      x->handoffFenced = false;
+    }
     if (off > x->handoffCap) {
       if (x->d_handoff) HIPCHK(hipFree(x->d_handoff));
       x->d_handoff = nullptr;
@@ -1843,6 +1852,15 @@ static int handoff_pack(lego_ctx* x, uint8_t* dst, uint64_t cap, const void** pa
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(s));
   if (packet) *packet = dst;
+  return LEGO_OK;
+}
+
+// lego_comm.hip: the packet buffer is read by a send enqueued on stream s;
+// the next pack into it waits for that point of s.
+int lego_handoff_fence(lego_ctx* x, hipStream_t s) {
+  if (!x->handoffFence) HIPCHK(hipEventCreateWithFlags(&x->handoffFence, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(x->handoffFence, s));
+  x->handoffFenced = true;
   return LEGO_OK;
 }
 

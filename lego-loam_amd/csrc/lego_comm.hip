@@ -28,6 +28,9 @@
 #include "lego_loam.h"
 
 void lego_set_error(const char* fmt, ...);  // lego_api.hip
+// lego_api.hip: the send of lego_handoff_pack's buffer in flight on stream s
+// (an event the next pack into that buffer waits for)
+extern "C" int lego_handoff_fence(lego_ctx* ctx, hipStream_t s);
 
 struct lego_comm {
   ncclComm_t nc = nullptr;
@@ -183,6 +186,9 @@ int lego_comm_gather_handoff_ex(lego_comm* c, lego_ctx* ctx, int32_t root, uint3
     COMM_TRY_NCCL(ncclSend(pkt, bytes, ncclUint8, root, c->nc, c->s), true);
   }
   COMM_TRY_NCCL(ncclGroupEnd(), false);
+  // root copied its own packet on c->s too: either way the context's buffer is
+  // read on c->s until this point of the stream
+  if (bytes && lego_handoff_fence(ctx, c->s) != LEGO_OK) return comm_abort(c, false, "lego_handoff_fence", "event");
   if (!(flags & LEGO_COMM_DEVICE_RESULT)) {
     if (isRoot) {
       const size_t need = c->offs[c->nranks];
@@ -204,6 +210,16 @@ int lego_comm_gather_handoff_ex(lego_comm* c, lego_ctx* ctx, int32_t root, uint3
 
 int lego_comm_gather_handoff(lego_comm* c, lego_ctx* ctx, int32_t root) {
   return lego_comm_gather_handoff_ex(c, ctx, root, 0);
+}
+
+int lego_comm_abort(lego_comm* c) {
+  if (!c) return LEGO_E_ARG;
+  if (c->device >= 0) (void)hipSetDevice(c->device);
+  if (c->nc) (void)ncclCommAbort(c->nc);  // cancels what is still queued on c->s
+  c->nc = nullptr;
+  c->dead = true;
+  c->haveResult = c->haveHost = false;
+  return LEGO_OK;
 }
 
 int lego_comm_wait(lego_comm* c) {

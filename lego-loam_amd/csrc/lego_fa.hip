@@ -821,6 +821,7 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
     cnt[0] = L.misc[M_NSH];
     cnt[1] = L.misc[M_NLS];
     cnt[2] = L.misc[M_NFL];
+    static_assert(kMaxHorizon < (1 << 15), "r_cnt[3] packs two ring counts (<= H) in 16 bits each");
     cnt[3] = nlf | (nlf << 16);  // high half: the less-flat count k_lf_voxel decides on (never overwritten)
   }
   if (ring == 0 && carry) {

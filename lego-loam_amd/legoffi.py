@@ -276,7 +276,7 @@ HIP_EXPORTS = ["lego_sensor_preset", "lego_create", "lego_fleet_create", "lego_d
                "lego_mo_set_map", "lego_mo_configure", "lego_mo_process", "lego_mo_loop_closure", "lego_last_error", "lego_stage_times",
                "lego_odom_profile", "lego_extract_profile", "lego_handoff_pack", "lego_handoff_pack_into", "lego_handoff_unpack", "lego_comm_unique_id",
                "lego_comm_create", "lego_comm_destroy", "lego_comm_gather_handoff", "lego_comm_handoff",
-               "lego_comm_gather_handoff_ex", "lego_comm_wait", "lego_comm_handoff_device",
+               "lego_comm_gather_handoff_ex", "lego_comm_wait", "lego_comm_handoff_device", "lego_comm_abort",
                "lego_voxel_grid", "lego_voxel_grid_stats", "lego_sort_permutation"]
 
 
@@ -324,6 +324,7 @@ def hip_lib() -> C.CDLL:
     lib.lego_comm_handoff.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]
     lib.lego_comm_gather_handoff_ex.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_uint32]
     lib.lego_comm_wait.argtypes = [C.c_void_p]
+    lib.lego_comm_abort.argtypes = [C.c_void_p]
     lib.lego_comm_handoff_device.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]
     lib.lego_voxel_grid.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_float, C.c_void_p,
                                     C.POINTER(C.c_int32)]

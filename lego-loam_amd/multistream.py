@@ -150,3 +150,63 @@ def native_gather_handoff(L, comm, ctx, root: int = 0, device: bool = False):
         out.append(pkt)
         r += 1
     return out
+
+
+def agree(dist, ok: bool, group=None) -> bool:
+    """True on every rank iff `ok` is True on every rank (an all-reduce of a
+    failure flag over `group`, the host control channel).  Raises if the
+    ranks cannot agree (the process then exits non-zero, as every rank does)."""
+    import torch
+
+    t = torch.tensor([0 if ok else 1], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return int(t.item()) == 0
+
+
+class HandoffTransport:
+    """The per-step hand-off of every rank's packet to rank 0, with ONE
+    transport for all ranks at every step.
+
+    `native()` runs the C-ABI collective (lego_comm_gather_handoff_ex) and
+    returns rank 0's result; `fallback()` gathers the same step's packet over
+    torch.distributed; `abort()` aborts the native communicator (lego_comm_abort:
+    cancels a send still queued, so nothing blocks on it later).  After every
+    native gather the ranks agree over `ctrl` (a gloo group: host only, never
+    queued behind device work) whether it succeeded everywhere.  If any rank
+    failed, EVERY rank aborts its communicator, gathers that step again over
+    the fallback and stays on the fallback from then on: no rank ever waits in
+    ncclGather / ncclRecv while another is in a torch collective."""
+
+    def __init__(self, dist, ctrl, native_ok: bool, native_error: str | None = None):
+        self.dist, self.ctrl = dist, ctrl
+        self.native = agree(dist, native_ok, ctrl)
+        self.errors = self._errors(native_error) if not self.native else []
+        self.switched_at = 0 if self.errors else None  # the step from which the fallback runs (None: never switched)
+        self.steps = 0
+
+    def _errors(self, mine):
+        box = [None] * self.dist.get_world_size()
+        self.dist.all_gather_object(box, mine, group=self.ctrl)
+        return [f"rank {r}: {e}" for r, e in enumerate(box) if e]
+
+    def step(self, native, fallback, abort):
+        """One step's gather; returns (transport name, rank 0's result)."""
+        out, err = None, None
+        if self.native:
+            try:
+                out = native()
+            except Exception as e:  # noqa: BLE001
+                err = f"step {self.steps}: {e}"
+            if agree(self.dist, err is None, self.ctrl):
+                self.steps += 1
+                return "native", out
+            self.native = False
+            self.switched_at = self.steps
+            self.errors = self._errors(err)
+            abort()
+        self.steps += 1
+        return "fallback", fallback()
+
+    @property
+    def name(self) -> str:
+        return "native" if self.native else "fallback"

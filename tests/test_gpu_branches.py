@@ -77,6 +77,7 @@ def _check_recs(recs, ref, label):
         exact += int(np.array_equal(ts.astype(np.float32).view(np.uint32),
                                     o["transform_sum"].astype(np.float32).view(np.uint32)))
     print(f"{label}: {len(recs)} scans, worst |dpose| {worst:.3g}, bit-exact {exact}/{len(recs)}")
+    assert exact == len(recs), f"{label}: only {exact}/{len(recs)} poses bit-exact"
 
 
 def test_sector_sort_ties_match_oracle(L):

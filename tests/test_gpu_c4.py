@@ -64,6 +64,7 @@ def _check(recs, ref, label):
         assert d <= POSE_TOL, (label, k, ts, o[0])
         worst = max(worst, d)
         exact += int(np.array_equal(ts.astype(np.float32), o[0].astype(np.float32)))
+    assert exact == len(recs), f"{label}: only {exact}/{len(recs)} poses bit-exact"
     return worst, exact
 
 

@@ -61,4 +61,5 @@ def test_c5_full_size_matches_oracle(L, c5, per_step):
     gpu.close()
     print(f"C5 full size (per_step={per_step}): {steps} steps, {iters / max(steps, 1):.1f} LM iterations/step, "
           f"worst |dpose| {worst:.3g}, bit-exact {exact}/{steps}")
+    assert exact == steps, f"only {exact}/{steps} mapped poses bit-exact"
     assert steps >= 3 and iters > steps  # several distinct steps, more than one iteration each on average

@@ -77,6 +77,7 @@ def _map_packets(L, packets, ref, label):
     m.close()
     assert steps >= 4
     print(f"{label}: {steps} mapping steps from packets, worst |dpose| {worst:.3g}, bit-exact {exact}/{steps}")
+    assert exact == steps, f"{label}: only {exact}/{steps} mapped poses bit-exact"
 
 
 def test_packet_equals_batch_fetch(L):

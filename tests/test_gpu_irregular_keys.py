@@ -48,6 +48,8 @@ def test_swapped_ring_labels_match_oracle(L):
         assert g["odom_valid"] == o["odom_valid"], k
         d = float(np.max(np.abs(np.asarray(g["transform_sum"], np.float64) - np.asarray(o["transform_sum"], np.float64))))
         assert d <= POSE_TOL, (k, g["transform_sum"], o["transform_sum"])
+        assert np.array_equal(np.asarray(g["transform_sum"], np.float32).view(np.uint32),
+                              np.asarray(o["transform_sum"], np.float32).view(np.uint32)), k
         worst = max(worst, d)
         del seg
     print(f"swapped ring labels: 12 scans, worst |dpose| {worst:.3g}")

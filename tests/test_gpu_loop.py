@@ -105,4 +105,5 @@ def test_loop_closure_mode_matches_oracle(L, search_num):
     gpu.close()
     print(f"loop-closure mode (search num {search_num}): {steps} mapping steps ({after} after the first loop), "
           f"{accepted} loops accepted, worst |dpose| {worst:.3g}, bit-exact {exact}/{steps}")
+    assert exact == steps, f"only {exact}/{steps} mapped poses bit-exact"
     assert accepted >= 1 and after >= 3

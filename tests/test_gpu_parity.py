@@ -85,9 +85,10 @@ def test_stream_parity_node_api(L, sensor, seed, nscans):
         d = float(np.max(np.abs(gf["transform_sum"].astype(np.float64) - of["transform_sum"])))
         worst = max(worst, d)
         assert d <= POSE_TOL, (k, gf["transform_sum"], of["transform_sum"])
+        assert np.array_equal(gf["transform_sum"].view(np.uint32), of["transform_sum"].view(np.uint32)), k
         if gf["publish_to_mapping"]:
             for key in ("corner_last", "surf_last", "outlier_last"):
-                assert np.allclose(gf[key].view(np.float32), of[key].view(np.float32), atol=POSE_TOL)
+                assert np.array_equal(gf[key].view(np.uint32), of[key].view(np.uint32)), (k, key)
     print(f"{sensor}: worst |dpose| = {worst:.3g}")
     gpu.close()
 
@@ -224,6 +225,7 @@ def test_scan_to_map_parity(L, sensor, seed, nscans, n_surf, n_corner):
         worst = max(worst, float(d))
         assert d <= POSE_TOL, (k, g["transform_aft_mapped"], o["transform_aft_mapped"], g["iterations"],
                                o["iterations"], g["n_rows_last"], o["n_rows_last"])
+        assert np.array_equal(g["transform_aft_mapped"].view(np.uint32), o["transform_aft_mapped"].view(np.uint32)), k
     print(f"scan-to-map: {steps} steps, {optimized} optimized, worst |dpose| = {worst:.3g}")
     assert steps >= 2 and optimized >= 1
     gpu.close()
@@ -269,6 +271,7 @@ def test_scan_to_map_keyframe_parity(L):
         d = np.max(np.abs(g["transform_aft_mapped"].astype(np.float64) - o["transform_aft_mapped"]))
         worst = max(worst, float(d))
         assert d <= POSE_TOL, (k, g["transform_aft_mapped"], o["transform_aft_mapped"])
+        assert np.array_equal(g["transform_aft_mapped"].view(np.uint32), o["transform_aft_mapped"].view(np.uint32)), k
     print(f"keyframe scan-to-map: {steps} steps, {optimized} optimized, worst |dpose| = {worst:.3g}")
     assert steps >= 5 and optimized >= 3
     gpu.close()

@@ -11,7 +11,8 @@ two batches in flight) and the host-buffer batch entry:
 
 Every scan's pose record is checked against the oracle run over the same
 stream: transformSum within the north-star 1e-4, feature counts and the
-odometry-valid flag exact; the fraction of bit-exact poses is printed."""
+odometry-valid flag exact, and every pose bit-exact (asserted: the bar the
+bench's pose_delta_vs_oracle reports)."""
 import time
 
 import numpy as np
@@ -53,6 +54,7 @@ def _check(recs, ref, label):
         worst = max(worst, d)
         exact += int(np.array_equal(ts.astype(np.float32), o[0].astype(np.float32)))
     print(f"{label}: {len(recs)} scans, worst |dpose| {worst:.3g}, bit-exact {exact}/{len(recs)}")
+    assert exact == len(recs), f"{label}: only {exact}/{len(recs)} poses bit-exact"  # the claimed bar
 
 
 def test_c2_full_stream_device_batches(L):
