@@ -256,20 +256,23 @@ def mapping_bench(L, steps: int, cpu: bool):
                 outs.append(o)
         return dts, outs
 
-    # the first step of a context warms its code paths: timed steps are 2..steps+1
+    # a throwaway context's first step loads the mapping kernels' code: the
+    # timed contexts then time steps 1..steps, the same steps the CPU leg runs
+    warm = L.Lego(L.sensor_cfg(sensor, L.hip_lib()), max_points=cap)
+    run(warm, True, 1)
+    warm.close()
     gpu = L.Lego(L.sensor_cfg(sensor, L.hip_lib()), max_points=cap)
-    dts, outs = run(gpu, True, steps + 1)
+    dts, outs = run(gpu, True, steps)
     gpu.close()
     gpu = L.Lego(L.sensor_cfg(sensor, L.hip_lib()), max_points=cap)
-    dts1, _ = run(gpu, False, steps + 1)
+    dts1, _ = run(gpu, False, steps)
     gpu.close()
-    dts, dts1 = dts[1:], dts1[1:]
     its = [o["iterations"] for o in outs]
     rows = [o["n_rows_last"] for o in outs]
     q = outs[-1]["n_corner_scan_ds"] + outs[-1]["n_surf_scan_ds"]
     med = statistics.median(dts)
     alg = statistics.mean(c5_alg_bytes(len(surf) + len(corner), o["n_corner_map_ds"] + o["n_surf_map_ds"],
-                                       o["n_corner_scan_ds"] + o["n_surf_scan_ds"], o["iterations"]) for o in outs[1:])
+                                       o["n_corner_scan_ds"] + o["n_surf_scan_ds"], o["iterations"]) for o in outs)
     res.update({"gpu_ms_per_step": med, "gpu_ms_per_step_mean": statistics.mean(dts),
                 "gpu_ms_per_step_min": min(dts),
                 "gpu_ms_per_step_map_installed_once": statistics.median(dts1),
@@ -286,8 +289,11 @@ def mapping_bench(L, steps: int, cpu: bool):
         res["cpu_sample"] = (f"first {n} mapping steps of the same consecutive scans through the oracle (1 thread; "
                              "map VoxelGrid + kd-tree build every step, as the reference)")
         res["same_iterations_as_gpu"] = res["cpu_iterations"] == its[:n]
-        res["cpu_vs_gpu_steps"] = (f"the oracle's steps 1..{n} (median of {n}) against the GPU's iterations of "
-                                   f"steps 1..{n} (GPU timing: 2..)")
+        res["gpu_ms_per_step_steps_1_to_%d" % n] = statistics.median(dts[:n])
+        res["cpu_over_gpu_same_steps"] = res["cpu_ms_per_step"] / statistics.median(dts[:n])
+        res["cpu_vs_gpu_steps"] = (f"like for like: the oracle's steps 1..{n} (median) against the GPU's steps "
+                                   f"1..{n} (median, gpu_ms_per_step_steps_1_to_{n}); gpu_ms_per_step is the median "
+                                   f"of all {steps} GPU steps")
     return res
 
 
@@ -330,6 +336,76 @@ def loop_bench(L, nscans: int, calls: int, cpu: bool):
             cd.append((time.perf_counter() - t0) * 1e3)
         res["cpu_ms_per_call"] = statistics.median(cd)
         res["cpu_sample"] = f"median of {calls} calls of the oracle (1 thread; kd-tree ICP as PCL)"
+    return res
+
+
+def node_path_bench(L, nscans: int, cpu: bool, cpu_scans: int = 40):
+    """Auxiliary (not the headline metric): the per-scan latency of the
+    node-shaped drop-in path a ROS deployment runs at 10 Hz (INTEGRATION.md's
+    adapter; imageProjection.cpp:181-197 cloudHandler, featureAssociation.cpp:
+    1817-1860 runFeatureAssociation, mapOptmization.cpp:1487-1522 run): for
+    every scan of the C2 stream (VLP-16, seed 1), one at a time from HOST
+    buffers, lego_ip_process -> lego_fa_process -> lego_mo_process (the
+    keyframe-built map, the reference's default; the call returns at once when
+    mapOptimization's 0.3 s gate is closed).  Host wall clock per scan around
+    the three calls, uploads and the library's host outputs included.  A
+    throwaway context runs first so module loading is not in the numbers.  CPU
+    leg: the oracle's same three calls over the first `cpu_scans` scans."""
+    sensor, seed = "VLP-16", 1
+    sc = L.synth_cfg(sensor, seed)
+    scans = [L.synth_scan(sc, k) for k in range(nscans)]
+    cap = max(len(p) for p, _ in scans) + 16
+
+    def run(lib, h, ipf, faf, mof, n):
+        ip, fa = L.IpOut(), L.FaOut()
+        per, t_ip, t_fa, t_mo, t_map = [], [], [], [], []
+        for pts, stamp in scans[:n]:
+            pts = np.ascontiguousarray(pts, dtype=L.XYZIR_DTYPE)
+            mo = L.MoOut()
+            t0 = time.perf_counter()
+            L.check(ipf(h, pts.ctypes.data, len(pts), stamp, 0, C.byref(ip)), "ip", lib)
+            t1 = time.perf_counter()
+            L.check(faf(h, C.byref(ip), C.byref(fa)), "fa", lib)
+            t2 = time.perf_counter()
+            L.check(mof(h, C.byref(fa), C.byref(mo)), "mo", lib)
+            t3 = time.perf_counter()
+            per.append((t3 - t0) * 1e3)
+            t_ip.append((t1 - t0) * 1e3)
+            t_fa.append((t2 - t1) * 1e3)
+            (t_map if mo.processed else t_mo).append((t3 - t2) * 1e3)
+        return per, t_ip, t_fa, t_mo, t_map
+
+    def pct(v, q):
+        v = sorted(v)
+        return v[min(len(v) - 1, int(round(q * (len(v) - 1))))] if v else None
+
+    def summary(per, t_ip, t_fa, t_mo, t_map):
+        return {"scans": len(per), "ms_per_scan_median": statistics.median(per), "ms_per_scan_p99": pct(per, 0.99),
+                "ms_per_scan_max": max(per), "ms_per_scan_mean": statistics.mean(per),
+                "ip_ms_median": statistics.median(t_ip), "fa_ms_median": statistics.median(t_fa),
+                "mo_gate_closed_ms_median": statistics.median(t_mo) if t_mo else None,
+                "mapping_steps": len(t_map),
+                "mapping_step_ms_median": statistics.median(t_map) if t_map else None,
+                "mapping_step_ms_max": max(t_map) if t_map else None}
+
+    lib = L.hip_lib()
+    warm = L.Lego(L.sensor_cfg(sensor, lib), max_points=cap)
+    run(lib, warm.h, lib.lego_ip_process, lib.lego_fa_process, lib.lego_mo_process, 8)
+    warm.close()
+    gpu = L.Lego(L.sensor_cfg(sensor, lib), max_points=cap)
+    res = {"workload": f"C2 stream (VLP-16 seed 1) one scan at a time from host buffers through the node API: "
+                       f"lego_ip_process -> lego_fa_process -> lego_mo_process (keyframe map), {nscans} scans",
+           "gpu": summary(*run(lib, gpu.h, lib.lego_ip_process, lib.lego_fa_process, lib.lego_mo_process,
+                               nscans))}
+    gpu.close()
+    res["gpu"]["fits_10hz"] = res["gpu"]["ms_per_scan_max"] < 100.0
+    if cpu:
+        olib = L.oracle_lib()
+        ora = L.Oracle(L.sensor_cfg(sensor))
+        res["cpu"] = summary(*run(olib, ora.h, olib.lego_oracle_ip_process, olib.lego_oracle_fa_process,
+                                  olib.lego_oracle_mo_process, cpu_scans))
+        res["cpu"]["sample"] = f"the oracle's same three calls over scans 0..{cpu_scans - 1} (1 thread)"
+        res["gpu_vs_cpu_note"] = "CPU over the first scans only (bounded leg): compare the medians"
     return res
 
 
@@ -474,6 +550,8 @@ def main():
                     help="streams of the fleet aux line (0 = skip); 256 = one odometry workgroup per stream and CU")
     ap.add_argument("--loop-scans", type=int, default=340, help="loop-closure aux stream length (0 = skip)")
     ap.add_argument("--dense-scans", type=int, default=200, help="C3 HDL-64E scans of the aux line (0 = skip)")
+    ap.add_argument("--node-scans", type=int, default=120,
+                    help="scans of the node-API latency line (aux.node_path; 0 = skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -630,18 +708,18 @@ def main():
                         L.hip_memcpy_d2h(C.addressof(h), ptr, C.sizeof(h))
                     hdrs.append(h)
                 sizes = [int(nb) for _, nb in gathered]
-                transport = ("lego_comm_gather_handoff_ex (C-ABI; RCCL ncclGather of sizes + ncclSend/ncclRecv "
-                             "of packets, LEGO_COMM_DEVICE_RESULT), every step in the timed region")
+                how = ("lego_comm_gather_handoff_ex (C-ABI; RCCL ncclGather of sizes + ncclSend/ncclRecv "
+                       "of packets, LEGO_COMM_DEVICE_RESULT), every step in the timed region")
             else:
                 hdrs = [L.handoff_header(g.cpu().numpy()) for g in gathered]
                 sizes = [int(g.numel()) for g in gathered]
-                transport = f"torch.distributed gather ({backend}) of lego_handoff_pack_into packets, in the timed region"
+                how = f"torch.distributed gather ({backend}) of lego_handoff_pack_into packets, in the timed region"
             handoff["gathered_to_rank0"] = {
                 "ranks": len(hdrs), "scans_per_rank": [h.nscans for h in hdrs],
                 "published_per_rank": [h.npub for h in hdrs], "bytes_per_rank": [h.bytes for h in hdrs],
                 "valid": len(hdrs) == world and all(h.magic == L.HANDOFF_MAGIC and h.nscans == B and h.bytes == n
                                                     for h, n in zip(hdrs, sizes)),
-                "transport": transport}
+                "transport": how}
         # the batch runs as chunks (lego_api.hip run_batch): k_odom launches per step
         launches = {k[2:]: v / args.steps for k, v in stage_acc.items() if k.startswith("n:")}
         stage_acc = {k: v for k, v in stage_acc.items() if not k.startswith("n:")}
@@ -720,6 +798,8 @@ def main():
             aux["dense_hdl64_c3"] = dense_bench(L, args.dense_scans, 20, local, cpu=not args.no_cpu)
         if args.loop_scans > 0 and world == 1:
             aux["loop_closure"] = loop_bench(L, args.loop_scans, 5, not args.no_cpu)
+        if args.node_scans > 0 and world == 1:
+            aux["node_path"] = node_path_bench(L, args.node_scans, not args.no_cpu)
         if cpu_all:
             aux["cpu_all_cores"] = cpu_all
         aux["host"] = host_info()

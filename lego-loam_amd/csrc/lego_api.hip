@@ -480,6 +480,18 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
     ob.gTS = gTS;
     A(ob.nC.gPts, G * ob.capCorner);
     A(ob.nS.gPts, G * ob.capSurf);
+    ob.capH = ob.capSurf + ob.capCorner;
+    ob.ring = nullptr;
+    ob.ringR = 0;
+    ob.ringStride = ob.ringCtl = ob.ringCopy = 0;
+    if (odom_ring_sensor((int)N)) {  // one copy of the last clouds and grids per stream (OdomBufs::ring)
+      ob.ringR = ring_slots((int)((B1 + S - 1) / S));
+      ob.ringStride = ring_stride(ob.G, gTS, gTC, ob.capH);
+      ob.ringCtl = ring_ctl_bytes(ob.G, gTS, gTC);
+      const size_t ringCopies = ob.wg >= 0 ? 2 : 1;
+      ob.ringCopy = ringCopies > 1 ? (size_t)ob.ringR * ob.ringStride : 0;
+      A(ob.ring, S * ringCopies * (size_t)ob.ringR * ob.ringStride);
+    }
     ob.capQ = (int)(N * kFlatPerRing);
     A(ob.qi, G * 3 * ob.capQ);
     // exchange block: 16-byte error word, then per stream one slot of capQ
@@ -641,6 +653,7 @@ static OdomBufs ob_slice(const OdomBufs& a, const DevCfg& c, int c0, int s0, int
   o.qi += w * 3 * a.capQ;
   o.xg += (size_t)s0 * a.roundsCap * a.capQ;
   o.xh += (size_t)s0 * 2 * 3 * a.capH;
+  if (a.ring) o.ring += (size_t)s0 * (a.ringCopy ? 2 : 1) * a.ringR * a.ringStride;
   o.sumOut += k * 6; o.curOut += k * 6; o.validOut += k; o.pubOut += k;
   o.cornerEnd += k * a.capLS; o.surfEnd += k * c.P;
   return o;

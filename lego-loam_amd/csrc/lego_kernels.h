@@ -83,10 +83,15 @@ struct OdomState {
   int cornerLastNum, surfLastNum;
   int nnCornerNum, nnSurfNum;  // sizes of the clouds the NN indexes were built on
   int frameCount;
-  int curBuf;    // HBM buffer holding the current last clouds
-  int snapBuf;   // HBM buffer holding the indexes' snapshot (== curBuf unless stale)
+  // HBM copy holding the current last clouds: 0 / 1 a workgroup-private
+  // buffer (LDS-resident sensors), >= 2 the stream's ring slot curBuf - 2
+  // (HBM-resident sensors, OdomBufs::ring)
+  int curBuf;
+  int snapBuf;   // the copy the indexes were built over (== curBuf unless stale), same encoding
   int resident;  // current last clouds (and indexes) are LDS-resident
-  unsigned seq;  // hand-offs so far (the hand-off exchange's tag; its granules are zeroed with it)
+  // LDS-resident sensors: hand-offs so far (the hand-off exchange's tag; its
+  // granules are zeroed with it).  Ring sensors: ring picks so far (ring_next).
+  unsigned seq;
 };
 
 // Device buffers of the odometry kernel for S independent streams (a fleet;
@@ -137,6 +142,25 @@ struct OdomBufs {
   size_t xhBytes;
   int capH;  // capSurf + capCorner
 
+  // Sensors whose last clouds do not fit LDS (HDL-64E, VLS-128): the stream's
+  // ONE copy of each hand-off's TransformToEnd'ed clouds and of their grids,
+  // as featureAssociation.cpp:1759-1815 keeps one per stream, instead of a
+  // private copy per workgroup.  ringR slots per stream, ringStride bytes
+  // each: control words (per share: claim / done of the two phases), the key
+  // tables and bucket counts / cursors (agent-scope atomics), then the clouds
+  // in index order (P) and in bucket order (Q).  Each workgroup transforms and
+  // stores its share of the points; a share whose owner has not claimed it in
+  // kStealTicks is done by the waiting workgroup.  Within a launch no slot is
+  // written twice and the indexes' snapshot slot is skipped (ring_next), so a
+  // slower workgroup never reads a rewritten slot; k_ring_prep zeroes the
+  // control words of the slots a launch can pick.  ring == nullptr: the
+  // LDS-resident sensors' private path.
+  unsigned char* ring;     // [S x copies x ringR x ringStride]
+  size_t ringStride;       // bytes per slot
+  size_t ringCtl;          // bytes of a slot's control words (zeroed per pick)
+  size_t ringCopy;         // the diagnostic silent workgroup's private ring (bytes past the stream's), else 0
+  int ringR;
+
   // per-scan outputs of the batch (workgroup 0)
   float* sumOut;        // [B*6]
   float* curOut;        // [B*6]
@@ -146,6 +170,22 @@ struct OdomBufs {
   float4* surfEnd;      // [B*P]      less-flat after TransformToEnd
   int capLS;
 };
+
+// Ring slot layout (OdomBufs::ring), shared by the host's allocation and the
+// kernels: [claimA, doneA, claimB, doneB] x G words, the key tables
+// (kRingKey words), the bucket counts and cursors (gTS + gTC words each), then
+// P and Q (capH points each).  Everything before P is a slot's control words.
+constexpr int kRingKey = 4 * kMaxRings + 2;
+__host__ __device__ inline size_t ring_al(size_t x) { return (x + 255) & ~(size_t)255; }
+__host__ __device__ inline size_t ring_ctl_bytes(int G, int gTS, int gTC) {
+  return ring_al((size_t)16 * G) + ring_al((size_t)4 * kRingKey) + 2 * ring_al((size_t)4 * (gTS + gTC));
+}
+__host__ __device__ inline size_t ring_stride(int G, int gTS, int gTC, int capH) {
+  return ring_ctl_bytes(G, gTS, gTC) + 2 * ring_al((size_t)16 * capH);
+}
+// Ring slots per stream for launches of up to K scans per stream: K picks,
+// the snapshot's slot and the launch's first current slot are never rewritten.
+__host__ __device__ inline int ring_slots(int K) { return K + 3; }
 
 void launch_gated(const BatchBufs& bb, const DevCfg& c, const GatedBufs& gb, hipStream_t s);
 void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hipStream_t s,
@@ -159,6 +199,8 @@ void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_ca
 int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int K, hipStream_t s,
                 StageTimer* tm, unsigned long long* prof);
 int odom_workgroups(int N, int cusAvailable);
+// sensors whose last clouds never fit LDS: the stream keeps one ring copy (OdomBufs::ring)
+bool odom_ring_sensor(int N);
 // workgroups per stream from which the LDS-resident odometry runs without grids
 constexpr int kGridlessMinWG = 16;
 

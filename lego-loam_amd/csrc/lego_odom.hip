@@ -928,7 +928,7 @@ struct OdomLds {
   int* n;            // [16] flags
   OdomState* st;     // the stream state, resident for the kernel's lifetime
 };
-enum { N_BREAK = 0, N_IRR_S = 1, N_IRR_C = 2, N_ROUND = 3 };
+enum { N_BREAK = 0, N_IRR_S = 1, N_IRR_C = 2, N_ROUND = 3, N_RING = 4, N_CLAIM = 5 };
 
 __host__ __device__ constexpr size_t odom_lds_bytes() {
   size_t s = 0;
@@ -983,21 +983,67 @@ __device__ __forceinline__ NNView<uint16_t> view_lds(bool surf, const OdomLds& L
   return NNView<uint16_t>{L.lastC, st->cornerLastNum, L.gEndC, L.gOrdC, nullptr, fine_T(st->cornerLastNum, kLdsGridC),
                           c.N, L.sufC, L.preC, L.n[N_IRR_C], gridless};
 }
+// A stream's ring slot (OdomBufs::ring; the protocol under "ring" below).
+struct RingSlot {
+  unsigned *claimA, *doneA, *claimB, *doneB;  // [G] each
+  int* key;        // [kRingKey]: first (max of INT_MAX - j), last (max of j + 1) per (cloud, key), irregular x 2
+  unsigned* cnt;   // [TS + TC] bucket counts
+  unsigned* fill;  // [TS + TC] scatter cursors
+  float4* P;       // [capH] less-flat [0, nS) then less-sharp [nS, nS + nC), TransformToEnd'ed
+  float4* Q;       // [capH] the same in bucket order (corner buckets after nS), .w = index in its cloud
+};
+__device__ __forceinline__ RingSlot ring_slot(const OdomBufs& ob, int slot) {
+  unsigned char* b = ob.ring + (size_t)slot * ob.ringStride;
+  RingSlot r;
+  r.claimA = (unsigned*)b;
+  r.doneA = r.claimA + ob.G;
+  r.claimB = r.doneA + ob.G;
+  r.doneB = r.claimB + ob.G;
+  b += ring_al((size_t)16 * ob.G);
+  r.key = (int*)b;
+  b += ring_al((size_t)4 * kRingKey);
+  r.cnt = (unsigned*)b;
+  b += ring_al((size_t)4 * (ob.gTS + ob.gTC));
+  r.fill = (unsigned*)b;
+  b += ring_al((size_t)4 * (ob.gTS + ob.gTC));
+  r.P = (float4*)b;
+  b += ring_al((size_t)16 * ob.capH);
+  r.Q = (float4*)b;
+  return r;
+}
+// The HBM copy `buf` of a last cloud (curBuf / snapBuf encoding, OdomState):
+// a private buffer, or the ring slot's P (the corner cloud after nSurf points).
+template <bool RING>
+__device__ __forceinline__ const float4* hbm_cloud(const OdomBufs& ob, int buf, bool surf, int nSurf) {
+  if (RING && buf >= 2) {
+    const float4* P = ring_slot(ob, buf - 2).P;
+    return surf ? P : P + nSurf;
+  }
+  return surf ? buf2(ob.surfLast, buf) : buf2(ob.cornerLast, buf);
+}
 // HBM-resident clouds: the LDS that holds the clouds, queries and counters of
 // the resident layout (lastS .. cnt, contiguous) is free, and takes both
 // grids' bucket arrays (the counting sort's counters, which end the build as
 // the bucket ends); the point-order arrays stay in HBM.
 constexpr int kHbmLdsCnt = (kLdsSurf * 16 + kLdsCorner * 16 + kLdsQ * 16 + (kLdsQ / 2) * 16 + kLdsCnt * 4) / 4;
 __device__ __forceinline__ unsigned* hbm_grid_ends(const OdomLds& L) { return (unsigned*)L.lastS; }
+template <bool RING>
 __device__ __forceinline__ NNView<uint32_t> view_hbm(bool surf, const OdomLds& L, const OdomBufs& ob,
                                                      const OdomState* st, const DevCfg& c) {
   unsigned* ends = hbm_grid_ends(L);
   const int TS = fine_T(st->surfLastNum, ob.gTS);
+  const float4* last = hbm_cloud<RING>(ob, st->curBuf, surf, st->surfLastNum);
+  const float4* gq = nullptr;
+  if (RING && st->curBuf >= 2) {  // the stream's ring slot: Q holds both clouds, corner after the surf points
+    const float4* Q = ring_slot(ob, st->curBuf - 2).Q;
+    gq = surf ? Q : Q + st->surfLastNum;
+  } else {
+    gq = surf ? ob.nS.gPts : ob.nC.gPts;
+  }
   if (surf)
-    return NNView<uint32_t>{buf2(ob.surfLast, st->curBuf), st->surfLastNum, ends, nullptr, ob.nS.gPts, TS, c.N,
-                            L.sufS, L.preS, L.n[N_IRR_S], 0};
-  return NNView<uint32_t>{buf2(ob.cornerLast, st->curBuf), st->cornerLastNum, ends + TS, nullptr, ob.nC.gPts,
-                          fine_T(st->cornerLastNum, ob.gTC), c.N, L.sufC, L.preC, L.n[N_IRR_C], 0};
+    return NNView<uint32_t>{last, st->surfLastNum, ends, nullptr, gq, TS, c.N, L.sufS, L.preS, L.n[N_IRR_S], 0};
+  return NNView<uint32_t>{last, st->cornerLastNum, ends + TS, nullptr, gq, fine_T(st->cornerLastNum, ob.gTC), c.N,
+                          L.sufC, L.preC, L.n[N_IRR_C], 0};
 }
 
 // The build arguments of both clouds' indexes over the current last clouds
@@ -1305,10 +1351,97 @@ __device__ __forceinline__ bool x_point(const unsigned long long* xh, int i, uns
   return true;
 }
 
+// ---------------------------------------------------------------- ring
+// HBM-resident sensors keep ONE copy per stream of each hand-off's last
+// clouds and grids (OdomBufs::ring; featureAssociation.cpp:1759-1815 keeps one
+// per stream), built in two phases over shares of whole 64-point chunks:
+//   A  TransformToEnd of the share into P (index order), the per-scan output
+//      clouds, the bucket counts and key tables (agent-scope atomics);
+//   B  the share scattered into Q (bucket order, .w = the point's index) at
+//      its bucket's start (from the counts) plus an agent-scope cursor.
+// A share is claimed (compare-and-swap) before it is done and flagged done
+// after: the owner claims its own at once; a share still unclaimed after
+// kStealTicks is claimed and done by a waiting workgroup, so nothing needs the
+// launch's workgroups to be resident together.  Stores are 8-byte agent-scope
+// (sc1) stores; every storing wave waits for its stores (vmcnt 0) before the
+// workgroup barrier behind which one lane flags the share; readers poll the
+// flags, then one agent acquire, then plain loads.  Within a launch no slot is
+// written twice (ring_next), so a slot is never read before it is complete.
+// The slot of the next hand-off: the next of the ring, skipping the indexes'
+// snapshot (k_ring_prep replays the same picks).
+__device__ __forceinline__ int ring_next(unsigned seq, int snapBuf, int R, unsigned* seqOut) {
+  const int snap = snapBuf >= 2 ? snapBuf - 2 : -1;
+  int s = (int)(seq % (unsigned)R);
+  if (s == snap) {
+    ++seq;
+    s = (int)(seq % (unsigned)R);
+  }
+  *seqOut = seq + 1;
+  return s;
+}
+__device__ __forceinline__ void ring_put(float4* p, float4 v) {
+  unsigned long long* q = (unsigned long long*)p;
+  x_publish(q, ((unsigned long long)__float_as_uint(v.y) << 32) | __float_as_uint(v.x));
+  x_publish(q + 1, ((unsigned long long)__float_as_uint(v.w) << 32) | __float_as_uint(v.z));
+}
+__device__ __forceinline__ unsigned ring_add(unsigned* p) {
+  return __hip_atomic_fetch_add((gu32*)p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ring_max(int* p, int v) {
+  __hip_atomic_fetch_max((__attribute__((address_space(1))) int*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool ring_claim(unsigned* p, unsigned who) {
+  unsigned e = 0u;
+  return __hip_atomic_compare_exchange_strong((gu32*)p, &e, who, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned ring_peek(const unsigned* p) {
+  return __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Per-key first / last tables (suffix minimum / prefix maximum) from
+// kfirst / klast, both clouds (all threads; a barrier follows).
+__device__ __forceinline__ void key_tables_lds(const OdomLds& L, int NK) {
+  for (int t = threadIdx.x; t < 2 * NK; t += kOdomThreads) {
+    const int c0 = t >= NK ? NK : 0, k = t - c0;
+    int m = INT_MAX, M = -1;
+    for (int j = k; j < NK; ++j) m = min(m, L.kfirst[c0 + j]);
+    for (int j = 0; j <= k; ++j) M = max(M, L.klast[c0 + j]);
+    (c0 ? L.sufC : L.sufS)[k] = m;
+    (c0 ? L.preC : L.preS)[k] = M;
+  }
+  if (threadIdx.x == 0) { L.sufS[NK] = INT_MAX; L.sufC[NK] = INT_MAX; }
+}
+// A ring slot's grids into LDS: bucket ends (counts scanned; corner ends less
+// nS, the corner cloud's points sit after nS in Q) and the key tables.
+__device__ __forceinline__ void ring_index_lds(const OdomLds& L, const RingSlot& R, int nS, int TS, int TC, int NK,
+                                               bool ends) {
+  unsigned* hc = hbm_grid_ends(L);
+  const int tid = threadIdx.x;
+  for (int b = tid; b < TS + TC; b += kOdomThreads) hc[b] = R.cnt[b];
+  for (int t = tid; t < 2 * NK; t += kOdomThreads) {
+    L.kfirst[t] = INT_MAX - R.key[t];
+    L.klast[t] = R.key[2 * NK + t] - 1;
+  }
+  if (tid == 0) {
+    L.n[N_IRR_S] = R.key[4 * NK] != 0;
+    L.n[N_IRR_C] = R.key[4 * NK + 1] != 0;
+  }
+  __syncthreads();
+  block_exscan(hc, TS + TC, L.wtot);  // bucket starts
+  key_tables_lds(L, NK);
+  if (ends) {
+    for (int b = tid; b < TS + TC; b += kOdomThreads) {
+      const unsigned e = hc[b] + R.cnt[b];
+      hc[b] = b >= TS ? e - (unsigned)nS : e;
+    }
+  }
+  __syncthreads();
+}
+
 // One LM loop (surf: <= 25 x {findCorrespondingSurfFeatures;
 // calculateTransformationSurf}; corner likewise) — updateTransformation
 // :1666-1695.  R: the last clouds and indexes are LDS-resident.
-template <bool R>
+template <bool R, bool RING>
 __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const OdomLds& L, const OdomBufs& ob,
                                         const DevCfg& c, Stamp& S) {
   using Idx = typename std::conditional<R, uint16_t, uint32_t>::type;
@@ -1323,13 +1456,13 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
     qi = L.qi; qs = kLdsQ;
     nn = view_lds(surf, L, st, c, ob.gridless);
   } else {
-    last = surf ? buf2(ob.surfLast, st->curBuf) : buf2(ob.cornerLast, st->curBuf);
+    last = hbm_cloud<RING>(ob, st->curBuf, surf, st->surfLastNum);
     qi = ob.qi; qs = ob.capQ;
-    nn = view_hbm(surf, L, ob, st, c);
+    nn = view_hbm<RING>(surf, L, ob, st, c);
   }
   const int lastN = surf ? st->surfLastNum : st->cornerLastNum;
   const bool stale = st->curBuf != st->snapBuf;
-  const float4* snap = surf ? buf2(ob.surfLast, st->snapBuf) : buf2(ob.cornerLast, st->snapBuf);
+  const float4* snap = hbm_cloud<RING>(ob, st->snapBuf, surf, st->nnSurfNum);
   const int snapN = surf ? st->nnSurfNum : st->nnCornerNum;
   const float4* qp;
   if constexpr (R) qp = surf ? L.qflat : L.qsharp;  // staged in LDS at the scan's start
@@ -1628,11 +1761,19 @@ __device__ __forceinline__ OdomBufs odom_private(OdomBufs ob) {
   ob.nC.gPts += w * ob.capCorner;
   ob.nS.gPts += w * ob.capSurf;
   ob.qi += w * 3 * ob.capQ;
+  if (ob.ring) {  // the stream's ring (the silent workgroup: its private copy after it)
+    ob.ring += (size_t)s * (ob.ringCopy ? 2 : 1) * ob.ringR * ob.ringStride;
+    if (ob.wg == silent) ob.ring += ob.ringCopy;
+  }
   return ob;
 }
 
 // K scans of each of the ob.S streams: block i runs stream i / G's scans
 // [s*K, s*K + K) of the batch.
+// RING: the sensor keeps its last clouds in the stream's ring (OdomBufs::ring,
+// HDL-64E / VLS-128); a separate instantiation, so the LDS-resident sensors'
+// kernel carries none of its code or registers.
+template <bool RING>
 __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs obShared, DevCfg c, int K,
                                                       unsigned long long* prof) {
   // Claim the whole register file of the SIMD (2 waves x 256): no other
@@ -1675,14 +1816,21 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
   // the indexes over them (unless the snapshot is stale: brute force then).
   S.start();
   if (st->inited) {
-    if (st->resident) {
+    if (!RING && st->resident) {
       const float4* gS = buf2(ob.surfLast, st->curBuf);
       const float4* gC = buf2(ob.cornerLast, st->curBuf);
       for (int t = tid; t < st->surfLastNum; t += kOdomThreads) L.lastS[t] = gS[t];
       for (int t = tid; t < st->cornerLastNum; t += kOdomThreads) L.lastC[t] = gC[t];
       __syncthreads();
     }
-    if (st->curBuf == st->snapBuf) build_indexes(L, ob, st, c);
+    if (st->curBuf == st->snapBuf) {
+      if (RING && st->curBuf >= 2) {  // the stream's ring slot: its grids' ends and key tables into LDS
+        ring_index_lds(L, ring_slot(ob, st->curBuf - 2), st->nnSurfNum, fine_T(st->nnSurfNum, ob.gTS),
+                       fine_T(st->nnCornerNum, ob.gTC), c.N, true);
+      } else if (!RING) {
+        build_indexes(L, ob, st, c);
+      }
+    }
   }
   S.add(P_RESID);
   for (int b = b0; b < b0 + K; ++b) {
@@ -1695,6 +1843,35 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     float4* cEnd = ob.cornerEnd + (size_t)b * ob.capLS;
     float4* sEnd = ob.surfEnd + (size_t)b * c.P;
     const bool init = !st->inited;
+#ifndef ODOM_TOUCH
+#define ODOM_TOUCH 1
+#endif
+    // L2 warm-up: the hand-off's inputs (this scan's less-flat / less-sharp,
+    // read by TransformToEnd after the LM) and the next scan's queries (flat /
+    // sharp, staged at its start) were written by k_fa_compact on other CUs,
+    // so their lines sit in MALL / HBM, and every chunk of the hand-off loop
+    // waited for one such miss.  One dword per 128-B line, at most two lines
+    // per lane, loaded now; the values are consumed only at the hand-off, so
+    // nothing waits for them here.
+    unsigned tch0 = 0, tch1 = 0;
+    if (ODOM_TOUCH) {
+      const int lf = (F.nLF + 7) >> 3, ls = (F.nLS + 7) >> 3;  // 8 points per line
+      const bool nx = b + 1 < b0 + K;
+      const int nf = nx ? (c.N * kFlatPerRing + 7) >> 3 : 0, nsh = nx ? (c.N * kSharpPerRing + 7) >> 3 : 0;
+      const size_t nb = (size_t)(b + 1);
+      auto line = [&](int l) -> const unsigned* {
+        if (l < lf) return (const unsigned*)(F.lflat + 8 * l);
+        l -= lf;
+        if (l < ls) return (const unsigned*)(F.lsharp + 8 * l);
+        l -= ls;
+        if (l < nf) return (const unsigned*)(bb.f_flat + nb * c.N * kFlatPerRing + 8 * l);
+        l -= nf;
+        return (const unsigned*)(bb.f_sharp + nb * c.N * kSharpPerRing + 8 * l);
+      };
+      const int tot = lf + ls + nf + nsh;
+      if (tid < tot) tch0 = *line(tid);
+      if (tid + kOdomThreads < tot) tch1 = *line(tid + kOdomThreads);
+    }
     // this scan's IMU terms (all zero without an IMU message: cos 0 = 1)
     ImuScan iq = {};
     if (bb.imu) iq = bb.imuScan[b];
@@ -1718,19 +1895,20 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
       __syncthreads();
       }
       if (st->cornerLastNum >= 10 && st->surfLastNum >= 100) {
-        if (st->resident) {
+        if (!RING && st->resident) {
           for (int t = tid; t < F.nFlat; t += kOdomThreads) L.qflat[t] = F.flat[t];
           for (int t = tid; t < F.nSharp; t += kOdomThreads) L.qsharp[t] = F.sharp[t];
           __syncthreads();
-          lm_loop<true>(true, F, L, ob, c, S);
-          lm_loop<true>(false, F, L, ob, c, S);
+          lm_loop<true, RING>(true, F, L, ob, c, S);
+          lm_loop<true, RING>(false, F, L, ob, c, S);
         } else {
-          lm_loop<false>(true, F, L, ob, c, S);
-          lm_loop<false>(false, F, L, ob, c, S);
+          lm_loop<false, RING>(true, F, L, ob, c, S);
+          lm_loop<false, RING>(false, F, L, ob, c, S);
         }
       }
     }
     S.start();
+    asm volatile("" ::"v"(tch0), "v"(tch1));  // the warm-up loads end here (long since landed)
     // hand-off: checkSystemInitialization (:1605-1637, no TransformToEnd) or
     // publishCloudsLast (:1759-1815).  The new last clouds go to the HBM
     // buffer that is not the index snapshot (so a stale snapshot survives),
@@ -1738,7 +1916,7 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     const int nbuf = st->snapBuf ^ 1;
     float4* gCn = buf2(ob.cornerLast, nbuf);
     float4* gSn = buf2(ob.surfLast, nbuf);
-    const bool fits = sensorRes && F.nLS <= kLdsCorner && F.nLF <= kLdsSurf;
+    const bool fits = !RING && sensorRes && F.nLS <= kLdsCorner && F.nLF <= kLdsSurf;
     float tcur[6];
     for (int i = 0; i < 6; ++i) tcur[i] = st->transformCur[i];
     const EndTrig et = end_trig(tcur);
@@ -1766,7 +1944,17 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     NNStore<uint32_t> hsC{hcnt + hTS, nullptr, ob.nC.gPts, L.sufC, L.preC, &L.n[N_IRR_C], ob.gTC};
     const BuildArgs<uint32_t> BH = build_args<uint32_t>(gSn, F.nLF, hsS, gCn, F.nLS, hsC, c.N, hcnt, L.wtot,
                                                         L.kfirst, L.klast);
-    if (rebuild) {  // the counters must be zero before the first chunk is counted
+    // HBM-resident sensors: the stream's ring slot of this hand-off, its shares
+    // (whole 64-point chunks) and this workgroup's claim on its own share
+    const bool ringMode = RING && ob.ring != nullptr && !fits;
+    unsigned rseq = 0;
+    const int rslot = ringMode ? ring_next(st->seq, st->snapBuf, ob.ringR, &rseq) : -1;
+    const int rn = F.nLF + F.nLS;
+    const int rper = max(64, ((rn + ob.G - 1) / ob.G + 63) & ~63);
+    const int rnsh = (rn + rper - 1) / rper;
+    if (ringMode && tid == 0)
+      L.n[N_CLAIM] = ob.wg < rnsh && ring_claim(&ring_slot(ob, rslot).claimA[ob.wg], (unsigned)ob.wg + 1u);
+    if (rebuild && !RING) {  // the counters must be zero before the first chunk is counted
       if (fits) build_zero(BL);
       else build_zero(BH);
     }
@@ -1775,7 +1963,7 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     // Only for the HBM-resident sensors: C3 +2.5%, while the LDS-resident
     // VLP-16 stream and the fleet measured equal (their chunks are few, and
     // the granules' latency costs what the transform saves).
-    const bool hx = ob.G > 1 && !init && !fits;
+    const bool hx = ob.G > 1 && !init && !fits && !ringMode;
     const unsigned seq = st->seq + 1u;
     const unsigned long long xtag = (unsigned long long)seq << 32;
     unsigned long long* const xh = ob.xh + (size_t)(seq & 1u) * 3 * ob.capH;
@@ -1907,10 +2095,127 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
         }
       }
     };
-    if (hx) {
+    // the stream's ring slot (HBM-resident sensors; see "ring"): phase A over
+    // the own share (waves 1-7 beside the integrating wave 0; at the first
+    // scan every wave), the other shares awaited or stolen; then, when the
+    // indexes are rebuilt, the counts and key tables into LDS and phase B
+    auto hand_off_ring = [&]() {
+      const RingSlot R = ring_slot(ob, rslot);
+      const int nS = F.nLF, n = rn, NK = c.N;
+      const int TS = fine_T(F.nLF, ob.gTS), TC = fine_T(F.nLS, ob.gTC);
+      unsigned* hc = hbm_grid_ends(L);
+      auto w_at = [&](int j) { return j < nS ? F.lflat[j].w : F.lsharp[j - nS].w; };
+      auto shareA = [&](int j, int u0, int ustep) {
+        const int a = j * rper, e = min(n, a + rper);
+        for (int i = a + u0; i < e; i += ustep) {
+          const bool corner = i >= nS;
+          const float4 r = corner ? F.lsharp[i - nS] : F.lflat[i];
+          const float wp = w_at(max(i - 1, 0)), wn = w_at(min(i + 1, n - 1));
+          const float4 p = init ? r : to_end(r, tcur, et, im, hasImu);
+          ring_put(R.P + i, p);
+          if (corner) cEnd[i - nS] = p;
+          else sEnd[i] = p;
+          if (rebuild) {
+            ring_add(&R.cnt[(corner ? TS : 0) + fine_bucket(cell_of(p.x), cell_of(p.y), cell_of(p.z), corner ? TC : TS)]);
+            int kp, kn;
+            nbr_keys(i, nS, n, wp, wn, kp, kn);
+            const int k = (int)p.w;
+            if (k < 0 || k >= NK || kp > k) {
+              ring_max(&R.key[4 * NK + (corner ? 1 : 0)], 1);
+            } else {
+              const int kk = k + (corner ? NK : 0), jj = i - (corner ? nS : 0);
+              if (kp != k) ring_max(&R.key[kk], INT_MAX - jj);
+              if (kn != k) ring_max(&R.key[2 * NK + kk], jj + 1);
+            }
+          }
+        }
+      };
+      auto shareB = [&](int j, int u0, int ustep) {
+        const int a = j * rper, e = min(n, a + rper);
+        for (int i = a + u0; i < e; i += ustep) {
+          const bool corner = i >= nS;
+          const float4 p = R.P[i];
+          const int bk = (corner ? TS : 0) + fine_bucket(cell_of(p.x), cell_of(p.y), cell_of(p.z), corner ? TC : TS);
+          const unsigned pos = hc[bk] + ring_add(&R.fill[bk]);
+          ring_put(R.Q + pos, make_float4(p.x, p.y, p.z, __int_as_float(i - (corner ? nS : 0))));
+        }
+      };
+      // every share of a phase done: wave 0 polls the done flags; a share still
+      // unclaimed after kStealTicks is claimed and done here by every wave;
+      // then one agent acquire before the plain loads of what the shares wrote
+      auto wait_shares = [&](unsigned* claim, unsigned* done, auto&& share) {
+        const unsigned long long tw0 = wall_clock64();
+        for (;;) {
+          if (tid < 64) {
+            int steal = INT_MAX;
+            bool pend = false;
+            const bool late = wall_clock64() - tw0 > kStealTicks;
+            for (int j = tid; j < rnsh; j += 64) {
+              if (ring_peek(&done[j])) continue;
+              pend = true;
+              if (late && ring_peek(&claim[j]) == 0u) steal = min(steal, j);
+            }
+            const bool any = __ballot(pend) != 0;
+            steal = wave_min_i32(steal);
+            // a share claimed but never flagged in kLateTicks (cannot happen: the
+            // claimer is running) ends the wait with the batch's error word set
+            // rather than hanging the device
+            const bool lost = any && wall_clock64() - tw0 > kLateTicks;
+            if (tid == 0) {
+              if (lost) *ob.xerr = 2u;
+              L.n[N_RING] = (!any || lost) ? -1 : (steal != INT_MAX ? steal : -2);
+            }
+          }
+          __syncthreads();
+          const int j = L.n[N_RING];
+          if (j == -1) break;
+          if (j >= 0) {
+            if (tid == 0) L.n[N_CLAIM] = ring_claim(&claim[j], (unsigned)ob.wg + 1u);
+            __syncthreads();
+            if (L.n[N_CLAIM]) {
+              share(j, tid, kOdomThreads);
+              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+              __syncthreads();
+              if (tid == 0) __hip_atomic_store((gu32*)&done[j], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+          } else if (tid == 0) {
+            __builtin_amdgcn_s_sleep(2);
+          }
+          __syncthreads();
+        }
+        if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      };
+      const bool mineA = L.n[N_CLAIM] != 0;  // claimed before the barrier above
+      if (mineA && t0 >= 0) shareA(ob.wg, t0, tstep);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // wave 0 joins after integrating
+      if (mineA && tid == 0)
+        __hip_atomic_store((gu32*)&R.doneA[ob.wg], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      wait_shares(R.claimA, R.doneA, shareA);
+      if (!rebuild) return;  // the indexes stay on their snapshot (stale: brute force next scan)
+      ring_index_lds(L, R, nS, TS, TC, NK, false);  // bucket starts + key tables
+      if (tid == 0) L.n[N_CLAIM] = ob.wg < rnsh && ring_claim(&R.claimB[ob.wg], (unsigned)ob.wg + 1u);
+      __syncthreads();
+      if (L.n[N_CLAIM]) {
+        shareB(ob.wg, tid, kOdomThreads);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store((gu32*)&R.doneB[ob.wg], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      wait_shares(R.claimB, R.doneB, shareB);
+      for (int bk = tid; bk < TS + TC; bk += kOdomThreads) {  // starts -> ends (corner ends less nS)
+        const unsigned e = hc[bk] + R.cnt[bk];
+        hc[bk] = bk >= TS ? e - (unsigned)nS : e;
+      }
+    };
+    if (ringMode) {
+      hand_off_ring();
+    } else if (!RING && hx) {
       if (fits) hand_off_x(BL);
       else hand_off_x(BH);
-    } else {
+    } else if (!RING) {
       if (fits) hand_off(BL);
       else hand_off(BH);
     }
@@ -1920,12 +2225,13 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     if (tid == 0) {
       st->cornerLastNum = F.nLS;
       st->surfLastNum = F.nLF;
-      st->curBuf = nbuf;
+      st->curBuf = ringMode ? rslot + 2 : nbuf;
       // the record's flag: this scan's LM ran on HBM-resident last clouds
       if (lead && !init && !st->resident) bb.fa_flags[b] |= LEGO_REC_ODOM_HBM;
       st->resident = fits ? 1 : 0;
       if (hx) st->seq = seq;
-      if (rebuild) { st->snapBuf = nbuf; st->nnCornerNum = F.nLS; st->nnSurfNum = F.nLF; }
+      if (ringMode) st->seq = rseq;
+      if (rebuild) { st->snapBuf = ringMode ? rslot + 2 : nbuf; st->nnCornerNum = F.nLS; st->nnSurfNum = F.nLF; }
       int pub = 0;
       if (init) {
         st->transformSum[0] += iq.pitchStart;  // checkSystemInitialization :1633-1634
@@ -1945,7 +2251,7 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     __syncthreads();
     unsigned long long tb = 0;
     if (prof && tid == 0) tb = wall_clock64();
-    if (rebuild) {
+    if (rebuild && !RING) {
       if (fits) build_finish(BL, prof);
       else build_finish(BH, prof);
     }
@@ -2055,9 +2361,38 @@ __global__ void k_odom_prep(unsigned* xerr, uint4* xg, size_t xgVec, const uint4
   for (size_t i = t; i < (size_t)stVec; i += T) stIn[i] = st[i];
 }
 
+// Zeroes the control words of the ring slots a launch of K scans per stream
+// can pick (ring_next from the state the previous launch left; the launch's
+// picks that skip the ring, LDS-resident hand-offs, only shorten that prefix),
+// in every copy (OdomBufs::ringCopy).  Block row s = stream s.
+__global__ void k_ring_prep(OdomBufs ob, int K) {
+  const int s = blockIdx.y;
+  const int copies = ob.ringCopy ? 2 : 1;
+  unsigned char* base = ob.ring + (size_t)s * copies * ob.ringR * ob.ringStride;
+  const size_t words = ob.ringCtl / 16;
+  unsigned seq = ob.st[s].seq;
+  const int snapBuf = ob.st[s].snapBuf;
+  for (int j = 0; j < K; ++j) {
+    unsigned nx;
+    const int slot = ring_next(seq, snapBuf, ob.ringR, &nx);
+    seq = nx;
+    for (int cp = 0; cp < copies; ++cp) {
+      uint4* w = (uint4*)(base + (size_t)cp * ob.ringCopy + (size_t)slot * ob.ringStride);
+      for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (size_t)gridDim.x * blockDim.x)
+        w[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+}
+
+bool odom_ring_sensor(int N) { return !(N * kFlatPerRing <= kLdsQ && N * kSharpPerRing <= kLdsQ / 2); }
+
 int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int K, hipStream_t s, StageTimer* tm,
                 unsigned long long* prof) {
   tm->mark("odom.lm", s);
+  if (ob.ring) {
+    const int gx = (int)std::min<size_t>(64, (ob.ringCtl / 16 + 255) / 256);
+    k_ring_prep<<<dim3(gx, ob.S), 256, 0, s>>>(ob, K);
+  }
   // zero the exchange slots of the rounds this launch can use (10 per scan)
   const size_t slot = (size_t)ob.capQ * sizeof(unsigned long long);
   const size_t bytes = ob.G <= 1 ? 0
@@ -2073,7 +2408,8 @@ int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int K,
       hipMemsetAsync((unsigned char*)ob.xblock + 16, 0, ob.xbytes - 16, s) != hipSuccess)
     return -1;
   // A plain launch: the exchange needs no co-residency (see "exchange").
-  k_odom<<<ob.S * ob.G, kOdomThreads, odom_lds_bytes(), s>>>(bb, ob, c, K, prof);
+  if (ob.ring) k_odom<true><<<ob.S * ob.G, kOdomThreads, odom_lds_bytes(), s>>>(bb, ob, c, K, prof);
+  else k_odom<false><<<ob.S * ob.G, kOdomThreads, odom_lds_bytes(), s>>>(bb, ob, c, K, prof);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -1,0 +1,37 @@
+#!/bin/bash
+# GPU-box session (round 4): the -m gpu suite, a default bench line, and the
+# N = 2 rehearsal (two ranks sharing device 0 over gloo: the collective
+# transport decision of bench.py's N > 1 path).  The first failure ends it.
+set -euo pipefail
+export TMPDIR=/tmp
+R="${GRAFT_REPO_ROOT:-$(pwd)}"
+O="$R/gpurun_out/${TAG:-r04}"
+mkdir -p "$O"
+cd "$R"
+git_rev=$(cat "$R/.commit" 2>/dev/null || echo unknown)
+echo "$git_rev" > "$O/COMMIT"
+if [ -n "${FIRST:-}" ]; then  # targeted tests first (fail fast)
+  timeout -k 10 600 python -u -m pytest $FIRST -m gpu -x -v -s --timeout 240 --timeout-method thread \
+    > "$O/first_tests.log" 2>&1
+  tail -2 "$O/first_tests.log"
+fi
+if [ -z "${SKIP_TESTS:-}" ]; then
+  timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -v -s --timeout 300 --timeout-method thread \
+    > "$O/gpu_tests.log" 2>&1
+  tail -2 "$O/gpu_tests.log"
+fi
+if [ -z "${SKIP_BENCH:-}" ]; then
+  timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > "$O/bench.json" 2> "$O/bench.err"
+  echo bench ok
+fi
+if [ -n "${N2:-}" ]; then
+  LEGO_BENCH_SHARE_GPU=1 LEGO_BENCH_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
+    --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 4 --warmup 1 \
+    > "$O/bench_n2.json" 2> "$O/bench_n2.err"
+  echo n2 ok
+fi
+if [ -n "${AB:-}" ]; then
+  bash scripts/ab.sh > "$O/ab.txt" 2>&1
+  cat "$O/ab.txt"
+fi
+echo done
