@@ -425,29 +425,40 @@ def dense_bench(L, nscans: int, batch: int, device: int, cpu: bool = False, budg
     recs = (L.PoseRec * batch)()
     sub = lambda j: g.submit_device(d_pts.data_ptr(), d_off[j].data_ptr(), stamps[j * batch:(j + 1) * batch],  # noqa: E731
                                     batch)
+    got = {}  # batch index -> its records (copied after each wait; the pose check runs after the timing)
+    order = []
+
+    def wait():
+        g.wait(recs)
+        cp = (L.PoseRec * batch)()
+        C.memmove(cp, recs, C.sizeof(recs))
+        got[order.pop(0)] = cp
+
     warm = 2  # as the headline loop: two warm-up batches, then the rest two deep
     for j in range(warm):
         sub(j)
+        order.append(j)
     for j in range(warm):
-        g.wait(recs)
+        wait()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     inflight = 0
     for j in range(warm, nb):
         if inflight == 2:
-            g.wait(recs)
+            wait()
             inflight -= 1
         sub(j)
+        order.append(j)
         inflight += 1
     while inflight:
-        g.wait(recs)
+        wait()
         inflight -= 1
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     g.close()
     n = (nb - warm) * batch
     j = nb - 1  # recs: the last batch's records
-    per_scan = statistics.mean(pipeline_alg_bytes(cfg, int(off[j * batch + k + 1] - off[j * batch + k]), recs[k])
+    per_scan = statistics.mean(pipeline_alg_bytes(cfg, int(off[j * batch + k + 1] - off[j * batch + k]), got[j][k])
                                for k in range(batch))
     res = {"workload": f"C3: HDL-64E 64x2048 synthetic stream (seed 2), {batch} scans per call, two in flight",
            "scans": n, "scans_per_s": n / dt, "ms_per_scan": dt / n * 1e3, "points_per_scan": int(maxn),
@@ -455,24 +466,32 @@ def dense_bench(L, nscans: int, batch: int, device: int, cpu: bool = False, budg
                         "peak_gbs": HBM_PEAK_GBS, "frac": per_scan * n / dt / 1e9 / HBM_PEAK_GBS,
                         "note": "SURVEY §8d whole-pipeline bytes per scan (pipeline_alg_bytes, the last batch's "
                                 "counts) x scans/s"}}
-    if cpu:  # the oracle on one core over the same stream (scans synthesised beforehand) until ~budget_s
+    if cpu:  # the oracle on one core over the same stream (scans synthesised beforehand): the CPU
+        # leg times its first ~budget_s, and the whole stream is the pose reference of every GPU scan
         sc = L.synth_cfg("HDL-64E", 2)
-        scans = [L.synth_scan(sc, k) for k in range(min(nscans, 40))]
         ora = L.Oracle(L.sensor_cfg("HDL-64E"))
-        done, t0 = 0, time.perf_counter()
-        while time.perf_counter() - t0 < budget_s and done < len(scans):
-            ora.ip(*scans[done])
-            ora.fa()
-            done += 1
-        v = done / (time.perf_counter() - t0)
+        ref, done, tc, timing = [], 0, 0.0, True
+        for k in range(nb * batch):
+            scan = L.synth_scan(sc, k)
+            t0 = time.perf_counter()
+            ora.ip(*scan)
+            f = ora.fa()
+            if timing:
+                tc += time.perf_counter() - t0
+                done += 1
+                timing = tc < budget_s
+            ref.append(f["transform_sum"])
+        v = done / tc
         res["cpu_baseline"] = {"value": v, "unit": "scans/s", "cores": 1, "kind": "port",
                                "sample": f"the first {done} scans of the same HDL-64E stream through oracle ip+fa "
                                          "incl. LM, 1 thread"}
         res["gpu_over_cpu"] = res["scans_per_s"] / v
+        res["pose_delta_vs_oracle"] = pose_delta_vs_oracle({j: got[j] for j in range(warm, nb)}, ref, batch)
+        res["pose_delta_vs_oracle"]["note"] = f"the {n} timed scans (batches {warm}..{nb - 1})"
     return res
 
 
-def fleet_bench(L, streams: int, k: int, steps: int, device: int):
+def fleet_bench(L, streams: int, k: int, steps: int, device: int, check: bool = False):
     """Auxiliary (not the headline metric): `streams` independent VLP-16
     streams in one fleet context (lego_fleet_create) on one GPU, k scans per
     stream per call, the stream-major batch resident in HBM.  Whole-GPU
@@ -519,7 +538,34 @@ def fleet_bench(L, streams: int, k: int, steps: int, device: int):
     # recs hold the last call's records (window nwin - 1), stream-major like its points
     per_scan = statistics.mean(pipeline_alg_bytes(cfg, npts[-1][i], recs[i]) for i in range(streams * k))
     sps = streams * k * steps / dt
-    return {"workload": f"fleet: {streams} independent VLP-16 streams (seeds 10..{9 + streams}) x {k} scans per "
+    pose = None
+    if check:  # every stream's last-call poses against the oracle's run of that stream (host threads, untimed)
+        ocfg = L.sensor_cfg("VLP-16")
+
+        def oracle_stream(d):
+            ora = L.Oracle(ocfg)
+            out = None
+            for j in range(k * nwin):
+                ora.ip(src[d][j], j * 0.1)
+                f = ora.fa()
+                if j >= k * (nwin - 1):
+                    out = f["transform_sum"] if out is None else np.vstack([out, f["transform_sum"]])
+            return out
+
+        with ThreadPoolExecutor(max_workers=max(1, min(16, host_info()["affinity"]))) as ex:
+            refs = list(ex.map(oracle_stream, range(streams)))
+        worst, exact = 0.0, 0
+        for d in range(streams):
+            for j in range(k):
+                g = np.array(list(recs[d * k + j].transform_sum), np.float32)
+                o = np.asarray(refs[d][j], np.float32)
+                worst = max(worst, float(np.max(np.abs(g.astype(np.float64) - o.astype(np.float64)))))
+                exact += int(np.array_equal(g.view(np.uint32), o.view(np.uint32)))
+        pose = {"scans": streams * k, "max_abs": worst, "bit_exact": exact, "tolerance": 1e-4,
+                "reference": f"the oracle's run of every stream over its {k * nwin} scans; the last call's "
+                             f"{k} scans of each of the {streams} streams compared"}
+    return {"pose_delta_vs_oracle": pose,
+            "workload": f"fleet: {streams} independent VLP-16 streams (seeds 10..{9 + streams}) x {k} scans per "
                         "call on one GPU (lego_fleet_create, two calls in flight), full per-scan pipeline incl. LM "
                         "odometry",
             "streams": streams, "scans_per_stream_per_call": k, "calls": steps,
@@ -793,7 +839,7 @@ def main():
         if args.mapping_steps > 0 and world == 1:
             aux["scan_to_map_c5"] = mapping_bench(L, args.mapping_steps, not args.no_cpu)
         if args.fleet_streams > 0 and world == 1:
-            aux["fleet_vlp16"] = fleet_bench(L, args.fleet_streams, 20, 3, local)
+            aux["fleet_vlp16"] = fleet_bench(L, args.fleet_streams, 20, 3, local, check=not args.no_cpu)
         if args.dense_scans > 0 and world == 1:
             aux["dense_hdl64_c3"] = dense_bench(L, args.dense_scans, 20, local, cpu=not args.no_cpu)
         if args.loop_scans > 0 and world == 1:

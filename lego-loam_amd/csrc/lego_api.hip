@@ -523,6 +523,9 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
     }
   }
   A(ob.sumOut, B * 6);
+  A(ob.intX, B * 6);
+  ob.integ = ob.G > 1 ? 1 : 0;  // integration on its own workgroup per stream (OdomBufs::integ)
+  if (const char* e = std::getenv("LEGO_ODOM_INTEG")) ob.integ = ob.G > 1 && std::atoi(e) != 0;  // diagnostic A/B
   A(ob.curOut, B * 6);
   A(ob.validOut, B);
   A(ob.pubOut, B);
@@ -654,7 +657,7 @@ static OdomBufs ob_slice(const OdomBufs& a, const DevCfg& c, int c0, int s0, int
   o.xg += (size_t)s0 * a.roundsCap * a.capQ;
   o.xh += (size_t)s0 * 2 * 3 * a.capH;
   if (a.ring) o.ring += (size_t)s0 * (a.ringCopy ? 2 : 1) * a.ringR * a.ringStride;
-  o.sumOut += k * 6; o.curOut += k * 6; o.validOut += k; o.pubOut += k;
+  o.sumOut += k * 6; o.curOut += k * 6; o.validOut += k; o.pubOut += k; o.intX += k * 6;
   o.cornerEnd += k * a.capLS; o.surfEnd += k * c.P;
   return o;
 }

@@ -161,6 +161,16 @@ struct OdomBufs {
   size_t ringCopy;         // the diagnostic silent workgroup's private ring (bytes past the stream's), else 0
   int ringR;
 
+  // integrateTransformation off the chain (G > 1): one more workgroup per
+  // stream, launched after the S x G chain workgroups, integrates every scan
+  // of the launch in order from the lead's transformCur, published per scan
+  // as six 8-byte granules {tag, float} (intX, zeroed per launch; tag =
+  // 2 (b + 1) + valid), and writes sumOut and the state's transformSum.  The
+  // chain's TransformToEnd then runs on all eight waves.  0: wave 0 of every
+  // chain workgroup integrates beside TransformToEnd (G = 1, LEGO_ODOM_INTEG=0).
+  int integ;
+  unsigned long long* intX;  // [B*6]
+
   // per-scan outputs of the batch (workgroup 0)
   float* sumOut;        // [B*6]
   float* curOut;        // [B*6]

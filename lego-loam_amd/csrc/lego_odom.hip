@@ -1770,6 +1770,46 @@ __device__ __forceinline__ OdomBufs odom_private(OdomBufs ob) {
 
 // K scans of each of the ob.S streams: block i runs stream i / G's scans
 // [s*K, s*K + K) of the batch.
+// integrateTransformation (:1697-1725) of every scan of the launch, in order,
+// off the odometry chain (OdomBufs::integ): wave 0 of the stream's extra
+// workgroup, from the launch's input transformSum and the lead's published
+// transformCur / valid flag of each scan (checkSystemInitialization's
+// increment at a stream's first scan, :1633-1634); writes sumOut and, at the
+// end, the state's transformSum (the lead leaves those words alone).
+__device__ __forceinline__ void odom_integrate(const BatchBufs& bb, const OdomBufs& ob, int K) {
+  const int lane = threadIdx.x;
+  const int s = blockIdx.x - ob.S * ob.G;
+  __shared__ float ts[6], tc[6];
+  if (lane < 6) ts[lane] = ob.stIn[s].transformSum[lane];
+  for (int b = s * K; b < s * K + K; ++b) {
+    unsigned long long g = 0;
+    const unsigned want = (unsigned)(b + 1);
+    if (lane < 6) {
+      for (;;) {
+        g = x_load(ob.intX + (size_t)b * 6 + lane);
+        if ((unsigned)(g >> 33) == want) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      tc[lane] = __uint_as_float((unsigned)g);
+    }
+    const bool valid = (__builtin_amdgcn_readfirstlane((int)(unsigned)(g >> 32)) & 1) != 0;
+    ImuScan iq = {};
+    if (bb.imu) iq = bb.imuScan[b];
+    if (!valid) {
+      if (lane == 0) {  // checkSystemInitialization :1633-1634
+        ts[0] += iq.pitchStart;
+        ts[2] += iq.rollStart;
+      }
+    } else {
+      const float bl[3] = {iq.pitchStart, iq.yawStart, iq.rollStart};
+      const float al[3] = {iq.pitchCur, iq.yawCur, iq.rollCur};  // imu*Last = imu*Cur (:1641-1643)
+      integrate_wave(ts, tc, bl, al);
+    }
+    if (lane < 6) ob.sumOut[(size_t)b * 6 + lane] = ts[lane];
+  }
+  if (lane < 6) ob.st[s].transformSum[lane] = ts[lane];
+}
+
 // RING: the sensor keeps its last clouds in the stream's ring (OdomBufs::ring,
 // HDL-64E / VLS-128); a separate instantiation, so the LDS-resident sensors'
 // kernel carries none of its code or registers.
@@ -1780,6 +1820,10 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
   // kernel's waves share a SIMD with the latency-bound chain while the next
   // chunk's extraction runs beside it.
   asm volatile("v_mov_b32 v255, 0" ::: "v255");
+  if (obShared.integ && (int)blockIdx.x >= obShared.S * obShared.G) {  // the stream's integrating workgroup
+    if (threadIdx.x < 64) odom_integrate(bb, obShared, K);
+    return;
+  }
   const OdomBufs ob = odom_private(obShared);
   const int b0 = (int)(blockIdx.x / ob.G) * K;
   const bool lead = ob.wg == 0;  // writes the stream's outputs and state
@@ -1931,7 +1975,8 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     // integrateTransformation (:1697-1725) on wave 0 while waves 1-7 run
     // TransformToEnd: both read the final transformCur, only the former
     // writes (transformSum)
-    const int t0 = init ? tid : tid - 64, tstep = init ? kOdomThreads : kOdomThreads - 64;
+    const bool waves8 = init || ob.integ;  // TransformToEnd on every wave (integration elsewhere or none)
+    const int t0 = waves8 ? tid : tid - 64, tstep = waves8 ? kOdomThreads : kOdomThreads - 64;
     const bool rebuild = init || (F.nLS > 10 && F.nLF > 100);
     // the new clouds' build arguments in the layout they will use
     NNStore<uint16_t> nsS{L.gEndS, L.gOrdS, nullptr, L.sufS, L.preS, &L.n[N_IRR_S], kLdsGridS};
@@ -1978,7 +2023,7 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
       }
     }
     const unsigned long long tw = prof && (tid == 0 || tid == 64) ? wall_clock64() : 0;
-    if (!init && tid < 64) {
+    if (!init && tid < 64 && !ob.integ) {
       const float bl[3] = {iq.pitchStart, iq.yawStart, iq.rollStart};
       const float al[3] = {iq.pitchCur, iq.yawCur, iq.rollCur};  // imu*Last = imu*Cur (:1641-1643)
       integrate_wave(st->transformSum, st->transformCur, bl, al);
@@ -2244,7 +2289,13 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
       if (lead) {
         ob.validOut[b] = init ? 0 : 1;
         ob.pubOut[b] = pub;
-        for (int i = 0; i < 6; ++i) { ob.sumOut[b * 6 + i] = st->transformSum[i]; ob.curOut[b * 6 + i] = st->transformCur[i]; }
+        for (int i = 0; i < 6; ++i) ob.curOut[b * 6 + i] = st->transformCur[i];
+        if (ob.integ) {  // the integrating workgroup's input: {tag, transformCur[i]} granules
+          const unsigned long long tag = (unsigned long long)(2u * (unsigned)(b + 1) + (init ? 0u : 1u)) << 32;
+          for (int i = 0; i < 6; ++i) x_publish(ob.intX + (size_t)b * 6 + i, tag | __float_as_uint(st->transformCur[i]));
+        } else {
+          for (int i = 0; i < 6; ++i) ob.sumOut[b * 6 + i] = st->transformSum[i];
+        }
       }
       __threadfence_block();
     }
@@ -2258,7 +2309,9 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     if (prof && tid == 0) prof[P_BUILD] += wall_clock64() - tb;
   }
   __syncthreads();
-  if (lead && tid < (int)(sizeof(OdomState) / 4)) ((int*)ob.st)[tid] = ((const int*)st)[tid];
+  // (with the integrating workgroup, transformSum's words 6..11 are its)
+  if (lead && tid < (int)(sizeof(OdomState) / 4) && !(ob.integ && tid >= 6 && tid < 12))
+    ((int*)ob.st)[tid] = ((const int*)st)[tid];
   if (lead && ob.late >= 0) {  // releases the diagnostic late workgroup
     __syncthreads();
     if (tid == 0) __hip_atomic_store((gu32*)&ob.xerr[1], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -2354,10 +2407,12 @@ int odom_workgroups(int N, int cusAvailable) {
 // the error word, the exchange slots of the rounds this launch can use, and
 // the read-only input state (OdomBufs::stIn) from the state the previous
 // launch left.
-__global__ void k_odom_prep(unsigned* xerr, uint4* xg, size_t xgVec, const uint4* st, uint4* stIn, int stVec) {
+__global__ void k_odom_prep(unsigned* xerr, uint4* xg, size_t xgVec, const uint4* st, uint4* stIn, int stVec,
+                            uint4* ix, int ixVec) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x, T = (size_t)gridDim.x * blockDim.x;
   if (t == 0) *xerr = 0u;
   for (size_t i = t; i < xgVec; i += T) xg[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (size_t i = t; i < (size_t)ixVec; i += T) ix[i] = make_uint4(0u, 0u, 0u, 0u);  // the integration granules
   for (size_t i = t; i < (size_t)stVec; i += T) stIn[i] = st[i];
 }
 
@@ -2402,14 +2457,17 @@ int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int K,
   const int stVec = (int)(sizeof(OdomState) * ob.S / 16);
   const size_t xgVec = bytes / 16;  // capQ is even: whole 16-byte words
   const int grid = (int)std::max<size_t>(1, std::min<size_t>(512, (std::max<size_t>(xgVec, stVec) + 255) / 256));
-  k_odom_prep<<<grid, 256, 0, s>>>(ob.xerr, (uint4*)ob.xg, xgVec, (const uint4*)ob.st, (uint4*)ob.stIn, stVec);
+  const int ixVec = ob.integ ? ob.S * K * 6 * 8 / 16 : 0;  // 6 granules of 8 bytes per scan
+  k_odom_prep<<<grid, 256, 0, s>>>(ob.xerr, (uint4*)ob.xg, xgVec, (const uint4*)ob.st, (uint4*)ob.stIn, stVec,
+                                   (uint4*)ob.intX, ixVec);
   if (ob.late >= 0 && hipMemsetAsync(ob.xerr + 1, 0, sizeof(unsigned), s) != hipSuccess) return -1;
   if (ob.wg >= 0 && ob.G > 1 &&  // the diagnostic silent workgroup's copy (single-stream contexts)
       hipMemsetAsync((unsigned char*)ob.xblock + 16, 0, ob.xbytes - 16, s) != hipSuccess)
     return -1;
   // A plain launch: the exchange needs no co-residency (see "exchange").
-  if (ob.ring) k_odom<true><<<ob.S * ob.G, kOdomThreads, odom_lds_bytes(), s>>>(bb, ob, c, K, prof);
-  else k_odom<false><<<ob.S * ob.G, kOdomThreads, odom_lds_bytes(), s>>>(bb, ob, c, K, prof);
+  const int blocks = ob.S * ob.G + (ob.integ ? ob.S : 0);  // the chains, then one integrating workgroup per stream
+  if (ob.ring) k_odom<true><<<blocks, kOdomThreads, odom_lds_bytes(), s>>>(bb, ob, c, K, prof);
+  else k_odom<false><<<blocks, kOdomThreads, odom_lds_bytes(), s>>>(bb, ob, c, K, prof);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 for r in 1 2 3; do
 for v in "$A" "$B"; do
   env "$VAR=$v" timeout -k 10 120 python bench.py --no-cpu --mapping-steps 0 --fleet-streams 0 --dense-scans 0 \
-    --loop-scans 0 2>/dev/null | python3 -c "
+    --loop-scans 0 --node-scans 0 2>>"${AB_ERR:-/dev/null}" | python3 -c "
 import json,sys; d=json.loads(sys.stdin.read())
 print('$VAR=$v', round(d['value']), round(d['roofline']['launch_ms'], 3))" || exit 1
 done; done

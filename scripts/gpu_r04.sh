@@ -30,6 +30,15 @@ if [ -n "${N2:-}" ]; then
     > "$O/bench_n2.json" 2> "$O/bench_n2.err"
   echo n2 ok
 fi
+if [ -n "${PROF:-}" ]; then
+  PARTS="$PROF" TAG="${TAG}p" bash scripts/gpu_profile_r04.sh
+  echo prof ok
+fi
+if [ -n "${ENVAB:-}" ]; then  # ENVAB="VAR A B"
+  set -- $ENVAB
+  VAR=$1 A=$2 B=$3 bash scripts/env_ab.sh > "$O/envab_$1.txt" 2>&1
+  cat "$O/envab_$1.txt"
+fi
 if [ -n "${AB:-}" ]; then
   bash scripts/ab.sh > "$O/ab.txt" 2>&1
   cat "$O/ab.txt"

@@ -5,6 +5,7 @@ FETCH_SIZE x2 (it reports half of wide coalesced reads), WRITE_SIZE as
 reported, KiB -> bytes.  Usage: pmc_summary.py <run dir> <out.json> <source note> [commit]"""
 import csv
 import json
+import re
 import sys
 from collections import defaultdict
 from pathlib import Path
@@ -15,7 +16,7 @@ def per_launch(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        name = r["Kernel_Name"].split("(")[0]
+        name = re.sub(r"<[^<>]*>", "", r["Kernel_Name"].split("(")[0]).replace("void ", "")  # k_odom<true> -> k_odom
         if name.startswith("__amd"):
             continue
         tot[name] += float(r["Counter_Value"])

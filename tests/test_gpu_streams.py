@@ -4,7 +4,7 @@ two batches in flight) and the host-buffer batch entry:
 
 * C2: the 600-scan VLP-16 stream (seed 1) the headline is measured on, in the
   bench's 100-scan batches;
-* C3: 40 scans of the HDL-64E stream (seed 2): the HBM-resident odometry
+* C3: the whole 200-scan HDL-64E stream (seed 2): the ring odometry
   (grid ends in LDS, points in bucket order, counting fused into
   TransformToEnd);
 * VLS-128 (C5's sensor, seed 3): 12 scans, 128 rings.
@@ -85,7 +85,7 @@ def test_c2_full_stream_device_batches(L):
     _check(recs, ref, "C2 VLP-16 seed 1")
 
 
-@pytest.mark.parametrize("sensor,seed,n,B", [("HDL-64E", 2, 40, 20), ("VLS-128", 3, 12, 6)])
+@pytest.mark.parametrize("sensor,seed,n,B", [("HDL-64E", 2, 200, 20), ("VLS-128", 3, 12, 6)])
 def test_dense_stream_host_batches(L, sensor, seed, n, B):
     """HBM-resident odometry over host-buffer batches (lego_odom_batch)."""
     scans, pts, off, stamps = _stream(L, sensor, seed, n)
