@@ -1166,6 +1166,10 @@ static int mo_alloc(lego_ctx* x, int nc, int ns) {
     MA(m.surfTotal, 2 * P); MA(m.surfTotalDS, 2 * P);
     m.rowCap = N * kLessSharpPerRing + 2 * P;
     MA(m.rows, (size_t)m.rowCap * 8);
+    m.candQ = std::min(m.rowCap, kCandQueries);
+    if (const char* e = std::getenv("LEGO_MO_CAND"); e && std::atoi(e) == 0) m.candQ = 0;  // diagnostic A/B
+    MA(m.cand, (size_t)m.candQ * kCand);
+    MA(m.candRef, (size_t)m.candQ);
     m.partCap = 4096;  // k_mo_rows' grid cap (grid_for)
     MA(m.part, (size_t)m.partCap * 28);
     HIPCHK(hipMemsetAsync(m.st, 0, sizeof(MoState), x->stream));

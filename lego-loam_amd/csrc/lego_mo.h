@@ -58,6 +58,12 @@ __device__ __forceinline__ unsigned mo_cell_hash(int ix, int iy, int iz) {
 __device__ __forceinline__ int cell1(float v) { return (int)floorf(v); }  // 1 m cells
 
 // 1 m hashed cells over a map cloud: points grouped by bucket (w = index).
+// k_mo_rows' candidate cache (MoDev::cand): points per query, queries cached,
+// the radius kept around the reference point and how far the query may move
+// from it (kCandR >= 1 + kCandMove, with room for rounding).
+constexpr int kCand = 96, kCandQueries = 65536;
+constexpr float kCandMove = 0.25f, kCandR = 1.27f;
+
 struct MoIndex {
   int* begin;
   int* end;
@@ -106,6 +112,15 @@ struct MoDev {
   int scanCap;
   float* rows;  // [rowCap x 8]
   int rowCap;
+  // Per-query 5-NN candidates across the LM iterations (k_mo_rows): the map
+  // points of the query's 27-cell block within kCandR of where its last full
+  // search put it (candRef.xyz; .w = their count, or < 0: none kept), so a
+  // later iteration that leaves the query in the same cell and within
+  // kCandMove of that point searches only those (every point within 1 m of
+  // it is among them: exact).  Queries [0, candQ).
+  float4* cand;     // [candQ x kCand]
+  float4* candRef;  // [candQ]
+  int candQ;
   double* part;  // [partCap x 28] the rows' AtA / AtB sums per k_mo_rows workgroup
   int partCap;
   // keyframe-built map (when no fixed map is installed)
@@ -114,9 +129,9 @@ struct MoDev {
   int fromMapCap;
   // Fork-join of a step's independent VoxelGrids (each is latency-bound and
   // fills a small part of the GPU): fork[0] (the context's odometry stream)
-  // takes the scan's outlier cloud, then the map's corner cloud and its
-  // index; fork[1] the scan's surf cloud, then surf + outlier; the step's
-  // stream the map's surf cloud and index, then the scan's corner cloud.
+  // takes the scan's outlier cloud, then surf + outlier; fork[1] the scan's
+  // surf cloud, then the map's corner cloud and its index; the step's stream
+  // the map's surf cloud and index, then the scan's corner cloud.
   // Each chain has its own VoxelGrid scratch.
   hipStream_t fork[2];
   hipEvent_t ev[6];

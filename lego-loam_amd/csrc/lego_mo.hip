@@ -62,35 +62,9 @@ constexpr int kKnnLanes = 32;
 __device__ __forceinline__ bool knn_less(float da, int ia, float db, int ib) {
   return da < db || (da == db && ia < ib);
 }
-__device__ __forceinline__ int knn5_group(const MoIndex& ix, float4 q, int* oi, float* od) {
-  const int gl = threadIdx.x & (kKnnLanes - 1);
-  float ld[5];
-  int li[5];
-  int n = 0;
-  if (gl < 27) {
-    const int bx = cell1(q.x) + gl % 3 - 1, by = cell1(q.y) + (gl / 3) % 3 - 1, bz = cell1(q.z) + gl / 9 - 1;
-    const unsigned b = mo_cell_hash(bx, by, bz) & (unsigned)(ix.T - 1);
-    const int lo = ix.begin[b], hi = ix.end[b];
-    for (int t = lo; t < hi; ++t) {
-      const float4 p = ix.sorted[t];
-      if (cell1(p.x) != bx || cell1(p.y) != by || cell1(p.z) != bz) continue;  // another cell's bucket mate
-      float d2 = 0.f, d;
-      d = q.x - p.x; d2 += d * d;
-      d = q.y - p.y; d2 += d * d;
-      d = q.z - p.z; d2 += d * d;
-      if (!(d2 < 1.0f)) continue;
-      const int id = __float_as_int(p.w);
-      if (n == 5 && !knn_less(d2, id, ld[4], li[4])) continue;
-      int pos = n < 5 ? n++ : 4;
-      while (pos > 0 && knn_less(d2, id, ld[pos - 1], li[pos - 1])) {
-        ld[pos] = ld[pos - 1];
-        li[pos] = li[pos - 1];
-        --pos;
-      }
-      ld[pos] = d2;
-      li[pos] = id;
-    }
-  }
+// The five rounds of the group's lexicographic (distance, index) minimum over
+// the lanes' sorted top-5 lists (ld / li, n entries each).
+__device__ __forceinline__ int knn5_merge(const float* ld, const int* li, int n, int* oi, float* od) {
   int head = 0, found = 0;
   for (int r = 0; r < 5; ++r) {
     float cd = head < n ? ld[head] : FLT_MAX;
@@ -109,6 +83,65 @@ __device__ __forceinline__ int knn5_group(const MoIndex& ix, float4 q, int* oi, 
     if (head < n && ci == mi) ++head;  // indices are unique: exactly one lane advances
   }
   return found;
+}
+// point p into the lane's sorted top 5 when it is within 1 m of q
+__device__ __forceinline__ void knn5_offer(float4 q, float4 p, float* ld, int* li, int& n) {
+  float d2 = 0.f, d;
+  d = q.x - p.x; d2 += d * d;
+  d = q.y - p.y; d2 += d * d;
+  d = q.z - p.z; d2 += d * d;
+  if (!(d2 < 1.0f)) return;
+  const int id = __float_as_int(p.w);
+  if (n == 5 && !knn_less(d2, id, ld[4], li[4])) return;
+  int pos = n < 5 ? n++ : 4;
+  while (pos > 0 && knn_less(d2, id, ld[pos - 1], li[pos - 1])) {
+    ld[pos] = ld[pos - 1];
+    li[pos] = li[pos - 1];
+    --pos;
+  }
+  ld[pos] = d2;
+  li[pos] = id;
+}
+// The 5-NN from the query's cached candidates (k_mo_rows): lane l takes
+// candidates l, l + 32, l + 64.
+__device__ __forceinline__ int knn5_cached(const float4* cand, int nc, float4 q, int* oi, float* od) {
+  const int gl = threadIdx.x & (kKnnLanes - 1);
+  float ld[5];
+  int li[5];
+  int n = 0;
+  for (int t = gl; t < nc; t += kKnnLanes) knn5_offer(q, cand[t], ld, li, n);
+  return knn5_merge(ld, li, n, oi, od);
+}
+
+// keep: the query's candidate list to refill (nullptr: none), *kept its count
+// via the group's LDS counter (-1 when it overflowed kCand)
+__device__ __forceinline__ int knn5_group(const MoIndex& ix, float4 q, int* oi, float* od, float4* keep = nullptr,
+                                          int* kept = nullptr) {
+  const int gl = threadIdx.x & (kKnnLanes - 1);
+  float ld[5];
+  int li[5];
+  int n = 0;
+  if (gl < 27) {
+    const int bx = cell1(q.x) + gl % 3 - 1, by = cell1(q.y) + (gl / 3) % 3 - 1, bz = cell1(q.z) + gl / 9 - 1;
+    const unsigned b = mo_cell_hash(bx, by, bz) & (unsigned)(ix.T - 1);
+    const int lo = ix.begin[b], hi = ix.end[b];
+    for (int t = lo; t < hi; ++t) {
+      const float4 p = ix.sorted[t];
+      if (cell1(p.x) != bx || cell1(p.y) != by || cell1(p.z) != bz) continue;  // another cell's bucket mate
+      if (keep) {  // a candidate of the later iterations: within kCandR of q
+        float r2 = 0.f, d;
+        d = q.x - p.x; r2 += d * d;
+        d = q.y - p.y; r2 += d * d;
+        d = q.z - p.z; r2 += d * d;
+        if (r2 < kCandR * kCandR) {
+          const int k = atomicAdd(kept, 1);
+          if (k < kCand) keep[k] = p;
+        }
+      }
+      knn5_offer(q, p, ld, li, n);
+    }
+  }
+  return knn5_merge(ld, li, n, oi, od);
 }
 
 // ---------------------------------------------------------------- state
@@ -265,7 +298,8 @@ __device__ __forceinline__ float4 associate_to_map(float4 pi, const MoState* st)
 // written by the group's lane 0 (the fit runs on every lane of the group).
 __device__ __forceinline__ bool mo_row(MoState* st, int nC, const float4* cornerDS, const float4* surfTotalDS,
                                        const MoIndex& cornerIx, const MoIndex& surfIx, const float4* cornerMap,
-                                       const float4* surfMap, float* rows, int q, double* red) {
+                                       const float4* surfMap, float* rows, int q, double* red, float4* cand,
+                                       float4* candRef, int candQ, int it, int* kept) {
   const bool lead = (threadIdx.x & (kKnnLanes - 1)) == 0;
   float* row = rows + (size_t)q * 8;
   if (lead) row[7] = 0.f;
@@ -274,7 +308,32 @@ __device__ __forceinline__ bool mo_row(MoState* st, int nC, const float4* corner
   const float4 sel = associate_to_map(po, st);
   int ind[5];
   float sq[5];
-  if (knn5_group(corner ? cornerIx : surfIx, sel, ind, sq) < 5) return false;
+  // the query's candidates from its last full search, when it has stayed in
+  // that search's cell and within kCandMove of its point (MoDev::cand)
+  bool cached = false;
+  float4 ref = make_float4(0.f, 0.f, 0.f, -1.f);
+  if (it > 0 && q < candQ) {
+    ref = candRef[q];
+    const float dx = sel.x - ref.x, dy = sel.y - ref.y, dz = sel.z - ref.z;
+    cached = ref.w >= 0.f && cell1(sel.x) == cell1(ref.x) && cell1(sel.y) == cell1(ref.y) &&
+             cell1(sel.z) == cell1(ref.z) && dx * dx + dy * dy + dz * dz <= kCandMove * kCandMove;
+  }
+  int found;
+  if (cached) {
+    found = knn5_cached(cand + (size_t)q * kCand, (int)ref.w, sel, ind, sq);
+  } else if (q < candQ) {  // a full search, refilling the query's candidates
+    if (lead) *kept = 0;
+    __builtin_amdgcn_wave_barrier();
+    found = knn5_group(corner ? cornerIx : surfIx, sel, ind, sq, cand + (size_t)q * kCand, kept);
+    __builtin_amdgcn_wave_barrier();
+    if (lead) {
+      const int k = *kept;
+      candRef[q] = make_float4(sel.x, sel.y, sel.z, k <= kCand ? (float)k : -1.f);
+    }
+  } else {
+    found = knn5_group(corner ? cornerIx : surfIx, sel, ind, sq);
+  }
+  if (found < 5) return false;
   float4 cf;
   if (corner) {  // cornerOptimization :1093-1174
     float cx = 0, cy = 0, cz = 0;
@@ -373,22 +432,27 @@ constexpr int kMoSums = 21 + 6 + 1;  // AtA upper triangle, AtB, row count
 // One 32-lane group per query; each workgroup also sums its rows' AtA / AtB
 // terms in double (products of floats are exact in double) into part[block],
 // so k_mo_solve reduces one partial per workgroup instead of every row.
-__global__ void __launch_bounds__(kMoRowsThreads) k_mo_rows(MoState* st, const MoCounts* cnt, const float4* cornerDS,
+__global__ void __launch_bounds__(kMoRowsThreads, 6) k_mo_rows(  // six waves per SIMD: kMoRowsGrid resident at once
+MoState* st, const MoCounts* cnt, const float4* cornerDS,
                                                            const float4* surfTotalDS, MoIndex cornerIx,
                                                            MoIndex surfIx, const float4* cornerMap,
                                                            const float4* surfMap, float* rows, int qcap,
-                                                           double* part) {
+                                                           double* part, float4* cand, float4* candRef, int candQ,
+                                                           int it) {
   if (!st->optimized || st->converged) return;
   const int nC = cnt->cornerDS, nQ = min(nC + cnt->surfTotalDS, qcap);
   constexpr int kGroups = kMoRowsThreads / kKnnLanes;
   __shared__ double red[kGroups][kMoSums];
+  __shared__ int kept[kGroups];  // a full search's candidate count (mo_row)
   const int g = (int)threadIdx.x / kKnnLanes;
   const bool lead = (threadIdx.x & (kKnnLanes - 1)) == 0;
   if (lead)
     for (int k = 0; k < kMoSums; ++k) red[g][k] = 0.0;
   for (int q0 = blockIdx.x * kGroups; q0 < nQ; q0 += gridDim.x * kGroups) {  // group-uniform
     const int q = q0 + g;
-    if (q < nQ) mo_row(st, nC, cornerDS, surfTotalDS, cornerIx, surfIx, cornerMap, surfMap, rows, q, red[g]);
+    if (q < nQ)
+      mo_row(st, nC, cornerDS, surfTotalDS, cornerIx, surfIx, cornerMap, surfMap, rows, q, red[g], cand, candRef,
+             candQ, it, &kept[g]);
   }
   __syncthreads();
   if (threadIdx.x < kMoSums) {
@@ -699,36 +763,42 @@ __global__ void k_kf_copy(MoKeyframes kf, const float4* cornerDS, const float4* 
   }
 }
 
-enum { EV_MAP_FORK, EV_MAP_CORNER, EV_SCAN_FORK, EV_SCAN_CORNER, EV_OUTLIER, EV_SCAN_DONE };
+enum { EV_MAP_FORK, EV_MAP_CORNER, EV_SCAN_FORK, EV_SCAN_CORNER, EV_SURF, EV_SCAN_DONE };
 
 static bool fork_wait(MoDev& m, int ev, hipStream_t from, hipStream_t to) {
   return hipEventRecord(m.ev[ev], from) == hipSuccess && hipStreamWaitEvent(to, m.ev[ev], 0) == hipSuccess;
 }
 
 // The map's VoxelGrids (corner 0.2 m, surf 0.4 m, :1058-1064) and NN indexes
-// (:1333-1334): the corner cloud on fork[0], the surf cloud on s, joined on s.
-static int map_filter(MoDev& m, const float4* corner, int nC, const float4* surf, int nS, hipStream_t s) {
+// (:1333-1334): the surf cloud on s, the corner cloud on f; joined on s here
+// when `join` (installing a map), else by the step's join_scan (f = fork[1],
+// after the scan's surf cloud there).
+static int map_filter(MoDev& m, const float4* corner, int nC, const float4* surf, int nS, hipStream_t s,
+                      hipStream_t f, bool join) {
   // enqueued longest first: the host's launches take longer than the GPU's
   // short kernels, so the order of enqueueing is the order the chains start
-  const hipStream_t f = m.fork[0];
   if (hipEventRecord(m.ev[EV_MAP_FORK], s) != hipSuccess) return -1;
   if (voxel_grid_device(surf, nS, nullptr, 0.4f, m.surfMapDS, &m.cnt->surfMapDS, m.vg, s)) return -1;
   if (index_build_device(m.surfMapDS, nS, &m.cnt->surfMapDS, m.surfIx, m.vg, s)) return -1;
   if (hipStreamWaitEvent(f, m.ev[EV_MAP_FORK], 0) != hipSuccess) return -1;
   const bool ok = voxel_grid_device(corner, nC, nullptr, 0.2f, m.cornerMapDS, &m.cnt->cornerMapDS, m.vgMap2, f) == 0 &&
                   index_build_device(m.cornerMapDS, nC, &m.cnt->cornerMapDS, m.cornerIx, m.vgMap2, f) == 0;
+  if (!join) return ok ? 0 : -1;  // the step's join_scan joins f (also on failure)
   return fork_wait(m, EV_MAP_CORNER, f, s) && ok ? 0 : -1;  // joined on failure too
 }
 
 // downsampleCurrentScan (:1067-1091) forked off s at EV_SCAN_FORK, in two
 // parts around the map's launches so that every chain starts early (the
-// host's launches are serial): first the outlier cloud on fork[0] (the map's
-// corner cloud follows it there) and the surf cloud on fork[1]; after the
-// map's launches the concatenation and its VoxelGrid on fork[1] (after the
-// outlier cloud).  The corner cloud runs on s after the map's surf cloud;
-// join_scan makes s wait for the forks.  (Enqueueing the concatenation
-// before the map's launches too delayed the map's surf cloud, the longest
-// chain, by the host's ~0.3 ms: 2.6 vs 2.3 ms.)
+// host's launches are serial): first the outlier cloud on fork[0] and the
+// surf cloud on fork[1] (the map's corner cloud follows it there); after the
+// map's launches the concatenation and its VoxelGrid on fork[0] (after the
+// outlier cloud and, through EV_SURF, the surf cloud).  The corner cloud runs
+// on s after the map's surf cloud; join_scan makes s wait for the forks.
+// The three chains come out about equal on C5 (outlier 0.7 + surf+outlier
+// 0.75 ms; surf 0.5 + map corner 0.85 ms; map surf 1.25 + scan corner 0.2 ms);
+// with the map's corner cloud after the outlier cloud fork[0] was the longest
+// (1.55 ms).  (Enqueueing the concatenation before the map's launches delayed
+// the map's surf cloud by the host's ~0.3 ms: 2.6 vs 2.3 ms.)
 // (Two forks: with the step's stream that is three hardware queues, as many
 // as a process gets besides the runtime's own; a third fork shared one.)
 static int scan_filter_begin(MoDev& m, const MoStepArgs& a) {
@@ -737,16 +807,16 @@ static int scan_filter_begin(MoDev& m, const MoStepArgs& a) {
   if (hipStreamWaitEvent(f1, m.ev[EV_SCAN_FORK], 0) != hipSuccess) return -1;
   if (voxel_grid_device(m.outlierLast, a.nOutlier, nullptr, 0.4f, m.outlierDS, &m.cnt->outlierDS, m.vgScan2, f0))
     return -1;
-  if (hipEventRecord(m.ev[EV_OUTLIER], f0) != hipSuccess) return -1;
   if (voxel_grid_device(m.surfLast, a.nSurf, nullptr, 0.4f, m.surfDS, &m.cnt->surfDS, m.vgScan1, f1)) return -1;
+  if (hipEventRecord(m.ev[EV_SURF], f1) != hipSuccess) return -1;
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 static int scan_filter_end(MoDev& m, const MoStepArgs& a) {
-  const hipStream_t f0 = m.fork[0], f1 = m.fork[1];
-  if (hipStreamWaitEvent(f1, m.ev[EV_OUTLIER], 0) != hipSuccess) return -1;
-  k_mo_concat<<<grid_for(a.nSurf + a.nOutlier), 256, 0, f1>>>(m.surfDS, m.outlierDS, m.cnt, m.surfTotal);
+  const hipStream_t f0 = m.fork[0];
+  if (hipStreamWaitEvent(f0, m.ev[EV_SURF], 0) != hipSuccess) return -1;
+  k_mo_concat<<<grid_for(a.nSurf + a.nOutlier), 256, 0, f0>>>(m.surfDS, m.outlierDS, m.cnt, m.surfTotal);
   if (voxel_grid_device(m.surfTotal, a.nSurf + a.nOutlier, &m.cnt->surfTotal, 0.4f, m.surfTotalDS,
-                        &m.cnt->surfTotalDS, m.vgScan1, f1))
+                        &m.cnt->surfTotalDS, m.vgScan2, f0))
     return -1;
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -755,7 +825,7 @@ static int join_scan(MoDev& m, hipStream_t s) {
 }
 
 static int kf_map_filter(MoDev& m, int nCM, int nSM, hipStream_t s) {
-  return map_filter(m, m.cornerFromMap, nCM, m.surfFromMap, nSM, s);
+  return map_filter(m, m.cornerFromMap, nCM, m.surfFromMap, nSM, s, m.fork[1], false);
 }
 
 // The surrounding map of the keyframe store, filtered and indexed.
@@ -817,7 +887,7 @@ int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, h
     const int st = kf_map(m, radius, s);
     if (st) return fail(st);
   } else if (m.mapPerStep) {  // the map VoxelGrids (:1058-1064) and kd-tree builds (:1333-1334) of every step
-    if (mo_set_map_device(m, m.nCornerMap, m.nSurfMap, s)) return fail(-1);
+    if (map_filter(m, m.cornerMap, m.nCornerMap, m.surfMap, m.nSurfMap, s, m.fork[1], false)) return fail(-1);
   }
   MO_HOSTPROF(1);
   if (scan_filter_end(m, a)) return fail(-1);
@@ -837,7 +907,8 @@ int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, h
   for (int it = 0; it < 10; ++it) {
     if (qcap > 0)
       k_mo_rows<<<nb, kMoRowsThreads, 0, s>>>(m.st, m.cnt, m.cornerDS, m.surfTotalDS, m.cornerIx, m.surfIx,
-                                                m.cornerMapDS, m.surfMapDS, m.rows, qcap, m.part);
+                                                m.cornerMapDS, m.surfMapDS, m.rows, qcap, m.part, m.cand, m.candRef,
+                                                m.candQ, it);
     k_mo_solve<<<1, kMoSolveThreads, 0, s>>>(m.st, m.part, nb, it);
   }
   k_mo_finish<<<1, 64, 0, s>>>(m.st, a.imuOn, a.imuRoll, a.imuPitch);
@@ -852,7 +923,7 @@ int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, h
 // Installs a fixed map: voxel filter (corner 0.2 m, surf 0.4 m, :1062-1064) and
 // NN index, once.
 int mo_set_map_device(MoDev& m, int nCornerMap, int nSurfMap, hipStream_t s) {
-  return map_filter(m, m.cornerMap, nCornerMap, m.surfMap, nSurfMap, s);
+  return map_filter(m, m.cornerMap, nCornerMap, m.surfMap, nSurfMap, s, m.fork[0], true);
 }
 
 }  // namespace lego

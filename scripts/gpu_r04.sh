@@ -10,6 +10,9 @@ mkdir -p "$O"
 cd "$R"
 git_rev=$(cat "$R/.commit" 2>/dev/null || echo unknown)
 echo "$git_rev" > "$O/COMMIT"
+if [ -n "${MB:-}" ]; then  # microbenchmarks built in-tree (build/)
+  for m in $MB; do timeout -k 10 120 "./build/$m" > "$O/$m.txt" 2>&1; cat "$O/$m.txt"; done
+fi
 if [ -n "${FIRST:-}" ]; then  # targeted tests first (fail fast)
   timeout -k 10 600 python -u -m pytest $FIRST -m gpu -x -v -s --timeout 240 --timeout-method thread \
     > "$O/first_tests.log" 2>&1
@@ -38,6 +41,11 @@ if [ -n "${ENVAB:-}" ]; then  # ENVAB="VAR A B"
   set -- $ENVAB
   VAR=$1 A=$2 B=$3 bash scripts/env_ab.sh > "$O/envab_$1.txt" 2>&1
   cat "$O/envab_$1.txt"
+fi
+if [ -n "${ENVAB5:-}" ]; then  # ENVAB5="VAR A B" on the C5 line
+  set -- $ENVAB5
+  VAR=$1 A=$2 B=$3 bash scripts/env_ab_c5.sh > "$O/envab5_$1.txt" 2>&1
+  cat "$O/envab5_$1.txt"
 fi
 if [ -n "${AB:-}" ]; then
   bash scripts/ab.sh > "$O/ab.txt" 2>&1
