@@ -1887,35 +1887,6 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     float4* cEnd = ob.cornerEnd + (size_t)b * ob.capLS;
     float4* sEnd = ob.surfEnd + (size_t)b * c.P;
     const bool init = !st->inited;
-#ifndef ODOM_TOUCH
-#define ODOM_TOUCH 1
-#endif
-    // L2 warm-up: the hand-off's inputs (this scan's less-flat / less-sharp,
-    // read by TransformToEnd after the LM) and the next scan's queries (flat /
-    // sharp, staged at its start) were written by k_fa_compact on other CUs,
-    // so their lines sit in MALL / HBM, and every chunk of the hand-off loop
-    // waited for one such miss.  One dword per 128-B line, at most two lines
-    // per lane, loaded now; the values are consumed only at the hand-off, so
-    // nothing waits for them here.
-    unsigned tch0 = 0, tch1 = 0;
-    if (ODOM_TOUCH) {
-      const int lf = (F.nLF + 7) >> 3, ls = (F.nLS + 7) >> 3;  // 8 points per line
-      const bool nx = b + 1 < b0 + K;
-      const int nf = nx ? (c.N * kFlatPerRing + 7) >> 3 : 0, nsh = nx ? (c.N * kSharpPerRing + 7) >> 3 : 0;
-      const size_t nb = (size_t)(b + 1);
-      auto line = [&](int l) -> const unsigned* {
-        if (l < lf) return (const unsigned*)(F.lflat + 8 * l);
-        l -= lf;
-        if (l < ls) return (const unsigned*)(F.lsharp + 8 * l);
-        l -= ls;
-        if (l < nf) return (const unsigned*)(bb.f_flat + nb * c.N * kFlatPerRing + 8 * l);
-        l -= nf;
-        return (const unsigned*)(bb.f_sharp + nb * c.N * kSharpPerRing + 8 * l);
-      };
-      const int tot = lf + ls + nf + nsh;
-      if (tid < tot) tch0 = *line(tid);
-      if (tid + kOdomThreads < tot) tch1 = *line(tid + kOdomThreads);
-    }
     // this scan's IMU terms (all zero without an IMU message: cos 0 = 1)
     ImuScan iq = {};
     if (bb.imu) iq = bb.imuScan[b];
@@ -1952,7 +1923,6 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
       }
     }
     S.start();
-    asm volatile("" ::"v"(tch0), "v"(tch1));  // the warm-up loads end here (long since landed)
     // hand-off: checkSystemInitialization (:1605-1637, no TransformToEnd) or
     // publishCloudsLast (:1759-1815).  The new last clouds go to the HBM
     // buffer that is not the index snapshot (so a stale snapshot survives),
