@@ -9,6 +9,6 @@ mkdir -p "$O"
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$O/trace" -o run \
   -- python3 "$R/bench.py" --no-cpu --no-handoff --steps 1 --warmup 0 --fleet-streams 0 --dense-scans 0 \
-  --loop-scans 0 --stream-len 100 --mapping-steps ${STEPS:-4} > "$O/bench.log" 2>&1
+  --loop-scans 0 --node-scans 0 --stream-len 100 --mapping-steps ${STEPS:-4} > "$O/bench.log" 2>&1
 find "$O" -name '*kernel_trace.csv' | head -1
 echo done

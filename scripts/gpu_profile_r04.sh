@@ -42,9 +42,22 @@ pmc c3 FETCH_SIZE $OFF --sensor HDL-64E --seed 2 --stream-len 200 --batch 20 --s
 pmc c3 WRITE_SIZE $OFF --sensor HDL-64E --seed 2 --stream-len 200 --batch 20 --steps 2 --warmup 1
 fi
 if [[ " $PARTS " == *" fleet "* ]]; then
-prof fleet --no-cpu --no-handoff --steps 1 --warmup 0 --mapping-steps 0 --dense-scans 0 --loop-scans 0 --node-scans 0 --stream-len 100
+FL="--no-cpu --no-handoff --steps 1 --warmup 0 --mapping-steps 0 --dense-scans 0 --loop-scans 0 --node-scans 0 --stream-len 100"
+prof fleet $FL
+pmc fleet FETCH_SIZE $FL
+pmc fleet WRITE_SIZE $FL
 fi
 if [[ " $PARTS " == *" c5 "* ]]; then
 prof c5 --no-cpu --no-handoff --steps 1 --warmup 0 --fleet-streams 0 --dense-scans 0 --loop-scans 0 --node-scans 0 --stream-len 100 --mapping-steps 15
+fi
+if [[ " $PARTS " == *" phases "* ]]; then  # the in-kernel odometry phase stamps of the C2 line
+  mkdir -p "$O/phases"
+  cd "$R"
+  timeout -k 10 300 python3 bench.py $OFF --steps 6 --warmup 2 --odom-profile > "$O/phases/bench.json" \
+    2> "$O/phases/odom_phase_profile.txt"
+  cd /tmp
+fi
+if [[ " $PARTS " == *" c5trace "* ]]; then
+  TAG="${TAG}/c5t" bash "$R/scripts/gpu_c5_trace.sh"
 fi
 echo done
