@@ -544,7 +544,12 @@ __device__ __forceinline__ void mo_solve_tail(MoState* st, const double* tot, in
     for (int j = 0; j < 6; ++j) Aq[i][j] = AtA[i][j];
   cv_solve_qr<6, 6>(Aq, AtB, X);
   float (&P)[6][6] = *reinterpret_cast<float(*)[6][6]>(st->matP);
-  if (iterCount == 0) {
+  if (iterCount == 0 && eig_min_above_n<6>(AtA, 100.0)) {
+    // every eigenvalue provably above the threshold: the degeneracy test finds
+    // nothing, and matP is read only while isDegenerate is set (:1281-1296);
+    // the Jacobi (most of this launch's time at iteration 0) is not needed
+    st->isDegenerate = 0;
+  } else if (iterCount == 0) {
     // eigen / inverse on LDS arrays (their loops index dynamically)
     float (&Ae)[6][6] = *reinterpret_cast<float(*)[6][6]>(ws);
     float (&V)[6][6] = *reinterpret_cast<float(*)[6][6]>(ws + 36);

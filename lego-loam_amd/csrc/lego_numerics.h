@@ -673,6 +673,38 @@ LEGO_HD bool eig_min_above(const float (&A)[3][3], double thr) {
   return d2 > 0;
 }
 
+// The same proof for an N x N system (mapOptimization's 6 x 6 AtA, threshold
+// 100, mapOptmization.cpp:1281-1296): A - t I positive definite by an LDL^T in
+// double, t = thr + 1e-4 * ||A||_F, so every eigenvalue, and the Jacobi
+// restatement's computed ones, exceed thr.  Checked against cv_eigen_sym<6>
+// by tests/native/eigmin_check.cpp.
+template <int N>
+LEGO_HD bool eig_min_above_n(const float (&A)[N][N], double thr) {
+  double fro2 = 0;
+#pragma unroll
+  for (int i = 0; i < N; i++)
+#pragma unroll
+    for (int j = 0; j < N; j++) fro2 += (double)A[i][j] * (double)A[i][j];
+  const double t = thr + 1e-4 * __builtin_sqrt(fro2);
+  double Lm[N][N], D[N];
+#pragma unroll
+  for (int j = 0; j < N; j++) {
+    double d = (double)A[j][j] - t;
+#pragma unroll
+    for (int k = 0; k < j; k++) d -= Lm[j][k] * Lm[j][k] * D[k];
+    if (!(d > 0)) return false;
+    D[j] = d;
+#pragma unroll
+    for (int i = j + 1; i < N; i++) {
+      double v = (double)A[i][j];
+#pragma unroll
+      for (int k = 0; k < j; k++) v -= Lm[i][k] * Lm[j][k] * D[k];
+      Lm[i][j] = v / d;
+    }
+  }
+  return true;
+}
+
 // matP = matV.inv() * matV2 (cv gemm: double accumulation, float store).
 template <int N>
 LEGO_HD void cv_matmul(const float (&A)[N][N], const float (&B)[N][N], float (&C)[N][N]) {
