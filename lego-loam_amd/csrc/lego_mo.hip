@@ -491,21 +491,22 @@ __device__ __forceinline__ void mo_solve_tail(MoState* st, const double* tot, in
 __global__ void __launch_bounds__(kMoSolveThreads) k_mo_solve(MoState* st, const double* part, int nb,
                                                              int iterCount) {
   if (!st->optimized || st->converged) return;
-  // the partials [nb x kMoSums] read coalesced: thread t < 9 * kMoSums sums
-  // element t % kMoSums of the partials b = t / kMoSums (mod 9), ascending,
-  // i.e. part[t], part[t + 252], ...; then thread 0 adds the nine in order
-  constexpr int kLanesPerSum = kMoSolveThreads / kMoSums;  // 9
-  constexpr int kStride = kLanesPerSum * kMoSums;           // 252
-  __shared__ double red[kLanesPerSum][kMoSums];
+  __shared__ double red[kMoSolveThreads / 64][kMoSums];
   __shared__ float ws[6 * 6 * 6 + 16];  // eigen / inverse workspace (thread 0)
   __shared__ int wsi[16];
-  const int tid = threadIdx.x;
-  if (tid < kStride) {
-    double acc = 0.0;
-    const size_t n = (size_t)nb * kMoSums;
-#pragma unroll 8
-    for (size_t i = tid; i < n; i += kStride) acc += part[i];
-    red[tid / kMoSums][tid % kMoSums] = acc;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  double acc[kMoSums];
+#pragma unroll
+  for (int k = 0; k < kMoSums; ++k) acc[k] = 0.0;
+  for (int b = tid; b < nb; b += kMoSolveThreads) {
+    const double* pb = part + (size_t)b * kMoSums;
+#pragma unroll
+    for (int k = 0; k < kMoSums; ++k) acc[k] += pb[k];
+  }
+#pragma unroll
+  for (int k = 0; k < kMoSums; ++k) {
+    const double w = mo_wave_sum(acc[k]);
+    if (lane == 0) red[wave][k] = w;
   }
   __syncthreads();
   if (tid != 0) return;
@@ -514,7 +515,7 @@ __global__ void __launch_bounds__(kMoSolveThreads) k_mo_solve(MoState* st, const
   for (int k = 0; k < kMoSums; ++k) {
     double sum = 0;
 #pragma unroll
-    for (int w = 0; w < kLanesPerSum; ++w) sum += red[w][k];
+    for (int w = 0; w < kMoSolveThreads / 64; ++w) sum += red[w][k];
     tot[k] = sum;
   }
   mo_solve_tail(st, tot, iterCount, ws, wsi);
