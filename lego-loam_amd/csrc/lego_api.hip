@@ -380,6 +380,10 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
   A(x->d_pts, B1 * max_points);
   A(x->d_off, B1 + 1);
   A(bb.owner, B * P);
+  if (hipMemset(bb.owner, 0xff, sizeof(int) * (size_t)B * P) != hipSuccess) {  // -1: no owner (k_pixels keeps it so)
+    set_err("hipMemset failed for the owner image");
+    return fail(LEGO_E_DEVICE);
+  }
   A(bb.range, B * P);
   A(bb.full, B * P);
   A(bb.ground, B * P);
