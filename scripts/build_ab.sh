@@ -6,6 +6,7 @@ set -euo pipefail
 cd "$(dirname "$0")/../lego-loam_amd"
 for v in A B; do
   f="${v}_FLAGS"
+  rm -rf "../build/ab/$v"  # the flags are not a make dependency: rebuild every object
   make -s -j8 OUT=../build/ab/$v EXTRA="${!f:-}" ../build/ab/$v/liblego_hip.so
 done
 ls -la ../build/ab/*/liblego_hip.so
