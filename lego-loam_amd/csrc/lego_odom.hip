@@ -1973,35 +1973,6 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
       if (fits) build_zero(BL);
       else build_zero(BH);
     }
-#ifndef ODOM_STAGE
-#define ODOM_STAGE 1
-#endif
-    // LDS-resident hand-off: the new clouds' raw points staged into the LDS
-    // slots they will occupy (the old last clouds are dead once the LM is
-    // done), every lane's loads in flight together, so the TransformToEnd
-    // loop below reads LDS instead of waiting on one global load per chunk;
-    // TransformToEnd then rewrites each slot in place (a slot is read and
-    // written by one lane only; its neighbours' keys, the .w words, are the
-    // same before and after)
-    const bool staged = ODOM_STAGE && fits;
-    if (staged) {
-      constexpr int kSU = 8;
-      const int nS = F.nLF, n = F.nLF + F.nLS;
-      for (int c = tid; c < n; c += kSU * kOdomThreads) {
-        float4 v[kSU];
-#pragma unroll
-        for (int u = 0; u < kSU; ++u) {
-          const int i = c + u * kOdomThreads;
-          if (i < n) v[u] = i < nS ? F.lflat[i] : F.lsharp[i - nS];
-        }
-#pragma unroll
-        for (int u = 0; u < kSU; ++u) {
-          const int i = c + u * kOdomThreads;
-          if (i < nS) L.lastS[i] = v[u];
-          else if (i < n) L.lastC[i - nS] = v[u];
-        }
-      }
-    }
     __syncthreads();
     // hand-off exchange: this workgroup's share of TransformToEnd, published.
     // Only for the HBM-resident sensors: C3 +2.5%, while the LDS-resident
@@ -2034,14 +2005,11 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     auto hand_off = [&](const auto& B) {
       if (t0 >= 0) {
         const int nS = F.nLF, n = F.nLF + F.nLS, lane = tid & 63;
-        // the raw points: staged in LDS (see above) or the feature clouds
-        const float4* srcS = staged ? L.lastS : F.lflat;
-        const float4* srcC = staged ? L.lastC : F.lsharp;
-        auto w_at = [&](int j) { return j < nS ? srcS[j].w : srcC[j - nS].w; };
+        auto w_at = [&](int j) { return j < nS ? F.lflat[j].w : F.lsharp[j - nS].w; };
         // the point and its neighbours' .w words, one chunk ahead
         auto fetch = [&](int i, float4& r, float& wp, float& wn) {
           if (i < n) {
-            r = i >= nS ? srcC[i - nS] : srcS[i];
+            r = i >= nS ? F.lsharp[i - nS] : F.lflat[i];
             wp = w_at(max(i - 1, 0));
             wn = w_at(min(i + 1, n - 1));
           }
