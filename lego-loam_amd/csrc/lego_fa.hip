@@ -853,7 +853,7 @@ __device__ __forceinline__ float4 lfv_centroid(const float4* slot, const uint16_
   float cx = 0, cy = 0, cz = 0, ci = 0;
   int u = t;
   for (; u < K && key[u] == k; ++u) {
-    const float4 q = slot[val[u]];
+    const float4 q = slot[min((int)val[u], K - 1)];  // bounded: a bad permutation fails parity, never faults
     cx += q.x; cy += q.y; cz += q.z; ci += q.w;
   }
   const float n = (float)(u - t);
@@ -997,7 +997,7 @@ __device__ __forceinline__ void lfv_block(const BatchBufs& bb, const DevCfg& c, 
     val[t] = (uint16_t)t;
   }
   __syncthreads();
-  vg_block_sort(vg_sort_carve(key, val, sc, K, (int)blockDim.x), K, -1, nullptr, true);
+  vg_block_sort_sid(vg_sort_carve(key, val, sc, K, (int)blockDim.x), K, -1, nullptr, true);
   // centroids into registers (every read of the slot done), then over the slot
   float4 cen[kLfvMaxPer];
   int at[kLfvMaxPer];

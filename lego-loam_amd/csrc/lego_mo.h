@@ -37,6 +37,7 @@ struct VgScratch {
   int* cut;         // [capBig] the round's cut per segment
   int* kcnt;        // [capBig] the round's swap count per segment
   int* tileOff;     // [capBig + 1] first tile of each segment
+  int* tileSeg;     // [capTiles] the round's tile -> its segment | its index in the segment << 16
   int* tileL;       // [capTiles] left stops per tile
   int* tileR;       // [capTiles] right stops per tile
   int4* loc;        // [capLoc] segments sorted in one workgroup (s, e, depth budget)

@@ -245,7 +245,10 @@ __device__ void vg_plan_big(const VgScratch& v, const int2* big, int nb, int* tm
     }
     int t;
     const int off = block_excl_scan(nt, tmp, &t);
-    if (b < nb) v.tileOff[b] = carry + off;
+    if (b < nb) {
+      v.tileOff[b] = carry + off;
+      for (int k = 0; k < nt; ++k) v.tileSeg[carry + off + k] = b | (k << 16);  // no search per tile
+    }
     carry += t;
   }
   if (threadIdx.x == 0) {
@@ -340,27 +343,15 @@ __global__ void __launch_bounds__(kVgPlanThreads) k_vg_plan(VgScratch v, int r, 
   vg_plan_big(v, next, carry, tmp);
 }
 
-// tile b of the current round -> its segment (binary search over tileOff)
-__device__ __forceinline__ int vg_tile_seg(const VgScratch& v, int b, int nb) {
-  int lo = 0, hi = nb - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (v.tileOff[mid] <= b) lo = mid;
-    else hi = mid - 1;
-  }
-  return lo;
-}
-
 // left / right stops of one tile
 __global__ void __launch_bounds__(kVgTileThreads) k_vg_count(VgScratch v, int r) {
   __shared__ int tmp[20];
   const int nt = v.ctl[C_NT];
   if ((int)blockIdx.x >= nt) return;
-  const int nb = v.ctl[C_NB];
   const int2* big = v.big + (r & 1) * v.capBig;
-  const int sg = vg_tile_seg(v, blockIdx.x, nb);
+  const int ts = v.tileSeg[blockIdx.x], sg = ts & 0xffff;
   const int s = big[sg].x, e = big[sg].y;
-  const int base = s + 1 + ((int)blockIdx.x - v.tileOff[sg]) * kVgTile;
+  const int base = s + 1 + (ts >> 16) * kVgTile;
   const unsigned p = v.keys[s];
   int cl = 0, cr = 0;
 #pragma unroll
@@ -385,12 +376,10 @@ __global__ void __launch_bounds__(kVgTileThreads) k_vg_decide(VgScratch v, int r
   __shared__ int rowL[kVgTilePer][4], rowR[kVgTilePer][4];
   const int nt = v.ctl[C_NT];
   if ((int)blockIdx.x >= nt) return;
-  const int nb = v.ctl[C_NB];
   const int2* big = v.big + (r & 1) * v.capBig;
-  const int sg = vg_tile_seg(v, blockIdx.x, nb);
+  const int ts = v.tileSeg[blockIdx.x], sg = ts & 0xffff, kt = ts >> 16;
   const int s = big[sg].x, e = big[sg].y;
-  const int t0 = v.tileOff[sg], t1 = v.tileOff[sg + 1];
-  const int kt = (int)blockIdx.x - t0;
+  const int t0 = (int)blockIdx.x - kt, t1 = t0 + (e - s - 1 + kVgTile - 1) / kVgTile;
   const int base = s + 1 + kt * kVgTile;
   const unsigned p = v.keys[s];
   int a = 0, bL = 0, bR = 0;
@@ -454,12 +443,11 @@ __global__ void __launch_bounds__(kVgTileThreads) k_vg_decide(VgScratch v, int r
 __global__ void __launch_bounds__(kVgTileThreads) k_vg_swap(VgScratch v, int r) {
   const int nt = v.ctl[C_NT];
   if ((int)blockIdx.x >= nt) return;
-  const int nb = v.ctl[C_NB];
   const int2* big = v.big + (r & 1) * v.capBig;
-  const int sg = vg_tile_seg(v, blockIdx.x, nb);
+  const int ts = v.tileSeg[blockIdx.x], sg = ts & 0xffff;
   const int s = big[sg].x;
   const int K = v.kcnt[sg];
-  const int q0 = ((int)blockIdx.x - v.tileOff[sg]) * kVgTile;
+  const int q0 = (ts >> 16) * kVgTile;
 #pragma unroll 4
   for (int j = 0; j < kVgTilePer; ++j) {
     const int q = q0 + j * kVgTileThreads + threadIdx.x;
@@ -536,7 +524,7 @@ __device__ void vg_local_sort(const VgScratch& v, uint32_t* key, uint16_t* lv, u
   vg_block_sort(vg_sort_carve(key, lv, sc, m, (int)blockDim.x), m, depth, v.ctl + C_HEAP, true);
   for (int i = threadIdx.x; i < m; i += blockDim.x) {
     v.keys[s + i] = key[i];
-    key[i] = (uint32_t)v.vals[s + lv[i]];
+    key[i] = (uint32_t)v.vals[s + min((int)lv[i], m - 1)];  // bounded (a bad permutation fails parity, never faults)
   }
   __syncthreads();
   for (int i = threadIdx.x; i < m; i += blockDim.x) v.vals[s + i] = (int)key[i];
@@ -574,11 +562,14 @@ __global__ void __launch_bounds__(kVgLocalThreads) k_vg_local(VgScratch v) {
   for (int t = blockIdx.x; t < nloc; t += gridDim.x) {
     const int4 g = v.loc[t];
     if (g.y - g.x <= kVgSplit) continue;  // k_vg_local_small's
-    if (g.y - g.x <= kVgLocal) {
-      vg_local_sort(v, key, lv, sc, g.x, g.y - g.x, g.z);
-      continue;
+    // one call site of the LDS sort (two inlined copies spilled registers);
+    // every thread has read sp's last value before it is set again
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      stk[0] = g;
+      sp = 1;
+      if (g.y - g.x > kVgLocal) atomicAdd(&v.ctl[C_SLOW], 1);
     }
-    if (threadIdx.x == 0) { stk[0] = g; sp = 1; atomicAdd(&v.ctl[C_SLOW], 1); }
     __syncthreads();
     while (sp > 0) {
       const int4 c = stk[sp - 1];
@@ -648,7 +639,7 @@ __global__ void __launch_bounds__(kHeadTile) k_vg_emit(const float4* in, int n, 
   float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
   int u = t;
   for (; u < m && v.keys[u] == k; ++u) {
-    const float4 p = in[v.vals[u]];
+    const float4 p = in[min(v.vals[u], nn - 1)];  // bounded (see vg_local_sort)
     c0 += p.x; c1 += p.y; c2 += p.z; c3 += p.w;
   }
   const float cnt = (float)(u - t);
@@ -715,6 +706,7 @@ int vg_scratch_alloc(VgScratch& v, int cap, void* ctx, int (*alloc)(void* ctx, v
       {(void**)&v.big, sizeof(int2) * 2 * (size_t)v.capBig},
       {(void**)&v.cut, sizeof(int) * (size_t)v.capBig},  {(void**)&v.kcnt, sizeof(int) * (size_t)v.capBig},
       {(void**)&v.tileOff, sizeof(int) * (size_t)(v.capBig + 1)},
+      {(void**)&v.tileSeg, sizeof(int) * (size_t)v.capTiles},
       {(void**)&v.tileL, sizeof(int) * (size_t)v.capTiles}, {(void**)&v.tileR, sizeof(int) * (size_t)v.capTiles},
       {(void**)&v.loc, sizeof(int4) * (size_t)v.capLoc},
       {(void**)&v.scanTiles, sizeof(int) * (size_t)v.capScanTiles},
@@ -749,15 +741,30 @@ __global__ void __launch_bounds__(1024) k_sort_perm(const uint32_t* keys, int n,
   vg_block_sort(vg_sort_carve(key, val, sc, n, (int)blockDim.x), n, -1, heap, wave >= 2);
   for (int i = threadIdx.x; i < n; i += blockDim.x) perm[i] = val[i];
 }
+// k_lf_voxel's form (segment ids in LDS, sumOrder), 256 threads; a kernel of
+// its own so that neither form's registers weigh on the other
+__global__ void __launch_bounds__(256) k_sort_perm_sid(const uint32_t* keys, int n, int* perm, int* heap) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  uint32_t* key = (uint32_t*)lds_raw;
+  uint16_t* val = (uint16_t*)(lds_raw + (size_t)4 * kSortPermBlockMax);
+  unsigned char* sc = lds_raw + (size_t)6 * kSortPermBlockMax;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) { key[i] = keys[i]; val[i] = (uint16_t)i; }
+  __syncthreads();
+  vg_block_sort_sid(vg_sort_carve(key, val, sc, n, (int)blockDim.x), n, -1, heap, true);
+  for (int i = threadIdx.x; i < n; i += blockDim.x) perm[i] = val[i];
+}
 size_t sort_perm_lds_bytes() { return (size_t)6 * kSortPermBlockMax + vg_sort_scratch_bytes(kSortPermBlockMax, 1024); }
 // wave = 2 / 3: the block sort as the VoxelGrids run it (sumOrder: heap pieces
 // whose centroids do not depend on their order ranked stably) with 256 threads
-// (k_lf_voxel's large rings, n <= 2048) / 1024 threads (n <= 8192).
+// in k_lf_voxel's form (vg_block_sort_sid, its large rings, n <= 2048) / 1024
+// threads in the mapping VoxelGrids' form (vg_block_sort, n <= 8192); wave = 0
+// the exact permutation of the mapping form.
 int sort_perm_device(const uint32_t* keys, int n, int wave, int* perm, int* heap, hipStream_t s) {
   const int cap = wave == 1 ? kVgWaveMax : wave == 2 ? vg_sort_max(256) : kSortPermBlockMax;
   if (n < 0 || n > cap || wave < 0 || wave > 3) return -1;
   if (n == 0) return 0;
-  k_sort_perm<<<1, wave == 2 ? 256 : 1024, sort_perm_lds_bytes(), s>>>(keys, n, wave == 1 ? 1 : wave, perm, heap);
+  if (wave == 2) k_sort_perm_sid<<<1, 256, sort_perm_lds_bytes(), s>>>(keys, n, perm, heap);
+  else k_sort_perm<<<1, 1024, sort_perm_lds_bytes(), s>>>(keys, n, wave, perm, heap);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

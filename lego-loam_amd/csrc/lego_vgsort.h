@@ -222,8 +222,392 @@ __device__ __forceinline__ VgSortLds<V> vg_sort_carve(uint32_t* key, V* val, uns
 // still heap-sorted exactly.  Off, the permutation itself is std::sort's
 // (lego_sort_permutation).
 constexpr int kVgMoveRows = 4;  // the moves' batch: rows of blockDim.x positions
+// The end of both block sorts: every position ranks itself within its leaf,
+// the sum-order heap pieces, the moves.  All threads of the block.
+template <typename V>
+__device__ void vg_block_finish(const VgSortLds<V>& S, int n, bool sumOrder) {
+  const int tid = threadIdx.x, T = blockDim.x;
+  // leaves: every position ranks itself within its leaf (its start the
+  // highest leaf-start bit at or below it, its end the next one; <= 16 keys,
+  // or a heap piece of up to T * kVgMoveRows with sumOrder)
+  for (int i = tid; i < n; i += T) {
+    const int wi = i >> 5, bi = i & 31;
+    const uint32_t hw = S.head[wi];
+    const uint32_t msk = bi == 31 ? ~0u : ((2u << bi) - 1);
+    uint32_t lo = hw & msk, hi = hw & ~msk;
+    int wl = wi, wh = wi;
+    while (!lo) lo = S.head[--wl];  // position 0 is always a leaf start
+    while (!hi && ((wh + 1) << 5) < n) hi = S.head[++wh];
+    const int ls = (wl << 5) + 31 - __builtin_clz(lo);
+    const int le = hi ? min(n, (wh << 5) + __builtin_ctz(hi)) : n;
+    const uint32_t k = S.key[i];
+    int lt = 0, eqb = 0, eq = 0;
+    for (int u0 = 0; u0 < le - ls; u0 += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int q = ls + u0 + u;
+        const uint32_t kq = S.key[min(q, n - 1)];
+        if (q < le) {
+          lt += kq < k ? 1 : 0;
+          eqb += (kq == k && q < i) ? 1 : 0;
+          eq += kq == k ? 1 : 0;
+        }
+      }
+    }
+    if (sumOrder && le - ls > kVgLeaf) {
+      // a key 3+ times, or the piece's smallest key twice when the pieces
+      // before it end with that key too (its sum then starts before the
+      // piece and the two addends no longer come first): exact heap sort.
+      // Every key before the piece is <= every key in it, so only the
+      // preceding leaf can hold it.
+      bool exact = eq >= 3;
+      if (!exact && eq == 2 && lt == 0 && eqb == 0 && ls > 0) {
+        int w = (ls - 1) >> 5;
+        uint32_t m = S.head[w] & bi_mask_le((ls - 1) & 31);
+        while (!m) m = S.head[--w];
+        const int pls = (w << 5) + 31 - __builtin_clz(m);
+        for (int q = pls; q < ls && !exact; ++q) exact = S.key[q] == k;
+      }
+      if (exact) S.pr[ls] = 1;
+    }
+    S.sid[i] = (uint16_t)(ls + lt + eqb);
+  }
+  __syncthreads();
+  if (sumOrder) {  // heap pieces holding a key 3+ times: std::__partial_sort after all
+    for (int i = tid; i < n; i += T) {
+      if (!((S.head[i >> 5] >> (i & 31)) & 1u)) continue;
+      int w = i >> 5;
+      uint32_t hi = S.head[w] & ~(bi_mask_le(i & 31));
+      while (!hi && ((w + 1) << 5) < n) hi = S.head[++w];
+      const int le = hi ? min(n, (w << 5) + __builtin_ctz(hi)) : n;
+      if (le - i <= kVgLeaf || !S.pr[i]) continue;
+      VgHeap<V>{S.key, S.val}.sort(i, le);
+      for (int q = i; q < le; ++q) S.sid[q] = (uint16_t)q;
+    }
+    __syncthreads();
+  }
+  // the moves, in batches of whole leaves (a batch ends at the highest leaf
+  // start within kVgMoveRows rows; every leaf fits in them): each batch's
+  // keys / vals / places to registers, then to their places
+  constexpr int MB = kVgMoveRows;
+  for (int b = 0; b < n;) {
+    int bn = b + T * MB;
+    if (bn >= n) {
+      bn = n;
+    } else {
+      int w = bn >> 5;
+      const int wb = b >> 5;
+      uint32_t m = S.head[w] & bi_mask_le(bn & 31);
+      if (w == wb) m &= ~bi_mask_le(b & 31);
+      while (!m) {
+        m = S.head[--w];
+        if (w == wb) m &= ~bi_mask_le(b & 31);
+      }
+      bn = (w << 5) + 31 - __builtin_clz(m);
+    }
+    uint32_t kk[MB], vd[MB];
+#pragma unroll
+    for (int j = 0; j < MB; ++j) {
+      const int i = b + j * T + tid;
+      const bool in = i < bn;
+      kk[j] = in ? S.key[i] : 0u;
+      vd[j] = in ? ((uint32_t)S.val[i] | ((uint32_t)S.sid[i] << 16)) : 0xffffffffu;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < MB; ++j)
+      if (vd[j] != 0xffffffffu) { S.key[vd[j] >> 16] = kk[j]; S.val[vd[j] >> 16] = (V)(vd[j] & 0xffffu); }
+    __syncthreads();
+    b = bn;
+  }
+  VG_STAMP(8);
+}
+
 template <typename V>
 __device__ void vg_block_sort(const VgSortLds<V>& S, int n, int depth = -1, int* heapStat = nullptr,
+                              bool sumOrder = false) {
+  constexpr int RM = kVgRowsMax;
+  const int tid = threadIdx.x, T = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = T >> 6;
+  const int cap = vg_list_cap(n);
+  const int D = depth >= 0 ? depth : (n > 1 ? 2 * (31 - __builtin_clz((unsigned)n)) : 0);
+  const int P = (((n + nw - 1) / nw) + 63) & ~63;  // positions per wave
+  const int w0 = wave * P;
+  const unsigned long long below = (1ull << lane) - 1;
+  int* wt = S.ctl + 2;  // [nw][2] the waves' stop totals
+  if (n <= 1) {
+    __syncthreads();
+    return;
+  }
+  for (int w = tid; w < (n + 31) / 32 + 1; w += T) S.head[w] = (w == 0 && n <= kVgLeaf) ? 1u : 0u;
+  if (tid == 0) {
+    S.ctl[0] = n > kVgLeaf ? 1 : 0;
+    S.tab[0] = VgSeg{0, (uint16_t)n, 0, 0, 0u, (uint32_t)n};
+    if (n > kVgLeaf && D > 0) vg_median_to_first(S.key, S.val, 0, 1, n / 2, n - 1);
+  }
+  // Per row j of this wave's positions, in registers for the whole loop: the
+  // position's segment at this level (table index SD(j), 0xffff in a leaf;
+  // two rows per word) and its bounds se[j] = s | e << 16.  Positions never
+  // change threads.
+  uint32_t rowact = 0;  // rows of this wave holding positions of a segment (wave-uniform)
+  uint32_t sdp[RM / 2], se[RM];
+#define SD(j) ((sdp[(j) >> 1] >> (((j) & 1) * 16)) & 0xffffu)
+#define SD_SET(j, x) (sdp[(j) >> 1] = (sdp[(j) >> 1] & (0xffff0000u >> (((j) & 1) * 16))) | ((uint32_t)(x) << (((j) & 1) * 16)))
+#pragma unroll
+  for (int j = 0; j < RM; ++j) {
+    const bool a = n > kVgLeaf && (j << 6) < P && w0 + (j << 6) + lane < n;
+    if ((j & 1) == 0) sdp[j >> 1] = 0xffffffffu;
+    SD_SET(j, a ? 0u : 0xffffu);
+    se[j] = (uint32_t)n << 16;
+    if (n > kVgLeaf && w0 + (j << 6) < n && (j << 6) < P) rowact |= 1u << j;
+  }
+  __syncthreads();
+  constexpr int BR = 4;  // rows whose operands are gathered together (registers)
+  // Five barriers per level: the stop flags and the waves' totals | the
+  // counts at the segments' ends | ranks, pairing, partners, cut | the swaps
+  // and the children | the positions' new segments and the children's
+  // medians of three (std::__move_median_to_first, before the next level's
+  // flags; not when the next level's depth budget is spent).
+  for (int r = 0;; ++r) {
+    const int nseg = S.ctl[r & 1];
+    if (nseg == 0) break;
+    VgSeg* cur = S.tab + (r & 1) * cap;
+    VgSeg* nxt = S.tab + ((r + 1) & 1) * cap;
+    if (D - r == 0) {  // depth budget spent: std::__partial_sort of every piece
+      for (int j = tid; j < nseg; j += T) {
+        const int s = cur[j].s, e = cur[j].e;
+        if (sumOrder && e - s <= T * kVgMoveRows) {  // a leaf of > 16 keys; pr[s]: a key occurs 3+ times
+          atomicOr(&S.head[s >> 5], 1u << (s & 31));
+          S.pr[s] = 0;
+        } else {
+          VgHeap<V>{S.key, S.val}.sort(s, e);
+          for (int q = s; q < e; ++q) atomicOr(&S.head[q >> 5], 1u << (q & 31));
+        }
+        if (heapStat) atomicAdd(heapStat, 1);
+      }
+      __syncthreads();
+      break;
+    }
+    if (tid == 0) S.ctl[(r + 1) & 1] = 0;  // last read at level r - 1's top; counted into below
+    VG_STAMP(0);
+    // stop flags (a bit per row) and the wave's totals
+    uint32_t fl = 0, fr = 0;
+    int totLw = 0, totRw = 0;
+    for (int j0 = 0; j0 < RM; j0 += BR) {
+      if (!((rowact >> j0) & ((1u << BR) - 1))) continue;
+      uint32_t kp[BR], ki[BR];
+#pragma unroll
+      for (int u = 0; u < BR; ++u) {
+        const int j = j0 + u, i = w0 + (j << 6) + lane, s = (int)(se[j] & 0xffffu);
+        const bool in = SD(j) != 0xffffu && i > s;
+        kp[u] = in ? S.key[s] : 0u;
+        ki[u] = in ? S.key[i] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < BR; ++u) {
+        const int j = j0 + u, i = w0 + (j << 6) + lane, s = (int)(se[j] & 0xffffu);
+        const bool in = SD(j) != 0xffffu && i > s;
+        const bool lf = in && !(ki[u] < kp[u]), rf = in && !(kp[u] < ki[u]);
+        fl |= (lf ? 1u : 0u) << j;
+        fr |= (rf ? 1u : 0u) << j;
+        totLw += (int)__popcll(__ballot(lf));
+        totRw += (int)__popcll(__ballot(rf));
+      }
+    }
+    if (lane == 0) { wt[2 * wave] = totLw; wt[2 * wave + 1] = totRw; }
+    __syncthreads();
+    VG_STAMP(1);
+    int baseL = 0, baseR = 0;
+    for (int w = 0; w < wave; ++w) { baseL += wt[2 * w]; baseR += wt[2 * w + 1]; }
+    {  // the block-wide inclusive counts at every segment's start and last position
+      int aL = baseL, aR = baseR;
+#pragma unroll
+      for (int j = 0; j < RM; ++j) {
+        const bool lf = (fl >> j) & 1u, rf = (fr >> j) & 1u;
+        const unsigned long long ml = __ballot(lf), mr = __ballot(rf);
+        const int SL = aL + (int)__popcll(ml & below) + (lf ? 1 : 0);
+        const int SR = aR + (int)__popcll(mr & below) + (rf ? 1 : 0);
+        aL += (int)__popcll(ml);
+        aR += (int)__popcll(mr);
+        const uint32_t id = SD(j);
+        if (id == 0xffffu) continue;
+        const int i = w0 + (j << 6) + lane, s = (int)(se[j] & 0xffffu), e = (int)(se[j] >> 16);
+        if (i == s) *(uint16_t*)&cur[id].ck = (uint16_t)SL;
+        if (i == e - 1) { cur[id].A = (uint16_t)SL; cur[id].B = (uint16_t)SR; }
+      }
+    }
+    __syncthreads();
+    VG_STAMP(2);
+    {  // ranks, the pairing rule, partners, the cut's candidates, the swap count
+      int aL = baseL, aR = baseR;
+      for (int j0 = 0; j0 < RM; j0 += BR) {
+        int SL[BR], SR[BR];
+#pragma unroll
+        for (int u = 0; u < BR; ++u) {
+          const int j = j0 + u;
+          const bool lf = (fl >> j) & 1u, rf = (fr >> j) & 1u;
+          const unsigned long long ml = __ballot(lf), mr = __ballot(rf);
+          SL[u] = aL + (int)__popcll(ml & below) + (lf ? 1 : 0);
+          SR[u] = aR + (int)__popcll(mr & below) + (rf ? 1 : 0);
+          aL += (int)__popcll(ml);
+          aR += (int)__popcll(mr);
+        }
+        if (!((rowact >> j0) & ((1u << BR) - 1))) continue;
+        uint2 g[BR];  // A | B << 16, ck
+#pragma unroll
+        for (int u = 0; u < BR; ++u) {
+          const int j = j0 + u;
+          g[u] = make_uint2(0u, 0u);
+          if (((fl | fr) >> j) & 1u) {
+            const uint32_t* c = (const uint32_t*)&cur[SD(j)];
+            g[u] = make_uint2(c[1], c[2]);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < BR; ++u) {
+          const int j = j0 + u;
+          if (!((rowact >> j) & 1u)) continue;
+          const bool lf = (fl >> j) & 1u, rf = (fr >> j) & 1u;
+          const int i = w0 + (j << 6) + lane;
+          const int s = (int)(se[j] & 0xffffu), e = (int)(se[j] >> 16);
+          const int A = (int)(g[u].x & 0xffffu), B = (int)(g[u].x >> 16), Cc = (int)(g[u].y & 0xffffu);
+          const int totL = A - Cc, Lab = A - SL[u], Rab = B - SR[u];  // left stops, stops after i
+          // right stop of rank Rab + 1 (from the right): swapped iff at least
+          // that many left stops precede it; left stop of rank totL - Lab:
+          // swapped iff at least that many right stops follow it
+          const bool rsw = rf && totL - Lab - (lf ? 1 : 0) >= Rab + 1;
+          const bool lsw = lf && Rab >= totL - Lab;
+          if (rsw) S.pr[s + Rab] = (uint16_t)i;
+          if (lsw) S.pr[s + ((e - s + 1) >> 1) + (totL - Lab) - 1] = (uint16_t)i;
+          const bool cand = (lf && !lsw) || rsw;
+          // one atomic per segment run of the row: its lowest candidate, its
+          // highest swapped left stop (ranks grow with the position)
+          const unsigned long long mc = __ballot(cand), mw = __ballot(lsw);
+          const int rb = i - lane;
+          if (cand && !(mc & below & ~((1ull << max(0, s - rb)) - 1))) atomicMin(&cur[SD(j)].cut, (uint32_t)i);
+          if (lsw) {
+            const int hiL = min(64, e - rb);
+            const unsigned long long abv = (hiL >= 64 ? ~0ull : ((1ull << hiL) - 1)) & ~below & ~(1ull << lane);
+            if (!(mw & abv)) atomicMax(&cur[SD(j)].ck, (uint32_t)Cc | ((uint32_t)(totL - Lab) << 16));
+          }
+        }
+      }
+    }
+    __syncthreads();
+    VG_STAMP(3);
+    for (int j0 = 0; j0 < RM; j0 += BR) {  // pair q of a segment, at the position s + q (its
+      // partners read beside the swap count, used when q is below it)
+      if (!((rowact >> j0) & ((1u << BR) - 1))) continue;
+      int pa[BR], pb[BR];
+      uint32_t K[BR];
+#pragma unroll
+      for (int u = 0; u < BR; ++u) {
+        const int j = j0 + u;
+        K[u] = 0u;
+        pa[u] = pb[u] = 0;
+        const uint32_t id = SD(j);
+        if (id == 0xffffu) continue;
+        const int x = w0 + (j << 6) + lane, s = (int)(se[j] & 0xffffu), e = (int)(se[j] >> 16), q = x - s;
+        const int half = (e - s + 1) >> 1;
+        if (q < half) {
+          K[u] = cur[id].ck >> 16;
+          pa[u] = (int)S.pr[s + half + q];
+          pb[u] = (int)S.pr[x];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < BR; ++u) {
+        const int j = j0 + u, x = w0 + (j << 6) + lane, s = (int)(se[j] & 0xffffu);
+        if ((uint32_t)(x - s) < K[u]) vg_swap(S.key, S.val, pa[u], pb[u]);
+      }
+    }
+    // the children: > 16 keys to the next level's table (its cut = its end
+    // until the partition), else a leaf start; cur[j].A | B (free since the
+    // ranks) takes the children's first slot | which are segments.  nseg <=
+    // vg_list_cap(n) < T: a thread per segment.
+    uint32_t cse0 = 0u, cse1 = 0u;  // this thread's segment's children (s | e << 16), 0: none / a leaf
+    if (tid < nseg) {
+      const uint4 g = *(const uint4*)&cur[tid];
+      const int s = (int)(g.x & 0xffffu), e = (int)(g.x >> 16), cut = (int)g.w;
+      const int aL = cut - s > kVgLeaf ? 1 : 0, aR = e - cut > kVgLeaf ? 1 : 0;
+      const int base = (aL + aR) ? atomicAdd(&S.ctl[(r + 1) & 1], aL + aR) : 0;
+      if (aL) {
+        nxt[base] = VgSeg{(uint16_t)s, (uint16_t)cut, 0, 0, 0u, (uint32_t)cut};
+        cse0 = (uint32_t)s | ((uint32_t)cut << 16);
+      } else {
+        atomicOr(&S.head[s >> 5], 1u << (s & 31));
+      }
+      if (aR) {
+        nxt[base + aL] = VgSeg{(uint16_t)cut, (uint16_t)e, 0, 0, 0u, (uint32_t)e};
+        cse1 = (uint32_t)cut | ((uint32_t)e << 16);
+      } else {
+        atomicOr(&S.head[cut >> 5], 1u << (cut & 31));
+      }
+      ((uint32_t*)&cur[tid])[1] = (uint32_t)base | ((uint32_t)(aL | (aR << 1)) << 16);
+    }
+    __syncthreads();
+    VG_STAMP(4);
+    {  // the positions' new segments
+      uint32_t act = 0;
+      for (int j0 = 0; j0 < RM; j0 += BR) {
+        if (!((rowact >> j0) & ((1u << BR) - 1))) continue;
+        uint2 g[BR];  // children's slot | which, cut
+#pragma unroll
+        for (int u = 0; u < BR; ++u) {
+          const int j = j0 + u;
+          g[u] = make_uint2(0u, 0u);
+          const uint32_t id = SD(j);
+          if (id != 0xffffu) {
+            const uint32_t* c = (const uint32_t*)&cur[id];
+            g[u] = make_uint2(c[1], c[3]);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < BR; ++u) {
+          const int j = j0 + u;
+          if (!((rowact >> j) & 1u)) continue;
+          const int i = w0 + (j << 6) + lane;
+          if (SD(j) != 0xffffu) {
+            const int ch = (int)(g[u].x >> 16), base = (int)(g[u].x & 0xffffu), cut = (int)g[u].y;
+            const uint32_t s = se[j] & 0xffffu, e = se[j] >> 16;
+            uint32_t nid = 0xffffu;
+            if (i < cut) {
+              if (ch & 1) { nid = (uint32_t)base; se[j] = s | ((uint32_t)cut << 16); }
+            } else if (ch & 2) {
+              nid = (uint32_t)(base + (ch & 1));
+              se[j] = (uint32_t)cut | (e << 16);
+            }
+            SD_SET(j, nid);
+          }
+          if (__ballot(SD(j) != 0xffffu)) act |= 1u << j;
+        }
+      }
+      rowact = act;
+    }
+    if (D - (r + 1) != 0) {  // the children's medians (their keys are final since the swaps)
+      if (cse0) {
+        const int s = (int)(cse0 & 0xffffu), e = (int)(cse0 >> 16);
+        vg_median_to_first(S.key, S.val, s, s + 1, s + (e - s) / 2, e - 1);
+      }
+      if (cse1) {
+        const int s = (int)(cse1 & 0xffffu), e = (int)(cse1 >> 16);
+        vg_median_to_first(S.key, S.val, s, s + 1, s + (e - s) / 2, e - 1);
+      }
+    }
+    __syncthreads();
+    VG_STAMP(6);
+  }
+#undef SD
+#undef SD_SET
+  VG_STAMP(7);
+  vg_block_finish(S, n, sumOrder);
+}
+
+// The same sort with the positions' segment ids in LDS (S.sid) instead of
+// registers: seven barriers per level and more LDS round trips, twelve
+// fewer VGPRs.  k_lf_voxel keeps it: at four workgroups per CU its 128-VGPR
+// budget does not hold the register form without spills.
+template <typename V>
+__device__ void vg_block_sort_sid(const VgSortLds<V>& S, int n, int depth = -1, int* heapStat = nullptr,
                               bool sumOrder = false) {
   constexpr int RM = kVgRowsMax;
   const int tid = threadIdx.x, T = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = T >> 6;
@@ -478,100 +862,7 @@ __device__ void vg_block_sort(const VgSortLds<V>& S, int n, int depth = -1, int*
     VG_STAMP(6);
   }
   VG_STAMP(7);
-  // leaves: every position ranks itself within its leaf (its start the
-  // highest leaf-start bit at or below it, its end the next one; <= 16 keys,
-  // or a heap piece of up to T * kVgMoveRows with sumOrder)
-  for (int i = tid; i < n; i += T) {
-    const int wi = i >> 5, bi = i & 31;
-    const uint32_t hw = S.head[wi];
-    const uint32_t msk = bi == 31 ? ~0u : ((2u << bi) - 1);
-    uint32_t lo = hw & msk, hi = hw & ~msk;
-    int wl = wi, wh = wi;
-    while (!lo) lo = S.head[--wl];  // position 0 is always a leaf start
-    while (!hi && ((wh + 1) << 5) < n) hi = S.head[++wh];
-    const int ls = (wl << 5) + 31 - __builtin_clz(lo);
-    const int le = hi ? min(n, (wh << 5) + __builtin_ctz(hi)) : n;
-    const uint32_t k = S.key[i];
-    int lt = 0, eqb = 0, eq = 0;
-    for (int u0 = 0; u0 < le - ls; u0 += 8) {
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int q = ls + u0 + u;
-        const uint32_t kq = S.key[min(q, n - 1)];
-        if (q < le) {
-          lt += kq < k ? 1 : 0;
-          eqb += (kq == k && q < i) ? 1 : 0;
-          eq += kq == k ? 1 : 0;
-        }
-      }
-    }
-    if (sumOrder && le - ls > kVgLeaf) {
-      // a key 3+ times, or the piece's smallest key twice when the pieces
-      // before it end with that key too (its sum then starts before the
-      // piece and the two addends no longer come first): exact heap sort.
-      // Every key before the piece is <= every key in it, so only the
-      // preceding leaf can hold it.
-      bool exact = eq >= 3;
-      if (!exact && eq == 2 && lt == 0 && eqb == 0 && ls > 0) {
-        int w = (ls - 1) >> 5;
-        uint32_t m = S.head[w] & bi_mask_le((ls - 1) & 31);
-        while (!m) m = S.head[--w];
-        const int pls = (w << 5) + 31 - __builtin_clz(m);
-        for (int q = pls; q < ls && !exact; ++q) exact = S.key[q] == k;
-      }
-      if (exact) S.pr[ls] = 1;
-    }
-    S.sid[i] = (uint16_t)(ls + lt + eqb);
-  }
-  __syncthreads();
-  if (sumOrder) {  // heap pieces holding a key 3+ times: std::__partial_sort after all
-    for (int i = tid; i < n; i += T) {
-      if (!((S.head[i >> 5] >> (i & 31)) & 1u)) continue;
-      int w = i >> 5;
-      uint32_t hi = S.head[w] & ~(bi_mask_le(i & 31));
-      while (!hi && ((w + 1) << 5) < n) hi = S.head[++w];
-      const int le = hi ? min(n, (w << 5) + __builtin_ctz(hi)) : n;
-      if (le - i <= kVgLeaf || !S.pr[i]) continue;
-      VgHeap<V>{S.key, S.val}.sort(i, le);
-      for (int q = i; q < le; ++q) S.sid[q] = (uint16_t)q;
-    }
-    __syncthreads();
-  }
-  // the moves, in batches of whole leaves (a batch ends at the highest leaf
-  // start within kVgMoveRows rows; every leaf fits in them): each batch's
-  // keys / vals / places to registers, then to their places
-  constexpr int MB = kVgMoveRows;
-  for (int b = 0; b < n;) {
-    int bn = b + T * MB;
-    if (bn >= n) {
-      bn = n;
-    } else {
-      int w = bn >> 5;
-      const int wb = b >> 5;
-      uint32_t m = S.head[w] & bi_mask_le(bn & 31);
-      if (w == wb) m &= ~bi_mask_le(b & 31);
-      while (!m) {
-        m = S.head[--w];
-        if (w == wb) m &= ~bi_mask_le(b & 31);
-      }
-      bn = (w << 5) + 31 - __builtin_clz(m);
-    }
-    uint32_t kk[MB], vd[MB];
-#pragma unroll
-    for (int j = 0; j < MB; ++j) {
-      const int i = b + j * T + tid;
-      const bool in = i < bn;
-      kk[j] = in ? S.key[i] : 0u;
-      vd[j] = in ? ((uint32_t)S.val[i] | ((uint32_t)S.sid[i] << 16)) : 0xffffffffu;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < MB; ++j)
-      if (vd[j] != 0xffffffffu) { S.key[vd[j] >> 16] = kk[j]; S.val[vd[j] >> 16] = (V)(vd[j] & 0xffffu); }
-    __syncthreads();
-    b = bn;
-  }
-  VG_STAMP(8);
+  vg_block_finish(S, n, sumOrder);
 }
 
 }  // namespace lego

@@ -13,10 +13,16 @@ echo "$git_rev" > "$O/COMMIT"
 if [ -n "${MB:-}" ]; then  # microbenchmarks built in-tree (build/)
   for m in $MB; do timeout -k 10 120 "./build/$m" > "$O/$m.txt" 2>&1; cat "$O/$m.txt"; done
 fi
+if [ -n "${MBSEG:-}" ]; then  # the C5 local-sort segment replays (scripts/mb_seg.sh)
+  bash scripts/mb_seg.sh > "$O/mb_seg.txt" 2>&1; cat "$O/mb_seg.txt"
+fi
 if [ -n "${FIRST:-}" ]; then  # targeted tests first (fail fast)
   timeout -k 10 600 python -u -m pytest $FIRST -m gpu -x -v -s --timeout 240 --timeout-method thread \
     > "$O/first_tests.log" 2>&1
   tail -2 "$O/first_tests.log"
+fi
+if [ -n "${PROBE:-}" ]; then  # diagnostic python scripts (scripts/*.py)
+  for p in $PROBE; do timeout -k 10 300 python -u "scripts/$p.py" > "$O/$p.txt" 2>&1; cat "$O/$p.txt"; done
 fi
 if [ -z "${SKIP_TESTS:-}" ]; then
   timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -v -s --timeout 300 --timeout-method thread \

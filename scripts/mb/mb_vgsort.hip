@@ -138,6 +138,92 @@ __global__ void __launch_bounds__(256) k_vgsort_var(const uint32_t* keys, const 
   for (int t = threadIdx.x; t < n; t += blockDim.x) { out[b0 + t] = key[t]; outv[b0 + t] = val[t]; }
 }
 
+// The mapping VoxelGrid's local sorts (k_vg_local / k_vg_local_small shape):
+// one segment per workgroup of T threads, dynamic LDS for CAP keys, sumOrder,
+// the segment's depth budget as given.
+template <int CAP, int T>
+__global__ void __launch_bounds__(T) k_vgsort_seg(const uint32_t* keys, const int* off, uint32_t* out, uint16_t* outv,
+                                                  int depth, int* heap) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  uint32_t* key = (uint32_t*)lds_raw;
+  uint16_t* lv = (uint16_t*)(lds_raw + (size_t)CAP * 4);
+  unsigned char* sc = lds_raw + (size_t)CAP * 6;
+  const int b0 = off[blockIdx.x], n = off[blockIdx.x + 1] - b0;
+  for (int t = threadIdx.x; t < n; t += T) { key[t] = keys[b0 + t]; lv[t] = (uint16_t)t; }
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x == 0) t_prev_ = clock64();
+  vg_block_sort(vg_sort_carve(key, lv, sc, n, T), n, depth, heap, true);
+  for (int t = threadIdx.x; t < n; t += T) { out[b0 + t] = key[t]; outv[b0 + t] = lv[t]; }
+}
+
+// ./mb_vgsort seg <file> <depth> [one=0]: the segments of a file written by
+// the C5 dump replay (deepest first), all at once (one per workgroup) and,
+// with one = 1, the deepest alone; block 0's phase stamps.
+static int run_seg(const char* path, int depth, int one) {
+  FILE* f = fopen(path, "rb");
+  if (!f) return 1;
+  int R;
+  if (fread(&R, 4, 1, f) != 1) return 1;
+  std::vector<int> off{0};
+  std::vector<uint32_t> keys;
+  int nmax = 0;
+  for (int r = 0; r < R; ++r) {
+    int n;
+    if (fread(&n, 4, 1, f) != 1) return 1;
+    const size_t b = keys.size();
+    keys.resize(b + n);
+    if (fread(keys.data() + b, 4, n, f) != (size_t)n) return 1;
+    off.push_back((int)keys.size());
+    nmax = std::max(nmax, n);
+  }
+  fclose(f);
+  uint32_t *dk, *dout;
+  uint16_t* dv;
+  int *doff, *dheap;
+  hipMalloc(&dk, keys.size() * 4); hipMalloc(&dout, keys.size() * 4); hipMalloc(&dv, keys.size() * 2);
+  hipMalloc(&doff, off.size() * 4); hipMalloc(&dheap, 4);
+  hipMemcpy(dk, keys.data(), keys.size() * 4, hipMemcpyHostToDevice);
+  hipMemcpy(doff, off.data(), off.size() * 4, hipMemcpyHostToDevice);
+  const bool big = nmax > 1024;
+  const size_t lds = big ? 8192 * 6 + vg_sort_scratch_bytes(8192, 1024) : 1024 * 6 + vg_sort_scratch_bytes(1024, 256);
+  const int G = one ? 1 : R;
+  auto launch = [&] {
+    if (big) k_vgsort_seg<8192, 1024><<<G, 1024, lds>>>(dk, doff, dout, dv, depth, dheap);
+    else k_vgsort_seg<1024, 256><<<G, 256, lds>>>(dk, doff, dout, dv, depth, dheap);
+  };
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  launch();
+  hipDeviceSynchronize();
+  hipEventRecord(e0);
+  for (int r = 0; r < 5; ++r) launch();
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms;
+  hipEventElapsedTime(&ms, e0, e1);
+  unsigned long long z[16] = {}, zl = 0;
+  hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), z, sizeof(z));
+  hipMemcpyToSymbol(HIP_SYMBOL(g_levels), &zl, sizeof(zl));
+  launch();
+  hipDeviceSynchronize();
+  hipMemcpyFromSymbol(z, HIP_SYMBOL(g_stamp), sizeof(z));
+  hipMemcpyFromSymbol(&zl, HIP_SYMBOL(g_levels), sizeof(zl));
+  std::vector<uint32_t> hk(keys.size());
+  hipMemcpy(hk.data(), dout, hk.size() * 4, hipMemcpyDeviceToHost);
+  int bad = 0;
+  for (int r = 0; r < G; ++r)
+    for (int i = off[r] + 1; i < off[r + 1]; ++i)
+      if (hk[i] < hk[i - 1]) { ++bad; break; }
+  printf("%s: %d segments (n max %d, %d threads), %d launched: %.1f us/launch, %d unsorted\n", path, R, nmax,
+         big ? 1024 : 256, G, 1000 * ms / 5, bad);
+  printf("  segment 0 (n=%d) phases (kcycles): median %.1f flags %.1f counts %.1f ranks %.1f swaps %.1f children %.1f "
+         "sid %.1f | loop-exit %.1f leaves %.1f  levels %llu\n",
+         off[1], z[0] / 1e3, z[1] / 1e3, z[2] / 1e3, z[3] / 1e3, z[4] / 1e3, z[5] / 1e3, z[6] / 1e3, z[7] / 1e3,
+         z[8] / 1e3, zl);
+  return 0;
+}
+
 static int run_file(const char* path, int reps) {
   FILE* f = fopen(path, "rb");
   if (!f) return 1;
@@ -253,6 +339,7 @@ static int run_wave(int n, int G) {
 
 int main(int argc, char** argv) {
   if (argc > 2 && std::string(argv[1]) == "file") return run_file(argv[2], argc > 3 ? atoi(argv[3]) : 3);
+  if (argc > 3 && std::string(argv[1]) == "seg") return run_seg(argv[2], atoi(argv[3]), argc > 4 ? atoi(argv[4]) : 0);
   if (argc > 3 && std::string(argv[1]) == "wave") return run_wave(atoi(argv[2]), atoi(argv[3]));
   const int n = argc > 1 ? atoi(argv[1]) : 1800;
   const int G = argc > 2 ? atoi(argv[2]) : 1536;
