@@ -1343,8 +1343,8 @@ int lego_voxel_grid(lego_ctx* x, const lego_point_xyzi* in, int32_t n, float lea
   }
   HIPCHK(hipMemcpy(out, x->vgOut, sizeof(float4) * nOut, hipMemcpyDeviceToHost));
   *n_out = nOut;
-  // ctl: C_M 0, C_NLOC 4, C_NONFIN 5, C_NOUT 6, C_SLOW 7, C_HEAP 8 (lego_vg.hip)
-  const int st[8] = {ctl[0], ctl[6], vg_rounds_for(n), ctl[4], ctl[7], ctl[8], ctl[5], (int)(ms * 1000.f)};
+  // ctl: C_M 0, C_NLOC 4, C_NONFIN 5, C_NOUT 6, C_SLOW 7, C_HEAP 8, C_NLOCB 9 (lego_vg.hip)
+  const int st[8] = {ctl[0], ctl[6], vg_rounds_for(n), ctl[4] + ctl[9], ctl[7], ctl[8], ctl[5], (int)(ms * 1000.f)};
   std::copy(st, st + 8, x->vgStats);
   return LEGO_OK;
 }

@@ -43,7 +43,7 @@
 namespace lego {
 
 constexpr unsigned kInvalidKey = 0xffffffffu;
-constexpr int kMoSolveThreads = 256;
+constexpr int kMoSolveThreads = 1024;  // the partials in two rounds of loads (1536 / 1024)
 
 static int grid_for(int n, int bs = 256) {
   int g = (n + bs - 1) / bs;
@@ -509,15 +509,18 @@ __global__ void __launch_bounds__(kMoSolveThreads) k_mo_solve(MoState* st, const
     if (lane == 0) red[wave][k] = w;
   }
   __syncthreads();
+  __shared__ double totS[kMoSums];
+  if (tid < kMoSums) {  // a thread per quantity over the waves, in wave order
+    double sum = 0;
+#pragma unroll
+    for (int w = 0; w < kMoSolveThreads / 64; ++w) sum += red[w][tid];
+    totS[tid] = sum;
+  }
+  __syncthreads();
   if (tid != 0) return;
   double tot[kMoSums];
 #pragma unroll
-  for (int k = 0; k < kMoSums; ++k) {
-    double sum = 0;
-#pragma unroll
-    for (int w = 0; w < kMoSolveThreads / 64; ++w) sum += red[w][k];
-    tot[k] = sum;
-  }
+  for (int k = 0; k < kMoSums; ++k) tot[k] = totS[k];
   mo_solve_tail(st, tot, iterCount, ws, wsi);
 }
 

@@ -48,7 +48,17 @@ constexpr int kVgRoundsMax = 16;
 constexpr int kVgPlanThreads = 1024;
 
 // VgScratch::ctl words
-enum { C_M = 0, C_D = 1, C_NB = 2, C_NT = 3, C_NLOC = 4, C_NONFIN = 5, C_NOUT = 6, C_SLOW = 7, C_HEAP = 8 };
+enum { C_M = 0, C_D = 1, C_NB = 2, C_NT = 3, C_NLOC = 4, C_NONFIN = 5, C_NOUT = 6, C_SLOW = 7, C_HEAP = 8, C_NLOCB = 9 };
+
+// The local list: segments of <= kVgSplit keys from the front of loc
+// (k_vg_local_small's, C_NLOC), larger ones from its back (k_vg_local's,
+// C_NLOCB), so that k_vg_local's workgroups take one large segment each
+// instead of striding over the small ones (a workgroup that drew two large
+// segments set the kernel's time).
+__device__ __forceinline__ void vg_push_local(const VgScratch& v, int s, int e, int depth) {
+  if (e - s > kVgSplit) v.loc[v.capLoc - 1 - atomicAdd(&v.ctl[C_NLOCB], 1)] = make_int4(s, e, depth, 0);
+  else v.loc[atomicAdd(&v.ctl[C_NLOC], 1)] = make_int4(s, e, depth, 0);
+}
 
 // ---------------------------------------------------------------- block scans
 // Exclusive scan of one int per thread over the block (<= 1024 threads);
@@ -260,7 +270,7 @@ __device__ void vg_plan_big(const VgScratch& v, const int2* big, int nb, int* tm
 
 // Removes non-finite points (stable), then the first level: the whole array as
 // one big segment (partitioned by the rounds) or one local segment.
-__global__ void __launch_bounds__(kVgPlanThreads) k_vg_plan0(int n, const int* nDev, VgScratch v, int rounds) {
+__global__ void __launch_bounds__(kVgPlanThreads) k_vg_plan0(int n, const int* nDev, VgScratch v, int rounds, int split) {
   __shared__ int tmp[20];
   const int nn = nDev ? min(n, *nDev) : n;
   int m = nn;
@@ -283,16 +293,16 @@ __global__ void __launch_bounds__(kVgPlanThreads) k_vg_plan0(int n, const int* n
     v.ctl[C_M] = m;
     v.ctl[C_D] = m > 1 ? 2 * lg2i(m) : 0;
     v.ctl[C_NLOC] = 0;
+    v.ctl[C_NLOCB] = 0;
   }
   __syncthreads();
   if (*v.overflow || m <= 1) {
     if (threadIdx.x == 0) { v.ctl[C_NB] = 0; v.ctl[C_NT] = 0; v.tileOff[0] = 0; }
     return;
   }
-  if (m <= kVgSplit || rounds == 0) {  // one workgroup (above kVgLocal: its global-memory partition)
+  if (m <= split || rounds == 0) {  // one workgroup (above kVgLocal: its global-memory partition)
     if (threadIdx.x == 0) {
-      v.loc[0] = make_int4(0, m, 2 * lg2i(m), 0);
-      v.ctl[C_NLOC] = 1;
+      vg_push_local(v, 0, m, 2 * lg2i(m));
       v.ctl[C_NB] = 0; v.ctl[C_NT] = 0; v.tileOff[0] = 0;
     }
     return;
@@ -303,10 +313,10 @@ __global__ void __launch_bounds__(kVgPlanThreads) k_vg_plan0(int n, const int* n
 }
 
 // After round r - 1 (big list in big[(r-1)&1]): the cuts make the children;
-// children larger than kVgSplit form the next round's big list (unless
-// flush), the others (and, when flushing, all) go to the local list with
-// their depth budget 2 lg m - r.
-__global__ void __launch_bounds__(kVgPlanThreads) k_vg_plan(VgScratch v, int r, int flush) {
+// children larger than split form the next round's big list (unless flush),
+// the others (and, when flushing, all) go to the local list with their depth
+// budget 2 lg m - r.
+__global__ void __launch_bounds__(kVgPlanThreads) k_vg_plan(VgScratch v, int r, int flush, int split) {
   __shared__ int tmp[20];
   const int nbp = v.ctl[C_NB];
   if (nbp == 0) return;  // uniform: nothing was partitioned
@@ -324,11 +334,10 @@ __global__ void __launch_bounds__(kVgPlanThreads) k_vg_plan(VgScratch v, int r, 
       ch[1] = make_int2(cut, e);
       for (int q = 0; q < 2; ++q) {
         const int sz = ch[q].y - ch[q].x;
-        if (!flush && sz > kVgSplit) {
+        if (!flush && sz > split) {
           ++nbig;
         } else if (sz > 1) {
-          const int at = atomicAdd(&v.ctl[C_NLOC], 1);
-          v.loc[at] = make_int4(ch[q].x, ch[q].y, depth, 0);
+          vg_push_local(v, ch[q].x, ch[q].y, depth);
         }
       }
     }
@@ -336,7 +345,7 @@ __global__ void __launch_bounds__(kVgPlanThreads) k_vg_plan(VgScratch v, int r, 
     int at = carry + block_excl_scan(nbig, tmp, &t);
     if (b < nbp)
       for (int q = 0; q < 2; ++q)
-        if (!flush && ch[q].y - ch[q].x > kVgSplit) next[at++] = ch[q];
+        if (!flush && ch[q].y - ch[q].x > split) next[at++] = ch[q];
     carry += t;
   }
   __syncthreads();  // the cut / kcnt slots are reused below
@@ -542,7 +551,7 @@ __global__ void __launch_bounds__(kVgSplitThreads) k_vg_local_small(VgScratch v)
   const int nloc = v.ctl[C_NLOC];
   for (int t = blockIdx.x; t < nloc; t += gridDim.x) {
     const int4 g = v.loc[t];
-    if (g.y - g.x <= kVgSplit) vg_local_sort(v, key, lv, sc, g.x, g.y - g.x, g.z);
+    vg_local_sort(v, key, lv, sc, g.x, g.y - g.x, g.z);
   }
 }
 
@@ -558,10 +567,9 @@ __global__ void __launch_bounds__(kVgLocalThreads) k_vg_local(VgScratch v) {
   uint32_t* key = (uint32_t*)lds_raw;
   uint16_t* lv = (uint16_t*)(lds_raw + (size_t)kVgLocal * 4);
   unsigned char* sc = lds_raw + (size_t)kVgLocal * 6;
-  const int nloc = v.ctl[C_NLOC];
-  for (int t = blockIdx.x; t < nloc; t += gridDim.x) {
-    const int4 g = v.loc[t];
-    if (g.y - g.x <= kVgSplit) continue;  // k_vg_local_small's
+  const int nlocb = v.ctl[C_NLOCB];
+  for (int t = blockIdx.x; t < nlocb; t += gridDim.x) {
+    const int4 g = v.loc[v.capLoc - 1 - t];
     // one call site of the LDS sort (two inlined copies spilled registers);
     // every thread has read sp's last value before it is set again
     __syncthreads();
@@ -646,14 +654,25 @@ __global__ void __launch_bounds__(kHeadTile) k_vg_emit(const float4* in, int n, 
   out[r] = make_float4(c0 / cnt, c1 / cnt, c2 / cnt, c3 / cnt);
 }
 
+// The partition rounds split a cloud's segments down to vg_split_for(n) keys.
+// Small clouds (the scan's, <= kVgSmallCloud) stop at kVgLocal: their few
+// rounds are launch-bound (four launches each for a few tiles), while a
+// level of the LDS sort costs a fraction of a round; the map's clouds stop at
+// kVgSplit, so that their thousand leftovers sort in many small workgroups.
+constexpr int kVgSmallCloud = 65536;
+int vg_split_for(int n) { return n <= kVgSmallCloud ? kVgLocal : kVgSplit; }
 int vg_rounds_for(int n) {
   static const int forced = std::getenv("LEGO_VG_ROUNDS") ? std::atoi(std::getenv("LEGO_VG_ROUNDS")) : -1;
   if (forced >= 0) return std::min(forced, kVgRoundsMax);
-  if (n <= kVgSplit) return 0;
+  const int split = vg_split_for(n);
+  if (n <= split) return 0;
   int r = 1;
-  while (((long long)kVgSplit << r) < n) ++r;
-  // one more round above 256 k keys: the C5 map's leftovers then fit one
-  // workgroup's LDS (kVgLocal) instead of its global-memory partition
+  while (((long long)split << r) < n) ++r;
+  // margins for unbalanced partitions: two rounds for a small cloud (C5's
+  // outlier cloud needs four where two halve it), one, plus one above 256 k
+  // keys, for a map cloud (the C5 map's leftovers then fit one workgroup's
+  // LDS instead of its global-memory partition)
+  if (split == kVgLocal) return std::min(r + 2, kVgRoundsMax);
   return std::min(r + 1 + (n > (1 << 18) ? 1 : 0), kVgRoundsMax);
 }
 
@@ -669,19 +688,22 @@ int voxel_grid_device(const float4* in, int n, const int* nDev, float leaf, floa
   k_vg_init<<<1, 64, 0, s>>>(v);
   k_vg_minmax<<<std::min(grid_for(n), 512), 256, 0, s>>>(in, n, nDev, v);
   k_vg_keys<<<grid_for(n), 256, 0, s>>>(in, n, nDev, leaf, v);
-  const int R = vg_rounds_for(n);
-  k_vg_plan0<<<1, kVgPlanThreads, 0, s>>>(n, nDev, v, R);
-  const int gt = tiles_for(n, kVgTile) + v.capBig;  // >= the tiles of any round
+  const int R = vg_rounds_for(n), split = vg_split_for(n);
+  k_vg_plan0<<<1, kVgPlanThreads, 0, s>>>(n, nDev, v, R, split);
+  // grids sized by this cloud's bound n, not the scratch's capacity: a round's
+  // tiles <= n / kVgTile + its segments (each > split keys)
+  const int gt = tiles_for(n, kVgTile) + std::min(v.capBig, n / split + 2);
   for (int r = 0; r < R; ++r) {
     k_vg_count<<<gt, kVgTileThreads, 0, s>>>(v, r);
     k_vg_decide<<<gt, kVgTileThreads, 0, s>>>(v, r);
     k_vg_swap<<<gt, kVgTileThreads, 0, s>>>(v, r);
-    k_vg_plan<<<1, kVgPlanThreads, 0, s>>>(v, r + 1, r + 1 == R ? 1 : 0);
+    k_vg_plan<<<1, kVgPlanThreads, 0, s>>>(v, r + 1, r + 1 == R ? 1 : 0, split);
   }
-  const int gl = n <= kVgSplit ? 1 : std::min(v.capLoc, 2048);
+  const int gl = n <= kVgSplit ? 1 : std::min({v.capLoc, 2048, std::max(64, n / 256)});  // grid-stride over the list
   k_vg_local_small<<<gl, kVgSplitThreads, vg_local_lds_bytes<kVgSplit, kVgSplitThreads>(), s>>>(v);
   if (n > kVgSplit)
-    k_vg_local<<<std::min(v.capLoc, 256), kVgLocalThreads, vg_local_lds_bytes<kVgLocal, kVgLocalThreads>(), s>>>(v);
+    k_vg_local<<<std::min({v.capLoc, 256, n / kVgSplit + 1}), kVgLocalThreads, vg_local_lds_bytes<kVgLocal, kVgLocalThreads>(),
+                 s>>>(v);
   const int ht = tiles_for(n, kHeadTile);
   k_vg_head_tiles<<<ht, kHeadTile, 0, s>>>(v);
   k_scan_top<<<1, 1024, 0, s>>>(v.scanTiles, ht, nullptr, v.ctl + C_NOUT);
