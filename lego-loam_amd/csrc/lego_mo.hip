@@ -799,14 +799,14 @@ static int map_filter(MoDev& m, const float4* corner, int nC, const float4* surf
 // parts around the map's launches so that every chain starts early (the
 // host's launches are serial): first the outlier cloud on fork[0] and the
 // surf cloud on fork[1] (the map's corner cloud follows it there); after the
-// map's launches the concatenation and its VoxelGrid on fork[0] (after the
-// outlier cloud and, through EV_SURF, the surf cloud).  The corner cloud runs
-// on s after the map's surf cloud; join_scan makes s wait for the forks.
-// The three chains come out about equal on C5 (outlier 0.7 + surf+outlier
-// 0.75 ms; surf 0.5 + map corner 0.85 ms; map surf 1.25 + scan corner 0.2 ms);
-// with the map's corner cloud after the outlier cloud fork[0] was the longest
-// (1.55 ms).  (Enqueueing the concatenation before the map's launches delayed
-// the map's surf cloud by the host's ~0.3 ms: 2.6 vs 2.3 ms.)
+// map's launches the concatenation, its VoxelGrid and the corner cloud's on
+// fork[0] (after the outlier cloud and, through EV_SURF, the surf cloud);
+// join_scan makes s wait for the forks.  The three chains come out about
+// equal on C5 (r04o VoxelGrid times alone: outlier 0.42 + surf+outlier 0.36 +
+// corner 0.11 ms; surf 0.35 + map corner 0.62 ms; map surf 0.93 ms); with the
+// map's corner cloud after the outlier cloud fork[0] was the longest.
+// (Enqueueing the concatenation before the map's launches delayed the map's
+// surf cloud by the host's ~0.3 ms: 2.6 vs 2.3 ms in round 3.)
 // (Two forks: with the step's stream that is three hardware queues, as many
 // as a process gets besides the runtime's own; a third fork shared one.)
 static int scan_filter_begin(MoDev& m, const MoStepArgs& a) {
@@ -819,12 +819,17 @@ static int scan_filter_begin(MoDev& m, const MoStepArgs& a) {
   if (hipEventRecord(m.ev[EV_SURF], f1) != hipSuccess) return -1;
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
-static int scan_filter_end(MoDev& m, const MoStepArgs& a) {
+static int scan_filter_end(MoDev& m, const MoStepArgs& a, bool cornerOnF0) {
   const hipStream_t f0 = m.fork[0];
   if (hipStreamWaitEvent(f0, m.ev[EV_SURF], 0) != hipSuccess) return -1;
   k_mo_concat<<<grid_for(a.nSurf + a.nOutlier), 256, 0, f0>>>(m.surfDS, m.outlierDS, m.cnt, m.surfTotal);
   if (voxel_grid_device(m.surfTotal, a.nSurf + a.nOutlier, &m.cnt->surfTotal, 0.4f, m.surfTotalDS,
                         &m.cnt->surfTotalDS, m.vgScan2, f0))
+    return -1;
+  // the scan's corner cloud (:1069-1073) last on fork[0] when s filters a
+  // map this step (its surf cloud is then the longest chain)
+  if (cornerOnF0 &&
+      voxel_grid_device(m.cornerLast, a.nCorner, nullptr, 0.2f, m.cornerDS, &m.cnt->cornerDS, m.vgScan2, f0))
     return -1;
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -898,9 +903,11 @@ int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, h
     if (map_filter(m, m.cornerMap, m.nCornerMap, m.surfMap, m.nSurfMap, s, m.fork[1], false)) return fail(-1);
   }
   MO_HOSTPROF(1);
-  if (scan_filter_end(m, a)) return fail(-1);
-  // the scan's corner cloud on s, after the map's surf cloud (:1069-1073)
-  if (voxel_grid_device(m.cornerLast, a.nCorner, nullptr, 0.2f, m.cornerDS, &m.cnt->cornerDS, m.vg, s)) return fail(-1);
+  // an installed map filtered once leaves s idle: the corner cloud runs there
+  const bool mapOnS = !fixedMap || m.mapPerStep;
+  if (scan_filter_end(m, a, mapOnS)) return fail(-1);
+  if (!mapOnS && voxel_grid_device(m.cornerLast, a.nCorner, nullptr, 0.2f, m.cornerDS, &m.cnt->cornerDS, m.vg, s))
+    return fail(-1);
   if (join_scan(m, s)) return -1;
   MO_HOSTPROF(2);
   k_mo_guard<<<1, 64, 0, s>>>(m.st, m.cnt);

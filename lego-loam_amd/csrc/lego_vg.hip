@@ -104,6 +104,30 @@ __device__ __forceinline__ int block_min(int v, int* tmp) {
   return r;
 }
 
+// K sums (or, with MIN, minima) over the block at once: one barrier pair for
+// all of them.  tmp: >= 16 K ints of LDS.  Ends with the block in sync.
+template <int K, bool MIN = false>
+__device__ __forceinline__ void block_reduce_k(int (&v)[K], int* tmp) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    for (int o = 32; o > 0; o >>= 1) {
+      const int y = __shfl_xor(v[k], o, 64);
+      v[k] = MIN ? min(v[k], y) : v[k] + y;
+    }
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < K; ++k) tmp[k * 16 + wave] = v[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    int a = tmp[k * 16];
+    for (int w = 1; w < nw; ++w) a = MIN ? min(a, tmp[k * 16 + w]) : a + tmp[k * 16 + w];
+    v[k] = a;
+  }
+  __syncthreads();
+}
+
 // Per-tile sums of in[0, n) (kScanTile elements per block).
 __global__ void __launch_bounds__(kScanThreads) k_scan_tiles(const int* in, int n, int* tiles) {
   __shared__ int tmp[20];
@@ -354,7 +378,7 @@ __global__ void __launch_bounds__(kVgPlanThreads) k_vg_plan(VgScratch v, int r, 
 
 // left / right stops of one tile
 __global__ void __launch_bounds__(kVgTileThreads) k_vg_count(VgScratch v, int r) {
-  __shared__ int tmp[20];
+  __shared__ int tmp[32];
   const int nt = v.ctl[C_NT];
   if ((int)blockIdx.x >= nt) return;
   const int2* big = v.big + (r & 1) * v.capBig;
@@ -372,8 +396,9 @@ __global__ void __launch_bounds__(kVgTileThreads) k_vg_count(VgScratch v, int r)
       cr += !(p < k);
     }
   }
-  const int L = block_sum(cl, tmp), R = block_sum(cr, tmp);
-  if (threadIdx.x == 0) { v.tileL[blockIdx.x] = L; v.tileR[blockIdx.x] = R; }
+  int lr[2] = {cl, cr};
+  block_reduce_k<2>(lr, tmp);
+  if (threadIdx.x == 0) { v.tileL[blockIdx.x] = lr[0]; v.tileR[blockIdx.x] = lr[1]; }
 }
 
 // Ranks every stop of one tile by the stops after it (tiles to the right from
@@ -381,7 +406,7 @@ __global__ void __launch_bounds__(kVgTileThreads) k_vg_count(VgScratch v, int r)
 // stops into pr by rank and the swapped left stops into pl by their partner's
 // rank, and folds the tile's cut candidates and swap count into the segment.
 __global__ void __launch_bounds__(kVgTileThreads) k_vg_decide(VgScratch v, int r) {
-  __shared__ int tmp[20];
+  __shared__ int tmp[48];
   __shared__ int rowL[kVgTilePer][4], rowR[kVgTilePer][4];
   const int nt = v.ctl[C_NT];
   if ((int)blockIdx.x >= nt) return;
@@ -391,19 +416,24 @@ __global__ void __launch_bounds__(kVgTileThreads) k_vg_decide(VgScratch v, int r
   const int t0 = (int)blockIdx.x - kt, t1 = t0 + (e - s - 1 + kVgTile - 1) / kVgTile;
   const int base = s + 1 + kt * kVgTile;
   const unsigned p = v.keys[s];
-  int a = 0, bL = 0, bR = 0;
+  unsigned kv[kVgTilePer];
+#pragma unroll
+  for (int j = 0; j < kVgTilePer; ++j) {  // the tile's keys in flight with the counts below
+    const int i = base + j * kVgTileThreads + threadIdx.x;
+    kv[j] = i < e ? v.keys[i] : 0u;
+  }
+  int abr[3] = {0, 0, 0};  // the segment's left stops; the left / right stops of the tiles after this one
   for (int q = t0 + threadIdx.x; q < t1; q += blockDim.x) {
     const int l = v.tileL[q];
-    a += l;
-    if (q > (int)blockIdx.x) { bL += l; bR += v.tileR[q]; }
+    abr[0] += l;
+    if (q > (int)blockIdx.x) { abr[1] += l; abr[2] += v.tileR[q]; }
   }
-  const int totL = block_sum(a, tmp), LabT = block_sum(bL, tmp), RabT = block_sum(bR, tmp);
+  block_reduce_k<3>(abr, tmp);
+  const int totL = abr[0], LabT = abr[1], RabT = abr[2];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  unsigned kv[kVgTilePer];
 #pragma unroll
   for (int j = 0; j < kVgTilePer; ++j) {
     const int i = base + j * kVgTileThreads + threadIdx.x;
-    kv[j] = i < e ? v.keys[i] : 0u;
     const bool in = i < e;
     const unsigned long long ml = __ballot(in && !(kv[j] < p)), mr = __ballot(in && !(p < kv[j]));
     if (lane == 0) { rowL[j][wave] = (int)__popcll(ml); rowR[j][wave] = (int)__popcll(mr); }
@@ -440,11 +470,12 @@ __global__ void __launch_bounds__(kVgTileThreads) k_vg_decide(VgScratch v, int r
     if ((kv[j] & 1u) && i < cmin) cmin = i;
     nsw += (kv[j] >> 1) & 1u;
   }
-  cmin = block_min(cmin, tmp);
-  nsw = block_sum(nsw, tmp);
+  int mn[1] = {cmin}, sw[1] = {nsw};
+  block_reduce_k<1, true>(mn, tmp);
+  block_reduce_k<1>(sw, tmp + 16);
   if (threadIdx.x == 0) {
-    if (cmin != INT_MAX) atomicMin(&v.cut[sg], cmin);
-    if (nsw) atomicAdd(&v.kcnt[sg], nsw);
+    if (mn[0] != INT_MAX) atomicMin(&v.cut[sg], mn[0]);
+    if (sw[0]) atomicAdd(&v.kcnt[sg], sw[0]);
   }
 }
 
@@ -457,14 +488,23 @@ __global__ void __launch_bounds__(kVgTileThreads) k_vg_swap(VgScratch v, int r) 
   const int s = big[sg].x;
   const int K = v.kcnt[sg];
   const int q0 = (ts >> 16) * kVgTile;
-#pragma unroll 4
+  // every pair's partners, then every key / value, then the stores (the
+  // swaps touch disjoint positions): two dependent load rounds per thread
+  int a[kVgTilePer], b[kVgTilePer];
+#pragma unroll
   for (int j = 0; j < kVgTilePer; ++j) {
     const int q = q0 + j * kVgTileThreads + threadIdx.x;
-    if (q < K) {
-      const int i = v.pl[s + q], k = v.pr[s + q];
-      vg_swap(v.keys, v.vals, i, k);
-    }
+    a[j] = q < K ? v.pl[s + q] : -1;
+    b[j] = q < K ? v.pr[s + q] : -1;
   }
+  unsigned ka[kVgTilePer], kb[kVgTilePer];
+  int va[kVgTilePer], vb[kVgTilePer];
+#pragma unroll
+  for (int j = 0; j < kVgTilePer; ++j)
+    if (a[j] >= 0) { ka[j] = v.keys[a[j]]; va[j] = v.vals[a[j]]; kb[j] = v.keys[b[j]]; vb[j] = v.vals[b[j]]; }
+#pragma unroll
+  for (int j = 0; j < kVgTilePer; ++j)
+    if (a[j] >= 0) { v.keys[a[j]] = kb[j]; v.vals[a[j]] = vb[j]; v.keys[b[j]] = ka[j]; v.vals[b[j]] = va[j]; }
 }
 
 // One workgroup partitions [s, e) in global memory (a segment still larger
