@@ -120,6 +120,12 @@ struct lego_ctx {
   std::vector<uint8_t> h_handoffHead;
   std::vector<lego_point_xyzi> h_info, h_gcloud, h_pure;
   std::vector<lego_point_xyzi> h_cornerLast, h_surfLast, h_outlLast;
+  // the device work generation: every call that launches into the batch
+  // slots bumps it; fetch_fa records the slot and generation its published
+  // clouds (h_cornerLast / h_surfLast / h_outlLast) came from, so that
+  // lego_mo_process can take them from the device when handed them back
+  uint64_t devGen = 0, faGen = ~0ull;
+  int faK = -1, faCnt[3] = {0, 0, 0};
   std::vector<int32_t> h_sri, h_eri, h_label, h_bad;
   std::vector<uint8_t> h_gflag;
   std::vector<uint32_t> h_col;
@@ -253,6 +259,7 @@ static int make_devcfg(const lego_sensor_cfg* c, DevCfg* d) {
 // stream — so batches already submitted finish with the old state and the
 // next one starts fresh (from a constant pinned image).
 static int ctx_reset(lego_ctx* x) {
+  ++x->devGen;
   HIPCHK(hipMemcpyAsync(x->ob.st, x->h_resetSt, sizeof(OdomState) * x->nStreams, hipMemcpyHostToDevice,
                         x->ostream));
   // the hand-off tags restart with the state: no granule of the old stream may match
@@ -766,6 +773,7 @@ static int run_ip(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offse
 // x->ostream after them, so they overlap the previous batch's odometry.
 static int submit_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offsets, int B, int on_device,
                         const lego_imu_msg* imu, int n_imu, const int32_t* imu_before) {
+  ++x->devGen;
   if (x->inflight >= 2) {
     set_err("two batches in flight: lego_odom_batch_wait before submitting another");
     return LEGO_E_STATE;
@@ -974,12 +982,16 @@ static int fetch_fa(lego_ctx* x, int k, lego_fa_out* o) {
     o->surf_last = x->h_surfLast.data(); o->n_surf_last = cnt[3];
     o->outlier_last = x->h_outlLast.data(); o->n_outlier_last = nout;
   }
+  x->faGen = x->devGen;
+  x->faK = k;
+  x->faCnt[0] = cnt[1]; x->faCnt[1] = cnt[3]; x->faCnt[2] = nout;
   return LEGO_OK;
 }
 
 int lego_ip_process(lego_ctx* x, const lego_point_xyzir* pts, int32_t n, double stamp,
                     uint32_t flags, lego_ip_out* out) {
   if (!x || !pts || !out || n <= 0) return LEGO_E_ARG;
+  ++x->devGen;
   if (n > x->maxPoints) return LEGO_E_CAPACITY;
   for (int i = 0; i < n; ++i)  // dense check (imageProjection.cpp:174)
     if (!std::isfinite(pts[i].x) || !std::isfinite(pts[i].y) || !std::isfinite(pts[i].z))
@@ -1034,6 +1046,7 @@ int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
     return LEGO_E_ARG;
   }
   HIPCHK(hipSetDevice(x->device));
+  ++x->devGen;
   const bool resident = x->lastIpDevice && in->segmented_cloud == x->h_seg.data() &&
                         in->n_segmented == x->lastIp.n_segmented;
   if (!resident) {
@@ -1622,14 +1635,27 @@ int lego_mo_process(lego_ctx* x, const lego_fa_out* in, lego_mo_out* out) {
   }
   HIPCHK(hipSetDevice(x->device));
   hipStream_t s = x->stream;
-  if (in->n_corner_last)
-    HIPCHK(hipMemcpyAsync(m.cornerLast, in->corner_last, sizeof(float4) * in->n_corner_last, hipMemcpyHostToDevice, s));
-  if (in->n_surf_last)
-    HIPCHK(hipMemcpyAsync(m.surfLast, in->surf_last, sizeof(float4) * in->n_surf_last, hipMemcpyHostToDevice, s));
-  if (in->n_outlier_last)
-    HIPCHK(hipMemcpyAsync(m.outlierLast, in->outlier_last, sizeof(float4) * in->n_outlier_last,
-                          hipMemcpyHostToDevice, s));
   MoStepArgs a;
+  // the clouds of this context's own last fa output (the node path's hand-off
+  // within one process): read where fetch_fa copied them from, on the device
+  const bool resident = x->faK >= 0 && x->faGen == x->devGen && in->corner_last == x->h_cornerLast.data() &&
+                        in->surf_last == x->h_surfLast.data() && in->outlier_last == x->h_outlLast.data() &&
+                        in->n_corner_last == x->faCnt[0] && in->n_surf_last == x->faCnt[1] &&
+                        in->n_outlier_last == x->faCnt[2];
+  if (resident) {
+    a.corner = x->ob.cornerEnd + (size_t)x->faK * x->ob.capLS;
+    a.surf = x->ob.surfEnd + (size_t)x->faK * P;
+    a.outlierRaw = x->bb.outl + (size_t)x->faK * P;  // adjustOutlierCloud's axis swap on the device
+  } else {
+    if (in->n_corner_last)
+      HIPCHK(hipMemcpyAsync(m.cornerLast, in->corner_last, sizeof(float4) * in->n_corner_last, hipMemcpyHostToDevice,
+                            s));
+    if (in->n_surf_last)
+      HIPCHK(hipMemcpyAsync(m.surfLast, in->surf_last, sizeof(float4) * in->n_surf_last, hipMemcpyHostToDevice, s));
+    if (in->n_outlier_last)
+      HIPCHK(hipMemcpyAsync(m.outlierLast, in->outlier_last, sizeof(float4) * in->n_outlier_last,
+                            hipMemcpyHostToDevice, s));
+  }
   for (int i = 0; i < 4; ++i) a.quat[i] = in->odom_quat[i];
   for (int i = 0; i < 3; ++i) a.pos[i] = in->odom_pos[i];
   a.nCorner = in->n_corner_last;

@@ -150,6 +150,12 @@ struct MoStepArgs {
   // kf.planPose (uploaded by the host), nCM / nSM the map clouds' sizes;
   // nPlan = -1: the radius-search map
   int nPlan = -1, nCM = 0, nSM = 0;
+  // the scan's clouds on the device when they need no upload (lego_mo_process:
+  // the context's own fa output); null: MoDev's cornerLast / surfLast /
+  // outlierLast.  outlierRaw is the outlier cloud before adjustOutlierCloud.
+  const float4* corner = nullptr;
+  const float4* surf = nullptr;
+  const float4* outlierRaw = nullptr;
 };
 
 // Loop closure (lego_loop.hip): the detection result and gather plan, the

@@ -272,6 +272,14 @@ __global__ void k_mo_guard(MoState* st, const MoCounts* cnt) {
   if (threadIdx.x == 0) st->optimized = (cnt->cornerMapDS > 10 && cnt->surfMapDS > 100) ? 1 : 0;
 }
 
+// adjustOutlierCloud (featureAssociation.cpp:1746-1757): (x, y, z) -> (y, z, x)
+__global__ void k_mo_outlier_in(const float4* raw, int n, float4* out) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const float4 p = raw[i];
+    out[i] = make_float4(p.y, p.z, p.x, p.w);
+  }
+}
+
 // surfTotalLast = surfLastDS + outlierLastDS (:1084-1086)
 __global__ void k_mo_concat(const float4* a, const float4* b, MoCounts* cnt, float4* out) {
   const int na = cnt->surfDS, nb = cnt->outlierDS;
@@ -813,9 +821,12 @@ static int scan_filter_begin(MoDev& m, const MoStepArgs& a) {
   const hipStream_t f0 = m.fork[0], f1 = m.fork[1];
   if (hipStreamWaitEvent(f0, m.ev[EV_SCAN_FORK], 0) != hipSuccess) return -1;
   if (hipStreamWaitEvent(f1, m.ev[EV_SCAN_FORK], 0) != hipSuccess) return -1;
+  if (a.outlierRaw && a.nOutlier > 0)
+    k_mo_outlier_in<<<grid_for(a.nOutlier), 256, 0, f0>>>(a.outlierRaw, a.nOutlier, m.outlierLast);
   if (voxel_grid_device(m.outlierLast, a.nOutlier, nullptr, 0.4f, m.outlierDS, &m.cnt->outlierDS, m.vgScan2, f0))
     return -1;
-  if (voxel_grid_device(m.surfLast, a.nSurf, nullptr, 0.4f, m.surfDS, &m.cnt->surfDS, m.vgScan1, f1)) return -1;
+  if (voxel_grid_device(a.surf ? a.surf : m.surfLast, a.nSurf, nullptr, 0.4f, m.surfDS, &m.cnt->surfDS, m.vgScan1, f1))
+    return -1;
   if (hipEventRecord(m.ev[EV_SURF], f1) != hipSuccess) return -1;
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -829,7 +840,8 @@ static int scan_filter_end(MoDev& m, const MoStepArgs& a, bool cornerOnF0) {
   // the scan's corner cloud (:1069-1073) last on fork[0] when s filters a
   // map this step (its surf cloud is then the longest chain)
   if (cornerOnF0 &&
-      voxel_grid_device(m.cornerLast, a.nCorner, nullptr, 0.2f, m.cornerDS, &m.cnt->cornerDS, m.vgScan2, f0))
+      voxel_grid_device(a.corner ? a.corner : m.cornerLast, a.nCorner, nullptr, 0.2f, m.cornerDS, &m.cnt->cornerDS,
+                        m.vgScan2, f0))
     return -1;
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -906,7 +918,8 @@ int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, h
   // an installed map filtered once leaves s idle: the corner cloud runs there
   const bool mapOnS = !fixedMap || m.mapPerStep;
   if (scan_filter_end(m, a, mapOnS)) return fail(-1);
-  if (!mapOnS && voxel_grid_device(m.cornerLast, a.nCorner, nullptr, 0.2f, m.cornerDS, &m.cnt->cornerDS, m.vg, s))
+  if (!mapOnS && voxel_grid_device(a.corner ? a.corner : m.cornerLast, a.nCorner, nullptr, 0.2f, m.cornerDS,
+                                   &m.cnt->cornerDS, m.vg, s))
     return fail(-1);
   if (join_scan(m, s)) return -1;
   MO_HOSTPROF(2);
