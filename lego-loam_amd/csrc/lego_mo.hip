@@ -58,7 +58,10 @@ static int grid_for(int n, int bs = 256) {
 // rounds of a group-wide lexicographic minimum pick the overall five (the
 // result depends only on the (distance, index) order, not on the split).
 // Every lane of the group returns the same list; the count (<= 5) is returned.
-constexpr int kKnnLanes = 32;
+#ifndef MO_KNN_LANES
+#define MO_KNN_LANES 32
+#endif
+constexpr int kKnnLanes = MO_KNN_LANES;  // lanes per query (a power of two, <= 32)
 __device__ __forceinline__ bool knn_less(float da, int ia, float db, int ib) {
   return da < db || (da == db && ia < ib);
 }
@@ -121,8 +124,8 @@ __device__ __forceinline__ int knn5_group(const MoIndex& ix, float4 q, int* oi, 
   float ld[5];
   int li[5];
   int n = 0;
-  if (gl < 27) {
-    const int bx = cell1(q.x) + gl % 3 - 1, by = cell1(q.y) + (gl / 3) % 3 - 1, bz = cell1(q.z) + gl / 9 - 1;
+  for (int cl = gl; cl < 27; cl += kKnnLanes) {  // the 3x3x3 cells over the group's lanes
+    const int bx = cell1(q.x) + cl % 3 - 1, by = cell1(q.y) + (cl / 3) % 3 - 1, bz = cell1(q.z) + cl / 9 - 1;
     const unsigned b = mo_cell_hash(bx, by, bz) & (unsigned)(ix.T - 1);
     const int lo = ix.begin[b], hi = ix.end[b];
     for (int t = lo; t < hi; ++t) {
