@@ -213,6 +213,8 @@ struct lego_ctx {
     if (mo.fork[1]) (void)hipStreamDestroy(mo.fork[1]);
     for (auto e : mo.ev)
       if (e) (void)hipEventDestroy(e);
+    for (auto e : mo.prof)
+      if (e) (void)hipEventDestroy(e);
     if (hstream) (void)hipStreamSynchronize(hstream);
     if (hstream) (void)hipStreamDestroy(hstream);
     if (ostream) (void)hipStreamDestroy(ostream);
@@ -1695,6 +1697,7 @@ int lego_mo_process(lego_ctx* x, const lego_fa_out* in, lego_mo_out* out) {
   HIPCHK(hipMemcpyAsync(&hc, m.cnt, sizeof(hc), hipMemcpyDeviceToHost, s));
   if (!x->moFixed) HIPCHK(hipMemcpyAsync(meta, m.kf.meta, sizeof(meta), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  mo_evprof_print(m);
   if (meta[KF_OVF]) {  // saveKeyFramesAndFactor of this very step found the store full (k_kf_save)
     x->moStoreFull = true;
     set_err("scan-to-map: the keyframe store is full (%d keyframes / %d arena points): this step's keyframe "

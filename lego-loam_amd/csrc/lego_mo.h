@@ -136,6 +136,7 @@ struct MoDev {
   // Each chain has its own VoxelGrid scratch.
   hipStream_t fork[2];
   hipEvent_t ev[6];
+  hipEvent_t prof[6] = {};  // LEGO_MO_EVPROF (diagnostic): the step's chain ends, timed
   VgScratch vgMap2, vgScan1, vgScan2;
 };
 
@@ -188,6 +189,7 @@ int voxel_grid_device(const float4* in, int n, const int* nDev, float leaf, floa
 // partition rounds voxel_grid_device launches for a cloud of n points
 // (LEGO_VG_ROUNDS overrides: diagnostic)
 int vg_rounds_for(int n);
+void mo_evprof_print(MoDev& m);  // after the step's stream is synchronised
 // the VgScratch counters of the last voxel_grid_device on s (16 ints, synchronous)
 int vg_read_ctl(const VgScratch& v, int* ctl16, hipStream_t s);
 int mo_set_map_device(MoDev& m, int nCornerMap, int nSurfMap, hipStream_t s);

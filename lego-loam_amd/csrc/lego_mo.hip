@@ -894,8 +894,31 @@ static const bool g_hostprof = std::getenv("LEGO_MO_HOSTPROF") != nullptr;
                    std::chrono::duration<double, std::micro>(hp[3] - hp[2]).count());                   \
   }
 
+// LEGO_MO_EVPROF (diagnostic): timing events at the step's start and at the
+// end of each chain (s: the map's surf cloud; fork[1]: surf, map corner;
+// fork[0]: outlier, surf + outlier, corner), after the join and after the LM;
+// mo_evprof_print writes their offsets (us) to stderr.
+static const bool g_evprof = std::getenv("LEGO_MO_EVPROF") != nullptr;
+static void evprof(MoDev& m, int k, hipStream_t st) {
+  if (!g_evprof) return;
+  if (!m.prof[k] && hipEventCreate(&m.prof[k]) != hipSuccess) return;
+  (void)hipEventRecord(m.prof[k], st);
+}
+void mo_evprof_print(MoDev& m) {
+  if (!g_evprof || !m.prof[0]) return;
+  static const char* names[6] = {"start", "s_map_surf", "f1_surf_mapcorner", "f0_outlier_total_corner", "join", "lm"};
+  std::fprintf(stderr, "mo evprof us:");
+  for (int k = 1; k < 6; ++k) {
+    float ms = -1.f;
+    if (m.prof[k] && hipEventElapsedTime(&ms, m.prof[0], m.prof[k]) != hipSuccess) ms = -1.f;
+    std::fprintf(stderr, " %s %.0f", names[k], ms * 1000.f);
+  }
+  std::fprintf(stderr, "\n");
+}
+
 int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, hipStream_t s) {
   std::chrono::steady_clock::time_point hp[4];
+  evprof(m, 0, s);
   k_mo_associate<<<1, 64, 0, s>>>(m.st, a.quat[0], a.quat[1], a.quat[2], a.quat[3], a.pos[0], a.pos[1], a.pos[2]);
   if (hipGetLastError() != hipSuccess) return -1;
   MO_HOSTPROF(0);
@@ -917,6 +940,8 @@ int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, h
   } else if (m.mapPerStep) {  // the map VoxelGrids (:1058-1064) and kd-tree builds (:1333-1334) of every step
     if (map_filter(m, m.cornerMap, m.nCornerMap, m.surfMap, m.nSurfMap, s, m.fork[1], false)) return fail(-1);
   }
+  evprof(m, 1, s);
+  evprof(m, 2, m.fork[1]);
   MO_HOSTPROF(1);
   // an installed map filtered once leaves s idle: the corner cloud runs there
   const bool mapOnS = !fixedMap || m.mapPerStep;
@@ -924,7 +949,9 @@ int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, h
   if (!mapOnS && voxel_grid_device(a.corner ? a.corner : m.cornerLast, a.nCorner, nullptr, 0.2f, m.cornerDS,
                                    &m.cnt->cornerDS, m.vg, s))
     return fail(-1);
+  evprof(m, 3, m.fork[0]);
   if (join_scan(m, s)) return -1;
+  evprof(m, 4, s);
   MO_HOSTPROF(2);
   k_mo_guard<<<1, 64, 0, s>>>(m.st, m.cnt);
   // scan2MapOptimization :1329-1350 — the iterations exit on the device once converged
@@ -943,6 +970,7 @@ int mo_step_device(MoDev& m, const MoStepArgs& a, bool fixedMap, float radius, h
     k_mo_solve<<<1, kMoSolveThreads, 0, s>>>(m.st, m.part, nb, it);
   }
   k_mo_finish<<<1, 64, 0, s>>>(m.st, a.imuOn, a.imuRoll, a.imuPitch);
+  evprof(m, 5, s);
   MO_HOSTPROF(3);
   if (!fixedMap) {  // saveKeyFramesAndFactor :1353-1454
     k_kf_save<<<1, 64, 0, s>>>(m.kf, m.st, m.cnt, a.stamp);
