@@ -369,6 +369,13 @@ typedef struct lego_mo_opts {
 /* Sets the options; takes effect at the next lego_mo_process.  Switching
  * loop_closure_enable needs a context with no saved keyframe (LEGO_E_STATE). */
 int lego_mo_configure(lego_ctx* ctx, const lego_mo_opts* opts);
+/* mapOptimization::run's scan-to-map step on the published clouds of `in`
+ * (mapOptmization.cpp:1487-1522).  When `in` is this context's own last
+ * lego_fa_process / lego_batch_fetch output, unchanged (its corner / surf /
+ * outlier pointers and counts, no projection, extraction or batch call in
+ * between), the clouds are read where that call copied them from, on the
+ * device: no upload.  The host buffers are then not read, so a caller that
+ * edits them in place must pass a copy; any other clouds are uploaded. */
 int lego_mo_process(lego_ctx* ctx, const lego_fa_out* in, lego_mo_out* out);
 /* performLoopClosure over the keyframes the mapping calls have saved (needs
  * the keyframe-built map, i.e. no lego_mo_set_map); LEGO_E_ARG otherwise. */
