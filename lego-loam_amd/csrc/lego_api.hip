@@ -78,6 +78,10 @@ void lego_set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
+constexpr int kFetchHdr = 32;  // header words of the host staging block (fetch_ip / fetch_fa)
+constexpr size_t kMoResBytes = ((sizeof(MoState) + 15) & ~(size_t)15) + ((sizeof(MoCounts) + 15) & ~(size_t)15) +
+                               sizeof(int) * kKfMeta;
+
 struct lego_ctx {
   lego_sensor_cfg cfg;
   DevCfg dc;
@@ -109,8 +113,14 @@ struct lego_ctx {
   // last batch
   int lastB = 0;
   std::vector<double> stamps;
-  // host staging (library-owned outputs)
-  std::vector<lego_point_xyzi> h_seg, h_outl, h_full, h_sharp, h_lsharp, h_flat, h_lflat;
+  // host staging (library-owned outputs): regions of one pinned block
+  // (hostBlock) that k_fetch writes directly, one launch and one sync per
+  // fetched scan (pageable staging cost a synchronous copy per array)
+  unsigned char* hostBlock = nullptr;
+  int32_t* h_hdr = nullptr;  // k_fetch's header words (counts, flags, orientation, transforms)
+  void* h_moRes = nullptr;   // lego_mo_process's MoState / MoCounts / keyframe words (kMoResBytes)
+  lego_point_xyzi *h_seg = nullptr, *h_outl = nullptr, *h_full = nullptr, *h_sharp = nullptr, *h_lsharp = nullptr,
+                  *h_flat = nullptr, *h_lflat = nullptr;
   GatedBufs gb{};  // LEGO_IP_GATED outputs (first use)
   uint8_t* d_handoff = nullptr;  // lego_handoff_pack's packet (grown on demand)
   hipStream_t hstream = nullptr; // the hand-off packing (first use)
@@ -118,19 +128,19 @@ struct lego_ctx {
   hipEvent_t handoffFence = nullptr;  // a lego_comm send of d_handoff in flight (lego_handoff_fence)
   bool handoffFenced = false;
   std::vector<uint8_t> h_handoffHead;
-  std::vector<lego_point_xyzi> h_info, h_gcloud, h_pure;
-  std::vector<lego_point_xyzi> h_cornerLast, h_surfLast, h_outlLast;
+  lego_point_xyzi *h_info = nullptr, *h_gcloud = nullptr, *h_pure = nullptr;
+  lego_point_xyzi *h_cornerLast = nullptr, *h_surfLast = nullptr, *h_outlLast = nullptr;
   // the device work generation: every call that launches into the batch
   // slots bumps it; fetch_fa records the slot and generation its published
   // clouds (h_cornerLast / h_surfLast / h_outlLast) came from, so that
   // lego_mo_process can take them from the device when handed them back
   uint64_t devGen = 0, faGen = ~0ull;
   int faK = -1, faCnt[3] = {0, 0, 0};
-  std::vector<int32_t> h_sri, h_eri, h_label, h_bad;
-  std::vector<uint8_t> h_gflag;
-  std::vector<uint32_t> h_col;
-  std::vector<float> h_range, h_rimg;
-  std::vector<int8_t> h_gimg;
+  int32_t *h_sri = nullptr, *h_eri = nullptr, *h_label = nullptr, *h_bad = nullptr;
+  uint8_t* h_gflag = nullptr;
+  uint32_t* h_col = nullptr;
+  float *h_range = nullptr, *h_rimg = nullptr;
+  int8_t* h_gimg = nullptr;
   lego_ip_out lastIp{};
   bool lastIpDevice = false;  // lastIp describes batch slot 0 on device
   bool lastBatch = false;     // lastB / lastBase describe a waited batch (lego_handoff_pack)
@@ -204,6 +214,7 @@ struct lego_ctx {
     if (h_offp) (void)hipHostFree(h_offp);
     if (h_resetSt) (void)hipHostFree(h_resetSt);
     if (h_resetCarry) (void)hipHostFree(h_resetCarry);
+    if (hostBlock) (void)hipHostFree(hostBlock);
     for (void* p : allocs) (void)hipFree(p);
     if (oJoin) (void)hipEventDestroy(oJoin);
     for (int i = 0; i < 2; ++i) {
@@ -559,13 +570,30 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
 #undef A
   bb.pts = x->d_pts;
   bb.off = x->d_off;
-  x->h_seg.resize(P); x->h_outl.resize(P); x->h_full.resize(P);
-  x->h_sharp.resize(N * kSharpPerRing); x->h_lsharp.resize(N * kLessSharpPerRing);
-  x->h_flat.resize(N * kFlatPerRing); x->h_lflat.resize(P);
-  x->h_cornerLast.resize(N * kLessSharpPerRing); x->h_surfLast.resize(P); x->h_outlLast.resize(P);
-  x->h_sri.resize(N); x->h_eri.resize(N); x->h_label.resize(P);
-  x->h_gflag.resize(P); x->h_col.resize(P); x->h_range.resize(P); x->h_rimg.resize(P);
-  x->h_gimg.resize(P);
+  {  // the pinned host staging block and its regions (256-byte aligned)
+    size_t at = 0;
+    std::vector<std::pair<void**, size_t>> reg;
+    auto R = [&](auto** ptr, size_t bytes) { reg.push_back({(void**)ptr, at}); at += (bytes + 255) & ~(size_t)255; };
+    const size_t P16 = sizeof(lego_point_xyzi) * P;
+    R(&x->h_hdr, sizeof(int32_t) * kFetchHdr);
+    R(&x->h_moRes, kMoResBytes);
+    R(&x->h_seg, P16); R(&x->h_outl, P16); R(&x->h_full, P16); R(&x->h_lflat, P16);
+    R(&x->h_surfLast, P16); R(&x->h_outlLast, P16); R(&x->h_info, P16); R(&x->h_gcloud, P16); R(&x->h_pure, P16);
+    R(&x->h_sharp, sizeof(lego_point_xyzi) * N * kSharpPerRing);
+    R(&x->h_lsharp, sizeof(lego_point_xyzi) * N * kLessSharpPerRing);
+    R(&x->h_cornerLast, sizeof(lego_point_xyzi) * N * kLessSharpPerRing);
+    R(&x->h_flat, sizeof(lego_point_xyzi) * N * kFlatPerRing);
+    R(&x->h_sri, sizeof(int32_t) * N); R(&x->h_eri, sizeof(int32_t) * N);
+    R(&x->h_label, sizeof(int32_t) * P); R(&x->h_col, sizeof(uint32_t) * P);
+    R(&x->h_range, sizeof(float) * P); R(&x->h_rimg, sizeof(float) * P);
+    R(&x->h_gflag, P); R(&x->h_gimg, P);
+    R(&x->h_bad, sizeof(int32_t) * (size_t)x->maxBatch);
+    if (hipHostMalloc((void**)&x->hostBlock, at, hipHostMallocDefault) != hipSuccess) {
+      set_err("hipHostMalloc failed for the host staging block (%zu bytes)", at);
+      return fail(LEGO_E_DEVICE);
+    }
+    for (auto& r : reg) *r.first = x->hostBlock + r.second;
+  }
   int st = ctx_reset(x);
   if (st != LEGO_OK) return fail(st);
   *out = x;
@@ -677,8 +705,10 @@ static OdomBufs ob_slice(const OdomBufs& a, const DevCfg& c, int c0, int s0, int
 
 // Validates a batch and points bb (a slot view) at its input points: the
 // caller's device arrays, or a copy of host arrays in the staging buffer.
+// node: the caller synchronises before returning (run_ip), so the offsets may
+// go through the pinned h_offp
 static int stage_inputs(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offsets, int B,
-                        int on_device, BatchBufs& bb) {
+                        int on_device, BatchBufs& bb, bool node = false) {
   HIPCHK(hipSetDevice(x->device));
   // Per-scan sizes are validated on the host in both modes: an empty scan is
   // undefined upstream (findStartEndAngle reads points[0] and points[size-1],
@@ -715,8 +745,12 @@ static int stage_inputs(lego_ctx* x, const lego_point_xyzir* pts, const int64_t*
     for (int k = 0; k <= B; ++k) off[k] -= base;
     HIPCHK(hipMemcpyAsync(x->d_pts, pts + base, sizeof(lego_point_xyzir) * total,
                           hipMemcpyHostToDevice, x->stream));
-    HIPCHK(hipMemcpyAsync(x->d_off, off.data(), sizeof(int64_t) * (B + 1), hipMemcpyHostToDevice,
-                          x->stream));
+    if (node) {  // pinned: an asynchronous copy (a pageable source is a synchronous staged one)
+      for (int k = 0; k <= B; ++k) x->h_offp[k] = off[k];
+      HIPCHK(hipMemcpyAsync(x->d_off, x->h_offp, sizeof(int64_t) * (B + 1), hipMemcpyHostToDevice, x->stream));
+    } else {
+      HIPCHK(hipMemcpyAsync(x->d_off, off.data(), sizeof(int64_t) * (B + 1), hipMemcpyHostToDevice, x->stream));
+    }
     bb.pts = x->d_pts;
     bb.off = x->d_off;
   }
@@ -724,16 +758,20 @@ static int stage_inputs(lego_ctx* x, const lego_point_xyzir* pts, const int64_t*
   return LEGO_OK;
 }
 
-// Image projection only (lego_ip_process*): slot 0, synchronous.
+static int fetch_ip(lego_ctx* x, int k, bool images, lego_ip_out* o, bool gated = false, int badN = 0);
+
+// Image projection only (lego_ip_process*): slot 0, synchronous; scan 0's
+// outputs are fetched into *out with the batch's not-dense flags (one sync).
 static int run_ip(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offsets, int B, int on_device,
-                  int want_labels, bool gated = false) {
+                  bool images, lego_ip_out* out, bool gated = false) {
+  const int want_labels = images ? 1 : 0;
   if (x->inflight) {
     set_err("node-shaped call while batches are in flight (lego_odom_batch_wait first)");
     return LEGO_E_STATE;
   }
   BatchBufs bb = x->bb;
   x->lastBatch = false;
-  int st = stage_inputs(x, pts, offsets, B, on_device, bb);
+  int st = stage_inputs(x, pts, offsets, B, on_device, bb, true);
   if (st != LEGO_OK) return st;
   HIPCHK(hipMemsetAsync(bb.bad, 0, sizeof(int) * B, x->stream));
   if (gated && !x->gb.n) {
@@ -742,7 +780,6 @@ static int run_ip(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offse
   if (x->alloc(&(ptr), (size_t)(n)) != hipSuccess) { set_err("hipMalloc failed for %s", #ptr); return LEGO_E_DEVICE; }
     MA(x->gb.info, P); MA(x->gb.ground, P); MA(x->gb.pure, P); MA(x->gb.n, 2);
 #undef MA
-    x->h_info.resize(P); x->h_gcloud.resize(P); x->h_pure.resize(P);
   }
   x->tm.begin();
   launch_ip(bb, x->dc, B, want_labels || gated ? 1 : 0, x->stream, &x->tm);
@@ -752,15 +789,14 @@ static int run_ip(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offse
   }
   x->tm.end(x->stream);
   HIPCHK(hipGetLastError());
-  x->h_bad.resize(B);
-  HIPCHK(hipMemcpyAsync(x->h_bad.data(), bb.bad, sizeof(int) * B, hipMemcpyDeviceToHost, x->stream));
-  HIPCHK(hipStreamSynchronize(x->stream));
+  x->lastB = B;
+  x->lastBase = 0;
+  st = fetch_ip(x, 0, images, out, gated, B);
+  if (st != LEGO_OK) return st;
   x->tnames.clear();
   x->tms.clear();
   std::vector<int> cnt;
   x->tm.collect(x->tnames, x->tms, cnt);
-  x->lastB = B;
-  x->lastBase = 0;
   for (int k = 0; k < B; ++k)
     if (x->h_bad[k]) {
       x->lastB = 0;
@@ -878,91 +914,153 @@ static int wait_batch(lego_ctx* x, lego_pose_rec* recs, int cap, int* nOut) {
   return LEGO_OK;
 }
 
+// ---------------------------------------------------------------- fetch
+// One scan's host outputs in one launch: k_fetch copies every array of the
+// list straight into the pinned staging block (the counts read on the device,
+// so no round trip sizes the copies), then the caller synchronises once.
+struct FetchItem {
+  const void* src;
+  void* dst;
+  const int* cnt;  // element count on the device (nullptr: n)
+  int n, elem, cap;  // elements, bytes per element, capacity of dst in elements
+};
+constexpr int kFetchItems = 24;
+struct FetchList {
+  FetchItem it[kFetchItems];
+};
+__global__ void __launch_bounds__(256) k_fetch(FetchList L) {
+  const FetchItem f = L.it[blockIdx.y];
+  int n = f.cnt ? *f.cnt : f.n;
+  n = n < 0 ? 0 : (n > f.cap ? f.cap : n);
+  const size_t bytes = (size_t)n * (size_t)f.elem;
+  const unsigned char* src = (const unsigned char*)f.src;
+  unsigned char* dst = (unsigned char*)f.dst;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x, T = (size_t)gridDim.x * blockDim.x;
+  const uintptr_t al = (uintptr_t)src | (uintptr_t)dst;
+  size_t done = 0;
+  if ((al & 15) == 0) {
+    const size_t v = bytes / 16;
+    for (size_t i = t; i < v; i += T) ((uint4*)dst)[i] = ((const uint4*)src)[i];
+    done = v * 16;
+  } else if ((al & 3) == 0) {
+    const size_t v = bytes / 4;
+    for (size_t i = t; i < v; i += T) ((uint32_t*)dst)[i] = ((const uint32_t*)src)[i];
+    done = v * 4;
+  }
+  for (size_t i = done + t; i < bytes; i += T) dst[i] = src[i];
+}
+struct FetchBuilder {
+  FetchList L{};
+  int n = 0;
+  void add(const void* src, void* dst, const int* cnt, size_t num, int elem, size_t cap) {
+    L.it[n++] = FetchItem{src, dst, cnt, (int)num, elem, (int)cap};
+  }
+  hipError_t run(hipStream_t s) {
+    k_fetch<<<dim3(8, n), 256, 0, s>>>(L);
+    const hipError_t e = hipGetLastError();
+    return e != hipSuccess ? e : hipStreamSynchronize(s);
+  }
+};
+// header words of h_hdr
+enum { FH_NS = 0, FH_NOUT = 1, FH_ORIENT = 2, FH_NG = 5, FH_CNT = 8, FH_VALID = 12, FH_PUB = 13, FH_FNOUT = 14,
+       FH_SUM = 16, FH_CUR = 22, FH_XERR = 28 };
+
 // copy scan k's image-projection outputs of the last batch into host staging
-static int fetch_ip(lego_ctx* x, int k, bool images, lego_ip_out* o, bool gated = false) {
+// (badN: also the first badN not-dense flags into h_bad)
+static int fetch_ip(lego_ctx* x, int k, bool images, lego_ip_out* o, bool gated, int badN) {
   const DevCfg& c = x->dc;
   const size_t P = c.P, N = c.N;
-  int ns = 0, nout = 0;
-  float orient[3];
-  hipStream_t s = x->stream;
-  HIPCHK(hipMemcpyAsync(&ns, x->bb.ns + k, sizeof(int), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(&nout, x->bb.nout + k, sizeof(int), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(orient, x->bb.orient + 3 * k, sizeof(orient), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(x->h_sri.data(), x->bb.sri + k * N, sizeof(int) * N, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(x->h_eri.data(), x->bb.eri + k * N, sizeof(int) * N, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  HIPCHK(hipMemcpyAsync(x->h_seg.data(), x->bb.seg + k * P, sizeof(float4) * ns, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(x->h_gflag.data(), x->bb.gflag + k * P, ns, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(x->h_col.data(), x->bb.col + k * P, sizeof(uint32_t) * ns, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(x->h_range.data(), x->bb.srange + k * P, sizeof(float) * ns, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(x->h_outl.data(), x->bb.outl + k * P, sizeof(float4) * nout, hipMemcpyDeviceToHost, s));
-  int ng[2] = {0, 0};
+  const BatchBufs& bb = x->bb;
+  int32_t* hd = x->h_hdr;
+  FetchBuilder F;
+  F.add(bb.ns + k, hd + FH_NS, nullptr, 1, 4, 1);
+  F.add(bb.nout + k, hd + FH_NOUT, nullptr, 1, 4, 1);
+  F.add(bb.orient + 3 * k, hd + FH_ORIENT, nullptr, 3, 4, 3);
+  F.add(bb.sri + k * N, x->h_sri, nullptr, N, 4, N);
+  F.add(bb.eri + k * N, x->h_eri, nullptr, N, 4, N);
+  F.add(bb.seg + k * P, x->h_seg, bb.ns + k, 0, 16, P);
+  F.add(bb.gflag + k * P, x->h_gflag, bb.ns + k, 0, 1, P);
+  F.add(bb.col + k * P, x->h_col, bb.ns + k, 0, 4, P);
+  F.add(bb.srange + k * P, x->h_range, bb.ns + k, 0, 4, P);
+  F.add(bb.outl + k * P, x->h_outl, bb.nout + k, 0, 16, P);
   if (gated) {  // scan 0 of a node-shaped call
-    HIPCHK(hipMemcpyAsync(ng, x->gb.n, sizeof(ng), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(x->h_info.data(), x->gb.info, sizeof(float4) * P, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    HIPCHK(hipMemcpyAsync(x->h_gcloud.data(), x->gb.ground, sizeof(float4) * ng[0], hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(x->h_pure.data(), x->gb.pure, sizeof(float4) * ng[1], hipMemcpyDeviceToHost, s));
+    F.add(x->gb.n, hd + FH_NG, nullptr, 2, 4, 2);
+    F.add(x->gb.info, x->h_info, nullptr, P, 16, P);
+    F.add(x->gb.ground, x->h_gcloud, x->gb.n, 0, 16, P);
+    F.add(x->gb.pure, x->h_pure, x->gb.n + 1, 0, 16, P);
   }
   if (images) {
-    HIPCHK(hipMemcpyAsync(x->h_full.data(), x->bb.full + k * P, sizeof(float4) * P, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(x->h_rimg.data(), x->bb.range + k * P, sizeof(float) * P, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(x->h_gimg.data(), x->bb.ground + k * P, P, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(x->h_label.data(), x->bb.label + k * P, sizeof(int) * P, hipMemcpyDeviceToHost, s));
+    F.add(bb.full + k * P, x->h_full, nullptr, P, 16, P);
+    F.add(bb.range + k * P, x->h_rimg, nullptr, P, 4, P);
+    F.add(bb.ground + k * P, x->h_gimg, nullptr, P, 1, P);
+    F.add(bb.label + k * P, x->h_label, nullptr, P, 4, P);
   }
-  HIPCHK(hipStreamSynchronize(s));
+  if (badN > 0) F.add(bb.bad, x->h_bad, nullptr, badN, 4, x->maxBatch);
+  HIPCHK(F.run(x->stream));
+  const int ns = hd[FH_NS], nout = hd[FH_NOUT];
+  float orient[3];
+  std::memcpy(orient, hd + FH_ORIENT, sizeof(orient));
   std::memset(o, 0, sizeof(*o));
   const int kr = k - x->lastBase;  // index within the batch
   o->info.stamp = (kr < (int)x->stamps.size()) ? x->stamps[kr] : 0.0;
-  o->info.start_ring_index = x->h_sri.data();
-  o->info.end_ring_index = x->h_eri.data();
+  o->info.start_ring_index = x->h_sri;
+  o->info.end_ring_index = x->h_eri;
   o->info.start_orientation = orient[0];
   o->info.end_orientation = orient[1];
   o->info.orientation_diff = orient[2];
-  o->info.segmented_cloud_ground_flag = x->h_gflag.data();
-  o->info.segmented_cloud_col_ind = x->h_col.data();
-  o->info.segmented_cloud_range = x->h_range.data();
-  o->segmented_cloud = x->h_seg.data();
+  o->info.segmented_cloud_ground_flag = x->h_gflag;
+  o->info.segmented_cloud_col_ind = x->h_col;
+  o->info.segmented_cloud_range = x->h_range;
+  o->segmented_cloud = x->h_seg;
   o->n_segmented = ns;
-  o->outlier_cloud = x->h_outl.data();
+  o->outlier_cloud = x->h_outl;
   o->n_outlier = nout;
   if (images) {
-    o->full_cloud = x->h_full.data();
-    o->range_image = x->h_rimg.data();
-    o->ground_image = x->h_gimg.data();
-    o->label_image = x->h_label.data();
+    o->full_cloud = x->h_full;
+    o->range_image = x->h_rimg;
+    o->ground_image = x->h_gimg;
+    o->label_image = x->h_label;
   }
   if (gated) {
-    o->full_info_cloud = x->h_info.data();
-    o->ground_cloud = x->h_gcloud.data();
-    o->n_ground = ng[0];
-    o->segmented_cloud_pure = x->h_pure.data();
-    o->n_segmented_pure = ng[1];
+    o->full_info_cloud = x->h_info;
+    o->ground_cloud = x->h_gcloud;
+    o->n_ground = hd[FH_NG];
+    o->segmented_cloud_pure = x->h_pure;
+    o->n_segmented_pure = hd[FH_NG + 1];
   }
   return LEGO_OK;
 }
 
-static int fetch_fa(lego_ctx* x, int k, lego_fa_out* o) {
+// scan k's extraction + odometry outputs; withXerr: also the batch's exchange
+// error word (h_hdr[FH_XERR], lego_fa_process)
+static int fetch_fa(lego_ctx* x, int k, lego_fa_out* o, bool withXerr = false) {
   const DevCfg& c = x->dc;
   const size_t P = c.P, N = c.N;
-  hipStream_t s = x->stream;
-  int cnt[4], valid = 0, pub = 0, nout = 0;
+  const BatchBufs& bb = x->bb;
+  int32_t* hd = x->h_hdr;
+  const int* fc = bb.f_cnt + 4 * k;
+  FetchBuilder F;
+  F.add(fc, hd + FH_CNT, nullptr, 4, 4, 4);
+  F.add(x->ob.validOut + k, hd + FH_VALID, nullptr, 1, 4, 1);
+  F.add(x->ob.pubOut + k, hd + FH_PUB, nullptr, 1, 4, 1);
+  F.add(bb.nout + k, hd + FH_FNOUT, nullptr, 1, 4, 1);
+  F.add(x->ob.sumOut + 6 * k, hd + FH_SUM, nullptr, 6, 4, 6);
+  F.add(x->ob.curOut + 6 * k, hd + FH_CUR, nullptr, 6, 4, 6);
+  if (withXerr) F.add(x->ob.xerr, hd + FH_XERR, nullptr, 1, 4, 1);
+  F.add(bb.f_sharp + k * N * kSharpPerRing, x->h_sharp, fc + 0, 0, 16, N * kSharpPerRing);
+  F.add(bb.f_lsharp + k * N * kLessSharpPerRing, x->h_lsharp, fc + 1, 0, 16, N * kLessSharpPerRing);
+  F.add(bb.f_flat + k * N * kFlatPerRing, x->h_flat, fc + 2, 0, 16, N * kFlatPerRing);
+  F.add(bb.f_lflat + k * P, x->h_lflat, fc + 3, 0, 16, P);
+  F.add(x->ob.cornerEnd + (size_t)k * x->ob.capLS, x->h_cornerLast, fc + 1, 0, 16, N * kLessSharpPerRing);
+  F.add(x->ob.surfEnd + k * P, x->h_surfLast, fc + 3, 0, 16, P);
+  F.add(bb.outl + k * P, x->h_outlLast, bb.nout + k, 0, 16, P);
+  HIPCHK(F.run(x->stream));
+  int cnt[4];
   float sum[6], cur[6];
-  HIPCHK(hipMemcpyAsync(cnt, x->bb.f_cnt + 4 * k, sizeof(cnt), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(&valid, x->ob.validOut + k, sizeof(int), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(&pub, x->ob.pubOut + k, sizeof(int), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(&nout, x->bb.nout + k, sizeof(int), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(sum, x->ob.sumOut + 6 * k, sizeof(sum), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(cur, x->ob.curOut + 6 * k, sizeof(cur), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  HIPCHK(hipMemcpyAsync(x->h_sharp.data(), x->bb.f_sharp + k * N * kSharpPerRing, sizeof(float4) * cnt[0], hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(x->h_lsharp.data(), x->bb.f_lsharp + k * N * kLessSharpPerRing, sizeof(float4) * cnt[1], hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(x->h_flat.data(), x->bb.f_flat + k * N * kFlatPerRing, sizeof(float4) * cnt[2], hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(x->h_lflat.data(), x->bb.f_lflat + k * P, sizeof(float4) * cnt[3], hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(x->h_cornerLast.data(), x->ob.cornerEnd + (size_t)k * x->ob.capLS, sizeof(float4) * cnt[1], hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(x->h_surfLast.data(), x->ob.surfEnd + k * P, sizeof(float4) * cnt[3], hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(x->h_outlLast.data(), x->bb.outl + k * P, sizeof(float4) * nout, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
+  std::memcpy(cnt, hd + FH_CNT, sizeof(cnt));
+  std::memcpy(sum, hd + FH_SUM, sizeof(sum));
+  std::memcpy(cur, hd + FH_CUR, sizeof(cur));
+  const int valid = hd[FH_VALID], pub = hd[FH_PUB], nout = hd[FH_FNOUT];
   // adjustOutlierCloud :1746-1757 (axis swap) on the published copy
   for (int i = 0; i < nout; ++i) {
     const lego_point_xyzi p = x->h_outlLast[i];
@@ -971,18 +1069,18 @@ static int fetch_fa(lego_ctx* x, int k, lego_fa_out* o) {
   std::memset(o, 0, sizeof(*o));
   const int kr = k - x->lastBase;
   o->stamp = (kr < (int)x->stamps.size()) ? x->stamps[kr] : 0.0;
-  o->sharp = x->h_sharp.data(); o->n_sharp = cnt[0];
-  o->less_sharp = x->h_lsharp.data(); o->n_less_sharp = cnt[1];
-  o->flat = x->h_flat.data(); o->n_flat = cnt[2];
-  o->less_flat = x->h_lflat.data(); o->n_less_flat = cnt[3];
+  o->sharp = x->h_sharp; o->n_sharp = cnt[0];
+  o->less_sharp = x->h_lsharp; o->n_less_sharp = cnt[1];
+  o->flat = x->h_flat; o->n_flat = cnt[2];
+  o->less_flat = x->h_lflat; o->n_less_flat = cnt[3];
   o->odom_valid = valid;
   for (int i = 0; i < 6; ++i) { o->transform_sum[i] = sum[i]; o->transform_cur[i] = cur[i]; }
   odom_quat(sum, o->odom_quat, o->odom_pos);
   o->publish_to_mapping = pub;
   if (pub) {
-    o->corner_last = x->h_cornerLast.data(); o->n_corner_last = cnt[1];
-    o->surf_last = x->h_surfLast.data(); o->n_surf_last = cnt[3];
-    o->outlier_last = x->h_outlLast.data(); o->n_outlier_last = nout;
+    o->corner_last = x->h_cornerLast; o->n_corner_last = cnt[1];
+    o->surf_last = x->h_surfLast; o->n_surf_last = cnt[3];
+    o->outlier_last = x->h_outlLast; o->n_outlier_last = nout;
   }
   x->faGen = x->devGen;
   x->faK = k;
@@ -1001,9 +1099,7 @@ int lego_ip_process(lego_ctx* x, const lego_point_xyzir* pts, int32_t n, double 
   int64_t off[2] = {0, n};
   x->stamps.assign(1, stamp);
   const bool gated = (flags & LEGO_IP_GATED) != 0;
-  int st = run_ip(x, pts, off, 1, 0, (flags & LEGO_IP_IMAGES) ? 1 : 0, gated);
-  if (st != LEGO_OK) return st;
-  st = fetch_ip(x, 0, (flags & LEGO_IP_IMAGES) != 0, out, gated);
+  const int st = run_ip(x, pts, off, 1, 0, (flags & LEGO_IP_IMAGES) != 0, out, gated);
   if (st != LEGO_OK) return st;
   x->lastIp = *out;
   x->lastIpDevice = true;
@@ -1049,7 +1145,7 @@ int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
   }
   HIPCHK(hipSetDevice(x->device));
   ++x->devGen;
-  const bool resident = x->lastIpDevice && in->segmented_cloud == x->h_seg.data() &&
+  const bool resident = x->lastIpDevice && in->segmented_cloud == x->h_seg &&
                         in->n_segmented == x->lastIp.n_segmented;
   if (!resident) {
     int st = upload_ip(x, in);
@@ -1073,18 +1169,18 @@ int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
   }
   x->tm.end(x->stream);
   HIPCHK(hipGetLastError());
-  unsigned xerr = 0;
-  HIPCHK(hipMemcpyAsync(&xerr, x->ob.xerr, sizeof(xerr), hipMemcpyDeviceToHost, x->stream));
-  HIPCHK(hipStreamSynchronize(x->stream));
-  if (xerr) {
-    set_err("odometry exchange overflow (more NN rounds than slots)");
-    return LEGO_E_DEVICE;
-  }
   x->lastB = 1;
   x->lastBase = 0;
   x->lastBatch = false;  // slot 0's buffers now hold this scan, not a waited batch
   x->lastIpDevice = false;
-  return fetch_fa(x, 0, out);
+  const int st = fetch_fa(x, 0, out, true);  // the exchange error word with the outputs: one sync
+  if (st != LEGO_OK) return st;
+  if (x->h_hdr[FH_XERR]) {
+    x->faK = -1;  // no resident hand-off of a failed scan
+    set_err("odometry exchange overflow (more NN rounds than slots)");
+    return LEGO_E_DEVICE;
+  }
+  return LEGO_OK;
 }
 
 int lego_odom_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offsets,
@@ -1640,8 +1736,8 @@ int lego_mo_process(lego_ctx* x, const lego_fa_out* in, lego_mo_out* out) {
   MoStepArgs a;
   // the clouds of this context's own last fa output (the node path's hand-off
   // within one process): read where fetch_fa copied them from, on the device
-  const bool resident = x->faK >= 0 && x->faGen == x->devGen && in->corner_last == x->h_cornerLast.data() &&
-                        in->surf_last == x->h_surfLast.data() && in->outlier_last == x->h_outlLast.data() &&
+  const bool resident = x->faK >= 0 && x->faGen == x->devGen && in->corner_last == x->h_cornerLast &&
+                        in->surf_last == x->h_surfLast && in->outlier_last == x->h_outlLast &&
                         in->n_corner_last == x->faCnt[0] && in->n_surf_last == x->faCnt[1] &&
                         in->n_outlier_last == x->faCnt[2];
   if (resident) {
@@ -1693,10 +1789,18 @@ int lego_mo_process(lego_ctx* x, const lego_fa_out* in, lego_mo_out* out) {
   MoState hs;
   MoCounts hc;
   int meta[kKfMeta] = {};
-  HIPCHK(hipMemcpyAsync(&hs, m.st, sizeof(hs), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(&hc, m.cnt, sizeof(hc), hipMemcpyDeviceToHost, s));
-  if (!x->moFixed) HIPCHK(hipMemcpyAsync(meta, m.kf.meta, sizeof(meta), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
+  {  // the step's state, counts and keyframe words in one k_fetch (pinned staging)
+    unsigned char* hb = (unsigned char*)x->h_moRes;
+    const size_t oc = (sizeof(MoState) + 15) & ~(size_t)15, om = oc + ((sizeof(MoCounts) + 15) & ~(size_t)15);
+    FetchBuilder F;
+    F.add(m.st, hb, nullptr, sizeof(MoState), 1, sizeof(MoState));
+    F.add(m.cnt, hb + oc, nullptr, sizeof(MoCounts), 1, sizeof(MoCounts));
+    if (!x->moFixed) F.add(m.kf.meta, hb + om, nullptr, sizeof(meta), 1, sizeof(meta));
+    HIPCHK(F.run(s));
+    std::memcpy(&hs, hb, sizeof(hs));
+    std::memcpy(&hc, hb + oc, sizeof(hc));
+    if (!x->moFixed) std::memcpy(meta, hb + om, sizeof(meta));
+  }
   mo_evprof_print(m);
   if (meta[KF_OVF]) {  // saveKeyFramesAndFactor of this very step found the store full (k_kf_save)
     x->moStoreFull = true;
@@ -1809,9 +1913,7 @@ int lego_ip_process_pc2(lego_ctx* x, const lego_pc2_msg* msg, uint32_t flags, le
   if (st != LEGO_OK) return st;
   x->stamps.assign(1, msg->stamp);
   const bool gated = (flags & LEGO_IP_GATED) != 0;
-  st = run_ip(x, x->d_pts, x->d_off, 1, 1, (flags & LEGO_IP_IMAGES) ? 1 : 0, gated);
-  if (st != LEGO_OK) return st;
-  st = fetch_ip(x, 0, (flags & LEGO_IP_IMAGES) != 0, out, gated);
+  st = run_ip(x, x->d_pts, x->d_off, 1, 1, (flags & LEGO_IP_IMAGES) != 0, out, gated);
   if (st != LEGO_OK) return st;
   x->lastIp = *out;
   x->lastIpDevice = true;

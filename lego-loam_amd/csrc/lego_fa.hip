@@ -939,6 +939,10 @@ __device__ __forceinline__ void lfv_wave(const BatchBufs& bb, const DevCfg& c, i
 
 constexpr int kLfvMaxPer = 8;  // voxels per thread (H <= kLfvMaxPer * kExtractThreads)
 constexpr int kLfvBlockRings = 2;  // rings per large-ring workgroup (k_lf_voxel; 1 / 2 / 4 / 8: fleet 254 / 256 / 245 / 253 k)
+// A launch of at most this many rings leaves most of the device idle (one
+// scan through the node API, a small batch): one large ring per workgroup
+// there, so the launch lasts one ring's sort instead of two in sequence.
+constexpr int kLfvSmallLaunchRings = 256;
 __host__ __device__ inline size_t lfvox_lds_bytes(int H) {
   return (((size_t)H * 6 + 15) & ~(size_t)15) + vg_sort_scratch_bytes(H, kExtractThreads) + 64;
 }
@@ -1164,8 +1168,8 @@ void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_ca
   const int g4 = waveOn ? (c.N + 3) / 4 : 0;
   // rings per large-ring workgroup (LEGO_LFV_BLOCK_RINGS, A/B knob; 1 = one
   // workgroup per ring)
-  static const int rpb = std::getenv("LEGO_LFV_BLOCK_RINGS") ? std::max(1, std::atoi(std::getenv("LEGO_LFV_BLOCK_RINGS")))
-                                                              : (waveOn ? kLfvBlockRings : 1);
+  static const int rpbEnv = std::getenv("LEGO_LFV_BLOCK_RINGS") ? std::max(1, std::atoi(std::getenv("LEGO_LFV_BLOCK_RINGS"))) : 0;
+  const int rpb = rpbEnv ? rpbEnv : (waveOn && B * c.N > kLfvSmallLaunchRings ? kLfvBlockRings : 1);
   const int gb = (c.N + rpb - 1) / rpb;
   k_lf_voxel<<<dim3(g4 + gb, B), kExtractThreads, std::max(kLfvWaveLds, lfvox_lds_bytes(c.H)), s>>>(bb, c, g4, gb);
   tm->mark("fa.compact", s);

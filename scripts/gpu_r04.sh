@@ -53,6 +53,14 @@ if [ -n "${ENVAB5:-}" ]; then  # ENVAB5="VAR A B" on the C5 line
   VAR=$1 A=$2 B=$3 bash scripts/env_ab_c5.sh > "$O/envab5_$1.txt" 2>&1
   cat "$O/envab5_$1.txt"
 fi
+if [ -n "${NODEAB:-}" ]; then  # NODEAB="VAR VALUE": node-API latency, default (A) vs VAR=VALUE (B), alternating
+  set -- $NODEAB
+  for k in 1 2 3; do
+    LABEL=A timeout -k 10 180 python -u scripts/ab_node.py >> "$O/ab_node.txt" 2>&1
+    env "$1=$2" LABEL=B timeout -k 10 180 python -u scripts/ab_node.py >> "$O/ab_node.txt" 2>&1
+  done
+  cat "$O/ab_node.txt"
+fi
 if [ -n "${AB:-}" ]; then
   bash scripts/ab.sh > "$O/ab.txt" 2>&1
   cat "$O/ab.txt"
