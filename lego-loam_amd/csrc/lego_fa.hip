@@ -939,10 +939,12 @@ __device__ __forceinline__ void lfv_wave(const BatchBufs& bb, const DevCfg& c, i
 
 constexpr int kLfvMaxPer = 8;  // voxels per thread (H <= kLfvMaxPer * kExtractThreads)
 constexpr int kLfvBlockRings = 2;  // rings per large-ring workgroup (k_lf_voxel; 1 / 2 / 4 / 8: fleet 254 / 256 / 245 / 253 k)
-// A launch of at most this many rings leaves most of the device idle (one
-// scan through the node API, a small batch): one large ring per workgroup
-// there, so the launch lasts one ring's sort instead of two in sequence.
-constexpr int kLfvSmallLaunchRings = 256;
+// A launch of at most this many rings leaves part of the device idle (one
+// scan through the node API, C2's 100-scan batch beside the odometry, C3):
+// one large ring per workgroup there, so a workgroup lasts one ring's sort
+// instead of two in sequence (C2 at 20 steps: fa.voxel 0.695 -> 0.667 ms,
+// profiles/r04_ab_lfv_rings.txt).  A fleet call keeps two (kLfvBlockRings).
+constexpr int kLfvSmallLaunchRings = 4096;
 __host__ __device__ inline size_t lfvox_lds_bytes(int H) {
   return (((size_t)H * 6 + 15) & ~(size_t)15) + vg_sort_scratch_bytes(H, kExtractThreads) + 64;
 }
