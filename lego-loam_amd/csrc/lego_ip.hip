@@ -477,6 +477,7 @@ __global__ void __launch_bounds__(1024) k_gated_write(BatchBufs bb, DevCfg c, Ga
 constexpr int kSegLdsMaxP = 32767;  // counts fit 15 bits; 128 KB of parents
 constexpr int kSegLdsMaxN = 16;     // the row mask fits 16 bits
 constexpr int kSegK = (kSegLdsMaxP + 1023) / 1024;  // 1024-pixel chunks per scan
+constexpr int kSegHbmMaxScans = 8;  // launches of up to this many scans segment in HBM (launch_ip)
 bool seg_lds_ok(const DevCfg& c) { return c.N <= kSegLdsMaxN && c.P <= kSegLdsMaxP && !c.segHbm; }
 
 __device__ __forceinline__ int lds_find(volatile int* par, int x) {
@@ -682,7 +683,11 @@ void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hip
   const int P = c.P;
   tm->mark("ip.memset", s);
   // launch-path errors are sticky: the caller checks hipGetLastError() after the batch
-  const bool segLds = seg_lds_ok(c);
+  // A launch of a few scans takes the HBM union-find: its grid-wide kernels
+  // finish sooner than k_seg_lds's one workgroup per scan (a node call: ip
+  // 0.20 -> 0.16 ms, profiles/r04_ab_node_seg.txt; the same labels, pinned by
+  // test_seg_lds_equals_hbm_union_find)
+  const bool segLds = seg_lds_ok(c) && B > kSegHbmMaxScans;
   // bb.owner is all -1 here: filled at creation, and k_pixels clears what k_project set
   if (!segLds) {  // the HBM union-find's size and row counters
     (void)hipMemsetAsync(bb.csize, 0, sizeof(int) * (size_t)B * P, s);

@@ -539,26 +539,36 @@ def test_reset_in_flight(L):
 
 @pytest.mark.parametrize("seed,extra", [(0, {}), (1, {}), (2, {"dup_frac": 0.05})])
 def test_seg_lds_equals_hbm_union_find(L, seed, extra):
-    """VLP-16 images are segmented in LDS (k_seg_lds); LEGO_SEG_HBM (diagnostic)
-    sends them through the HBM union-find (k_ccl_* + k_compact) that the
-    larger sensors use.  Both equal the oracle and each other, labels, images
-    and clouds byte for byte, on 12 consecutive scans."""
+    """VLP-16 batches of more than kSegHbmMaxScans (8) scans are segmented in
+    LDS (k_seg_lds); node calls (one scan) and LEGO_SEG_HBM (diagnostic) go
+    through the HBM union-find (k_ccl_* + k_compact) that the larger sensors
+    use.  All equal the oracle, clouds and cloud_info byte for byte on 12
+    consecutive scans (and labels / images through the node calls)."""
     import os
 
     sc = L.synth_cfg("VLP-16", seed, **extra)
     scans = [L.synth_scan(sc, k) for k in range(12)]
     ora = L.Oracle(L.sensor_cfg("VLP-16"))
     ref = [ora.ip(p, s, images=True) for p, s in scans]
+    cap = max(len(p) for p, _ in scans) + 16
+    pts = np.concatenate([p for p, _ in scans])
+    offs = np.concatenate([[0], np.cumsum([len(p) for p, _ in scans])]).astype(np.int64)
+    stamps = np.array([s for _, s in scans], dtype=np.float64)
     outs = {}
     for mode in ("lds", "hbm"):
         if mode == "hbm":
             os.environ["LEGO_SEG_HBM"] = "1"
         try:
-            gpu = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=max(len(p) for p, _ in scans) + 16)
-            outs[mode] = [gpu.ip(p, s, images=True) for p, s in scans]
+            gpu = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=cap, max_batch=len(scans))
+            gpu.odom_batch(pts, offs, stamps)
+            outs[mode] = [gpu.batch_fetch(k)[0] for k in range(len(scans))]
             gpu.close()
         finally:
             os.environ.pop("LEGO_SEG_HBM", None)
+    node = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=cap)
+    outs["node"] = [node.ip(p, s, images=True) for p, s in scans]
+    node.close()
     for k in range(len(scans)):
-        assert_ip_equal(outs["lds"][k], ref[k])
-        assert_ip_equal(outs["hbm"][k], ref[k])
+        assert_ip_equal(outs["lds"][k], ref[k], images=False)
+        assert_ip_equal(outs["hbm"][k], ref[k], images=False)
+        assert_ip_equal(outs["node"][k], ref[k])
