@@ -945,6 +945,10 @@ constexpr int kLfvBlockRings = 2;  // rings per large-ring workgroup (k_lf_voxel
 // instead of two in sequence (C2 at 20 steps: fa.voxel 0.695 -> 0.667 ms,
 // profiles/r04_ab_lfv_rings.txt).  A fleet call keeps two (kLfvBlockRings).
 constexpr int kLfvSmallLaunchRings = 4096;
+// launches of up to this many rings (a node call) take 1024-thread workgroups:
+// node fa 0.30 -> 0.28 ms; a C2 batch's VoxelGrid 0.67 -> 1.52 ms that way
+// (profiles/r04_ab_lfv_wide.txt)
+constexpr int kLfvWideLaunchRings = 128;
 __host__ __device__ inline size_t lfvox_lds_bytes(int H) {
   return (((size_t)H * 6 + 15) & ~(size_t)15) + vg_sort_scratch_bytes(H, kExtractThreads) + 64;
 }
@@ -956,7 +960,7 @@ __device__ __forceinline__ void lfv_block(const BatchBufs& bb, const DevCfg& c, 
   uint16_t* val = (uint16_t*)(lds_raw + (size_t)H * 4);
   unsigned char* sc = lds_raw + (((size_t)H * 6 + 15) & ~(size_t)15);
   int* misc = (int*)(sc + vg_sort_scratch_bytes(H, kExtractThreads));  // [16]
-  __shared__ float mm[4][6];
+  __shared__ float mm[16][6];  // per wave (up to 1024 threads)
   int* cnt = bb.r_cnt + ((size_t)b * c.N + ring) * 4;
   float4* slot = bb.r_lflat + (size_t)b * c.P + (size_t)ring * H;
   const int K = cnt[3] >> 16;  // as k_extract wrote it (lfv_wave)
@@ -1038,10 +1042,13 @@ __device__ __forceinline__ void lfv_block(const BatchBufs& bb, const DevCfg& c, 
 #ifndef LFV_MINB
 #define LFV_MINB 4
 #endif
-__global__ void __launch_bounds__(kExtractThreads, LFV_MINB) k_lf_voxel(BatchBufs bb, DevCfg c, int g4, int gb) {
+// T = 1024 (small launches): every ring by a whole workgroup (g4 = 0).
+template <int T>
+__global__ void __launch_bounds__(T, T == kExtractThreads ? LFV_MINB : 1) k_lf_voxel(BatchBufs bb, DevCfg c, int g4,
+                                                                                   int gb) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   const int b = blockIdx.y;
-  if ((int)blockIdx.x < g4) {
+  if (T == kExtractThreads && (int)blockIdx.x < g4) {
     lfv_wave(bb, c, (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6), b, lds_raw);
     return;
   }
@@ -1173,7 +1180,16 @@ void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_ca
   static const int rpbEnv = std::getenv("LEGO_LFV_BLOCK_RINGS") ? std::max(1, std::atoi(std::getenv("LEGO_LFV_BLOCK_RINGS"))) : 0;
   const int rpb = rpbEnv ? rpbEnv : (waveOn && B * c.N > kLfvSmallLaunchRings ? kLfvBlockRings : 1);
   const int gb = (c.N + rpb - 1) / rpb;
-  k_lf_voxel<<<dim3(g4 + gb, B), kExtractThreads, std::max(kLfvWaveLds, lfvox_lds_bytes(c.H)), s>>>(bb, c, g4, gb);
+  // a launch that leaves the device idle but for itself (a node call): every
+  // ring by a 1024-thread workgroup, the sort's levels over four times the
+  // lanes (LEGO_LFV_WIDE, A/B knob)
+  static const int wideEnv = std::getenv("LEGO_LFV_WIDE") ? std::atoi(std::getenv("LEGO_LFV_WIDE")) : -1;
+  const bool wide = wideEnv >= 0 ? wideEnv != 0 : B * c.N <= kLfvWideLaunchRings;
+  if (wide)
+    k_lf_voxel<1024><<<dim3(c.N, B), 1024, lfvox_lds_bytes(c.H), s>>>(bb, c, 0, c.N);
+  else
+    k_lf_voxel<kExtractThreads>
+        <<<dim3(g4 + gb, B), kExtractThreads, std::max(kLfvWaveLds, lfvox_lds_bytes(c.H)), s>>>(bb, c, g4, gb);
   tm->mark("fa.compact", s);
   k_fa_compact<<<dim3(c.N, B), 256, 0, s>>>(bb, c);
 }
