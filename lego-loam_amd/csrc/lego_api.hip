@@ -1161,8 +1161,7 @@ int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
     if (st != LEGO_OK) return st;
   }
   x->tm.begin();
-  HIPCHK(hipMemsetAsync(x->ob.xerr, 0, sizeof(unsigned), x->stream));
-  launch_fa(bb, x->dc, 1, 1, x->d_carry, x->stream, &x->tm);
+  launch_fa(bb, x->dc, 1, 1, x->d_carry, x->stream, &x->tm);  // launch_odom's prep zeroes *ob.xerr
   if (launch_odom(bb, x->ob, x->dc, 1, x->stream, &x->tm, x->profOn ? x->d_prof : nullptr) != 0) {
     set_err("odometry launch failed (%d workgroups)", x->ob.G);
     return LEGO_E_DEVICE;

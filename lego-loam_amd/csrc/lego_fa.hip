@@ -1158,11 +1158,20 @@ __global__ void k_fa_compact(BatchBufs bb, DevCfg c) {
     bb.f_lflat[(size_t)b * c.P + off[3] + t] = bb.r_lflat[(size_t)b * c.P + (size_t)r * c.H + t];
 }
 
+// the batch's per-scan words k_fa_half / the extraction accumulate into (one
+// launch instead of two fills)
+__global__ void k_fa_init(BatchBufs bb, int B) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) {
+    bb.firsthalf[b] = 0x7f7f7f7f;  // atomicMin's identity for the first-half index
+    bb.fa_flags[b] = 0;
+  }
+}
+
 void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_carry, hipStream_t s,
                StageTimer* tm) {
   tm->mark("fa.deskew", s);
-  (void)hipMemsetAsync(bb.firsthalf, 0x7f, sizeof(int) * B, s);
-  (void)hipMemsetAsync(bb.fa_flags, 0, sizeof(int) * B, s);
+  k_fa_init<<<(B + 255) / 256, 256, 0, s>>>(bb, B);
   dim3 gpts((c.P + 255) / 256, B);
   k_fa_half<<<gpts, 256, 0, s>>>(bb, c);
   if (bb.imu) k_fa_imu_start<<<(B + 63) / 64, 64, 0, s>>>(bb, c);

@@ -133,6 +133,10 @@ __global__ void k_ccl_init(BatchBufs bb, DevCfg c) {
   const size_t base = (size_t)b * c.P;
   const int L = bb.label[base + p];
   bb.parent[base + p] = (L == 0) ? p : -1;
+  // the size and row counters k_ccl_root accumulates into (two launches later)
+  bb.csize[base + p] = 0;
+  bb.rowmask[(base + p) * 2] = 0ull;
+  bb.rowmask[(base + p) * 2 + 1] = 0ull;
   uint8_t e = 0;
   if (L == 0) {
     const int row = p / c.H, col = p - row * c.H;
@@ -689,10 +693,6 @@ void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hip
   // test_seg_lds_equals_hbm_union_find)
   const bool segLds = seg_lds_ok(c) && B > kSegHbmMaxScans;
   // bb.owner is all -1 here: filled at creation, and k_pixels clears what k_project set
-  if (!segLds) {  // the HBM union-find's size and row counters
-    (void)hipMemsetAsync(bb.csize, 0, sizeof(int) * (size_t)B * P, s);
-    (void)hipMemsetAsync(bb.rowmask, 0, sizeof(unsigned long long) * 2 * (size_t)B * P, s);
-  }
   tm->mark("ip.project", s);
   dim3 gpts((bb.Nmax + 255) / 256, B), gpix((P + 255) / 256, B), gcol((c.H + 255) / 256, B);
   k_project<<<gpts, 256, 0, s>>>(bb, c);
