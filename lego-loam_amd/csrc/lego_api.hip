@@ -1093,9 +1093,17 @@ int lego_ip_process(lego_ctx* x, const lego_point_xyzir* pts, int32_t n, double 
   if (!x || !pts || !out || n <= 0) return LEGO_E_ARG;
   ++x->devGen;
   if (n > x->maxPoints) return LEGO_E_CAPACITY;
-  for (int i = 0; i < n; ++i)  // dense check (imageProjection.cpp:174)
-    if (!std::isfinite(pts[i].x) || !std::isfinite(pts[i].y) || !std::isfinite(pts[i].z))
-      return LEGO_E_NOT_DENSE;
+  {  // dense check (imageProjection.cpp:174): an all-ones exponent is inf / nan;
+     // accumulated without branches so the loop vectorises
+    uint32_t nonfinite = 0;
+    for (int i = 0; i < n; ++i) {
+      uint32_t u[3];
+      std::memcpy(u, &pts[i].x, sizeof(u));
+      nonfinite |= (uint32_t)((u[0] & 0x7f800000u) == 0x7f800000u) | (uint32_t)((u[1] & 0x7f800000u) == 0x7f800000u) |
+                   (uint32_t)((u[2] & 0x7f800000u) == 0x7f800000u);
+    }
+    if (nonfinite) return LEGO_E_NOT_DENSE;
+  }
   int64_t off[2] = {0, n};
   x->stamps.assign(1, stamp);
   const bool gated = (flags & LEGO_IP_GATED) != 0;
