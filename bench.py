@@ -15,6 +15,7 @@ Prints ONE JSON line on rank 0 (contract in the task statement).
 from __future__ import annotations
 
 import argparse
+import datetime
 import ctypes as C
 import importlib.util
 import json
@@ -611,15 +612,28 @@ def main():
     import torch
 
     dist = None
+    ms = load_multistream()
+    # N > 1 fails fast and says where: finite timeouts on the process groups
+    # (LEGO_BENCH_PG_TIMEOUT_S) and a per-rank watchdog (LEGO_BENCH_WATCHDOG_S)
+    # that ends a rank making no progress with a message naming the step and
+    # phase (multistream.Watchdog: os._exit, never a re-exec).  The native
+    # gather's own waits are bounded by LEGO_COMM_TIMEOUT_MS (lego_comm_create).
+    wd = None
+    pg_timeout = datetime.timedelta(seconds=float(os.environ.get("LEGO_BENCH_PG_TIMEOUT_S", "300")))
     if world > 1:
         import torch.distributed as dist
 
+        wd = ms.Watchdog(float(os.environ.get("LEGO_BENCH_WATCHDOG_S", "240")), rank)
+        wd.mark(None, "init_process_group")
         torch.cuda.set_device(local)
-        dist.init_process_group(backend)
+        dist.init_process_group(backend, timeout=pg_timeout)
     dev = torch.device("cuda", local)
 
+    def mark(step, phase):
+        if wd is not None:
+            wd.mark(step, phase)
+
     L = load_ffi()
-    ms = load_multistream()
     lib = L.hip_lib()
     cfg = L.sensor_cfg(args.sensor, lib)
     # N=1: the C2 stream (seed 1).  N>1: C4, stream `rank` (seed 10 + rank).
@@ -648,20 +662,29 @@ def main():
     # gather, and a failure on any rank moves EVERY rank to the torch gather at
     # the same step (never RCCL on some ranks and torch on others: a hang).
     comm, transport = None, None
+    comm_ranks = None
     if dist is not None:
-        ctrl = dist.new_group(backend="gloo") if backend != "gloo" else None
+        mark(None, "control group")
+        ctrl = dist.new_group(backend="gloo", timeout=pg_timeout) if backend != "gloo" else None
         want_native = backend == "nccl"
         create_error = None
         if want_native:
+            mark(None, "lego_comm_create")
             try:
                 comm = ms.native_comm(L, dist, local)
             except Exception as e:  # noqa: BLE001
                 create_error = f"lego_comm_create: {e}"
+        mark(None, "transport agreement")
         transport = ms.HandoffTransport(dist, ctrl, want_native and comm is not None, create_error)
         if not transport.native and comm is not None:
             lib.lego_comm_abort(comm)
             lib.lego_comm_destroy(comm)
             comm = None
+        if comm is not None:  # the communicator's rank count as RCCL reports it
+            n = C.c_int32()
+            comm_ranks = int(n.value) if lib.lego_comm_count(comm, C.byref(n)) == L.LEGO_OK else None
+        else:
+            comm_ranks = dist.get_world_size()
 
     # Steps are pipelined two deep (lego_odom_batch_submit / _wait): step i+1's
     # projection + extraction run while step i's odometry chain does.
@@ -669,6 +692,7 @@ def main():
 
     def retire():
         i = inflight.pop(0)
+        mark(i, "lego_odom_batch_wait")
         gpu.wait(recs)
         cp = (L.PoseRec * B)()
         C.memmove(cp, recs, C.sizeof(recs))
@@ -678,6 +702,8 @@ def main():
         # by the torch gather of the packet packed into HBM
         pkt = None
         if transport is not None:
+            mark(i, "hand-off gather (" + transport.name + ")")
+
             def fallback():
                 t = gpu.handoff_tensor(dev)
                 return ms.gather_packets(t if backend == "nccl" else t.cpu(), dist, to_host=False)
@@ -693,6 +719,7 @@ def main():
             gpu.reset()  # a new pass over the stream starts from a fresh state (in stream order)
         if len(inflight) == 2:
             done.append(retire())
+        mark(i, "lego_odom_batch_submit")
         gpu.submit_device(d_pts.data_ptr(), d_off[j].data_ptr(), stamps[j * B:(j + 1) * B], B)
         inflight.append(i)
         return done
@@ -702,8 +729,11 @@ def main():
     while inflight:
         retire()
     if dist:
+        mark(None, "barrier before the timed region")
         dist.barrier()
     torch.cuda.synchronize()
+    if transport is not None:  # per-step host costs of the timed steps only
+        transport.t_gather = transport.t_agree = 0.0
     stage_acc: dict[str, float] = {}
     gathered = None
     t0 = time.perf_counter()
@@ -731,12 +761,15 @@ def main():
         account([retire()])
     torch.cuda.synchronize()
     if dist:
+        mark(None, "barrier after the timed region")
         dist.barrier()
     dt = time.perf_counter() - t0
     if dist:
+        mark(None, "max-over-ranks all_reduce")
         t = torch.tensor([dt], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+        wd.disarm()
     total_scans = args.steps * B * world
     value = total_scans / dt
     ms_per_step = dt / args.steps * 1e3
@@ -874,7 +907,14 @@ def main():
                                    + ": per step, pose records + published clouds to rank 0, one transport on every "
                                      "rank (agreed over a gloo control group)") if transport else None),
                        "gather_native_error": (transport.errors or None) if transport else None,
-                       "gather_fallback_from_step": transport.switched_at if transport else None},
+                       "gather_fallback_from_step": transport.switched_at if transport else None,
+                       "comm_ranks": comm_ranks,
+                       "gather_host_ms_per_step": ({
+                           "gather": transport.t_gather / args.steps * 1e3,
+                           "agreement": transport.t_agree / args.steps * 1e3,
+                           "note": "rank 0's host time per timed step in the hand-off call (native: pack, size "
+                                   "gather and root's sync on the sizes, send/recv enqueue) and in the gloo "
+                                   "agreement after it"} if transport else None)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "traffic_over_alg": (traffic / (alg_bytes / args.steps * 1.0 / n_odom)

@@ -441,8 +441,15 @@ int lego_handoff_unpack(const void* packet, uint64_t bytes, int32_t k, lego_pose
  * (the caller broadcasts the 128 bytes, e.g. over MPI or torch.distributed). */
 typedef struct lego_comm lego_comm;
 int lego_comm_unique_id(uint8_t id[128]);
+/* Every wait a call makes on the communicator's stream is bounded by the
+ * LEGO_COMM_TIMEOUT_MS environment value read here (default 60000): a peer
+ * that never joins a collective makes the waiting call abort the
+ * communicator and return LEGO_E_DEVICE with the wait named in
+ * lego_last_error, instead of blocking the process. */
 int lego_comm_create(const uint8_t id[128], int32_t nranks, int32_t rank, int32_t device, lego_comm** out);
 int lego_comm_destroy(lego_comm* comm);
+/* The communicator's rank count as RCCL reports it (ncclCommCount). */
+int lego_comm_count(lego_comm* comm, int32_t* nranks);
 /* Aborts the communicator (ncclCommAbort): every operation still queued on it
  * is cancelled, so its stream drains, and every later call returns
  * LEGO_E_STATE.  Call it on every rank once any rank reports a failed gather
@@ -475,7 +482,8 @@ int lego_comm_gather_handoff(lego_comm* comm, lego_ctx* ctx, int32_t root);
  * caller's buffer and does not wait. */
 #define LEGO_COMM_DEVICE_RESULT 1u
 int lego_comm_gather_handoff_ex(lego_comm* comm, lego_ctx* ctx, int32_t root, uint32_t flags);
-/* Blocks until the last gather on the communicator has completed. */
+/* Blocks until the last gather on the communicator has completed (within the
+ * LEGO_COMM_TIMEOUT_MS bound, see lego_comm_create). */
 int lego_comm_wait(lego_comm* comm);
 /* On root after lego_comm_gather_handoff: rank r's packet in host memory,
  * valid until the next gather on the communicator. */
@@ -509,7 +517,13 @@ int lego_voxel_grid_stats(lego_ctx* ctx, int32_t stats[8]);
  * (n <= 8192): heap-sorted pieces whose voxel sums do not depend on their
  * order (each key at most twice, the smallest not continuing the preceding
  * piece) come back in stable order instead of std::sort's, every other
- * position as std::sort leaves it.  heap_pieces (may be NULL): how many pieces
+ * position as std::sort leaves it.  Modes 4..8 cover the rest of the
+ * workgroup sort's two forms (segment ids in registers, "reg", or in LDS,
+ * "lds") by block size and rule, each compiled under the register budget of
+ * the kernel that runs it (256 threads: k_lf_voxel's): 4 reg/256/exact,
+ * 5 reg/256/sum-order, 6 lds/256/exact, 7 lds/1024/exact, 8 lds/1024/sum-order
+ * (mode 0 = reg/1024/exact, 2 = lds/256/sum-order, 3 = reg/1024/sum-order).
+ * 256-thread modes hold n <= 2048.  heap_pieces (may be NULL): how many pieces
  * the depth budget sent to std::__partial_sort. */
 int lego_sort_permutation(lego_ctx* ctx, const uint32_t* keys, int32_t n, int32_t wave, int32_t* perm,
                           int32_t* heap_pieces);

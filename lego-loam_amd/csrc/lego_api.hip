@@ -765,6 +765,10 @@ static int fetch_ip(lego_ctx* x, int k, bool images, lego_ip_out* o, bool gated 
 static int run_ip(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offsets, int B, int on_device,
                   bool images, lego_ip_out* out, bool gated = false) {
   const int want_labels = images ? 1 : 0;
+  // every projection launch writes slot 0 (the outlier cloud among it): a
+  // resident hand-off of an earlier lego_fa_process is stale from here on
+  // (lego_ip_process and lego_ip_process_pc2 alike)
+  ++x->devGen;
   if (x->inflight) {
     set_err("node-shaped call while batches are in flight (lego_odom_batch_wait first)");
     return LEGO_E_STATE;
@@ -798,7 +802,7 @@ static int run_ip(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offse
   std::vector<int> cnt;
   x->tm.collect(x->tnames, x->tms, cnt);
   for (int k = 0; k < B; ++k)
-    if (x->h_bad[k]) {
+    if (x->h_bad[k] & kBadNotDense) {
       x->lastB = 0;
       set_err("scan %d of the batch has non-finite xyz (the cloud must be dense)", k);
       return LEGO_E_NOT_DENSE;
@@ -883,9 +887,14 @@ static int wait_batch(lego_ctx* x, lego_pose_rec* recs, int cap, int* nOut) {
     return LEGO_E_DEVICE;
   }
   for (int k = 0; k < B; ++k)
-    if (pk[k].bad) {
+    if (pk[k].bad & kBadNotDense) {
       set_err("scan %d of the batch has non-finite xyz (the cloud must be dense)", k);
       return LEGO_E_NOT_DENSE;
+    }
+  for (int k = 0; k < B; ++k)
+    if (pk[k].bad & kBadPermutation) {
+      set_err("scan %d: per-ring VoxelGrid sort returned a payload outside its input (device fault)", k);
+      return LEGO_E_DEVICE;
     }
   if (cap < B) {
     set_err("record buffer of %d < %d scans", cap, B);
@@ -963,7 +972,7 @@ struct FetchBuilder {
 };
 // header words of h_hdr
 enum { FH_NS = 0, FH_NOUT = 1, FH_ORIENT = 2, FH_NG = 5, FH_CNT = 8, FH_VALID = 12, FH_PUB = 13, FH_FNOUT = 14,
-       FH_SUM = 16, FH_CUR = 22, FH_XERR = 28 };
+       FH_SUM = 16, FH_CUR = 22, FH_XERR = 28, FH_BAD = 29 };
 
 // copy scan k's image-projection outputs of the last batch into host staging
 // (badN: also the first badN not-dense flags into h_bad)
@@ -1046,7 +1055,10 @@ static int fetch_fa(lego_ctx* x, int k, lego_fa_out* o, bool withXerr = false) {
   F.add(bb.nout + k, hd + FH_FNOUT, nullptr, 1, 4, 1);
   F.add(x->ob.sumOut + 6 * k, hd + FH_SUM, nullptr, 6, 4, 6);
   F.add(x->ob.curOut + 6 * k, hd + FH_CUR, nullptr, 6, 4, 6);
-  if (withXerr) F.add(x->ob.xerr, hd + FH_XERR, nullptr, 1, 4, 1);
+  if (withXerr) {
+    F.add(x->ob.xerr, hd + FH_XERR, nullptr, 1, 4, 1);
+    F.add(bb.bad + k, hd + FH_BAD, nullptr, 1, 4, 1);
+  }
   F.add(bb.f_sharp + k * N * kSharpPerRing, x->h_sharp, fc + 0, 0, 16, N * kSharpPerRing);
   F.add(bb.f_lsharp + k * N * kLessSharpPerRing, x->h_lsharp, fc + 1, 0, 16, N * kLessSharpPerRing);
   F.add(bb.f_flat + k * N * kFlatPerRing, x->h_flat, fc + 2, 0, 16, N * kFlatPerRing);
@@ -1091,7 +1103,6 @@ static int fetch_fa(lego_ctx* x, int k, lego_fa_out* o, bool withXerr = false) {
 int lego_ip_process(lego_ctx* x, const lego_point_xyzir* pts, int32_t n, double stamp,
                     uint32_t flags, lego_ip_out* out) {
   if (!x || !pts || !out || n <= 0) return LEGO_E_ARG;
-  ++x->devGen;
   if (n > x->maxPoints) return LEGO_E_CAPACITY;
   {  // dense check (imageProjection.cpp:174): an all-ones exponent is inf / nan;
      // accumulated without branches so the loop vectorises
@@ -1168,6 +1179,7 @@ int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
     const int st = imu_stage(x, 1, nullptr, 0, nullptr, &bb.imu);
     if (st != LEGO_OK) return st;
   }
+  HIPCHK(hipMemsetAsync(bb.bad, 0, sizeof(int), x->stream));  // ip reported its own bit; k_lf_voxel's below
   x->tm.begin();
   launch_fa(bb, x->dc, 1, 1, x->d_carry, x->stream, &x->tm);  // launch_odom's prep zeroes *ob.xerr
   if (launch_odom(bb, x->ob, x->dc, 1, x->stream, &x->tm, x->profOn ? x->d_prof : nullptr) != 0) {
@@ -1185,6 +1197,11 @@ int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
   if (x->h_hdr[FH_XERR]) {
     x->faK = -1;  // no resident hand-off of a failed scan
     set_err("odometry exchange overflow (more NN rounds than slots)");
+    return LEGO_E_DEVICE;
+  }
+  if (x->h_hdr[FH_BAD] & kBadPermutation) {
+    x->faK = -1;
+    set_err("per-ring VoxelGrid: the device sort returned a payload outside its input (device fault)");
     return LEGO_E_DEVICE;
   }
   return LEGO_OK;
@@ -1314,6 +1331,7 @@ static int mo_alloc(lego_ctx* x, int nc, int ns) {
   if (v2cap > m.vgMap2.cap && vg_scratch_alloc(m.vgMap2, v2cap, x, ctx_alloc)) return fail("VoxelGrid scratch");
   if (2 * P > m.vgScan1.cap && vg_scratch_alloc(m.vgScan1, 2 * P, x, ctx_alloc)) return fail("VoxelGrid scratch");
   if (P > m.vgScan2.cap && vg_scratch_alloc(m.vgScan2, P, x, ctx_alloc)) return fail("VoxelGrid scratch");
+  for (VgScratch* v : {&m.vg, &m.vgMap2, &m.vgScan1, &m.vgScan2}) v->err = &m.cnt->derr;  // read after every step
   if (nc > m.mapCornerCap) {
     m.mapCornerCap = nc;
     MA(m.cornerMap, nc); MA(m.cornerMapDS, nc);
@@ -1390,8 +1408,8 @@ int lego_mo_set_map(lego_ctx* x, const lego_point_xyzi* corner, int32_t n_corner
 
 int lego_sort_permutation(lego_ctx* x, const uint32_t* keys, int32_t n, int32_t wave, int32_t* perm,
                           int32_t* heap_pieces) {
-  if (!x || n < 0 || (n > 0 && (!keys || !perm)) || wave < 0 || wave > 3) return LEGO_E_ARG;
-  const int cap = wave == 1 ? 512 : wave == 2 ? 2048 : 8192;
+  const int cap = sort_perm_cap(wave);
+  if (!x || n < 0 || (n > 0 && (!keys || !perm)) || cap < 0) return LEGO_E_ARG;
   if (n > cap) {
     set_err("lego_sort_permutation: n = %d above the mode-%d sort's %d", n, wave, cap);
     return LEGO_E_CAPACITY;
@@ -1457,6 +1475,10 @@ int lego_voxel_grid(lego_ctx* x, const lego_point_xyzi* in, int32_t n, float lea
   HIPCHK(hipEventElapsedTime(&ms, e0, e1));
   if (rc != 0 || vg_read_ctl(x->vgApi, ctl, x->stream) != 0) {
     set_err("VoxelGrid launch failed");
+    return LEGO_E_DEVICE;
+  }
+  if (ctl[10]) {  // C_ERR (lego_vg.hip): a sorted payload outside the cloud
+    set_err("VoxelGrid: the sort returned a payload outside the cloud (device fault)");
     return LEGO_E_DEVICE;
   }
   HIPCHK(hipMemcpy(out, x->vgOut, sizeof(float4) * nOut, hipMemcpyDeviceToHost));
@@ -1530,6 +1552,15 @@ int lego_mo_loop_closure(lego_ctx* x, lego_loop_out* out) {
   if (rs != 0) {
     set_err("loop closure launch failed");
     return LEGO_E_DEVICE;
+  }
+  {  // the history cloud's VoxelGrid error word (MoCounts::derr; the state read above synchronised)
+    int derr = 0;
+    HIPCHK(hipMemcpy(&derr, &m.cnt->derr, sizeof(int), hipMemcpyDeviceToHost));
+    if (derr) {
+      HIPCHK(hipMemset(&m.cnt->derr, 0, sizeof(int)));
+      set_err("loop closure: a VoxelGrid sort returned a payload outside its cloud (device fault)");
+      return LEGO_E_DEVICE;
+    }
   }
   if (!hs.detected) return LEGO_OK;
   out->detected = 1;
@@ -1809,6 +1840,11 @@ int lego_mo_process(lego_ctx* x, const lego_fa_out* in, lego_mo_out* out) {
     if (!x->moFixed) std::memcpy(meta, hb + om, sizeof(meta));
   }
   mo_evprof_print(m);
+  if (hc.derr) {  // a VoxelGrid sort handed back a payload outside its cloud (MoCounts::derr)
+    HIPCHK(hipMemsetAsync(&m.cnt->derr, 0, sizeof(int), s));
+    set_err("scan-to-map: a VoxelGrid sort returned a payload outside its cloud (device fault)");
+    return LEGO_E_DEVICE;
+  }
   if (meta[KF_OVF]) {  // saveKeyFramesAndFactor of this very step found the store full (k_kf_save)
     x->moStoreFull = true;
     set_err("scan-to-map: the keyframe store is full (%d keyframes / %d arena points): this step's keyframe "

@@ -16,13 +16,20 @@
 // others never wait for it; an RCCL or device error once the communicator is
 // in use closes any open group and aborts the communicator (ncclCommAbort),
 // and the communicator is dead from then on.  Only root sizes buffers after
-// the size exchange; it aborts if that fails.
+// the size exchange; it aborts if that fails.  Every wait on the
+// communicator's stream is bounded (LEGO_COMM_TIMEOUT_MS, default 60 s): a
+// peer that never joins a collective makes the call abort the communicator
+// and return LEGO_E_DEVICE naming the wait, instead of blocking the rank.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "lego_loam.h"
@@ -45,6 +52,7 @@ struct lego_comm {
   std::vector<uint64_t> sizes, offs;
   bool haveResult = false, haveHost = false;
   bool dead = false;
+  int timeoutMs = 60000;  // bound of every wait on s (LEGO_COMM_TIMEOUT_MS)
   ~lego_comm() {
     if (device >= 0) (void)hipSetDevice(device);
     if (s) (void)hipStreamSynchronize(s);
@@ -116,7 +124,20 @@ int lego_comm_create(const uint8_t id[128], int32_t nranks, int32_t rank, int32_
   }
   c->sizes.assign(nranks, 0);
   c->offs.assign(nranks + 1, 0);
+  if (const char* e = std::getenv("LEGO_COMM_TIMEOUT_MS")) c->timeoutMs = std::max(1, std::atoi(e));
   *out = c;
+  return LEGO_OK;
+}
+
+int lego_comm_count(lego_comm* c, int32_t* nranks) {
+  if (!c || !nranks) return LEGO_E_ARG;
+  if (!c->nc) {
+    lego_set_error("lego_comm_count: the communicator was aborted");
+    return LEGO_E_STATE;
+  }
+  int n = 0;
+  COMM_NCCL(ncclCommCount(c->nc, &n));
+  *nranks = n;
   return LEGO_OK;
 }
 
@@ -145,6 +166,26 @@ static int comm_abort(lego_comm* c, bool inGroup, const char* what, const char* 
     if (r_ != ncclSuccess) return comm_abort(c, inGroup, #call, ncclGetErrorString(r_)); \
   } while (0)
 
+// Waits for the communicator's stream within c->timeoutMs: polls
+// hipStreamQuery (a peer that never joins leaves the collective's kernel
+// spinning, so an unbounded hipStreamSynchronize would never return).
+static int comm_sync(lego_comm* c, const char* what) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int spin = 0;; ++spin) {
+    const hipError_t e = hipStreamQuery(c->s);
+    if (e == hipSuccess) return LEGO_OK;
+    if (e != hipErrorNotReady) return comm_abort(c, false, what, hipGetErrorString(e));
+    const auto ms =
+        std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
+    if (ms > c->timeoutMs) {
+      char why[96];
+      std::snprintf(why, sizeof(why), "timed out after %lld ms (a peer never joined?)", (long long)ms);
+      return comm_abort(c, false, what, why);
+    }
+    if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
 int lego_comm_gather_handoff_ex(lego_comm* c, lego_ctx* ctx, int32_t root, uint32_t flags) {
   if (!c || !ctx || root < 0 || root >= c->nranks || (flags & ~LEGO_COMM_DEVICE_RESULT)) return LEGO_E_ARG;
   if (c->dead) {
@@ -154,7 +195,7 @@ int lego_comm_gather_handoff_ex(lego_comm* c, lego_ctx* ctx, int32_t root, uint3
   c->haveResult = c->haveHost = false;
   COMM_HIP(hipSetDevice(c->device));
   // the previous gather's send reads ctx's packet buffer, which the pack reuses
-  COMM_TRY_HIP(hipStreamSynchronize(c->s), false);
+  if (comm_sync(c, "previous gather") != LEGO_OK) return LEGO_E_DEVICE;
   const void* pkt = nullptr;
   uint64_t bytes = 0;
   const int packSt = lego_handoff_pack(ctx, &pkt, &bytes);  // complete on return
@@ -165,7 +206,7 @@ int lego_comm_gather_handoff_ex(lego_comm* c, lego_ctx* ctx, int32_t root, uint3
   if (isRoot) {
     COMM_TRY_HIP(hipMemcpyAsync(c->sizes.data(), c->dSizes, sizeof(uint64_t) * c->nranks, hipMemcpyDeviceToHost, c->s),
                  false);
-    COMM_TRY_HIP(hipStreamSynchronize(c->s), false);
+    if (comm_sync(c, "ncclGather of the packet sizes") != LEGO_OK) return LEGO_E_DEVICE;
     for (int r = 0; r < c->nranks; ++r) c->offs[r + 1] = c->offs[r] + ((c->sizes[r] + 255) & ~(uint64_t)255);
     const size_t need = c->offs[c->nranks];
     if (need > c->recvCap) {
@@ -201,7 +242,7 @@ int lego_comm_gather_handoff_ex(lego_comm* c, lego_ctx* ctx, int32_t root, uint3
       }
       COMM_TRY_HIP(hipMemcpyAsync(c->hRecv, c->dRecv, need, hipMemcpyDeviceToHost, c->s), false);
     }
-    COMM_TRY_HIP(hipStreamSynchronize(c->s), false);
+    if (comm_sync(c, "packet transfer") != LEGO_OK) return LEGO_E_DEVICE;
     c->haveHost = isRoot;
   }
   c->haveResult = isRoot;
@@ -226,8 +267,7 @@ int lego_comm_wait(lego_comm* c) {
   if (!c) return LEGO_E_ARG;
   if (c->dead) return LEGO_E_STATE;
   COMM_HIP(hipSetDevice(c->device));
-  COMM_TRY_HIP(hipStreamSynchronize(c->s), false);
-  return LEGO_OK;
+  return comm_sync(c, "lego_comm_wait");
 }
 
 int lego_comm_handoff_device(lego_comm* c, int32_t rank, const void** dpacket, uint64_t* bytes) {

@@ -97,6 +97,11 @@ struct GatedBufs {
   int* n;          // [2] ground, pure counts
 };
 
+// BatchBufs::bad bits (per scan, zeroed before each batch): the host returns
+// LEGO_E_NOT_DENSE for the first, LEGO_E_DEVICE for the second (a VoxelGrid
+// sort handed back a payload outside its input: it cannot happen unless the
+// device's LDS or registers are corrupted, and is never clamped into range).
+constexpr int kBadNotDense = 1, kBadPermutation = 2;
 struct BatchBufs {
   int B;
   const ImuSnap* imu;        // [B] or null: no IMU message delivered to this batch's stream(s)
@@ -116,7 +121,7 @@ struct BatchBufs {
   int* csize;                // [B*P]
   unsigned long long* rowmask;  // [B*P*2]
   float* rawang;             // [B*2]
-  int* bad;                  // [B]  non-finite xyz seen (imageProjection.cpp:174-176)
+  int* bad;                  // [B]  kBadNotDense: non-finite xyz seen (imageProjection.cpp:174-176); kBadPermutation
   // ---- segmented cloud + cloud_info
   float4* seg;               // [B*P]
   uint8_t* gflag;            // [B*P]

@@ -16,6 +16,7 @@
 //                 stream order and re-runs ring 0 where the real carry differs.
 //   k_fa_compact  concatenates the per-ring slots in ring order.
 #include <climits>
+#include <cstdio>
 
 #include "lego_device.h"
 #include "lego_introsort.h"
@@ -847,13 +848,21 @@ __device__ __forceinline__ void extract_ring(const BatchBufs& bb, const DevCfg& 
 // the less-flat set's size to the voxels'.
 // the per-voxel centroid of PCL's VoxelGrid: the points of sorted positions
 // [t, u) (one voxel), summed in that order from the ring's slot
+// A payload at or past K cannot come out of a sort (every form only moves
+// the payloads 0..K-1 it was given); if one does, the scan's error word gets
+// kBadPermutation (the host returns LEGO_E_DEVICE) and the addend is skipped.
 __device__ __forceinline__ float4 lfv_centroid(const float4* slot, const uint16_t* val, const uint32_t* key, int t,
-                                               int K) {
+                                               int K, int* bad) {
   const uint32_t k = key[t];
   float cx = 0, cy = 0, cz = 0, ci = 0;
   int u = t;
   for (; u < K && key[u] == k; ++u) {
-    const float4 q = slot[min((int)val[u], K - 1)];  // bounded: a bad permutation fails parity, never faults
+    const int vi = (int)val[u];
+    if (vi >= K) {
+      atomicOr(bad, kBadPermutation);
+      continue;
+    }
+    const float4 q = slot[vi];
     cx += q.x; cy += q.y; cz += q.z; ci += q.w;
   }
   const float n = (float)(u - t);
@@ -925,7 +934,7 @@ __device__ __forceinline__ void lfv_wave(const BatchBufs& bb, const DevCfg& c, i
     const bool head = t < K && (t == 0 || key[t] != key[t - 1]);
     const unsigned long long m = __ballot(head);
     if (head) {
-      cen[j] = lfv_centroid(slot, val, key, t, K);
+      cen[j] = lfv_centroid(slot, val, key, t, K, bb.bad + b);
       at[j] = outc + (int)__popcll(m & below);
     }
     outc += (int)__popcll(m);
@@ -937,7 +946,6 @@ __device__ __forceinline__ void lfv_wave(const BatchBufs& bb, const DevCfg& c, i
   if (lane == 0) cnt[3] = outc | (K << 16);
 }
 
-constexpr int kLfvMaxPer = 8;  // voxels per thread (H <= kLfvMaxPer * kExtractThreads)
 constexpr int kLfvBlockRings = 2;  // rings per large-ring workgroup (k_lf_voxel; 1 / 2 / 4 / 8: fleet 254 / 256 / 245 / 253 k)
 // A launch of at most this many rings leaves part of the device idle (one
 // scan through the node API, C2's 100-scan batch beside the odometry, C3):
@@ -949,11 +957,19 @@ constexpr int kLfvSmallLaunchRings = 4096;
 // node fa 0.30 -> 0.28 ms; a C2 batch's VoxelGrid 0.67 -> 1.52 ms that way
 // (profiles/r04_ab_lfv_wide.txt)
 constexpr int kLfvWideLaunchRings = 128;
+#ifndef LFV_DIAG
+#define LFV_DIAG 0
+#endif
+#if LFV_DIAG
+__device__ int g_lfv_diag;  // printed violations (capped)
+#endif
 __host__ __device__ inline size_t lfvox_lds_bytes(int H) {
   return (((size_t)H * 6 + 15) & ~(size_t)15) + vg_sort_scratch_bytes(H, kExtractThreads) + 64;
 }
+template <int T>
 __device__ __forceinline__ void lfv_block(const BatchBufs& bb, const DevCfg& c, int ring, int b, int waveMax,
                           unsigned char* lds_raw) {
+  constexpr int MP = (kMaxHorizon + T - 1) / T;  // voxels per thread (<= H of them per ring)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int H = c.H;
   uint32_t* key = (uint32_t*)lds_raw;
@@ -1007,13 +1023,29 @@ __device__ __forceinline__ void lfv_block(const BatchBufs& bb, const DevCfg& c, 
     val[t] = (uint16_t)t;
   }
   __syncthreads();
+  // The LDS-id form of the block sort.  The register form (vg_block_sort,
+  // segment ids in registers, five barriers per level instead of seven) is
+  // not built into this kernel: both builds of it here spilled under the
+  // 128-VGPR cap and both faulted on the GPU (round 4's
+  // 256-thread build; round 5's 1024-thread instance, a VM fault on VLS-128
+  // scan 0, gpurun_out r05a / r05c, profiles/r05_lfv_fault.txt), while the
+  // same sort is exact at both block sizes in kernels of its own.
   vg_block_sort_sid(vg_sort_carve(key, val, sc, K, (int)blockDim.x), K, -1, nullptr, true);
+#if LFV_DIAG  // diagnostic build (scripts/lfv_diag.sh): the sort's output checked before any use
+  for (int t = tid; t < K; t += blockDim.x) {
+    const bool badv = (int)val[t] >= K, bado = t > 0 && key[t - 1] > key[t];
+    if ((badv || bado) && atomicAdd(&g_lfv_diag, 1) < 24)
+      printf("LFV_DIAG sort T=%d b=%d ring=%d K=%d t=%d val=%d key[t-1]=%u key[t]=%u\n", (int)blockDim.x, b, ring,
+             K, t, (int)val[t], t > 0 ? key[t - 1] : 0u, key[t]);
+  }
+  __syncthreads();
+#endif
   // centroids into registers (every read of the slot done), then over the slot
-  float4 cen[kLfvMaxPer];
-  int at[kLfvMaxPer];
+  float4 cen[MP];
+  int at[MP];
   int outc = 0;
 #pragma unroll
-  for (int j = 0; j < kLfvMaxPer; ++j) {
+  for (int j = 0; j < MP; ++j) {
     at[j] = -1;
     const int t = j * (int)blockDim.x + tid;
     if (j * (int)blockDim.x >= K) continue;  // uniform
@@ -1021,14 +1053,24 @@ __device__ __forceinline__ void lfv_block(const BatchBufs& bb, const DevCfg& c, 
     int tot;
     const int r = block_rank(head, misc, &tot);
     if (head) {
-      cen[j] = lfv_centroid(slot, val, key, t, K);
+      cen[j] = lfv_centroid(slot, val, key, t, K, bb.bad + b);
       at[j] = outc + r;
     }
     outc += tot;
   }
   __syncthreads();
+#if LFV_DIAG
+  for (int j = 0; j < MP; ++j)
+    if (at[j] >= K && atomicAdd(&g_lfv_diag, 1) < 24) {
+      printf("LFV_DIAG store T=%d b=%d ring=%d K=%d j=%d at=%d outc=%d\n", (int)blockDim.x, b, ring, K, j, at[j],
+             outc);
+      at[j] = -1;
+    }
+  if (tid == 0 && (outc > K || outc < 0) && atomicAdd(&g_lfv_diag, 1) < 24)
+    printf("LFV_DIAG count T=%d b=%d ring=%d K=%d outc=%d\n", (int)blockDim.x, b, ring, K, outc);
+#endif
 #pragma unroll
-  for (int j = 0; j < kLfvMaxPer; ++j)
+  for (int j = 0; j < MP; ++j)
     if (at[j] >= 0) slot[at[j]] = cen[j];
   if (tid == 0) cnt[3] = outc | (K << 16);
 }
@@ -1039,10 +1081,8 @@ __device__ __forceinline__ void lfv_block(const BatchBufs& bb, const DevCfg& c, 
 // larger rings with the whole workgroup (lfv_block), workgroup k the rings
 // k, k + gb, ... (gb < N: fewer workgroups that find no large ring).  g4 = 0
 // (diagnostic LEGO_LFV_WAVE=0): every ring by a workgroup.
-#ifndef LFV_MINB
-#define LFV_MINB 4
-#endif
 // T = 1024 (small launches): every ring by a whole workgroup (g4 = 0).
+// LFV_MINB: lego_vgsort.h.
 template <int T>
 __global__ void __launch_bounds__(T, T == kExtractThreads ? LFV_MINB : 1) k_lf_voxel(BatchBufs bb, DevCfg c, int g4,
                                                                                    int gb) {
@@ -1053,7 +1093,7 @@ __global__ void __launch_bounds__(T, T == kExtractThreads ? LFV_MINB : 1) k_lf_v
     return;
   }
   for (int ring = (int)blockIdx.x - g4; ring < c.N; ring += gb) {
-    lfv_block(bb, c, ring, b, g4 > 0 ? kVgWaveMax : 0, lds_raw);
+    lfv_block<T>(bb, c, ring, b, g4 > 0 ? kVgWaveMax : 0, lds_raw);
     __syncthreads();  // the next ring reuses the LDS
   }
 }
@@ -1147,6 +1187,11 @@ __global__ void k_fa_compact(BatchBufs bb, DevCfg c) {
     }
   }
   __syncthreads();
+#if LFV_DIAG
+  if (tid == 0 && ((cnt[r * 4 + 3] & 0xffff) > c.H || off[3] + (cnt[r * 4 + 3] & 0xffff) > c.P) &&
+      atomicAdd(&g_lfv_diag, 1) < 24)
+    printf("LFV_DIAG compact b=%d ring=%d cnt3=%x off3=%d\n", b, r, cnt[r * 4 + 3], off[3]);
+#endif
   const size_t rb = (size_t)b * c.N + r;
   for (int t = tid; t < cnt[r * 4 + 0]; t += blockDim.x)
     bb.f_sharp[(size_t)b * c.N * kSharpPerRing + off[0] + t] = bb.r_sharp[rb * kSharpPerRing + t];
@@ -1168,19 +1213,33 @@ __global__ void k_fa_init(BatchBufs bb, int B) {
   }
 }
 
+// LEGO_FA_SYNCCHECK (diagnostic, host only): synchronise after every launch
+// of launch_fa and name the kernel whose execution returned an error.
+static void fa_synccheck(hipStream_t s, const char* what) {
+  static const bool on = std::getenv("LEGO_FA_SYNCCHECK") != nullptr;
+  if (!on) return;
+  const hipError_t e = hipStreamSynchronize(s);
+  std::fprintf(stderr, "LEGO_FA_SYNCCHECK %s: %s\n", what, hipGetErrorString(e));
+}
+
 void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_carry, hipStream_t s,
                StageTimer* tm) {
   tm->mark("fa.deskew", s);
   k_fa_init<<<(B + 255) / 256, 256, 0, s>>>(bb, B);
+  fa_synccheck(s, "k_fa_init");
   dim3 gpts((c.P + 255) / 256, B);
   k_fa_half<<<gpts, 256, 0, s>>>(bb, c);
+  fa_synccheck(s, "k_fa_half");
   if (bb.imu) k_fa_imu_start<<<(B + 63) / 64, 64, 0, s>>>(bb, c);
   k_fa_point<<<gpts, 256, 0, s>>>(bb, c);
+  fa_synccheck(s, "k_fa_point");
   tm->mark("fa.extract", s);
   const size_t lds = extract_lds_bytes(c.H);
   k_extract<<<dim3(c.N, B), kExtractThreads, lds, s>>>(bb, c);
+  fa_synccheck(s, "k_extract");
   tm->mark("fa.fixup", s);
   k_fa_fixup<<<S, kExtractThreads, lds, s>>>(bb, c, B / S, d_carry);
+  fa_synccheck(s, "k_fa_fixup");
   tm->mark("fa.voxel", s);
   static const bool waveOn = !std::getenv("LEGO_LFV_WAVE") || std::atoi(std::getenv("LEGO_LFV_WAVE")) != 0;
   const int g4 = waveOn ? (c.N + 3) / 4 : 0;
@@ -1192,15 +1251,19 @@ void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_ca
   // a launch that leaves the device idle but for itself (a node call): every
   // ring by a 1024-thread workgroup, the sort's levels over four times the
   // lanes (LEGO_LFV_WIDE, A/B knob)
-  static const int wideEnv = std::getenv("LEGO_LFV_WIDE") ? std::atoi(std::getenv("LEGO_LFV_WIDE")) : -1;
+  // (read per launch, so a test can switch it)
+  const char* wideS = std::getenv("LEGO_LFV_WIDE");
+  const int wideEnv = wideS ? std::atoi(wideS) : -1;
   const bool wide = wideEnv >= 0 ? wideEnv != 0 : B * c.N <= kLfvWideLaunchRings;
   if (wide)
     k_lf_voxel<1024><<<dim3(c.N, B), 1024, lfvox_lds_bytes(c.H), s>>>(bb, c, 0, c.N);
   else
     k_lf_voxel<kExtractThreads>
         <<<dim3(g4 + gb, B), kExtractThreads, std::max(kLfvWaveLds, lfvox_lds_bytes(c.H)), s>>>(bb, c, g4, gb);
+  fa_synccheck(s, wide ? "k_lf_voxel<1024>" : "k_lf_voxel<256>");
   tm->mark("fa.compact", s);
   k_fa_compact<<<dim3(c.N, B), 256, 0, s>>>(bb, c);
+  fa_synccheck(s, "k_fa_compact");
 }
 
 }  // namespace lego

@@ -37,7 +37,7 @@ __global__ void k_project(BatchBufs bb, DevCfg c) {
   const uint16_t ring = pp->ring;
   const float x = xyz.x, y = xyz.y, z = xyz.z;
   if (!__builtin_isfinite(x) || !__builtin_isfinite(y) || !__builtin_isfinite(z)) {
-    bb.bad[b] = 1;  // the host rejects the batch with LEGO_E_NOT_DENSE
+    bb.bad[b] = kBadNotDense;  // the host rejects the batch with LEGO_E_NOT_DENSE
     return;
   }
   if (i == 0) bb.rawang[2 * b] = -lego_atan2f(y, x);                   // :201

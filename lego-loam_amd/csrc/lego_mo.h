@@ -24,7 +24,7 @@ struct MoState {
 struct MoCounts {
   int cornerMapDS, surfMapDS;
   int cornerDS, surfDS, outlierDS, surfTotal, surfTotalDS;
-  int _pad;
+  int derr;  // the step's VoxelGrids' error word (VgScratch::err): nonzero = a sort returned a foreign payload
 };
 
 // VoxelGrid / index-build scratch for clouds of up to cap points (lego_vg.hip).
@@ -45,6 +45,12 @@ struct VgScratch {
   int* ctl;         // [16] counters (lego_vg.hip C_*)
   int* mm;          // [6] ordered-int min / max
   int* overflow;    // [1]
+  // error word: set (atomicOr 1) when a sorted payload lies outside the cloud,
+  // which no sort can produce unless the device's LDS / registers were
+  // corrupted; the payload is then not read.  ctl + C_ERR after
+  // vg_scratch_alloc (lego_voxel_grid reads it per call); a mapping context
+  // points its scratches at MoCounts::derr (read after every step).
+  int* err;
   int cap, capBig, capTiles, capLoc, capScanTiles;
 };
 
@@ -194,9 +200,11 @@ void mo_evprof_print(MoDev& m);  // after the step's stream is synchronised
 int vg_read_ctl(const VgScratch& v, int* ctl16, hipStream_t s);
 int mo_set_map_device(MoDev& m, int nCornerMap, int nSurfMap, hipStream_t s);
 // libstdc++'s std::sort permutation of (key, index) by key on the device
-// (lego_vg.hip): wave = 0 the block sort (n <= 8192), 1 one wave's (n <= 512);
-// heap: the heap-sorted pieces are counted into it.
-int sort_perm_device(const uint32_t* keys, int n, int wave, int* perm, int* heap, hipStream_t s);
+// (lego_vg.hip): mode 0..8 picks the form, block size and sum-order rule
+// (lego_sort_permutation); heap: the heap-sorted pieces are counted into it.
+// sort_perm_cap: the largest n of a mode, -1 for an unknown mode.
+int sort_perm_cap(int mode);
+int sort_perm_device(const uint32_t* keys, int n, int mode, int* perm, int* heap, hipStream_t s);
 int index_build_device(const float4* pts, int n, const int* nDev, MoIndex& ix, const VgScratch& v, hipStream_t s);
 // One performLoopClosure over the keyframe store (tnow = timeLaserOdometry).
 // Returns MO_OK (hostState holds the result), MO_E_LAUNCH, or MO_E_MAP_CAP when

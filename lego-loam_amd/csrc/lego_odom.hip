@@ -1368,7 +1368,7 @@ __device__ __forceinline__ bool x_point(const unsigned long long* xh, int i, uns
 // flags, then one agent acquire, then plain loads.  Within a launch no slot is
 // written twice (ring_next), so a slot is never read before it is complete.
 // The slot of the next hand-off: the next of the ring, skipping the indexes'
-// snapshot (k_ring_prep replays the same picks).
+// snapshot the launch started with (k_ring_prep replays the same picks).
 __device__ __forceinline__ int ring_next(unsigned seq, int snapBuf, int R, unsigned* seqOut) {
   const int snap = snapBuf >= 2 ? snapBuf - 2 : -1;
   int s = (int)(seq % (unsigned)R);
@@ -1963,7 +1963,11 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     // (whole 64-point chunks) and this workgroup's claim on its own share
     const bool ringMode = RING && ob.ring != nullptr && !fits;
     unsigned rseq = 0;
-    const int rslot = ringMode ? ring_next(st->seq, st->snapBuf, ob.ringR, &rseq) : -1;
+    // the skip is the LAUNCH's input snapshot (ob.stIn), the slot k_ring_prep
+    // left alone: a snapshot this launch makes is a slot already behind seq,
+    // never picked again within the launch (<= K + 1 consecutive picks of
+    // R = K + 3), so the kernel replays prep's picks exactly
+    const int rslot = ringMode ? ring_next(st->seq, ob.stIn->snapBuf, ob.ringR, &rseq) : -1;
     const int rn = F.nLF + F.nLS;
     const int rper = max(64, ((rn + ob.G - 1) / ob.G + 63) & ~63);
     const int rnsh = (rn + rper - 1) / rper;

@@ -48,7 +48,8 @@ constexpr int kVgRoundsMax = 16;
 constexpr int kVgPlanThreads = 1024;
 
 // VgScratch::ctl words
-enum { C_M = 0, C_D = 1, C_NB = 2, C_NT = 3, C_NLOC = 4, C_NONFIN = 5, C_NOUT = 6, C_SLOW = 7, C_HEAP = 8, C_NLOCB = 9 };
+enum { C_M = 0, C_D = 1, C_NB = 2, C_NT = 3, C_NLOC = 4, C_NONFIN = 5, C_NOUT = 6, C_SLOW = 7, C_HEAP = 8, C_NLOCB = 9,
+       C_ERR = 10 };
 
 // The local list: segments of <= kVgSplit keys from the front of loc
 // (k_vg_local_small's, C_NLOC), larger ones from its back (k_vg_local's,
@@ -573,7 +574,9 @@ __device__ void vg_local_sort(const VgScratch& v, uint32_t* key, uint16_t* lv, u
   vg_block_sort(vg_sort_carve(key, lv, sc, m, (int)blockDim.x), m, depth, v.ctl + C_HEAP, true);
   for (int i = threadIdx.x; i < m; i += blockDim.x) {
     v.keys[s + i] = key[i];
-    key[i] = (uint32_t)v.vals[s + min((int)lv[i], m - 1)];  // bounded (a bad permutation fails parity, never faults)
+    const int li = (int)lv[i];
+    if (li >= m) atomicOr(v.err, 1);  // cannot come out of the sort (VgScratch::err): reported, never read
+    key[i] = (uint32_t)v.vals[s + (li < m ? li : i)];
   }
   __syncthreads();
   for (int i = threadIdx.x; i < m; i += blockDim.x) v.vals[s + i] = (int)key[i];
@@ -687,7 +690,12 @@ __global__ void __launch_bounds__(kHeadTile) k_vg_emit(const float4* in, int n, 
   float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
   int u = t;
   for (; u < m && v.keys[u] == k; ++u) {
-    const float4 p = in[min(v.vals[u], nn - 1)];  // bounded (see vg_local_sort)
+    const int vi = v.vals[u];
+    if ((unsigned)vi >= (unsigned)nn) {  // see vg_local_sort: reported, never read
+      atomicOr(v.err, 1);
+      continue;
+    }
+    const float4 p = in[vi];
     c0 += p.x; c1 += p.y; c2 += p.z; c3 += p.w;
   }
   const float cnt = (float)(u - t);
@@ -776,6 +784,7 @@ int vg_scratch_alloc(VgScratch& v, int cap, void* ctx, int (*alloc)(void* ctx, v
   };
   for (auto& a : as)
     if (alloc(ctx, a.p, a.b)) return -1;
+  v.err = v.ctl + C_ERR;
   return 0;
 }
 
@@ -803,30 +812,55 @@ __global__ void __launch_bounds__(1024) k_sort_perm(const uint32_t* keys, int n,
   vg_block_sort(vg_sort_carve(key, val, sc, n, (int)blockDim.x), n, -1, heap, wave >= 2);
   for (int i = threadIdx.x; i < n; i += blockDim.x) perm[i] = val[i];
 }
-// k_lf_voxel's form (segment ids in LDS, sumOrder), 256 threads; a kernel of
-// its own so that neither form's registers weigh on the other
-__global__ void __launch_bounds__(256) k_sort_perm_sid(const uint32_t* keys, int n, int* perm, int* heap) {
+// Either block form at either block size (modes 2, 4-8), compiled under the
+// register budget of the kernel that runs it in the product: 256 threads with
+// k_lf_voxel's LFV_MINB workgroups per CU (the 128-VGPR build that spills),
+// 1024 threads with one.  REG: segment ids in registers (vg_block_sort) or in
+// LDS (vg_block_sort_sid).  One instance per kernel, so that no form's
+// registers weigh on another's.
+template <int T, bool REG, bool SUM>
+__global__ void __launch_bounds__(T, T == 256 ? LFV_MINB : 1) k_sort_perm_form(const uint32_t* keys, int n, int* perm,
+                                                                            int* heap) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   uint32_t* key = (uint32_t*)lds_raw;
   uint16_t* val = (uint16_t*)(lds_raw + (size_t)4 * kSortPermBlockMax);
   unsigned char* sc = lds_raw + (size_t)6 * kSortPermBlockMax;
   for (int i = threadIdx.x; i < n; i += blockDim.x) { key[i] = keys[i]; val[i] = (uint16_t)i; }
   __syncthreads();
-  vg_block_sort_sid(vg_sort_carve(key, val, sc, n, (int)blockDim.x), n, -1, heap, true);
+  if (REG) vg_block_sort(vg_sort_carve(key, val, sc, n, (int)blockDim.x), n, -1, heap, SUM);
+  else vg_block_sort_sid(vg_sort_carve(key, val, sc, n, (int)blockDim.x), n, -1, heap, SUM);
   for (int i = threadIdx.x; i < n; i += blockDim.x) perm[i] = val[i];
 }
 size_t sort_perm_lds_bytes() { return (size_t)6 * kSortPermBlockMax + vg_sort_scratch_bytes(kSortPermBlockMax, 1024); }
-// wave = 2 / 3: the block sort as the VoxelGrids run it (sumOrder: heap pieces
-// whose centroids do not depend on their order ranked stably) with 256 threads
-// in k_lf_voxel's form (vg_block_sort_sid, its large rings, n <= 2048) / 1024
-// threads in the mapping VoxelGrids' form (vg_block_sort, n <= 8192); wave = 0
-// the exact permutation of the mapping form.
-int sort_perm_device(const uint32_t* keys, int n, int wave, int* perm, int* heap, hipStream_t s) {
-  const int cap = wave == 1 ? kVgWaveMax : wave == 2 ? vg_sort_max(256) : kSortPermBlockMax;
-  if (n < 0 || n > cap || wave < 0 || wave > 3) return -1;
+// Modes (lego_sort_permutation):
+//   0 register form, 1024 threads, exact      3 register form, 1024, sumOrder
+//   1 one wave (n <= kVgWaveMax)               2 LDS-id form, 256, sumOrder (k_lf_voxel's)
+//   4 register form, 256, exact                5 register form, 256, sumOrder
+//   6 LDS-id form, 256, exact                  7 LDS-id form, 1024, exact
+//   8 LDS-id form, 1024, sumOrder
+// 256-thread forms hold n <= vg_sort_max(256) = 2048, 1024-thread ones 8192.
+int sort_perm_cap(int mode) {
+  switch (mode) {
+    case 1: return kVgWaveMax;
+    case 2: case 4: case 5: case 6: return vg_sort_max(256);
+    case 0: case 3: case 7: case 8: return kSortPermBlockMax;
+    default: return -1;
+  }
+}
+int sort_perm_device(const uint32_t* keys, int n, int mode, int* perm, int* heap, hipStream_t s) {
+  const int cap = sort_perm_cap(mode);
+  if (cap < 0 || n < 0 || n > cap) return -1;
   if (n == 0) return 0;
-  if (wave == 2) k_sort_perm_sid<<<1, 256, sort_perm_lds_bytes(), s>>>(keys, n, perm, heap);
-  else k_sort_perm<<<1, 1024, sort_perm_lds_bytes(), s>>>(keys, n, wave, perm, heap);
+  const size_t lds = sort_perm_lds_bytes();
+  switch (mode) {
+    case 0: case 1: case 3: k_sort_perm<<<1, 1024, lds, s>>>(keys, n, mode, perm, heap); break;
+    case 2: k_sort_perm_form<256, false, true><<<1, 256, lds, s>>>(keys, n, perm, heap); break;
+    case 4: k_sort_perm_form<256, true, false><<<1, 256, lds, s>>>(keys, n, perm, heap); break;
+    case 5: k_sort_perm_form<256, true, true><<<1, 256, lds, s>>>(keys, n, perm, heap); break;
+    case 6: k_sort_perm_form<256, false, false><<<1, 256, lds, s>>>(keys, n, perm, heap); break;
+    case 7: k_sort_perm_form<1024, false, false><<<1, 1024, lds, s>>>(keys, n, perm, heap); break;
+    case 8: k_sort_perm_form<1024, false, true><<<1, 1024, lds, s>>>(keys, n, perm, heap); break;
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -131,6 +131,13 @@ struct VgHeap {
 
 constexpr int kVgLeaf = 16;  // _S_threshold
 
+// k_lf_voxel's 256-thread workgroups are built for LFV_MINB workgroups per CU
+// (a 128-VGPR budget); the permutation tests compile their 256-thread sorts
+// under the same bound (lego_vg.hip k_sort_perm_form).
+#ifndef LFV_MINB
+#define LFV_MINB 4
+#endif
+
 // bits 0..b of a word
 __device__ __forceinline__ uint32_t bi_mask_le(int b) { return b == 31 ? ~0u : ((2u << b) - 1); }
 
@@ -604,8 +611,10 @@ __device__ void vg_block_sort(const VgSortLds<V>& S, int n, int depth = -1, int*
 
 // The same sort with the positions' segment ids in LDS (S.sid) instead of
 // registers: seven barriers per level and more LDS round trips, twelve
-// fewer VGPRs.  k_lf_voxel keeps it: at four workgroups per CU its 128-VGPR
-// budget does not hold the register form without spills.
+// fewer VGPRs.  k_lf_voxel keeps it: inside that kernel the register form
+// spilled under the 128-VGPR cap at both block sizes, and both such builds
+// faulted on the GPU, though the form itself is exact in
+// kernels of its own (modes 0, 3, 4, 5 of lego_sort_permutation).
 template <typename V>
 __device__ void vg_block_sort_sid(const VgSortLds<V>& S, int n, int depth = -1, int* heapStat = nullptr,
                               bool sumOrder = false) {

@@ -277,7 +277,7 @@ HIP_EXPORTS = ["lego_sensor_preset", "lego_create", "lego_fleet_create", "lego_d
                "lego_odom_profile", "lego_extract_profile", "lego_handoff_pack", "lego_handoff_pack_into", "lego_handoff_unpack", "lego_comm_unique_id",
                "lego_comm_create", "lego_comm_destroy", "lego_comm_gather_handoff", "lego_comm_handoff",
                "lego_comm_gather_handoff_ex", "lego_comm_wait", "lego_comm_handoff_device", "lego_comm_abort",
-               "lego_voxel_grid", "lego_voxel_grid_stats", "lego_sort_permutation"]
+               "lego_comm_count", "lego_voxel_grid", "lego_voxel_grid_stats", "lego_sort_permutation"]
 
 
 def hip_lib() -> C.CDLL:
@@ -325,6 +325,7 @@ def hip_lib() -> C.CDLL:
     lib.lego_comm_gather_handoff_ex.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_uint32]
     lib.lego_comm_wait.argtypes = [C.c_void_p]
     lib.lego_comm_abort.argtypes = [C.c_void_p]
+    lib.lego_comm_count.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
     lib.lego_comm_handoff_device.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]
     lib.lego_voxel_grid.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_float, C.c_void_p,
                                     C.POINTER(C.c_int32)]
@@ -729,9 +730,11 @@ class Lego:
                 "device_us")
         return out[:n.value].copy(), dict(zip(keys, list(st)))
 
-    def sort_permutation(self, keys: np.ndarray, wave: bool = False) -> tuple[np.ndarray, int]:
+    def sort_permutation(self, keys: np.ndarray, wave: bool | int = False) -> tuple[np.ndarray, int]:
         """lego_sort_permutation: std::sort's permutation of (key, index) by key
-        on the device (block or one-wave sort) and the heap-sorted piece count."""
+        on the device and the heap-sorted piece count; `wave` is the mode
+        (False / 0: block sort, True / 1: one wave, 2..8: the block sort's
+        forms and rules, lego_loam.h)."""
         keys = np.ascontiguousarray(keys, dtype=np.uint32)
         perm = np.zeros(max(len(keys), 1), np.int32)
         heap = C.c_int32()

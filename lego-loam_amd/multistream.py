@@ -14,6 +14,10 @@ xGMI; the CPU tests drive the same code over gloo.
 from __future__ import annotations
 
 import ctypes as C
+import os
+import sys
+import threading
+import time
 
 import numpy as np
 
@@ -152,6 +156,56 @@ def native_gather_handoff(L, comm, ctx, root: int = 0, device: bool = False):
     return out
 
 
+class Watchdog:
+    """Ends a rank that stops making progress, with a message that names the
+    step and phase it stalled in, instead of leaving it (and the ranks waiting
+    on it in a collective) to the launcher's time limit.
+
+    `mark(step, phase)` records progress; a daemon thread checks every
+    `poll_s` seconds and, once `bound_s` seconds pass without a mark while
+    armed, writes one line to stderr and calls os._exit(exit_code) — the
+    process ends where it stands (no re-exec, no interpreter teardown that
+    could block on the device or a collective).  `disarm()` stops the checks.
+    A rank whose peer died is itself stuck in that collective until its own
+    bound: every rank exits non-zero within about bound_s."""
+
+    def __init__(self, bound_s: float, rank: int = 0, exit_code: int = 3, poll_s: float = 0.25, out=None):
+        self.bound_s, self.rank, self.exit_code, self.poll_s = float(bound_s), rank, exit_code, poll_s
+        self.out = out if out is not None else sys.stderr
+        self._lock = threading.Lock()
+        self._t = time.monotonic()
+        self._where = (None, "start")
+        self._armed = True
+        self._thread = threading.Thread(target=self._run, name="lego-watchdog", daemon=True)
+        self._thread.start()
+
+    def mark(self, step, phase: str) -> None:
+        with self._lock:
+            self._t = time.monotonic()
+            self._where = (step, phase)
+
+    def disarm(self) -> None:
+        with self._lock:
+            self._armed = False
+
+    def _run(self) -> None:
+        while True:
+            time.sleep(self.poll_s)
+            with self._lock:
+                if not self._armed:
+                    return
+                idle = time.monotonic() - self._t
+                step, phase = self._where
+            if idle > self.bound_s:
+                try:
+                    self.out.write(f"lego watchdog: rank {self.rank} made no progress for {idle:.1f} s "
+                                   f"(bound {self.bound_s:g} s) in step {step}, phase '{phase}'; exiting "
+                                   f"with status {self.exit_code}\n")
+                    self.out.flush()
+                finally:
+                    os._exit(self.exit_code)
+
+
 def agree(dist, ok: bool, group=None) -> bool:
     """True on every rank iff `ok` is True on every rank (an all-reduce of a
     failure flag over `group`, the host control channel).  Raises if the
@@ -183,6 +237,10 @@ class HandoffTransport:
         self.errors = self._errors(native_error) if not self.native else []
         self.switched_at = 0 if self.errors else None  # the step from which the fallback runs (None: never switched)
         self.steps = 0
+        # this rank's host seconds in the step's gather and in the agreement
+        # after it, summed over steps (bench.py reports them per step)
+        self.t_gather = 0.0
+        self.t_agree = 0.0
 
     def _errors(self, mine):
         box = [None] * self.dist.get_world_size()
@@ -193,11 +251,16 @@ class HandoffTransport:
         """One step's gather; returns (transport name, rank 0's result)."""
         out, err = None, None
         if self.native:
+            t0 = time.perf_counter()
             try:
                 out = native()
             except Exception as e:  # noqa: BLE001
                 err = f"step {self.steps}: {e}"
-            if agree(self.dist, err is None, self.ctrl):
+            t1 = time.perf_counter()
+            ok = agree(self.dist, err is None, self.ctrl)
+            self.t_gather += t1 - t0
+            self.t_agree += time.perf_counter() - t1
+            if ok:
                 self.steps += 1
                 return "native", out
             self.native = False
@@ -205,7 +268,10 @@ class HandoffTransport:
             self.errors = self._errors(err)
             abort()
         self.steps += 1
-        return "fallback", fallback()
+        t0 = time.perf_counter()
+        out = fallback()
+        self.t_gather += time.perf_counter() - t0
+        return "fallback", out
 
     @property
     def name(self) -> str:

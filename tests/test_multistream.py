@@ -247,3 +247,62 @@ def test_handoff_transport_is_collective(tmp_path, fail_rank, fail_step, create_
     mp.spawn(_transport_worker, args=(2, _free_port(), str(out), fail_rank, fail_step, create_fail), nprocs=2,
              join=True)
     assert out.read_text() == "ok"
+
+
+_STALL_SCRIPT = r"""
+import datetime, os, sys, time
+sys.path.insert(0, {ms_dir!r})
+import multistream as ms
+import torch.distributed as dist
+rank = int(os.environ["RANK"])
+wd = ms.Watchdog({bound}, rank)
+wd.mark(None, "init_process_group")
+dist.init_process_group("gloo", rank=rank, world_size=2, timeout=datetime.timedelta(seconds=120))
+wd.mark(0, "barrier before the timed region")
+dist.barrier()
+if rank == {stall_rank}:
+    wd.mark(3, "lego_odom_batch_wait")
+    time.sleep(120)  # a stalled device call
+else:
+    wd.mark(3, "hand-off gather (native)")
+    dist.barrier()  # waits for the stalled peer
+print("unreachable", flush=True)
+"""
+
+
+@pytest.mark.parametrize("stall_rank", [1, 0])
+def test_watchdog_stalled_rank_exits_nonzero(stall_rank):
+    """one rank stalls inside a step (a device call that
+    never returns), the other waits for it in a collective.  Both ranks must
+    exit non-zero within the watchdog's bound (bench.py's N > 1 path:
+    multistream.Watchdog), each naming its step and phase, instead of hanging
+    until the launcher's time limit (the process group's own timeout here is
+    120 s, far above the bound)."""
+    import subprocess
+    import time
+
+    bound = 3.0
+    script = _STALL_SCRIPT.format(ms_dir=str(REPO / "lego-loam_amd"), bound=bound, stall_rank=stall_rank)
+    port = _free_port()
+    t0 = time.monotonic()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), WORLD_SIZE="2")
+        procs.append(subprocess.Popen([sys.executable, "-c", script], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=90))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    wall = time.monotonic() - t0
+    for r, (p, (so, se)) in enumerate(zip(procs, outs)):
+        assert p.returncode == 3, (r, p.returncode, se[-2000:])
+        assert "unreachable" not in so
+        assert f"rank {r} made no progress" in se and "step 3" in se, se[-2000:]
+        phase = "lego_odom_batch_wait" if r == stall_rank else "hand-off gather (native)"
+        assert f"phase '{phase}'" in se, se[-2000:]
+    assert wall < 60, wall  # the bound plus process start-up, not the 120 s group timeout
