@@ -846,7 +846,8 @@ def main():
                   f" scan-line indexed {prof[20] / nsc:.1f}, scan-line literal {prof[13] / nsc:.1f}",
                   file=sys.stderr)
             for i, nm in ((21, "rows (excl. reduce)"), (22, "solve_qr+eig it0"), (23, "solve_qr it>0"),
-                          (24, "nn local work"), (25, "to_end loop (wave 1)"),                           (27, "build: key tables+scan"), (29, "build: scatter pass"), (31, "build: bucket ends")):
+                          (24, "nn local work"), (25, "to_end loop (wave 1)"),                           (26, "build: pass 1"), (27, "build: key tables+scan"), (29, "build: scatter pass"),
+                          (31, "build: bucket ends")):
                 print(f"  odom.{nm:20s} {prof[i] / 100.0 / nsc:9.2f} us/scan", file=sys.stderr)
             nq0 = max(prof[30], 1)
             for i, nm in ((28, "wave0 q: nn i1"), (16, "wave0 q: to_start"), (17, "wave0 q: closest"),

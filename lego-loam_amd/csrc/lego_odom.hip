@@ -372,6 +372,16 @@ enum { P_SURF_NN = 0, P_SURF = 1, P_CORN_NN = 2, P_CORN = 3, P_SOLVE = 4, P_INTE
        P_T_ROWS = 21, P_T_SOLVE0 = 22, P_T_SOLVE = 23, P_X_LOCAL = 24, P_TOEND_LOOP = 25,
        P_B_PASS1 = 26, P_B_SCAN = 27, P_B_SCATTER = 29, P_B_ENDS = 31,  // index-build sub-phases
        P_NPROF = 32 };
+// ODOM_RESID_PROBE (diagnostic build, scripts/build_ab.sh): the stretches of a
+// scan outside the stamped phases, on the build sub-phase slots (unused by the
+// gridless C2 stream): 26 scan top -> first LM iteration, 27 the LM loops'
+// prologues / epilogues, 29 the hand-off before its loop, 31 after it to the
+// scan's end (includes P_BUILD)
+#ifndef ODOM_RESID_PROBE
+#define ODOM_RESID_PROBE 0
+#endif
+#define RP_START(S) do { if (ODOM_RESID_PROBE) (S).start(); } while (0)
+#define RP_ADD(S, k) do { if (ODOM_RESID_PROBE) (S).add(k); } while (0)
 struct Stamp {
   unsigned long long* prof;
   unsigned long long t;
@@ -916,8 +926,8 @@ struct OdomLds {
   float4* lastS;     // [kLdsSurf]
   float4* lastC;     // [kLdsCorner]
   int* qi;           // [3 * kLdsQ] correspondence indices
-  float4* qflat;     // [kLdsQ]      this scan's flat features (LM queries)
-  float4* qsharp;    // [kLdsQ / 2]  this scan's sharp features
+  float4* qflat;     // [2][kLdsQ]      flat features (LM queries): scan k in buffer k & 1
+  float4* qsharp;    // [2][kLdsQ / 2]  sharp features
   unsigned* cnt;     // [kLdsGridS] index-build counters
   uint16_t *gEndS, *gOrdS, *gEndC, *gOrdC;  // fine grids
   int *sufS, *preS, *sufC, *preC;           // [kKeyTab] per-key first / last
@@ -928,12 +938,13 @@ struct OdomLds {
   int* n;            // [16] flags
   OdomState* st;     // the stream state, resident for the kernel's lifetime
 };
-enum { N_BREAK = 0, N_IRR_S = 1, N_IRR_C = 2, N_ROUND = 3, N_RING = 4, N_CLAIM = 5 };
+enum { N_BREAK = 0, N_IRR_S = 1, N_IRR_C = 2, N_ROUND = 3, N_RING = 4, N_CLAIM = 5,
+       N_NEXT = 8, N_PRE = 12 };  // [8, 12): the next scan's f_cnt, prefetched; N_PRE: it and its queries are
 
 __host__ __device__ constexpr size_t odom_lds_bytes() {
   size_t s = 0;
   s += (size_t)kLdsSurf * 16 + (size_t)kLdsCorner * 16 + (size_t)kLdsCnt * 4 + (size_t)3 * kLdsQ * 4;
-  s += (size_t)kLdsQ * 16 + (size_t)(kLdsQ / 2) * 16;
+  s += 2 * ((size_t)kLdsQ * 16 + (size_t)(kLdsQ / 2) * 16);
   s += (size_t)(kLdsGridS + kLdsSurf + kLdsGridC + kLdsCorner) * 2;
   s += (size_t)4 * kKeyTab * 4 + (size_t)4 * kMaxRings * 4;
   s += (size_t)2 * kOdomWaves * 4 * 10 * 8 + 256 + (size_t)kOdomWaves * 4 + 16 * 4 + 128;
@@ -947,8 +958,8 @@ __device__ __forceinline__ OdomLds odom_carve(unsigned char* base) {
   size_t o = 0;
   L.lastS = (float4*)(base + o); o += (size_t)kLdsSurf * 16;
   L.lastC = (float4*)(base + o); o += (size_t)kLdsCorner * 16;
-  L.qflat = (float4*)(base + o); o += (size_t)kLdsQ * 16;
-  L.qsharp = (float4*)(base + o); o += (size_t)(kLdsQ / 2) * 16;
+  L.qflat = (float4*)(base + o); o += (size_t)2 * kLdsQ * 16;
+  L.qsharp = (float4*)(base + o); o += (size_t)2 * (kLdsQ / 2) * 16;
   L.cnt = (unsigned*)(base + o); o += (size_t)kLdsCnt * 4;
   L.qi = (int*)(base + o); o += (size_t)3 * kLdsQ * 4;
   L.red = (double*)(base + o); o += (size_t)2 * kOdomWaves * 4 * 10 * 8;
@@ -1144,6 +1155,7 @@ struct ScanFeat {
   const float4* lsharp; int nLS;
   const float4* flat; int nFlat;
   const float4* lflat; int nLF;
+  int qpar;  // LDS-resident path: the query buffer (OdomLds::qflat / qsharp) this scan's queries are in
 };
 
 // The degeneracy analysis of iteration 0 (:1336-1357, :1437-1458): Jacobi
@@ -1465,7 +1477,7 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
   const float4* snap = hbm_cloud<RING>(ob, st->snapBuf, surf, st->nnSurfNum);
   const int snapN = surf ? st->nnSurfNum : st->nnCornerNum;
   const float4* qp;
-  if constexpr (R) qp = surf ? L.qflat : L.qsharp;  // staged in LDS at the scan's start
+  if constexpr (R) qp = surf ? L.qflat + F.qpar * kLdsQ : L.qsharp + F.qpar * (kLdsQ / 2);  // staged in LDS
   else qp = surf ? F.flat : F.sharp;
   const int nQ = surf ? F.nFlat : F.nSharp;
   const int jend = min(nQ, lastN);  // the reference bounds by the query count (:1062, :1173)
@@ -1485,6 +1497,7 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
   // yields the SIMD to the wave that carries the chain on (+0.45% on C2, A/B;
   // the same for the whole kernel, or only around the solve: equal / -0.8%)
   if (tid < 4 * 64) __builtin_amdgcn_s_setprio(2);
+  RP_ADD(S, P_B_SCAN);
   for (int it = 0; it < 25; it++) {
     S.start();
     S.count(surf ? P_ITERS_S : P_ITERS_C);
@@ -1726,6 +1739,7 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
     S.add(P_SOLVE);
     if (brk) break;
   }
+  RP_START(S);
   __builtin_amdgcn_s_setprio(0);
   // write the loop's state back once (all waves hold the same values)
   if (tid == 0) {
@@ -1736,6 +1750,7 @@ __device__ __forceinline__ void lm_loop(bool surf, const ScanFeat& F, const Odom
     st->isDegenerate = isDeg;
   }
   __syncthreads();
+  RP_ADD(S, P_B_SCAN);
 }
 
 // This workgroup's private HBM buffers (the launch's workgroups never share
@@ -1878,12 +1893,24 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
   }
   S.add(P_RESID);
   for (int b = b0; b < b0 + K; ++b) {
+    RP_START(S);
     ScanFeat F;
-    const int* fc = bb.f_cnt + b * 4;
-    F.sharp = bb.f_sharp + (size_t)b * c.N * kSharpPerRing; F.nSharp = fc[0];
-    F.lsharp = bb.f_lsharp + (size_t)b * c.N * kLessSharpPerRing; F.nLS = fc[1];
-    F.flat = bb.f_flat + (size_t)b * c.N * kFlatPerRing; F.nFlat = fc[2];
-    F.lflat = bb.f_lflat + (size_t)b * c.P; F.nLF = fc[3];
+    // the counts and (LDS-resident path) the queries of every scan but the
+    // launch's first were fetched during the previous scan's hand-off (N_PRE):
+    // no global-memory round trip on the chain between two scans
+    const bool pre = b > b0 && __builtin_amdgcn_readfirstlane(L.n[N_PRE]);
+    const int par = (b - b0) & 1;
+    int4 fc;
+    // (readfirstlane: an LDS word is a VGPR to the compiler, and a count it
+    // cannot prove uniform turns the loops it bounds divergent: +26 spills)
+    if (pre) fc = make_int4(__builtin_amdgcn_readfirstlane(L.n[N_NEXT]), __builtin_amdgcn_readfirstlane(L.n[N_NEXT + 1]),
+                            __builtin_amdgcn_readfirstlane(L.n[N_NEXT + 2]), __builtin_amdgcn_readfirstlane(L.n[N_NEXT + 3]));
+    else fc = *(const int4*)(bb.f_cnt + b * 4);
+    F.sharp = bb.f_sharp + (size_t)b * c.N * kSharpPerRing; F.nSharp = fc.x;
+    F.lsharp = bb.f_lsharp + (size_t)b * c.N * kLessSharpPerRing; F.nLS = fc.y;
+    F.flat = bb.f_flat + (size_t)b * c.N * kFlatPerRing; F.nFlat = fc.z;
+    F.lflat = bb.f_lflat + (size_t)b * c.P; F.nLF = fc.w;
+    F.qpar = par;
     float4* cEnd = ob.cornerEnd + (size_t)b * ob.capLS;
     float4* sEnd = ob.surfEnd + (size_t)b * c.P;
     const bool init = !st->inited;
@@ -1911,12 +1938,16 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
       }
       if (st->cornerLastNum >= 10 && st->surfLastNum >= 100) {
         if (!RING && st->resident) {
-          for (int t = tid; t < F.nFlat; t += kOdomThreads) L.qflat[t] = F.flat[t];
-          for (int t = tid; t < F.nSharp; t += kOdomThreads) L.qsharp[t] = F.sharp[t];
-          __syncthreads();
+          if (!pre) {
+            for (int t = tid; t < F.nFlat; t += kOdomThreads) L.qflat[par * kLdsQ + t] = F.flat[t];
+            for (int t = tid; t < F.nSharp; t += kOdomThreads) L.qsharp[par * (kLdsQ / 2) + t] = F.sharp[t];
+            __syncthreads();
+          }
+          RP_ADD(S, P_B_PASS1);
           lm_loop<true, RING>(true, F, L, ob, c, S);
           lm_loop<true, RING>(false, F, L, ob, c, S);
         } else {
+          RP_ADD(S, P_B_PASS1);
           lm_loop<false, RING>(true, F, L, ob, c, S);
           lm_loop<false, RING>(false, F, L, ob, c, S);
         }
@@ -1934,6 +1965,7 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     float tcur[6];
     for (int i = 0; i < 6; ++i) tcur[i] = st->transformCur[i];
     const EndTrig et = end_trig(tcur);
+    if (ODOM_RESID_PROBE == 2) S.add(P_B_ENDS);
     // updateImuRollPitchYawStartSinCos (:1761) and the imu*Last terms of TransformToEnd
     ImuEnd im{1.f, 1.f, 1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 1.f, 0.f, 1.f, 0.f};  // cos 0 / sin 0
     const bool hasImu = bb.imu != nullptr;
@@ -1978,6 +2010,30 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
       else build_zero(BH);
     }
     __syncthreads();
+    // the next scan's counts and queries, copied into the other query buffer
+    // while this hand-off runs: direct global -> LDS loads (no VGPRs held;
+    // the LDS image is lane-linear, slot = thread), every query slot up to the
+    // sensor's caps so nothing waits for the counts (slots past a scan's count
+    // hold whatever the extraction left, never read).  The barriers after the
+    // hand-off retire them.
+    const bool nxt = !RING && sensorRes && b + 1 < b0 + K;
+    if (nxt) {
+      // (the lane index laundered through an empty asm: otherwise the compiler
+      // hoists the three per-lane addresses out of the scan loop and spills
+      // them, and each copy then waits for a scratch reload)
+      int t = tid;
+      asm volatile("" : "+v"(t));
+      const size_t bn = (size_t)b + 1;
+      const int nf = c.N * kFlatPerRing, nsh = c.N * kSharpPerRing, wb = t & ~63;
+      if (t < nf)
+        __builtin_amdgcn_global_load_lds((const void*)(bb.f_flat + bn * nf + t),
+                                         (void*)(L.qflat + (par ^ 1) * kLdsQ + wb), 16, 0, 0);
+      if (t < nsh)
+        __builtin_amdgcn_global_load_lds((const void*)(bb.f_sharp + bn * nsh + t),
+                                         (void*)(L.qsharp + (par ^ 1) * (kLdsQ / 2) + wb), 16, 0, 0);
+      if (t < 4)
+        __builtin_amdgcn_global_load_lds((const void*)(bb.f_cnt + bn * 4 + t), (void*)(L.n + N_NEXT), 4, 0, 0);
+    }
     // hand-off exchange: this workgroup's share of TransformToEnd, published.
     // Only for the HBM-resident sensors: C3 +2.5%, while the LDS-resident
     // VLP-16 stream and the fleet measured equal (their chunks are few, and
@@ -2229,6 +2285,7 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
         hc[bk] = bk >= TS ? e - (unsigned)nS : e;
       }
     };
+    RP_ADD(S, P_B_SCATTER);
     if (ringMode) {
       hand_off_ring();
     } else if (!RING && hx) {
@@ -2239,6 +2296,8 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
       else hand_off(BH);
     }
     if (prof && tid == 64) prof[P_TOEND_LOOP] += wall_clock64() - tw;  // wave 1's chunks
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA copies have landed
+    if (tid == 0) L.n[N_PRE] = nxt ? 1 : 0;  // read at the next scan's top, after the barriers below
     __syncthreads();
     S.add(P_TOEND);
     if (tid == 0) {
@@ -2281,6 +2340,7 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
       else build_finish(BH, prof);
     }
     if (prof && tid == 0) prof[P_BUILD] += wall_clock64() - tb;
+    if (ODOM_RESID_PROBE == 1) S.add(P_B_ENDS);
   }
   __syncthreads();
   // (with the integrating workgroup, transformSum's words 6..11 are its)
