@@ -1898,7 +1898,7 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     // the counts and (LDS-resident path) the queries of every scan but the
     // launch's first were fetched during the previous scan's hand-off (N_PRE):
     // no global-memory round trip on the chain between two scans
-    const bool pre = b > b0 && __builtin_amdgcn_readfirstlane(L.n[N_PRE]);
+    const bool pre = !RING && b > b0 && __builtin_amdgcn_readfirstlane(L.n[N_PRE]);
     const int par = (b - b0) & 1;
     int4 fc;
     // (readfirstlane: an LDS word is a VGPR to the compiler, and a count it
