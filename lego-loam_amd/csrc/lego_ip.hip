@@ -20,6 +20,8 @@
 // (SURVEY.md §9.2); compiled with -ffp-contract=off.
 #include <cfloat>
 
+#include <cstdlib>
+
 #include "lego_device.h"
 #include "lego_kernels.h"
 #include "lego_seg.h"
@@ -173,6 +175,23 @@ __device__ __forceinline__ void uf_unite(int* par, int a, int b) {
   }
 }
 
+__device__ __forceinline__ int lds_find(volatile int* par, int x) {
+  while (true) {
+    const int p = par[x];
+    if (p == x) return x;
+    x = p;
+  }
+}
+__device__ __forceinline__ void lds_unite(int* par, int a, int b) {
+  while (true) {
+    a = lds_find(par, a);
+    b = lds_find(par, b);
+    if (a == b) return;
+    if (a < b) { const int t = a; a = b; b = t; }  // the larger root under the smaller
+    if (atomicCAS(&par[a], a, b) == a) return;
+  }
+}
+
 __global__ void k_ccl_union(BatchBufs bb, DevCfg c) {
   const int b = blockIdx.y;
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -186,19 +205,131 @@ __global__ void k_ccl_union(BatchBufs bb, DevCfg c) {
   if (e & 2) uf_unite(par, p, p + c.H);
 }
 
+// Each pixel's root, and the roots' sizes and row masks.  The counts are
+// aggregated per wave first (a wave's 64 consecutive pixels lie in one or two
+// rows and mostly share their root): one atomic per distinct root of the
+// wave, not one per pixel on the same word (a large segment's thousands of
+// pixels had serialised on its root's counters).
 __global__ void k_ccl_root(BatchBufs bb, DevCfg c) {
   const int b = blockIdx.y;
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= c.P) return;
   const size_t base = (size_t)b * c.P;
-  if (bb.parent[base + p] < 0) return;
-  const int r = uf_find(bb.parent + base, p);
-  bb.root[base + p] = r;
-  atomicAdd(&bb.csize[base + r], 1);
-  if (r != p) {  // lineCountFlag is set only for pushed (non-seed) pixels (:431)
-    const int row = p / c.H;
-    atomicOr(&bb.rowmask[(base + r) * 2 + (row >> 6)], 1ull << (row & 63));
+  const bool cand = p < c.P && bb.parent[base + p] >= 0;
+  int r = -1;
+  if (cand) {
+    r = uf_find(bb.parent + base, p);
+    bb.root[base + p] = r;
   }
+  const int row = p / c.H;
+  // lineCountFlag is set only for pushed (non-seed) pixels (:431)
+  const unsigned long long rbit = (cand && r != p) ? 1ull << (row & 63) : 0ull;
+  const int lane = threadIdx.x & 63;
+  for (unsigned long long act = __ballot(cand); act;) {
+    const int lead = __ffsll((long long)act) - 1;
+    const int r0 = __shfl(r, lead, 64);
+    const bool mine = cand && r == r0;
+    const unsigned long long same = __ballot(mine);
+    unsigned long long lo = mine && row < 64 ? rbit : 0ull, hi = mine && row >= 64 ? rbit : 0ull;
+    for (int o = 32; o > 0; o >>= 1) {
+      lo |= __shfl_xor(lo, o, 64);
+      hi |= __shfl_xor(hi, o, 64);
+    }
+    if (lane == lead) {
+      atomicAdd(&bb.csize[base + r0], (int)__popcll(same));
+      if (lo) atomicOr(&bb.rowmask[(base + r0) * 2], lo);
+      if (hi) atomicOr(&bb.rowmask[(base + r0) * 2 + 1], hi);
+    }
+    act &= ~same;
+  }
+}
+
+// The union-find in column tiles (images too large for k_seg_lds's one
+// workgroup): a 1024-thread workgroup per (scan, tile of TW columns x all
+// rows, <= kCclTilePx pixels) unites the tile's pixels over its own right and
+// down edges in LDS (lds_unite: the larger root under the smaller, so a
+// root is its component's smallest index, row-major within the tile as in
+// the image), then writes every pixel's tile root as its parent (a forest of
+// depth one) and zeroes the counters k_ccl_root accumulates.  k_ccl_seam then
+// unites across the tiles' seams (the column wrap among them, :403-406) in
+// HBM; the smallest tile root of a component becomes its root, the same
+// index the HBM-only union-find (k_ccl_init / _union) gives.
+constexpr int kCclTilePx = 32768;  // 128 KB of parents
+int ccl_tile_width(const DevCfg& c) {
+  int tw = kCclTilePx / c.N;
+  if (tw >= c.H) return c.H;
+  return tw;
+}
+__global__ void __launch_bounds__(1024) k_ccl_tile(BatchBufs bb, DevCfg c, int TW) {
+  extern __shared__ int par[];  // [N * tw], index row * tw + (col - c0)
+  volatile int* vpar = par;
+  const int b = blockIdx.y, c0 = blockIdx.x * TW, tid = threadIdx.x;
+  const int H = c.H, tw = min(TW, H - c0), n = c.N * tw;
+  const bool whole = tw == H;  // one tile: the column wrap is inside it
+  const size_t base = (size_t)b * c.P;
+  const TanBand tb = seg_tan_band(c);
+  for (int l = tid; l < n; l += blockDim.x) {
+    const int row = l / tw, p = row * H + c0 + (l - row * tw);
+    par[l] = bb.label[base + p] == 0 ? l : -1;
+    bb.csize[base + p] = 0;
+    bb.rowmask[(base + p) * 2] = 0ull;
+    bb.rowmask[(base + p) * 2 + 1] = 0ull;
+  }
+  __syncthreads();
+  for (int l0 = 0; l0 < n; l0 += 4 * (int)blockDim.x) {  // four pixels' ranges in flight per thread
+    float rp[4], rr_[4], rd[4];
+    int pp[4], qrl[4], qrp[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int l = l0 + u * (int)blockDim.x + tid;
+      rp[u] = rr_[u] = rd[u] = 0.f;
+      pp[u] = -1;
+      qrl[u] = qrp[u] = -1;
+      if (l < n) {
+        const int row = l / tw, cc = l - row * tw, p = row * H + c0 + cc;
+        pp[u] = p;
+        if (cc + 1 < tw) { qrl[u] = l + 1; qrp[u] = p + 1; }
+        else if (whole) { qrl[u] = row * tw; qrp[u] = row * H; }
+        rp[u] = bb.range[base + p];
+        if (qrp[u] >= 0) rr_[u] = bb.range[base + qrp[u]];
+        if (row + 1 < c.N) rd[u] = bb.range[base + p + H];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int l = l0 + u * (int)blockDim.x + tid;
+      if (pp[u] < 0 || vpar[l] < 0) continue;  // candidates keep a parent >= 0 throughout
+      if (qrl[u] >= 0 && vpar[qrl[u]] >= 0 && seg_edge_fast(rp[u], rr_[u], c.sinAX, c.cosAX, c.theta, tb))
+        lds_unite(par, l, qrl[u]);
+      if (l + tw < n && vpar[l + tw] >= 0 && seg_edge_fast(rp[u], rd[u], c.sinAY, c.cosAY, c.theta, tb))
+        lds_unite(par, l, l + tw);
+    }
+  }
+  __syncthreads();
+  for (int l = tid; l < n; l += blockDim.x) {
+    const int row = l / tw, p = row * H + c0 + (l - row * tw);
+    int pr = -1;
+    if (vpar[l] >= 0) {
+      const int r = lds_find(vpar, l), rrow = r / tw;
+      pr = rrow * H + c0 + (r - rrow * tw);
+    }
+    bb.parent[base + p] = pr;
+  }
+}
+// The seams between column tiles, one thread per (scan, seam, row): tile t's
+// last column against the next column (tile t + 1's first; the last tile's
+// against column 0, the wrap).
+__global__ void k_ccl_seam(BatchBufs bb, DevCfg c, int TW, int nTiles) {
+  const int b = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nTiles * c.N) return;
+  const int t = i / c.N, row = i - t * c.N, H = c.H;
+  const int ce = min(H, (t + 1) * TW);  // the first column past tile t
+  const size_t base = (size_t)b * c.P;
+  const int p = row * H + ce - 1, q = row * H + (ce == H ? 0 : ce);
+  int* par = bb.parent + base;
+  if (uf_load(&par[p]) < 0 || uf_load(&par[q]) < 0) return;
+  const TanBand tb = seg_tan_band(c);
+  if (seg_edge_fast(bb.range[base + p], bb.range[base + q], c.sinAX, c.cosAX, c.theta, tb)) uf_unite(par, p, q);
 }
 
 // Block-wide exclusive scan of up to 3 counters for 1024-thread blocks.
@@ -484,22 +615,6 @@ constexpr int kSegK = (kSegLdsMaxP + 1023) / 1024;  // 1024-pixel chunks per sca
 constexpr int kSegHbmMaxScans = 8;  // launches of up to this many scans segment in HBM (launch_ip)
 bool seg_lds_ok(const DevCfg& c) { return c.N <= kSegLdsMaxN && c.P <= kSegLdsMaxP && !c.segHbm; }
 
-__device__ __forceinline__ int lds_find(volatile int* par, int x) {
-  while (true) {
-    const int p = par[x];
-    if (p == x) return x;
-    x = p;
-  }
-}
-__device__ __forceinline__ void lds_unite(int* par, int a, int b) {
-  while (true) {
-    a = lds_find(par, a);
-    b = lds_find(par, b);
-    if (a == b) return;
-    if (a < b) { const int t = a; a = b; b = t; }  // the larger root under the smaller
-    if (atomicCAS(&par[a], a, b) == a) return;
-  }
-}
 
 __global__ void __launch_bounds__(1024) k_seg_lds(BatchBufs bb, DevCfg c, int want_labels) {
   extern __shared__ int par[];          // [P]
@@ -706,8 +821,17 @@ void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hip
     return;
   }
   tm->mark("ip.ccl", s);
-  k_ccl_init<<<gpix, 256, 0, s>>>(bb, c);
-  k_ccl_union<<<gpix, 256, 0, s>>>(bb, c);
+  // the union-find: in LDS column tiles plus the seams (LEGO_CCL_TILES=0,
+  // diagnostic: every edge in HBM, k_ccl_init / k_ccl_union)
+  static const bool tiles = !std::getenv("LEGO_CCL_TILES") || std::atoi(std::getenv("LEGO_CCL_TILES")) != 0;
+  if (tiles) {
+    const int TW = ccl_tile_width(c), nT = (c.H + TW - 1) / TW;
+    k_ccl_tile<<<dim3(nT, B), 1024, (size_t)c.N * TW * sizeof(int), s>>>(bb, c, TW);
+    if (nT > 1) k_ccl_seam<<<dim3((nT * c.N + 255) / 256, B), 256, 0, s>>>(bb, c, TW, nT);
+  } else {
+    k_ccl_init<<<gpix, 256, 0, s>>>(bb, c);
+    k_ccl_union<<<gpix, 256, 0, s>>>(bb, c);
+  }
   k_ccl_root<<<gpix, 256, 0, s>>>(bb, c);
   tm->mark("ip.compact", s);
   const dim3 gch((P + 1023) / 1024, B);

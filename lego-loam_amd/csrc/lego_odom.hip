@@ -2429,10 +2429,18 @@ void launch_pack_recs(const BatchBufs& bb, const OdomBufs& ob, int B, PackedRec*
 // copy per scan: four queries per wave balance that redundant build against
 // the search split (HDL-64E: 48 workgroups; measured 1.4 k scans/s at 192,
 // 2.7 k at 48, 2.6 k at 24).  Capped at the CU count.
+// LDS-resident sensors: one wave per corner query.  HBM-resident ones (the
+// ring): two flat queries per wave, at most 128 workgroups — C3 (HDL-64E,
+// 20-scan batches beside the next batch's front end) measured 9.3 / 9.8 /
+// 9.8 / 9.0 k scans/s at 64 / 96 / 128 / 160 workgroups, 8.9 k at the four
+// queries per wave of round 4 (48; profiles/r05_wg_c3.txt): more workgroups
+// shorten the chain's NN rounds and hand-off shares but take CUs from the
+// overlapped front end.
 int odom_workgroups(int N, int cusAvailable) {
   const bool resident = N * kFlatPerRing <= kLdsQ && N * kSharpPerRing <= kLdsQ / 2;
-  const int g = resident ? (N * kSharpPerRing + kOdomWaves - 1) / kOdomWaves
-                         : (N * kFlatPerRing + 4 * kOdomWaves - 1) / (4 * kOdomWaves);
+  int g = resident ? (N * kSharpPerRing + kOdomWaves - 1) / kOdomWaves
+                   : (N * kFlatPerRing + 2 * kOdomWaves - 1) / (2 * kOdomWaves);
+  if (!resident && g > 128) g = 128;
   return g < cusAvailable ? g : cusAvailable;
 }
 
