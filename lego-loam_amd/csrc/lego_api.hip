@@ -96,6 +96,7 @@ struct lego_ctx {
   hipEvent_t faDone[2] = {nullptr, nullptr};    // extraction of the slot's batch finished
   hipEvent_t recsDone[2] = {nullptr, nullptr};  // the slot's packed records are on the host
   hipEvent_t oJoin = nullptr;                   // ostream work so far (node calls order after it)
+  hipEvent_t lfFork = nullptr;                  // a node call's features, before its side-stream VoxelGrid
   int nextSlot = 0, inflight = 0, oldest = 0;
   int slotB[2] = {0, 0};
   std::vector<double> slotStamps[2];
@@ -217,6 +218,7 @@ struct lego_ctx {
     if (hostBlock) (void)hipHostFree(hostBlock);
     for (void* p : allocs) (void)hipFree(p);
     if (oJoin) (void)hipEventDestroy(oJoin);
+    if (lfFork) (void)hipEventDestroy(lfFork);
     for (int i = 0; i < 2; ++i) {
       if (faDone[i]) (void)hipEventDestroy(faDone[i]);
       if (recsDone[i]) (void)hipEventDestroy(recsDone[i]);
@@ -383,6 +385,7 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
   if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess) return fail(LEGO_E_DEVICE);
   if (hipStreamCreateWithFlags(&x->ostream, hipStreamNonBlocking) != hipSuccess) return fail(LEGO_E_DEVICE);
   if (hipEventCreateWithFlags(&x->oJoin, hipEventDisableTiming) != hipSuccess) return fail(LEGO_E_DEVICE);
+  if (hipEventCreateWithFlags(&x->lfFork, hipEventDisableTiming) != hipSuccess) return fail(LEGO_E_DEVICE);
   for (int i = 0; i < 2; ++i)
     if (hipEventCreateWithFlags(&x->faDone[i], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&x->recsDone[i], hipEventDisableTiming) != hipSuccess)
@@ -441,6 +444,7 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
   A(bb.f_flat, B * N * kFlatPerRing);
   A(bb.f_lflat, B * P);
   A(bb.f_cnt, B * 4);
+  A(bb.lfReady, B);
   A(bb.imuScan, B);
   A(x->d_desc, B);
   if (hipHostMalloc(&x->h_pack, sizeof(PackedRec) * 2 * (B1 + 1), hipHostMallocMapped | hipHostMallocCoherent) !=
@@ -678,6 +682,7 @@ static BatchBufs bb_slice(const BatchBufs& a, const DevCfg& c, int c0, int n) {
   b.spec_out += k; b.fa_flags += k;
   b.f_sharp += k * N * kSharpPerRing; b.f_lsharp += k * N * kLessSharpPerRing;
   b.f_flat += k * N * kFlatPerRing; b.f_lflat += k * P; b.f_cnt += k * 4;
+  b.lfReady += k;
   return b;
 }
 
@@ -1181,12 +1186,24 @@ int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
   }
   HIPCHK(hipMemsetAsync(bb.bad, 0, sizeof(int), x->stream));  // ip reported its own bit; k_lf_voxel's below
   x->tm.begin();
-  launch_fa(bb, x->dc, 1, 1, x->d_carry, x->stream, &x->tm);  // launch_odom's prep zeroes *ob.xerr
-  if (launch_odom(bb, x->ob, x->dc, 1, x->stream, &x->tm, x->profOn ? x->d_prof : nullptr) != 0) {
+  // the per-ring less-flat VoxelGrid (featureAssociation.cpp:778-782) feeds
+  // only the hand-off (publishCloudsLast, :1759-1815): it runs on ostream
+  // beside the LM, and the hand-off waits for it (OdomBufs::lfWait)
+  // (LEGO_NODE_OVERLAP=0: everything on one stream, A/B knob, read per call)
+  const char* ovS = std::getenv("LEGO_NODE_OVERLAP");
+  const bool overlap = !ovS || std::atoi(ovS) != 0;
+  launch_fa(bb, x->dc, 1, 1, x->d_carry, x->stream, &x->tm, overlap ? x->ostream : nullptr, x->lfFork);
+  OdomBufs ob = x->ob;  // launch_odom's prep zeroes *ob.xerr
+  ob.lfWait = overlap ? 1 : 0;
+  if (launch_odom(bb, ob, x->dc, 1, x->stream, &x->tm, x->profOn ? x->d_prof : nullptr) != 0) {
     set_err("odometry launch failed (%d workgroups)", x->ob.G);
     return LEGO_E_DEVICE;
   }
   x->tm.end(x->stream);
+  if (overlap) {  // the fetch reads f_lflat: the side stream first
+    HIPCHK(hipEventRecord(x->oJoin, x->ostream));
+    HIPCHK(hipStreamWaitEvent(x->stream, x->oJoin, 0));
+  }
   HIPCHK(hipGetLastError());
   x->lastB = 1;
   x->lastBase = 0;
@@ -1194,6 +1211,12 @@ int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
   x->lastIpDevice = false;
   const int st = fetch_fa(x, 0, out, true);  // the exchange error word with the outputs: one sync
   if (st != LEGO_OK) return st;
+  {  // the call's stage times (fa.*, odom.lm) for lego_stage_times; events are complete after the sync
+    x->tnames.clear();
+    x->tms.clear();
+    std::vector<int> cnt;
+    x->tm.collect(x->tnames, x->tms, cnt);
+  }
   if (x->h_hdr[FH_XERR]) {
     x->faK = -1;  // no resident hand-off of a failed scan
     set_err("odometry exchange overflow (more NN rounds than slots)");
@@ -1202,6 +1225,11 @@ int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
   if (x->h_hdr[FH_BAD] & kBadPermutation) {
     x->faK = -1;
     set_err("per-ring VoxelGrid: the device sort returned a payload outside its input (device fault)");
+    return LEGO_E_DEVICE;
+  }
+  if (x->h_hdr[FH_BAD] & kBadLfLate) {
+    x->faK = -1;
+    set_err("the hand-off waited more than 2 s for the per-ring VoxelGrid on the side stream");
     return LEGO_E_DEVICE;
   }
   return LEGO_OK;

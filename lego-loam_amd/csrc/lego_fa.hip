@@ -970,7 +970,9 @@ template <int T>
 __device__ __forceinline__ void lfv_block(const BatchBufs& bb, const DevCfg& c, int ring, int b, int waveMax,
                           unsigned char* lds_raw) {
   constexpr int MP = (kMaxHorizon + T - 1) / T;  // voxels per thread (<= H of them per ring)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));  // the lane terms computed per ring, not held across k_lf_voxel's ring loop
+  const int lane = tid & 63, wave = tid >> 6;
   const int H = c.H;
   uint32_t* key = (uint32_t*)lds_raw;
   uint16_t* val = (uint16_t*)(lds_raw + (size_t)H * 4);
@@ -1166,7 +1168,13 @@ __global__ void __launch_bounds__(kExtractThreads) k_fa_fixup(BatchBufs bb, DevC
 // earlier rings' counts (wave 0, a lane per ring), then its four slots are
 // copied.  (A workgroup per scan walking its rings serially cost ~185 us on
 // a single VLS-128 scan: 128 dependent rounds of small copies.)
+// PART: 0 all four clouds; 1 the LM's three (sharp, less-sharp, flat: a node
+// call, before the odometry); 2 the less-flat cloud only (the node call's
+// side stream, after k_lf_voxel), each workgroup then counting its ring into
+// lfReady (release) for the hand-off's wait.
+template <int PART>
 __global__ void k_fa_compact(BatchBufs bb, DevCfg c) {
+  constexpr int F0 = PART == 2 ? 3 : 0, F1 = PART == 1 ? 3 : 4;  // the clouds [F0, F1)
   __shared__ int off[4];
   const int r = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   const int* cnt = bb.r_cnt + (size_t)b * c.N * 4;
@@ -1174,13 +1182,13 @@ __global__ void k_fa_compact(BatchBufs bb, DevCfg c) {
     int s[4] = {0, 0, 0, 0};
     for (int q = tid; q < r; q += 64)
 #pragma unroll
-      for (int f = 0; f < 4; ++f) s[f] += cnt[q * 4 + f] & 0xffff;  // [3]: the VoxelGrid's count, low half
+      for (int f = F0; f < F1; ++f) s[f] += cnt[q * 4 + f] & 0xffff;  // [3]: the VoxelGrid's count, low half
 #pragma unroll
-    for (int f = 0; f < 4; ++f)
+    for (int f = F0; f < F1; ++f)
       for (int o = 32; o > 0; o >>= 1) s[f] += __shfl_xor(s[f], o, 64);
     if (tid == 0) {
 #pragma unroll
-      for (int f = 0; f < 4; ++f) {
+      for (int f = F0; f < F1; ++f) {
         off[f] = s[f];
         if (r == c.N - 1) bb.f_cnt[b * 4 + f] = s[f] + (cnt[r * 4 + f] & 0xffff);
       }
@@ -1193,14 +1201,22 @@ __global__ void k_fa_compact(BatchBufs bb, DevCfg c) {
     printf("LFV_DIAG compact b=%d ring=%d cnt3=%x off3=%d\n", b, r, cnt[r * 4 + 3], off[3]);
 #endif
   const size_t rb = (size_t)b * c.N + r;
-  for (int t = tid; t < cnt[r * 4 + 0]; t += blockDim.x)
-    bb.f_sharp[(size_t)b * c.N * kSharpPerRing + off[0] + t] = bb.r_sharp[rb * kSharpPerRing + t];
-  for (int t = tid; t < cnt[r * 4 + 1]; t += blockDim.x)
-    bb.f_lsharp[(size_t)b * c.N * kLessSharpPerRing + off[1] + t] = bb.r_lsharp[rb * kLessSharpPerRing + t];
-  for (int t = tid; t < cnt[r * 4 + 2]; t += blockDim.x)
-    bb.f_flat[(size_t)b * c.N * kFlatPerRing + off[2] + t] = bb.r_flat[rb * kFlatPerRing + t];
-  for (int t = tid; t < (cnt[r * 4 + 3] & 0xffff); t += blockDim.x)
-    bb.f_lflat[(size_t)b * c.P + off[3] + t] = bb.r_lflat[(size_t)b * c.P + (size_t)r * c.H + t];
+  if (PART != 2) {
+    for (int t = tid; t < cnt[r * 4 + 0]; t += blockDim.x)
+      bb.f_sharp[(size_t)b * c.N * kSharpPerRing + off[0] + t] = bb.r_sharp[rb * kSharpPerRing + t];
+    for (int t = tid; t < cnt[r * 4 + 1]; t += blockDim.x)
+      bb.f_lsharp[(size_t)b * c.N * kLessSharpPerRing + off[1] + t] = bb.r_lsharp[rb * kLessSharpPerRing + t];
+    for (int t = tid; t < cnt[r * 4 + 2]; t += blockDim.x)
+      bb.f_flat[(size_t)b * c.N * kFlatPerRing + off[2] + t] = bb.r_flat[rb * kFlatPerRing + t];
+  }
+  if (PART != 1)
+    for (int t = tid; t < (cnt[r * 4 + 3] & 0xffff); t += blockDim.x)
+      bb.f_lflat[(size_t)b * c.P + off[3] + t] = bb.r_lflat[(size_t)b * c.P + (size_t)r * c.H + t];
+  if (PART == 2) {
+    __threadfence();  // every wave's stores (and, ring N-1, f_cnt) visible device-wide
+    __syncthreads();  // ... before the ring's count
+    if (tid == 0) __hip_atomic_fetch_add(bb.lfReady + b, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // the batch's per-scan words k_fa_half / the extraction accumulate into (one
@@ -1210,6 +1226,7 @@ __global__ void k_fa_init(BatchBufs bb, int B) {
   if (b < B) {
     bb.firsthalf[b] = 0x7f7f7f7f;  // atomicMin's identity for the first-half index
     bb.fa_flags[b] = 0;
+    bb.lfReady[b] = 0u;
   }
 }
 
@@ -1223,7 +1240,7 @@ static void fa_synccheck(hipStream_t s, const char* what) {
 }
 
 void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_carry, hipStream_t s,
-               StageTimer* tm) {
+               StageTimer* tm, hipStream_t side, hipEvent_t fork) {
   tm->mark("fa.deskew", s);
   k_fa_init<<<(B + 255) / 256, 256, 0, s>>>(bb, B);
   fa_synccheck(s, "k_fa_init");
@@ -1240,7 +1257,16 @@ void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_ca
   tm->mark("fa.fixup", s);
   k_fa_fixup<<<S, kExtractThreads, lds, s>>>(bb, c, B / S, d_carry);
   fa_synccheck(s, "k_fa_fixup");
-  tm->mark("fa.voxel", s);
+  if (side) {  // a node call: the LM's clouds now, the less-flat VoxelGrid beside the odometry
+    tm->mark("fa.compact", s);
+    k_fa_compact<1><<<dim3(c.N, B), 256, 0, s>>>(bb, c);
+    fa_synccheck(s, "k_fa_compact<1>");
+    (void)hipEventRecord(fork, s);
+    (void)hipStreamWaitEvent(side, fork, 0);
+    s = side;
+  } else {
+    tm->mark("fa.voxel", s);
+  }
   static const bool waveOn = !std::getenv("LEGO_LFV_WAVE") || std::atoi(std::getenv("LEGO_LFV_WAVE")) != 0;
   const int g4 = waveOn ? (c.N + 3) / 4 : 0;
   // rings per large-ring workgroup (LEGO_LFV_BLOCK_RINGS, A/B knob; 1 = one
@@ -1261,8 +1287,13 @@ void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_ca
     k_lf_voxel<kExtractThreads>
         <<<dim3(g4 + gb, B), kExtractThreads, std::max(kLfvWaveLds, lfvox_lds_bytes(c.H)), s>>>(bb, c, g4, gb);
   fa_synccheck(s, wide ? "k_lf_voxel<1024>" : "k_lf_voxel<256>");
+  if (side) {
+    k_fa_compact<2><<<dim3(c.N, B), 256, 0, s>>>(bb, c);
+    fa_synccheck(s, "k_fa_compact<2>");
+    return;
+  }
   tm->mark("fa.compact", s);
-  k_fa_compact<<<dim3(c.N, B), 256, 0, s>>>(bb, c);
+  k_fa_compact<0><<<dim3(c.N, B), 256, 0, s>>>(bb, c);
   fa_synccheck(s, "k_fa_compact");
 }
 

@@ -939,7 +939,7 @@ struct OdomLds {
   OdomState* st;     // the stream state, resident for the kernel's lifetime
 };
 enum { N_BREAK = 0, N_IRR_S = 1, N_IRR_C = 2, N_ROUND = 3, N_RING = 4, N_CLAIM = 5,
-       N_NEXT = 8, N_PRE = 12 };  // [8, 12): the next scan's f_cnt, prefetched; N_PRE: it and its queries are
+       N_NEXT = 8, N_PRE = 12, N_LF = 13 };  // [8, 12): the next scan's f_cnt, prefetched; N_PRE: it and its queries are
 
 __host__ __device__ constexpr size_t odom_lds_bytes() {
   size_t s = 0;
@@ -1293,6 +1293,7 @@ typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
 constexpr unsigned long long kStealTicks = 4000;  // 40 us at the 100 MHz wall clock
 constexpr unsigned long long kLateTicks = 200000000;  // 2 s: the diagnostic late workgroup's bound
+constexpr unsigned long long kLfWaitTicks = 200000000;  // 2 s: a node call's hand-off waiting for the less-flat cloud
 __device__ __forceinline__ void x_publish(unsigned long long* p, unsigned long long v) {
   __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1827,8 +1828,10 @@ __device__ __forceinline__ void odom_integrate(const BatchBufs& bb, const OdomBu
 
 // RING: the sensor keeps its last clouds in the stream's ring (OdomBufs::ring,
 // HDL-64E / VLS-128); a separate instantiation, so the LDS-resident sensors'
-// kernel carries none of its code or registers.
-template <bool RING>
+// kernel carries none of its code or registers.  LFW: a node call's form,
+// whose hand-off waits for the side stream's less-flat cloud (OdomBufs::
+// lfWait); also separate, so the batch kernels keep their registers.
+template <bool RING, bool LFW>
 __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs obShared, DevCfg c, int K,
                                                       unsigned long long* prof) {
   // Claim the whole register file of the SIMD (2 waves x 256): no other
@@ -1952,6 +1955,19 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
           lm_loop<false, RING>(false, F, L, ob, c, S);
         }
       }
+    }
+    if (LFW) {  // a node call: the less-flat cloud comes from the side stream (launch_fa)
+      if (tid == 0) {
+        const unsigned long long t0 = wall_clock64();
+        bool ok;
+        while (!(ok = __hip_atomic_load(bb.lfReady + b, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)c.N) &&
+               wall_clock64() - t0 < kLfWaitTicks)
+          __builtin_amdgcn_s_sleep(2);
+        L.n[N_LF] = ok ? __hip_atomic_load(bb.f_cnt + b * 4 + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        if (!ok && lead) atomicOr(bb.bad + b, kBadLfLate);
+      }
+      __syncthreads();
+      F.nLF = __builtin_amdgcn_readfirstlane(L.n[N_LF]);
     }
     S.start();
     // hand-off: checkSystemInitialization (:1605-1637, no TransformToEnd) or
@@ -2508,8 +2524,14 @@ int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int K,
     return -1;
   // A plain launch: the exchange needs no co-residency (see "exchange").
   const int blocks = ob.S * ob.G + (ob.integ ? ob.S : 0);  // the chains, then one integrating workgroup per stream
-  if (ob.ring) k_odom<true><<<blocks, kOdomThreads, odom_lds_bytes(), s>>>(bb, ob, c, K, prof);
-  else k_odom<false><<<blocks, kOdomThreads, odom_lds_bytes(), s>>>(bb, ob, c, K, prof);
+  const size_t lds = odom_lds_bytes();
+  if (ob.lfWait) {
+    if (ob.ring) k_odom<true, true><<<blocks, kOdomThreads, lds, s>>>(bb, ob, c, K, prof);
+    else k_odom<false, true><<<blocks, kOdomThreads, lds, s>>>(bb, ob, c, K, prof);
+  } else {
+    if (ob.ring) k_odom<true, false><<<blocks, kOdomThreads, lds, s>>>(bb, ob, c, K, prof);
+    else k_odom<false, false><<<blocks, kOdomThreads, lds, s>>>(bb, ob, c, K, prof);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

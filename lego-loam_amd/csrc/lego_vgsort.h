@@ -32,8 +32,9 @@
 //  * Segments are disjoint, so their order of processing does not matter: the
 //    recursion runs level by level (a segment's depth budget is the same
 //    2*lg(n) - level for every segment of a level), the segments of a level
-//    spread over the waves; a segment left with no budget is heap-sorted by one
-//    lane exactly as std::__partial_sort(first, last, last) does.
+//    spread over the waves; a segment left with no budget is heap-sorted by a
+//    wave (vg_heap_sort_wave) exactly as std::__partial_sort(first, last,
+//    last) does.
 //
 // tests/native/vgsort_check.cpp checks the pairing/cut rules against std::sort
 // on adversarial inputs; the GPU tests compare the per-ring less-flat clouds
@@ -128,6 +129,109 @@ struct VgHeap {
     }
   }
 };
+
+// The same std::__partial_sort(first, last, last) by one wave (all 64 lanes,
+// first / last uniform; the piece synced to the wave before the call), with
+// exactly VgHeap::sort's element moves:
+//  * make_heap's __adjust_heap calls (parents (len-2)/2 down to 0) each touch
+//    only the parent's subtree, so the parents of one heap level are
+//    independent: levels deepest first, a lane per parent (VgHeap's own
+//    adjust_heap), the order inside a level immaterial;
+//  * a sort_heap pop moves the hole from the root down the larger child (the
+//    right one unless right < left, __adjust_heap's rule; the single left
+//    child at (len-2)/2 of an even heap) to where it stops, then __push_heap
+//    moves the popped value up while its parent is < it.  The walk only reads
+//    keys below the hole, all as they were before the pop, so it runs in
+//    chunks of six levels: lane l < 63 holds the chunk root's descendant l
+//    (heap order) and loads its two children, the chunk's choices are two
+//    ballots and the walk is scalar bit tests.  The path's shifted keys are
+//    the walked children's, so the push stops below the deepest path node
+//    whose key is not < the value (one ballot), and the pop's stores (the
+//    path shifted up to the stop, the value there) go out together.
+// One LDS round trip per chunk and pop instead of two dependent ones per
+// level (VLS-128's per-ring pieces of ~600 keys: the serial form took most of
+// k_lf_voxel's 0.8 ms).
+constexpr int kVgHeapWaveMax = 1 << 13;  // two chunks: internal levels < 12 (vg_sort_max(1024) keys)
+template <typename V>
+__device__ void vg_heap_sort_wave(uint32_t* key, V* val, int first, int last) {
+  int lane = threadIdx.x & 63;
+  asm volatile("" : "+v"(lane));  // the lane terms are computed here, not hoisted over the caller's loops
+  const int len = last - first;
+  if (len < 2) return;
+  if (len > kVgHeapWaveMax) {
+    if (lane == 0) VgHeap<V>{key, val}.sort(first, last);
+    vg_wave_sync();
+    return;
+  }
+  uint32_t* K = key + first;
+  V* W = val + first;
+  const VgHeap<V> Hp{K, W};
+  const int lastP = (len - 2) / 2;
+  for (int d = 31 - __builtin_clz((unsigned)lastP + 1); d >= 0; --d) {
+    const int hi = min(lastP + 1, (2 << d) - 1);
+    for (int p = (1 << d) - 1 + lane; p < hi; p += 64) Hp.adjust_heap(0, p, len, K[p], W[p]);
+    vg_wave_sync();
+  }
+  const int dl = 31 - __builtin_clz((unsigned)lane + 1);  // the lane's level in a chunk (lane 63: 6, unused)
+  const int jl = lane + 1 - (1 << dl);
+  constexpr int NC = 2;
+  for (int m = len - 1; m >= 1; --m) {
+    const uint32_t vk = __builtin_amdgcn_readfirstlane(K[m]);
+    const uint32_t vv = __builtin_amdgcn_readfirstlane((uint32_t)W[m]);
+    if (lane == 0) { K[m] = K[0]; W[m] = W[0]; }  // outside the heap [0, m): the chunks never read it
+    const int lim = (m - 1) / 2, tnode = (m & 1) == 0 ? (m - 2) / 2 : -1;
+    uint32_t ck[NC], cv[NC];
+    int px[NC];       // the lane's path index << 16 | its node (-1: off the path), its chosen child's key / payload
+    int h = 0, k = 0; // the chunk's root, the path's steps so far
+    bool more = true;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      ck[c] = 0u; cv[c] = 0u; px[c] = -1;
+      if (!more) continue;
+      const int x = (h + 1) * (1 << dl) - 1 + jl;
+      const bool two = lane < 63 && x < lim, one = lane < 63 && x == tnode;
+      uint32_t kl = 0u, kr = 0u, vl = 0u, vr = 0u;
+      if (two || one) { kl = K[2 * x + 1]; vl = (uint32_t)W[2 * x + 1]; }
+      if (two) { kr = K[2 * x + 2]; vr = (uint32_t)W[2 * x + 2]; }
+      const bool right = two && !(kr < kl);
+      ck[c] = right ? kr : kl;
+      cv[c] = right ? vr : vl;
+      const unsigned long long G = __ballot(two || one), R = __ballot(right);
+      int l = 0;
+      unsigned long long path = 0ull;
+      for (int s = 0; s < 6; ++s) {
+        if (!((G >> l) & 1ull)) break;
+        path |= 1ull << l;
+        l = 2 * l + 1 + (int)((R >> l) & 1ull);
+      }
+      if ((path >> lane) & 1ull) px[c] = ((k + dl) << 16) | x;
+      k += (int)__popcll(path);
+      const int dL = 31 - __builtin_clz((unsigned)l + 1);
+      h = (h + 1) * (1 << dL) - 1 + (l + 1 - (1 << dL));  // where the walk stopped
+      more = dL == 6;  // six levels walked: the next chunk starts there
+    }
+    // the push: the hole stops at path node j = 1 + the deepest path index
+    // whose chosen child's key is not < the value (0 if none)
+    int j = 0;
+    bool found = false;
+#pragma unroll
+    for (int c = NC - 1; c >= 0; --c) {
+      const unsigned long long F = __ballot(px[c] >= 0 && !(ck[c] < vk));
+      if (!found && F) {
+        j = (__builtin_amdgcn_readlane(px[c], 63 - __builtin_clzll(F)) >> 16) + 1;
+        found = true;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int pi = px[c] >> 16, x = px[c] & 0xffff;
+      if (px[c] >= 0 && pi < j) { K[x] = ck[c]; W[x] = (V)cv[c]; }
+      if (px[c] >= 0 && pi == j) { K[x] = vk; W[x] = (V)vv; }
+    }
+    if (j == k && lane == 0) { K[h] = vk; W[h] = (V)vv; }
+    vg_wave_sync();
+  }
+}
 
 constexpr int kVgLeaf = 16;  // _S_threshold
 
@@ -225,7 +329,7 @@ __device__ __forceinline__ VgSortLds<V> vg_sort_carve(uint32_t* key, V* val, uns
 // end the pieces before it, then yields the same sums from a stable order: a
 // key's one or two points in the piece are its voxel's first addends, and
 // 0 + a + b == 0 + b + a (IEEE addition commutes).  Such a piece is ranked in
-// parallel like a leaf instead of heap-sorted by one lane; any other piece is
+// parallel like a leaf instead of heap-sorted; any other piece is
 // still heap-sorted exactly.  Off, the permutation itself is std::sort's
 // (lego_sort_permutation).
 constexpr int kVgMoveRows = 4;  // the moves' batch: rows of blockDim.x positions
@@ -233,10 +337,13 @@ constexpr int kVgMoveRows = 4;  // the moves' batch: rows of blockDim.x position
 // the sum-order heap pieces, the moves.  All threads of the block.
 template <typename V>
 __device__ void vg_block_finish(const VgSortLds<V>& S, int n, bool sumOrder) {
-  const int tid = threadIdx.x, T = blockDim.x;
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));  // nothing of this pass hoisted over the levels
+  const int T = blockDim.x;
   // leaves: every position ranks itself within its leaf (its start the
   // highest leaf-start bit at or below it, its end the next one; <= 16 keys,
   // or a heap piece of up to T * kVgMoveRows with sumOrder)
+  if (tid == 0) S.ctl[0] = 0;  // the heap pieces' count (read last at the final level's top: 0 or behind a barrier)
   for (int i = tid; i < n; i += T) {
     const int wi = i >> 5, bi = i & 31;
     const uint32_t hw = S.head[wi];
@@ -247,6 +354,10 @@ __device__ void vg_block_finish(const VgSortLds<V>& S, int n, bool sumOrder) {
     while (!hi && ((wh + 1) << 5) < n) hi = S.head[++wh];
     const int ls = (wl << 5) + 31 - __builtin_clz(lo);
     const int le = hi ? min(n, (wh << 5) + __builtin_ctz(hi)) : n;
+    if (le - ls > kVgLeaf && S.pr[ls] == 2) {  // heap-sorted below
+      S.sid[i] = (uint16_t)i;
+      continue;
+    }
     const uint32_t k = S.key[i];
     int lt = 0, eqb = 0, eq = 0;
     for (int u0 = 0; u0 < le - ls; u0 += 8) {
@@ -280,7 +391,10 @@ __device__ void vg_block_finish(const VgSortLds<V>& S, int n, bool sumOrder) {
     S.sid[i] = (uint16_t)(ls + lt + eqb);
   }
   __syncthreads();
-  if (sumOrder) {  // heap pieces holding a key 3+ times: std::__partial_sort after all
+  {  // the heap pieces (pr = 2, or 1: holding a key 3+ times), std::__partial_sort
+    // listed (the segment tables are free now; ctl[0] zeroed in the leaf
+    // pass), then a wave per piece; each position becomes a leaf
+    int2* hl = (int2*)S.tab;
     for (int i = tid; i < n; i += T) {
       if (!((S.head[i >> 5] >> (i & 31)) & 1u)) continue;
       int w = i >> 5;
@@ -288,8 +402,17 @@ __device__ void vg_block_finish(const VgSortLds<V>& S, int n, bool sumOrder) {
       while (!hi && ((w + 1) << 5) < n) hi = S.head[++w];
       const int le = hi ? min(n, (w << 5) + __builtin_ctz(hi)) : n;
       if (le - i <= kVgLeaf || !S.pr[i]) continue;
-      VgHeap<V>{S.key, S.val}.sort(i, le);
-      for (int q = i; q < le; ++q) S.sid[q] = (uint16_t)q;
+      hl[atomicAdd(&S.ctl[0], 1)] = make_int2(i, le);
+    }
+    __syncthreads();
+    const int nh = S.ctl[0];
+    for (int q = tid >> 6; q < nh; q += T >> 6) {
+      const int2 pc = hl[q];
+      vg_heap_sort_wave(S.key, S.val, pc.x, pc.y);
+      for (int i = pc.x + (tid & 63); i < pc.y; i += 64) {
+        S.sid[i] = (uint16_t)i;
+        atomicOr(&S.head[i >> 5], 1u << (i & 31));
+      }
     }
     __syncthreads();
   }
@@ -334,7 +457,9 @@ template <typename V>
 __device__ void vg_block_sort(const VgSortLds<V>& S, int n, int depth = -1, int* heapStat = nullptr,
                               bool sumOrder = false) {
   constexpr int RM = kVgRowsMax;
-  const int tid = threadIdx.x, T = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = T >> 6;
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));  // the lane terms computed per call, not held across the caller's loops
+  const int T = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = T >> 6;
   const int cap = vg_list_cap(n);
   const int D = depth >= 0 ? depth : (n > 1 ? 2 * (31 - __builtin_clz((unsigned)n)) : 0);
   const int P = (((n + nw - 1) / nw) + 63) & ~63;  // positions per wave
@@ -380,15 +505,13 @@ __device__ void vg_block_sort(const VgSortLds<V>& S, int n, int depth = -1, int*
     VgSeg* cur = S.tab + (r & 1) * cap;
     VgSeg* nxt = S.tab + ((r + 1) & 1) * cap;
     if (D - r == 0) {  // depth budget spent: std::__partial_sort of every piece
+      // pieces of > 16 keys, heap-sorted in vg_block_finish (pr[s] = 2),
+      // or with sumOrder a leaf unless a key occurs 3+ times (pr[s] = 0, set
+      // to 1 there if so)
       for (int j = tid; j < nseg; j += T) {
         const int s = cur[j].s, e = cur[j].e;
-        if (sumOrder && e - s <= T * kVgMoveRows) {  // a leaf of > 16 keys; pr[s]: a key occurs 3+ times
-          atomicOr(&S.head[s >> 5], 1u << (s & 31));
-          S.pr[s] = 0;
-        } else {
-          VgHeap<V>{S.key, S.val}.sort(s, e);
-          for (int q = s; q < e; ++q) atomicOr(&S.head[q >> 5], 1u << (q & 31));
-        }
+        atomicOr(&S.head[s >> 5], 1u << (s & 31));
+        S.pr[s] = sumOrder && e - s <= T * kVgMoveRows ? 0 : 2;
         if (heapStat) atomicAdd(heapStat, 1);
       }
       __syncthreads();
@@ -619,7 +742,9 @@ template <typename V>
 __device__ void vg_block_sort_sid(const VgSortLds<V>& S, int n, int depth = -1, int* heapStat = nullptr,
                               bool sumOrder = false) {
   constexpr int RM = kVgRowsMax;
-  const int tid = threadIdx.x, T = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = T >> 6;
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));  // the lane terms computed per call, not held across the caller's loops
+  const int T = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = T >> 6;
   const int cap = vg_list_cap(n);
   const int D = depth >= 0 ? depth : (n > 1 ? 2 * (31 - __builtin_clz((unsigned)n)) : 0);
   const int P = (((n + nw - 1) / nw) + 63) & ~63;  // positions per wave
@@ -649,15 +774,13 @@ __device__ void vg_block_sort_sid(const VgSortLds<V>& S, int n, int depth = -1, 
     VgSeg* cur = S.tab + (r & 1) * cap;
     VgSeg* nxt = S.tab + ((r + 1) & 1) * cap;
     if (D - r == 0) {  // depth budget spent: std::__partial_sort of every piece
+      // pieces of > 16 keys, heap-sorted in vg_block_finish (pr[s] = 2),
+      // or with sumOrder a leaf unless a key occurs 3+ times (pr[s] = 0, set
+      // to 1 there if so)
       for (int j = tid; j < nseg; j += T) {
         const int s = cur[j].s, e = cur[j].e;
-        if (sumOrder && e - s <= T * kVgMoveRows) {  // a leaf of > 16 keys; pr[s]: a key occurs 3+ times
-          atomicOr(&S.head[s >> 5], 1u << (s & 31));
-          S.pr[s] = 0;
-        } else {
-          VgHeap<V>{S.key, S.val}.sort(s, e);
-          for (int q = s; q < e; ++q) atomicOr(&S.head[q >> 5], 1u << (q & 31));
-        }
+        atomicOr(&S.head[s >> 5], 1u << (s & 31));
+        S.pr[s] = sumOrder && e - s <= T * kVgMoveRows ? 0 : 2;
         if (heapStat) atomicAdd(heapStat, 1);
       }
       __syncthreads();

@@ -45,7 +45,7 @@ __device__ __forceinline__ unsigned long long vg_range(int a, int b) {
 // by popcounts of ballots, the partners as the n-th set bit, the swaps as lane
 // permutations), the pieces of <= 16 are stable-sorted by rank, and each key
 // lands at its final position.  depth: the segment's budget; when it runs out
-// the pieces still larger than 16 are heap-sorted (lane 0, in LDS).
+// the pieces still larger than 16 are heap-sorted (the wave, in LDS).
 template <typename V>
 __device__ void vg_wave_sort64(uint32_t* key, V* val, int s, int m, int depth, int* heapStat) {
   const int lane = threadIdx.x & 63;
@@ -63,10 +63,8 @@ __device__ void vg_wave_sort64(uint32_t* key, V* val, int s, int m, int depth, i
       while (starts) {
         const int st = (int)__ffsll((long long)starts) - 1;
         const int en = __builtin_amdgcn_readlane(hi, st);
-        if (lane == 0) {
-          VgHeap<V>{key, val}.sort(s + st, s + en);
-          if (heapStat) atomicAdd(heapStat, 1);
-        }
+        vg_heap_sort_wave(key, val, s + st, s + en);
+        if (heapStat && lane == 0) atomicAdd(heapStat, 1);
         starts &= starts - 1;
       }
       vg_wave_sync();
@@ -136,7 +134,7 @@ __device__ void vg_wave_sort64(uint32_t* key, V* val, int s, int m, int depth, i
 // from its middle), the cut by an LDS atomicMin at the piece's start; the
 // swaps through the key array.  Then every slot ranks itself (stably) in its
 // piece of <= 16 and moves there.  The depth budget runs out: every piece
-// still above 16 is heap-sorted by its first lane.
+// still above 16 is heap-sorted by the wave.
 template <typename V>
 __device__ void vg_wave_sortR(uint32_t* key, V* val, uint32_t* c, int s, int m, int depth, int* heapStat) {
   constexpr int RM = kVgWaveRowsW;
@@ -169,11 +167,14 @@ __device__ void vg_wave_sortR(uint32_t* key, V* val, uint32_t* c, int s, int m, 
         if (j < R && x < m) c[s + x] = (((big >> j) & 1u) && x == VG_LO(j)) ? (uint32_t)VG_HI(j) : 0u;
       }
       vg_wave_sync();
-      for (int q = lane; q < m; q += 64) {
-        const int h = (int)c[s + q];
-        if (h) {
-          VgHeap<V>{key, val}.sort(s + q, s + h);
-          if (heapStat) atomicAdd(heapStat, 1);
+      for (int q0 = 0; q0 < m; q0 += 64) {  // the pieces row by row, the wave on each
+        const int h = q0 + lane < m ? (int)c[s + q0 + lane] : 0;
+        unsigned long long starts = __ballot(h != 0);
+        while (starts) {
+          const int st = (int)__ffsll((long long)starts) - 1;
+          vg_heap_sort_wave(key, val, s + q0 + st, s + __builtin_amdgcn_readlane(h, st));
+          if (heapStat && lane == 0) atomicAdd(heapStat, 1);
+          starts &= starts - 1;
         }
       }
       vg_wave_sync();
