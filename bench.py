@@ -340,26 +340,27 @@ def loop_bench(L, nscans: int, calls: int, cpu: bool):
     return res
 
 
-def node_path_bench(L, nscans: int, cpu: bool, cpu_scans: int = 40):
+def node_path_bench(L, nscans: int, cpu: bool, cpu_scans: int = 40, sensor: str = "VLP-16", seed: int = 1):
     """Auxiliary (not the headline metric): the per-scan latency of the
     node-shaped drop-in path a ROS deployment runs at 10 Hz (INTEGRATION.md's
     adapter; imageProjection.cpp:181-197 cloudHandler, featureAssociation.cpp:
     1817-1860 runFeatureAssociation, mapOptmization.cpp:1487-1522 run): for
-    every scan of the C2 stream (VLP-16, seed 1), one at a time from HOST
+    every scan of the C2 stream (VLP-16, seed 1; or `sensor` / `seed`), one at a time from HOST
     buffers, lego_ip_process -> lego_fa_process -> lego_mo_process (the
     keyframe-built map, the reference's default; the call returns at once when
     mapOptimization's 0.3 s gate is closed).  Host wall clock per scan around
     the three calls, uploads and the library's host outputs included.  A
     throwaway context runs first so module loading is not in the numbers.  CPU
-    leg: the oracle's same three calls over the first `cpu_scans` scans."""
-    sensor, seed = "VLP-16", 1
+    leg: the oracle's same three calls over the first `cpu_scans` scans, with
+    the GPU's summary over those same scans beside it (gpu_same_scans)."""
     sc = L.synth_cfg(sensor, seed)
     scans = [L.synth_scan(sc, k) for k in range(nscans)]
     cap = max(len(p) for p, _ in scans) + 16
 
     def run(lib, h, ipf, faf, mof, n):
+        """per scan: (total, ip, fa, mo) ms and whether mapping ran"""
         ip, fa = L.IpOut(), L.FaOut()
-        per, t_ip, t_fa, t_mo, t_map = [], [], [], [], []
+        out = []
         for pts, stamp in scans[:n]:
             pts = np.ascontiguousarray(pts, dtype=L.XYZIR_DTYPE)
             mo = L.MoOut()
@@ -370,20 +371,21 @@ def node_path_bench(L, nscans: int, cpu: bool, cpu_scans: int = 40):
             t2 = time.perf_counter()
             L.check(mof(h, C.byref(fa), C.byref(mo)), "mo", lib)
             t3 = time.perf_counter()
-            per.append((t3 - t0) * 1e3)
-            t_ip.append((t1 - t0) * 1e3)
-            t_fa.append((t2 - t1) * 1e3)
-            (t_map if mo.processed else t_mo).append((t3 - t2) * 1e3)
-        return per, t_ip, t_fa, t_mo, t_map
+            out.append(((t3 - t0) * 1e3, (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3, bool(mo.processed)))
+        return out
 
     def pct(v, q):
         v = sorted(v)
         return v[min(len(v) - 1, int(round(q * (len(v) - 1))))] if v else None
 
-    def summary(per, t_ip, t_fa, t_mo, t_map):
+    def summary(recs):
+        per = [r[0] for r in recs]
+        t_mo = [r[3] for r in recs if not r[4]]
+        t_map = [r[3] for r in recs if r[4]]
         return {"scans": len(per), "ms_per_scan_median": statistics.median(per), "ms_per_scan_p99": pct(per, 0.99),
                 "ms_per_scan_max": max(per), "ms_per_scan_mean": statistics.mean(per),
-                "ip_ms_median": statistics.median(t_ip), "fa_ms_median": statistics.median(t_fa),
+                "ip_ms_median": statistics.median(r[1] for r in recs),
+                "fa_ms_median": statistics.median(r[2] for r in recs),
                 "mo_gate_closed_ms_median": statistics.median(t_mo) if t_mo else None,
                 "mapping_steps": len(t_map),
                 "mapping_step_ms_median": statistics.median(t_map) if t_map else None,
@@ -394,19 +396,24 @@ def node_path_bench(L, nscans: int, cpu: bool, cpu_scans: int = 40):
     run(lib, warm.h, lib.lego_ip_process, lib.lego_fa_process, lib.lego_mo_process, 8)
     warm.close()
     gpu = L.Lego(L.sensor_cfg(sensor, lib), max_points=cap)
-    res = {"workload": f"C2 stream (VLP-16 seed 1) one scan at a time from host buffers through the node API: "
-                       f"lego_ip_process -> lego_fa_process -> lego_mo_process (keyframe map), {nscans} scans",
-           "gpu": summary(*run(lib, gpu.h, lib.lego_ip_process, lib.lego_fa_process, lib.lego_mo_process,
-                               nscans))}
+    name = "C2 stream (VLP-16 seed 1)" if (sensor, seed) == ("VLP-16", 1) else f"{sensor} seed {seed} stream"
+    res = {"workload": f"{name} one scan at a time from host buffers through the node API: "
+                       f"lego_ip_process -> lego_fa_process -> lego_mo_process (keyframe map), {nscans} scans"}
+    recs = run(lib, gpu.h, lib.lego_ip_process, lib.lego_fa_process, lib.lego_mo_process, nscans)
     gpu.close()
+    res["gpu"] = summary(recs)
     res["gpu"]["fits_10hz"] = res["gpu"]["ms_per_scan_max"] < 100.0
     if cpu:
         olib = L.oracle_lib()
         ora = L.Oracle(L.sensor_cfg(sensor))
-        res["cpu"] = summary(*run(olib, ora.h, olib.lego_oracle_ip_process, olib.lego_oracle_fa_process,
-                                  olib.lego_oracle_mo_process, cpu_scans))
+        res["cpu"] = summary(run(olib, ora.h, olib.lego_oracle_ip_process, olib.lego_oracle_fa_process,
+                                 olib.lego_oracle_mo_process, cpu_scans))
         res["cpu"]["sample"] = f"the oracle's same three calls over scans 0..{cpu_scans - 1} (1 thread)"
-        res["gpu_vs_cpu_note"] = "CPU over the first scans only (bounded leg): compare the medians"
+        # like for like: the GPU's calls on the same scans (the mapping gate
+        # opens on the same scans of both)
+        res["gpu_same_scans"] = summary(recs[:cpu_scans])
+        res["gpu_vs_cpu_note"] = (f"cpu and gpu_same_scans cover the same scans 0..{cpu_scans - 1} (medians and p99 "
+                                  f"comparable); gpu covers all {nscans}")
     return res
 
 
@@ -829,7 +836,11 @@ def main():
                    "sample": f"{n} scans ({passes} pass(es) over the {args.stream_len}-scan "
                              f"{args.sensor} stream, seed {seed}) through oracle ip+fa incl. LM, 1 thread"}
             # min(streams, cores) threads, the streams being the fleet line's
-            thr = max(1, min(max(args.fleet_streams, 1), host_info()["affinity"]))
+            # (the cores this process may use: its affinity, capped by the cgroup's quota)
+            usable = host_info()["affinity"]
+            if cgroup_cpus():
+                usable = min(usable, max(1, int(cgroup_cpus())))
+            thr = max(1, min(max(args.fleet_streams, 1), usable))
             # each thread repeats its own stream; the streams' synthesis is kept to ~3.8 k scans
             cpu_all = cpu_all_cores(L, args.sensor, thr, max(10, 3840 // thr), args.cpu_budget)
         if args.odom_profile:
@@ -880,6 +891,9 @@ def main():
             aux["loop_closure"] = loop_bench(L, args.loop_scans, 5, not args.no_cpu)
         if args.node_scans > 0 and world == 1:
             aux["node_path"] = node_path_bench(L, args.node_scans, not args.no_cpu)
+            # the dense single-scan path (VLS-128: 128 rings per VoxelGrid launch)
+            aux["node_path_vls128"] = node_path_bench(L, max(8, args.node_scans // 3), not args.no_cpu,
+                                                      cpu_scans=8, sensor="VLS-128", seed=3)
         if cpu_all:
             aux["cpu_all_cores"] = cpu_all
         aux["host"] = host_info()

@@ -97,6 +97,7 @@ struct lego_ctx {
   hipEvent_t recsDone[2] = {nullptr, nullptr};  // the slot's packed records are on the host
   hipEvent_t oJoin = nullptr;                   // ostream work so far (node calls order after it)
   hipEvent_t lfFork = nullptr;                  // a node call's features, before its side-stream VoxelGrid
+  unsigned* d_lfReady = nullptr;                // [1] its rings counted as their less-flat clouds land
   int nextSlot = 0, inflight = 0, oldest = 0;
   int slotB[2] = {0, 0};
   std::vector<double> slotStamps[2];
@@ -444,7 +445,7 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
   A(bb.f_flat, B * N * kFlatPerRing);
   A(bb.f_lflat, B * P);
   A(bb.f_cnt, B * 4);
-  A(bb.lfReady, B);
+  A(x->d_lfReady, 1);
   A(bb.imuScan, B);
   A(x->d_desc, B);
   if (hipHostMalloc(&x->h_pack, sizeof(PackedRec) * 2 * (B1 + 1), hipHostMallocMapped | hipHostMallocCoherent) !=
@@ -682,7 +683,6 @@ static BatchBufs bb_slice(const BatchBufs& a, const DevCfg& c, int c0, int n) {
   b.spec_out += k; b.fa_flags += k;
   b.f_sharp += k * N * kSharpPerRing; b.f_lsharp += k * N * kLessSharpPerRing;
   b.f_flat += k * N * kFlatPerRing; b.f_lflat += k * P; b.f_cnt += k * 4;
-  b.lfReady += k;
   return b;
 }
 
@@ -888,7 +888,8 @@ static int wait_batch(lego_ctx* x, lego_pose_rec* recs, int cap, int* nOut) {
   x->lastB = 0;
   x->lastBatch = false;
   if (pk[B].bad) {
-    set_err("odometry exchange overflow (more NN rounds than slots)");
+    set_err("odometry error word %d (1: more NN rounds than slots, 2: a ring share never done, 3: the "
+            "integration never saw a scan's transform)", pk[B].bad);
     return LEGO_E_DEVICE;
   }
   for (int k = 0; k < B; ++k)
@@ -1192,10 +1193,11 @@ int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
   // (LEGO_NODE_OVERLAP=0: everything on one stream, A/B knob, read per call)
   const char* ovS = std::getenv("LEGO_NODE_OVERLAP");
   const bool overlap = !ovS || std::atoi(ovS) != 0;
-  launch_fa(bb, x->dc, 1, 1, x->d_carry, x->stream, &x->tm, overlap ? x->ostream : nullptr, x->lfFork);
-  OdomBufs ob = x->ob;  // launch_odom's prep zeroes *ob.xerr
-  ob.lfWait = overlap ? 1 : 0;
-  if (launch_odom(bb, ob, x->dc, 1, x->stream, &x->tm, x->profOn ? x->d_prof : nullptr) != 0) {
+  launch_fa(bb, x->dc, 1, 1, x->d_carry, x->stream, &x->tm, overlap ? x->ostream : nullptr, x->lfFork,
+            x->d_lfReady);
+  // launch_odom's prep zeroes *ob.xerr
+  if (launch_odom(bb, x->ob, x->dc, 1, x->stream, &x->tm, x->profOn ? x->d_prof : nullptr,
+                  overlap ? x->d_lfReady : nullptr) != 0) {
     set_err("odometry launch failed (%d workgroups)", x->ob.G);
     return LEGO_E_DEVICE;
   }
@@ -1219,7 +1221,8 @@ int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
   }
   if (x->h_hdr[FH_XERR]) {
     x->faK = -1;  // no resident hand-off of a failed scan
-    set_err("odometry exchange overflow (more NN rounds than slots)");
+    set_err("odometry error word %u (1: more NN rounds than slots, 2: a ring share never done, 3: the "
+            "integration never saw a scan's transform)", (unsigned)x->h_hdr[FH_XERR]);
     return LEGO_E_DEVICE;
   }
   if (x->h_hdr[FH_BAD] & kBadPermutation) {
@@ -1334,7 +1337,7 @@ static int mo_alloc(lego_ctx* x, int nc, int ns) {
     m.rowCap = N * kLessSharpPerRing + 2 * P;
     MA(m.rows, (size_t)m.rowCap * 8);
     m.candQ = std::min(m.rowCap, kCandQueries);
-    if (const char* e = std::getenv("LEGO_MO_CAND"); e && std::atoi(e) == 0) m.candQ = 0;  // diagnostic A/B
+    if (const char* e = std::getenv("LEGO_MO_CAND"); e && std::atoi(e) == 0) m.candQ = 0;  // no cache (device memory)
     MA(m.cand, (size_t)m.candQ * kCand);
     MA(m.candRef, (size_t)m.candQ);
     m.partCap = 4096;  // k_mo_rows' grid cap (grid_for)

@@ -102,7 +102,7 @@ struct GatedBufs {
 // sort handed back a payload outside its input: it cannot happen unless the
 // device's LDS or registers are corrupted, and is never clamped into range).
 // kBadLfLate (LEGO_E_DEVICE): a node call's hand-off gave up waiting for the
-// less-flat VoxelGrid on the side stream (OdomBufs::lfWait).
+// less-flat VoxelGrid on the side stream (launch_odom's lfReady).
 constexpr int kBadNotDense = 1, kBadPermutation = 2, kBadLfLate = 4;
 struct BatchBufs {
   int B;
@@ -153,11 +153,6 @@ struct BatchBufs {
   float4* f_flat;            // [B*N*24]
   float4* f_lflat;           // [B*P]
   int* f_cnt;                // [B*4]
-  // [B] rings of the scan whose less-flat cloud k_fa_compact has stored in
-  // f_lflat (release; zeroed by k_fa_init).  A node call runs the per-ring
-  // VoxelGrid and that compaction on a second stream beside the LM, and
-  // k_odom's hand-off waits for all N (OdomBufs::lfWait).
-  unsigned* lfReady;
 };
 
 // Buffer views inside the batch for scan b.

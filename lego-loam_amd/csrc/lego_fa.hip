@@ -1173,7 +1173,7 @@ __global__ void __launch_bounds__(kExtractThreads) k_fa_fixup(BatchBufs bb, DevC
 // side stream, after k_lf_voxel), each workgroup then counting its ring into
 // lfReady (release) for the hand-off's wait.
 template <int PART>
-__global__ void k_fa_compact(BatchBufs bb, DevCfg c) {
+__global__ void k_fa_compact(BatchBufs bb, DevCfg c, unsigned* lfReady) {
   constexpr int F0 = PART == 2 ? 3 : 0, F1 = PART == 1 ? 3 : 4;  // the clouds [F0, F1)
   __shared__ int off[4];
   const int r = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
@@ -1215,18 +1215,18 @@ __global__ void k_fa_compact(BatchBufs bb, DevCfg c) {
   if (PART == 2) {
     __threadfence();  // every wave's stores (and, ring N-1, f_cnt) visible device-wide
     __syncthreads();  // ... before the ring's count
-    if (tid == 0) __hip_atomic_fetch_add(bb.lfReady + b, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_fetch_add(lfReady + b, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
 // the batch's per-scan words k_fa_half / the extraction accumulate into (one
 // launch instead of two fills)
-__global__ void k_fa_init(BatchBufs bb, int B) {
+__global__ void k_fa_init(BatchBufs bb, int B, unsigned* lfReady) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b < B) {
     bb.firsthalf[b] = 0x7f7f7f7f;  // atomicMin's identity for the first-half index
     bb.fa_flags[b] = 0;
-    bb.lfReady[b] = 0u;
+    if (lfReady) lfReady[b] = 0u;
   }
 }
 
@@ -1240,9 +1240,9 @@ static void fa_synccheck(hipStream_t s, const char* what) {
 }
 
 void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_carry, hipStream_t s,
-               StageTimer* tm, hipStream_t side, hipEvent_t fork) {
+               StageTimer* tm, hipStream_t side, hipEvent_t fork, unsigned* lfReady) {
   tm->mark("fa.deskew", s);
-  k_fa_init<<<(B + 255) / 256, 256, 0, s>>>(bb, B);
+  k_fa_init<<<(B + 255) / 256, 256, 0, s>>>(bb, B, side ? lfReady : nullptr);
   fa_synccheck(s, "k_fa_init");
   dim3 gpts((c.P + 255) / 256, B);
   k_fa_half<<<gpts, 256, 0, s>>>(bb, c);
@@ -1259,7 +1259,7 @@ void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_ca
   fa_synccheck(s, "k_fa_fixup");
   if (side) {  // a node call: the LM's clouds now, the less-flat VoxelGrid beside the odometry
     tm->mark("fa.compact", s);
-    k_fa_compact<1><<<dim3(c.N, B), 256, 0, s>>>(bb, c);
+    k_fa_compact<1><<<dim3(c.N, B), 256, 0, s>>>(bb, c, nullptr);
     fa_synccheck(s, "k_fa_compact<1>");
     (void)hipEventRecord(fork, s);
     (void)hipStreamWaitEvent(side, fork, 0);
@@ -1288,12 +1288,12 @@ void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_ca
         <<<dim3(g4 + gb, B), kExtractThreads, std::max(kLfvWaveLds, lfvox_lds_bytes(c.H)), s>>>(bb, c, g4, gb);
   fa_synccheck(s, wide ? "k_lf_voxel<1024>" : "k_lf_voxel<256>");
   if (side) {
-    k_fa_compact<2><<<dim3(c.N, B), 256, 0, s>>>(bb, c);
+    k_fa_compact<2><<<dim3(c.N, B), 256, 0, s>>>(bb, c, lfReady);
     fa_synccheck(s, "k_fa_compact<2>");
     return;
   }
   tm->mark("fa.compact", s);
-  k_fa_compact<0><<<dim3(c.N, B), 256, 0, s>>>(bb, c);
+  k_fa_compact<0><<<dim3(c.N, B), 256, 0, s>>>(bb, c, nullptr);
   fa_synccheck(s, "k_fa_compact");
 }
 

@@ -171,12 +171,6 @@ struct OdomBufs {
   int integ;
   unsigned long long* intX;  // [B*6]
 
-  // a node call (launch_fa with a side stream): the scan's less-flat
-  // VoxelGrid is still running when the LM starts; the hand-off, its only
-  // reader (publishCloudsLast, featureAssociation.cpp:1759-1815), first waits
-  // until BatchBufs::lfReady[b] counts every ring (bounded: kLfWaitTicks,
-  // then BatchBufs::bad[b] |= kBadLfLate and no less-flat points)
-  int lfWait;
 
   // per-scan outputs of the batch (workgroup 0)
   float* sumOut;        // [B*6]
@@ -211,14 +205,20 @@ void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hip
 // order); d_carry[S].
 // side (node calls, B = 1): the per-ring less-flat VoxelGrid and its
 // compaction go to that stream after `fork` is recorded on s, beside the
-// odometry launched next on s (OdomBufs::lfWait); the caller joins side into
-// s before reading f_lflat.  null: everything on s.
+// odometry launched next on s, each ring counted into lfReady[b] (release;
+// zeroed here first); the caller passes lfReady to launch_odom and joins side
+// into s before reading f_lflat.  null: everything on s.
 void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_carry, hipStream_t s,
-               StageTimer* tm, hipStream_t side = nullptr, hipEvent_t fork = nullptr);
+               StageTimer* tm, hipStream_t side = nullptr, hipEvent_t fork = nullptr, unsigned* lfReady = nullptr);
 // K scans per stream over ob.S streams (the caller zeroes *ob.xerr once per
-// batch).  Returns 0 on a successful launch.
+// batch).  Returns 0 on a successful launch.  lfReady (a node call, launch_fa
+// with a side stream): the scan's less-flat VoxelGrid is still running when
+// the LM starts; the hand-off, its only reader (publishCloudsLast,
+// featureAssociation.cpp:1759-1815), first waits until lfReady[b] counts
+// every ring (bounded: kLfWaitTicks, then bad[b] |= kBadLfLate and no
+// less-flat points).
 int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int K, hipStream_t s,
-                StageTimer* tm, unsigned long long* prof);
+                StageTimer* tm, unsigned long long* prof, unsigned* lfReady = nullptr);
 int odom_workgroups(int N, int cusAvailable);
 // sensors whose last clouds never fit LDS: the stream keeps one ring copy (OdomBufs::ring)
 bool odom_ring_sensor(int N);

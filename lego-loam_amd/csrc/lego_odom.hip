@@ -1293,6 +1293,9 @@ typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
 constexpr unsigned long long kStealTicks = 4000;  // 40 us at the 100 MHz wall clock
 constexpr unsigned long long kLateTicks = 200000000;  // 2 s: the diagnostic late workgroup's bound
+// odom_integrate's polls of one scan's granules before it gives up (each
+// s_sleep 2 = 128 clocks; ~20 M polls, seconds)
+constexpr unsigned kIntegPolls = 20000000u;
 constexpr unsigned long long kLfWaitTicks = 200000000;  // 2 s: a node call's hand-off waiting for the less-flat cloud
 __device__ __forceinline__ void x_publish(unsigned long long* p, unsigned long long v) {
   __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1800,13 +1803,18 @@ __device__ __forceinline__ void odom_integrate(const BatchBufs& bb, const OdomBu
   for (int b = s * K; b < s * K + K; ++b) {
     unsigned long long g = 0;
     const unsigned want = (unsigned)(b + 1);
+    unsigned polls = 0;
     if (lane < 6) {
       for (;;) {
         g = x_load(ob.intX + (size_t)b * 6 + lane);
-        if ((unsigned)(g >> 33) == want) break;
+        if ((unsigned)(g >> 33) == want || ++polls > kIntegPolls) break;
         __builtin_amdgcn_s_sleep(2);
       }
       tc[lane] = __uint_as_float((unsigned)g);
+    }
+    if (__ballot(polls > kIntegPolls)) {  // the batch's error word (3), not a hung device
+      if (lane == 0) *ob.xerr = 3u;
+      return;
     }
     const bool valid = (__builtin_amdgcn_readfirstlane((int)(unsigned)(g >> 32)) & 1) != 0;
     ImuScan iq = {};
@@ -1829,11 +1837,12 @@ __device__ __forceinline__ void odom_integrate(const BatchBufs& bb, const OdomBu
 // RING: the sensor keeps its last clouds in the stream's ring (OdomBufs::ring,
 // HDL-64E / VLS-128); a separate instantiation, so the LDS-resident sensors'
 // kernel carries none of its code or registers.  LFW: a node call's form,
-// whose hand-off waits for the side stream's less-flat cloud (OdomBufs::
-// lfWait); also separate, so the batch kernels keep their registers.
+// whose hand-off waits for the side stream's less-flat cloud (launch_odom's
+// lfReady, a trailing argument so the batch kernels' arguments keep their
+// offsets); also separate, so the batch kernels keep their registers.
 template <bool RING, bool LFW>
 __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs obShared, DevCfg c, int K,
-                                                      unsigned long long* prof) {
+                                                      unsigned long long* prof, const unsigned* lfReady) {
   // Claim the whole register file of the SIMD (2 waves x 256): no other
   // kernel's waves share a SIMD with the latency-bound chain while the next
   // chunk's extraction runs beside it.
@@ -1960,7 +1969,7 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
       if (tid == 0) {
         const unsigned long long t0 = wall_clock64();
         bool ok;
-        while (!(ok = __hip_atomic_load(bb.lfReady + b, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)c.N) &&
+        while (!(ok = __hip_atomic_load(lfReady + b, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)c.N) &&
                wall_clock64() - t0 < kLfWaitTicks)
           __builtin_amdgcn_s_sleep(2);
         L.n[N_LF] = ok ? __hip_atomic_load(bb.f_cnt + b * 4 + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
@@ -2500,7 +2509,7 @@ __global__ void k_ring_prep(OdomBufs ob, int K) {
 bool odom_ring_sensor(int N) { return !(N * kFlatPerRing <= kLdsQ && N * kSharpPerRing <= kLdsQ / 2); }
 
 int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int K, hipStream_t s, StageTimer* tm,
-                unsigned long long* prof) {
+                unsigned long long* prof, unsigned* lfReady) {
   tm->mark("odom.lm", s);
   if (ob.ring) {
     const int gx = (int)std::min<size_t>(64, (ob.ringCtl / 16 + 255) / 256);
@@ -2525,12 +2534,12 @@ int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int K,
   // A plain launch: the exchange needs no co-residency (see "exchange").
   const int blocks = ob.S * ob.G + (ob.integ ? ob.S : 0);  // the chains, then one integrating workgroup per stream
   const size_t lds = odom_lds_bytes();
-  if (ob.lfWait) {
-    if (ob.ring) k_odom<true, true><<<blocks, kOdomThreads, lds, s>>>(bb, ob, c, K, prof);
-    else k_odom<false, true><<<blocks, kOdomThreads, lds, s>>>(bb, ob, c, K, prof);
+  if (lfReady) {
+    if (ob.ring) k_odom<true, true><<<blocks, kOdomThreads, lds, s>>>(bb, ob, c, K, prof, lfReady);
+    else k_odom<false, true><<<blocks, kOdomThreads, lds, s>>>(bb, ob, c, K, prof, lfReady);
   } else {
-    if (ob.ring) k_odom<true, false><<<blocks, kOdomThreads, lds, s>>>(bb, ob, c, K, prof);
-    else k_odom<false, false><<<blocks, kOdomThreads, lds, s>>>(bb, ob, c, K, prof);
+    if (ob.ring) k_odom<true, false><<<blocks, kOdomThreads, lds, s>>>(bb, ob, c, K, prof, nullptr);
+    else k_odom<false, false><<<blocks, kOdomThreads, lds, s>>>(bb, ob, c, K, prof, nullptr);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
