@@ -172,44 +172,53 @@ __device__ void vg_heap_sort_wave(uint32_t* key, V* val, int first, int last) {
     for (int p = (1 << d) - 1 + lane; p < hi; p += 64) Hp.adjust_heap(0, p, len, K[p], W[p]);
     vg_wave_sync();
   }
-  const int dl = 31 - __builtin_clz((unsigned)lane + 1);  // the lane's level in a chunk (lane 63: 6, unused)
+  // lane l < 63 of a chunk: its level dl and offset jl under the chunk's
+  // root, the bits of its ancestors (anc) and of those whose right child
+  // leads to it (ancR): the walk reaches l exactly when every ancestor moves
+  // (G) and chose (R) that way, two mask tests instead of a serial walk
+  const int dl = 31 - __builtin_clz((unsigned)lane + 1);
   const int jl = lane + 1 - (1 << dl);
+  unsigned long long anc = 0ull, ancR = 0ull;
+  for (int i = 0; i < dl; ++i) {
+    const int a = ((lane + 1) >> (dl - i)) - 1;
+    anc |= 1ull << a;
+    if (((lane + 1) >> (dl - i - 1)) & 1) ancR |= 1ull << a;
+  }
   constexpr int NC = 2;
   for (int m = len - 1; m >= 1; --m) {
-    const uint32_t vk = __builtin_amdgcn_readfirstlane(K[m]);
-    const uint32_t vv = __builtin_amdgcn_readfirstlane((uint32_t)W[m]);
-    if (lane == 0) { K[m] = K[0]; W[m] = W[0]; }  // outside the heap [0, m): the chunks never read it
     const int lim = (m - 1) / 2, tnode = (m & 1) == 0 ? (m - 2) / 2 : -1;
     uint32_t ck[NC], cv[NC];
-    int px[NC];       // the lane's path index << 16 | its node (-1: off the path), its chosen child's key / payload
+    int px[NC];       // the lane's path index << 16 | its node (-1: not moved), its chosen child's key / payload
     int h = 0, k = 0; // the chunk's root, the path's steps so far
     bool more = true;
+    uint32_t vk = 0u, vv = 0u, rk = 0u, rv = 0u;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       ck[c] = 0u; cv[c] = 0u; px[c] = -1;
       if (!more) continue;
-      const int x = (h + 1) * (1 << dl) - 1 + jl;
+      const int x = c == 0 ? lane : (h + 1) * (1 << dl) - 1 + jl;
       const bool two = lane < 63 && x < lim, one = lane < 63 && x == tnode;
-      uint32_t kl = 0u, kr = 0u, vl = 0u, vr = 0u;
-      if (two || one) { kl = K[2 * x + 1]; vl = (uint32_t)W[2 * x + 1]; }
-      if (two) { kr = K[2 * x + 2]; vr = (uint32_t)W[2 * x + 2]; }
+      const int il = two || one ? 2 * x + 1 : 0, ir = two ? 2 * x + 2 : 0;
+      if (c == 0) {  // the popped value and the root with the first chunk's children: one round trip
+        vk = K[m]; vv = (uint32_t)W[m]; rk = K[0]; rv = (uint32_t)W[0];
+      }
+      const uint32_t kl = K[il], kr = K[ir], vl = (uint32_t)W[il], vr = (uint32_t)W[ir];
       const bool right = two && !(kr < kl);
       ck[c] = right ? kr : kl;
       cv[c] = right ? vr : vl;
       const unsigned long long G = __ballot(two || one), R = __ballot(right);
-      int l = 0;
-      unsigned long long path = 0ull;
-      for (int s = 0; s < 6; ++s) {
-        if (!((G >> l) & 1ull)) break;
-        path |= 1ull << l;
-        l = 2 * l + 1 + (int)((R >> l) & 1ull);
-      }
-      if ((path >> lane) & 1ull) px[c] = ((k + dl) << 16) | x;
-      k += (int)__popcll(path);
-      const int dL = 31 - __builtin_clz((unsigned)l + 1);
-      h = (h + 1) * (1 << dL) - 1 + (l + 1 - (1 << dL));  // where the walk stopped
-      more = dL == 6;  // six levels walked: the next chunk starts there
+      const bool on = lane < 63 && (G & anc) == anc && (R & anc) == ancR;
+      const unsigned long long P = __ballot(on);  // the walk's nodes in this chunk, one per level
+      if (on && (two || one)) px[c] = ((k + dl) << 16) | x;
+      k += (int)__popcll(P & G);
+      const int last = 63 - __builtin_clzll(P);
+      const int dL = 31 - __builtin_clz((unsigned)last + 1);
+      const int xl = (h + 1) * (1 << dL) - 1 + (last + 1 - (1 << dL));
+      more = ((G >> last) & 1ull) != 0;  // the chunk's last level moves on: the next chunk starts at its child
+      h = more ? 2 * xl + 1 + (int)((R >> last) & 1ull) : xl;
     }
+    vk = __builtin_amdgcn_readfirstlane(vk);
+    vv = __builtin_amdgcn_readfirstlane(vv);
     // the push: the hole stops at path node j = 1 + the deepest path index
     // whose chosen child's key is not < the value (0 if none)
     int j = 0;
@@ -222,6 +231,7 @@ __device__ void vg_heap_sort_wave(uint32_t* key, V* val, int first, int last) {
         found = true;
       }
     }
+    if (lane == 0) { K[m] = rk; W[m] = (V)rv; }  // outside the heap [0, m)
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int pi = px[c] >> 16, x = px[c] & 0xffff;

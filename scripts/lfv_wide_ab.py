@@ -18,7 +18,9 @@ import legoffi as L  # noqa: E402
 
 n = int(os.environ.get("SCANS", "24"))
 lib = L.hip_lib()
-for sensor, seed in (("VLP-16", 1), ("HDL-64E", 2), ("VLS-128", 3)):
+SENS = {"VLP-16": 1, "HDL-64E": 2, "VLS-128": 3}
+for sensor in os.environ.get("SENSORS", "VLP-16,HDL-64E,VLS-128").split(","):
+    seed = SENS[sensor]
     sc = L.synth_cfg(sensor, seed)
     scans = [L.synth_scan(sc, k) for k in range(n)]
     g = L.Lego(L.sensor_cfg(sensor, lib), max_points=max(len(p) for p, _ in scans) + 16)

@@ -1,0 +1,41 @@
+"""Per-ring time of the device's VoxelGrid block sort (GPU box): every ring of
+tests/golden/dense_ring_keys.npz (VLS-128 seed 3 scan 0, HDL-64E seed 2 scan 0)
+through lego_sort_permutation in the mode k_lf_voxel's node form runs (8: the
+LDS-id form, 1024 threads, sum order) and mode 7 (the same, exact order), host
+wall clock per call minus the call's floor (a 2-key sort), min of 5.  Prints
+the slowest rings with their heap-sorted piece counts.  Diagnostic."""
+import os
+import sys
+import time
+
+import numpy as np
+
+R = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, os.path.join(R, "lego-loam_amd"))
+import legoffi as L  # noqa: E402
+
+d = np.load(os.path.join(R, "tests/golden/dense_ring_keys.npz"))
+g = L.Lego(L.sensor_cfg("VLS-128", L.hip_lib()), max_points=4096)
+
+
+def t(keys, mode):
+    best = 1e9
+    for _ in range(5):
+        t0 = time.perf_counter()
+        _, heap = g.sort_permutation(keys, mode)
+        best = min(best, time.perf_counter() - t0)
+    return best * 1e6, heap
+
+
+floor = min(t(np.array([2, 1], np.uint32), m)[0] for m in (7, 8))
+print(f"call floor {floor:.1f} us")
+for mode in (8, 7):
+    rows = []
+    for k in d.files:
+        us, heap = t(d[k], mode)
+        rows.append((us - floor, k, len(d[k]), heap))
+    rows.sort(reverse=True)
+    print(f"mode {mode}: sum over rings {sum(r[0] for r in rows):.0f} us; slowest:")
+    for us, k, n, heap in rows[:8]:
+        print(f"  {k:14s} n {n:5d} heap pieces {heap:3d}  {us:8.1f} us")
+g.close()

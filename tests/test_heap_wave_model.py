@@ -2,7 +2,8 @@
 lane by lane in Python, against std::__partial_sort(first, last, last) as
 libstdc++ runs it (make_heap + sort_heap, stl_heap.h; VgHeap in lego_vgsort.h
 is its device port).  The wave form runs make_heap a heap level at a time and
-each sort_heap pop as a six-level chunked walk, a ballot for the push and one
+each sort_heap pop as a six-level chunked walk (the path's nodes found by
+mask tests against the chunk's ballots), a ballot for the push and one
 batch of stores; it must leave every (key, payload) pair where the serial form
 does, duplicates included (a VoxelGrid sums a voxel's points in that order).
 CPU model test; the device code itself is checked against std::sort by
@@ -59,12 +60,18 @@ def wave_heap_sort(K, W):
             adjust_heap(K, W, p, n, K[p], W[p])
     dl = [level(lane + 1) for lane in range(64)]
     jl = [lane + 1 - (1 << dl[lane]) for lane in range(64)]
+    anc, anc_r = [0] * 64, [0] * 64  # the lane's ancestors in a chunk, and those that go right toward it
+    for lane in range(64):
+        for i in range(dl[lane]):
+            a = ((lane + 1) >> (dl[lane] - i)) - 1
+            anc[lane] |= 1 << a
+            if ((lane + 1) >> (dl[lane] - i - 1)) & 1:
+                anc_r[lane] |= 1 << a
     for m in range(n - 1, 0, -1):
-        vk, vv = K[m], W[m]
-        K[m], W[m] = K[0], W[0]
         lim, tnode = (m - 1) // 2, ((m - 2) // 2 if m % 2 == 0 else -1)
         h = k = 0
         more = True
+        vk, vv, rk, rv = K[m], W[m], K[0], W[0]
         chunks = []
         for _ in range(2):
             px, ck, cv = [-1] * 64, [0] * 64, [0] * 64
@@ -73,31 +80,29 @@ def wave_heap_sort(K, W):
                 continue
             G = R = 0
             xs = [(h + 1) * (1 << dl[lane]) - 1 + jl[lane] for lane in range(64)]
+            go = [False] * 64
             for lane in range(64):
                 x = xs[lane]
                 two, one = lane < 63 and x < lim, lane < 63 and x == tnode
-                kl = kr = vl = vr = 0
-                if two or one:
-                    kl, vl = K[2 * x + 1], W[2 * x + 1]
-                if two:
-                    kr, vr = K[2 * x + 2], W[2 * x + 2]
+                il, ir = (2 * x + 1 if two or one else 0), (2 * x + 2 if two else 0)
+                kl, kr, vl, vr = K[il], K[ir], W[il], W[ir]
                 right = two and not kr < kl
                 ck[lane], cv[lane] = (kr, vr) if right else (kl, vl)
-                G |= (two or one) << lane
+                go[lane] = two or one
+                G |= go[lane] << lane
                 R |= right << lane
-            l, path = 0, 0
-            for _s in range(6):  # the scalar walk
-                if not (G >> l) & 1:
-                    break
-                path |= 1 << l
-                l = 2 * l + 1 + ((R >> l) & 1)
+            on = [lane < 63 and (G & anc[lane]) == anc[lane] and (R & anc[lane]) == anc_r[lane]
+                  for lane in range(64)]
+            P = sum(1 << lane for lane in range(64) if on[lane])
             for lane in range(64):
-                if (path >> lane) & 1:
+                if on[lane] and go[lane]:
                     px[lane] = ((k + dl[lane]) << 16) | xs[lane]
-            k += bin(path).count("1")
-            dL = level(l + 1)
-            h = (h + 1) * (1 << dL) - 1 + (l + 1 - (1 << dL))
-            more = dL == 6
+            k += bin(P & G).count("1")
+            last = P.bit_length() - 1
+            dL = level(last + 1)
+            xl = (h + 1) * (1 << dL) - 1 + (last + 1 - (1 << dL))
+            more = bool((G >> last) & 1)
+            h = 2 * xl + 1 + ((R >> last) & 1) if more else xl
             chunks.append((px, ck, cv))
         j = 0
         for px, ck, cv in reversed(chunks):  # the push: one ballot per chunk, deepest first
@@ -105,6 +110,7 @@ def wave_heap_sort(K, W):
             if F:
                 j = (px[max(F)] >> 16) + 1
                 break
+        K[m], W[m] = rk, rv
         for px, ck, cv in chunks:
             for lane in range(64):
                 if px[lane] < 0:
