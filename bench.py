@@ -881,16 +881,27 @@ def main():
         gpu.close()
         gpu = None
         aux = {"mapping_handoff": handoff}
+        t_aux = time.perf_counter()
+
+        def progress(leg):  # one stderr line per aux leg (a long run is seen to advance)
+            print(f"bench: {leg} at {time.perf_counter() - t_aux:.0f} s", file=sys.stderr, flush=True)
+
         if args.mapping_steps > 0 and world == 1:
+            progress("C5")
             aux["scan_to_map_c5"] = mapping_bench(L, args.mapping_steps, not args.no_cpu)
         if args.fleet_streams > 0 and world == 1:
+            progress("fleet")
             aux["fleet_vlp16"] = fleet_bench(L, args.fleet_streams, 20, 3, local, check=not args.no_cpu)
         if args.dense_scans > 0 and world == 1:
+            progress("C3")
             aux["dense_hdl64_c3"] = dense_bench(L, args.dense_scans, 20, local, cpu=not args.no_cpu)
         if args.loop_scans > 0 and world == 1:
+            progress("loop closure")
             aux["loop_closure"] = loop_bench(L, args.loop_scans, 5, not args.no_cpu)
         if args.node_scans > 0 and world == 1:
+            progress("node path")
             aux["node_path"] = node_path_bench(L, args.node_scans, not args.no_cpu)
+            progress("node path VLS-128")
             # the dense single-scan path (VLS-128: 128 rings per VoxelGrid launch)
             aux["node_path_vls128"] = node_path_bench(L, max(8, args.node_scans // 3), not args.no_cpu,
                                                       cpu_scans=8, sensor="VLS-128", seed=3)
