@@ -20,6 +20,7 @@
 // (SURVEY.md §9.2); compiled with -ffp-contract=off.
 #include <cfloat>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "lego_device.h"
@@ -254,10 +255,16 @@ __global__ void k_ccl_root(BatchBufs bb, DevCfg c) {
 // HBM; the smallest tile root of a component becomes its root, the same
 // index the HBM-only union-find (k_ccl_init / _union) gives.
 constexpr int kCclTilePx = 32768;  // 128 KB of parents
-int ccl_tile_width(const DevCfg& c) {
-  int tw = kCclTilePx / c.N;
-  if (tw >= c.H) return c.H;
-  return tw;
+// A launch of few scans takes narrower tiles, so that it still spreads over
+// kCclMinTiles workgroups: one VLP-16 scan was one tile, one workgroup's
+// serial unions (68 us in the node call's trace, gpurun_out r05p/node), now 64
+// tiles of 29 columns and their seams.
+constexpr int kCclMinTiles = 64, kCclMinWidth = 16;
+int ccl_tile_width(const DevCfg& c, int B) {
+  const int byLds = std::max(1, kCclTilePx / c.N);
+  const int byGrid = std::max(kCclMinWidth, (c.H * B + kCclMinTiles - 1) / kCclMinTiles);
+  const int tw = std::min(byLds, byGrid);
+  return tw >= c.H ? c.H : tw;
 }
 __global__ void __launch_bounds__(1024) k_ccl_tile(BatchBufs bb, DevCfg c, int TW) {
   extern __shared__ int par[];  // [N * tw], index row * tw + (col - c0)
@@ -825,7 +832,7 @@ void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hip
   // diagnostic: every edge in HBM, k_ccl_init / k_ccl_union)
   static const bool tiles = !std::getenv("LEGO_CCL_TILES") || std::atoi(std::getenv("LEGO_CCL_TILES")) != 0;
   if (tiles) {
-    const int TW = ccl_tile_width(c), nT = (c.H + TW - 1) / TW;
+    const int TW = ccl_tile_width(c, B), nT = (c.H + TW - 1) / TW;
     k_ccl_tile<<<dim3(nT, B), 1024, (size_t)c.N * TW * sizeof(int), s>>>(bb, c, TW);
     if (nT > 1) k_ccl_seam<<<dim3((nT * c.N + 255) / 256, B), 256, 0, s>>>(bb, c, TW, nT);
   } else {
