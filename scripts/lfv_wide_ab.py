@@ -27,9 +27,10 @@ for sensor in os.environ.get("SENSORS", "VLP-16,HDL-64E,VLS-128").split(","):
     on = (C.c_float * 1)()
     nn = C.c_int32()
     lib.lego_stage_times(g.h, None, on, 0, C.byref(nn))  # stage events on
-    res = {0: ([], [], []), 1: ([], [], [])}
+    wides = [int(w) for w in os.environ.get("WIDES", "1,0").split(",")]
+    res = {w: ([], [], []) for w in wides}
     for k, (p, s) in enumerate(scans):
-        wide = k % 2
+        wide = wides[k % len(wides)]
         os.environ["LEGO_LFV_WIDE"] = str(wide)
         g.ip(p, s)
         t0 = time.perf_counter()
@@ -41,7 +42,7 @@ for sensor in os.environ.get("SENSORS", "VLP-16,HDL-64E,VLS-128").split(","):
             res[wide][1].append(st.get("fa.voxel", float("nan")))
             res[wide][2].append(st)
     g.close()
-    for w in (1, 0):
+    for w in wides:
         print(f"{sensor:8s} wide={w}  fa median {statistics.median(res[w][0]):.3f} ms  "
               f"k_lf_voxel median {statistics.median(res[w][1]) * 1e3:.1f} us  (n={len(res[w][0])})", flush=True)
         print("   stages (us): " + "  ".join(f"{k} {statistics.median(d.get(k, 0.0) for d in res[w][2]) * 1e3:.1f}"
