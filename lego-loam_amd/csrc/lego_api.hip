@@ -98,6 +98,11 @@ struct lego_ctx {
   hipEvent_t oJoin = nullptr;                   // ostream work so far (node calls order after it)
   hipEvent_t lfFork = nullptr;                  // a node call's features, before its side-stream VoxelGrid
   unsigned* d_lfReady = nullptr;                // [1] its rings counted as their less-flat clouds land
+  // A fleet batch's projection + extraction in parts of whole streams, part
+  // p > 0 on fstream[p - 1] (created on first use; front_parts)
+  static constexpr int kFrontPartsMax = 4;
+  hipStream_t fstream[kFrontPartsMax - 1] = {};
+  hipEvent_t fFork = nullptr, fJoin[kFrontPartsMax - 1] = {};
   int nextSlot = 0, inflight = 0, oldest = 0;
   int slotB[2] = {0, 0};
   std::vector<double> slotStamps[2];
@@ -112,6 +117,7 @@ struct lego_ctx {
   std::vector<void*> allocs;
   StageTimer tm, otm;            // node-shaped calls
   StageTimer stm[2], sotm[2];    // per batch slot: extraction / odometry stages
+  StageTimer ftm;                // the front-end parts p > 0 (never enabled)
   // last batch
   int lastB = 0;
   std::vector<double> stamps;
@@ -205,6 +211,8 @@ struct lego_ctx {
     if (device >= 0) (void)hipSetDevice(device);
     if (stream) (void)hipStreamSynchronize(stream);  // batches still in flight
     if (ostream) (void)hipStreamSynchronize(ostream);
+    for (auto f : fstream)
+      if (f) (void)hipStreamSynchronize(f);
     if (mo.fork[1]) (void)hipStreamSynchronize(mo.fork[1]);  // the mapping VoxelGrids' fork
     if (d_raw) (void)hipFree(d_raw);
     if (handoffFenced) (void)hipEventSynchronize(handoffFence);  // a send still reading d_handoff
@@ -220,6 +228,11 @@ struct lego_ctx {
     for (void* p : allocs) (void)hipFree(p);
     if (oJoin) (void)hipEventDestroy(oJoin);
     if (lfFork) (void)hipEventDestroy(lfFork);
+    if (fFork) (void)hipEventDestroy(fFork);
+    for (auto e : fJoin)
+      if (e) (void)hipEventDestroy(e);
+    for (auto f : fstream)
+      if (f) (void)hipStreamDestroy(f);
     for (int i = 0; i < 2; ++i) {
       if (faDone[i]) (void)hipEventDestroy(faDone[i]);
       if (recsDone[i]) (void)hipEventDestroy(recsDone[i]);
@@ -815,6 +828,29 @@ static int run_ip(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offse
   return LEGO_OK;
 }
 
+// Parts of a fleet batch's front end (submit_batch): LEGO_FRONT_PARTS (read
+// per call; A/B knob), else kFrontPartsDefault; at most kFrontPartsMax,
+// reduced until it divides the streams.  A single stream is one part (its
+// scans chain through the extraction's carry).
+constexpr int kFrontPartsDefault = 2;  // profiles/r05_ab_front_parts.txt
+static int front_parts(int S) {
+  int p = kFrontPartsDefault;
+  if (const char* e = std::getenv("LEGO_FRONT_PARTS")) p = std::atoi(e);
+  p = std::max(1, std::min(p, lego_ctx::kFrontPartsMax));
+  while (S % p) --p;
+  return p;
+}
+
+static int front_streams(lego_ctx* x, int parts) {
+  HIPCHK(hipSetDevice(x->device));
+  if (!x->fFork) HIPCHK(hipEventCreateWithFlags(&x->fFork, hipEventDisableTiming));
+  for (int p = 1; p < parts; ++p) {
+    if (!x->fstream[p - 1]) HIPCHK(hipStreamCreateWithFlags(&x->fstream[p - 1], hipStreamNonBlocking));
+    if (!x->fJoin[p - 1]) HIPCHK(hipEventCreateWithFlags(&x->fJoin[p - 1], hipEventDisableTiming));
+  }
+  return LEGO_OK;
+}
+
 // Enqueues ip + fa + odometry for a batch (x->stamps) in the next slot and
 // returns.  Projection and extraction run on x->stream, the odometry on
 // x->ostream after them, so they overlap the previous batch's odometry.
@@ -841,8 +877,30 @@ static int submit_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t*
   bb.xprof = x->profOn ? x->d_prof + 32 : nullptr;
   tm.begin();
   otm.begin();
-  launch_ip(bb, x->dc, B, 0, x->stream, &tm);
-  launch_fa(bb, x->dc, B, S, x->d_carry, x->stream, &tm);
+  // a fleet's streams are independent up to the odometry: their projection
+  // and extraction in parts of whole streams (the batch is stream-major), on
+  // HIP streams of their own, so that one part's LDS-bound kernels
+  // (segmentation, VoxelGrids) share the CUs with another's HBM-bound ones
+  const int parts = front_parts(S);
+  if (parts > 1) {
+    st = front_streams(x, parts);
+    if (st != LEGO_OK) return st;
+    HIPCHK(hipEventRecord(x->fFork, x->stream));
+    for (int p = 1; p < parts; ++p) HIPCHK(hipStreamWaitEvent(x->fstream[p - 1], x->fFork, 0));
+  }
+  const int Sp = S / parts, Bp = B / parts;
+  for (int p = 0; p < parts; ++p) {
+    hipStream_t s = p ? x->fstream[p - 1] : x->stream;
+    StageTimer* t = p ? &x->ftm : &tm;  // the stage times are part 0's
+    BatchBufs q = parts > 1 ? bb_slice(bb, x->dc, p * Bp, Bp) : bb;
+    if (p) q.xprof = nullptr;
+    launch_ip(q, x->dc, Bp, 0, s, t);
+    launch_fa(q, x->dc, Bp, Sp, x->d_carry + p * Sp, s, t);
+  }
+  for (int p = 1; p < parts; ++p) {
+    HIPCHK(hipEventRecord(x->fJoin[p - 1], x->fstream[p - 1]));
+    HIPCHK(hipStreamWaitEvent(x->stream, x->fJoin[p - 1], 0));
+  }
   tm.end(x->stream);
   HIPCHK(hipEventRecord(x->faDone[h], x->stream));
   HIPCHK(hipStreamWaitEvent(x->ostream, x->faDone[h], 0));
