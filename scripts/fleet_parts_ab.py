@@ -78,7 +78,7 @@ def main():
             fl.wait(recs)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
-            print(json.dumps({"round": r, "parts": int(p), "scans_per_s": round(S * K * args.calls / dt),
+            print(json.dumps({"round": r, "parts": p, "scans_per_s": round(S * K * args.calls / dt),
                               "ms_per_call": round(dt / args.calls * 1e3, 3),
                               "valid": sum(x.odom_valid for x in recs)}), flush=True)
     fl.close()
