@@ -10,7 +10,7 @@
 namespace lego {
 
 #ifndef VG_WSTAMP
-#define VG_WSTAMP(k, t0)
+#define VG_WSTAMP(k, t0) (void)(t0)
 #endif
 #ifndef VG_CLOCK
 #define VG_CLOCK() 0ull
