@@ -89,39 +89,56 @@ __global__ void __launch_bounds__(256) k_pixels(BatchBufs bb, DevCfg c) {
 }
 
 // groundMat column walk.  Carry form of the overwrite semantics:
-// G[i] is final once pair (i, i+1) has been examined.
+// G[i] is final once pair (i, i+1) has been examined.  Rows in chunks of
+// kGroundRows: the chunk's points and ranges are loaded before any of its
+// stores (one memory latency per chunk; the stores' possible aliasing kept
+// the per-row form's loads behind the previous row's stores: ~13.5 us for a
+// single VLP-16 scan, 16 dependent rows).
+constexpr int kGroundRows = 8;
 __global__ void k_ground(BatchBufs bb, DevCfg c) {
   const int b = blockIdx.y;
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= c.H) return;
   const size_t base = (size_t)b * c.P;
   int cur = 0;  // value G[i] holds before pair i is examined
-  for (int i = 0; i < c.N; ++i) {
-    int G;
-    int next = 0;
-    if (i < c.g) {
-      const float4 lo = bb.full[base + i * c.H + j];
-      const float4 up = bb.full[base + (i + 1) * c.H + j];
-      if (lo.w == -1.0f || up.w == -1.0f) {
-        G = -1;
-      } else {
-        const float dX = up.x - lo.x, dY = up.y - lo.y, dZ = up.z - lo.z;
-        const float angle =
-            (float)((double)(lego_atan2f(dZ, __builtin_sqrtf(dX * dX + dY * dY)) * 180.0f) / M_PI);
-        if (lfabsf(angle - c.mount_angle) <= 10) {
-          G = 1;
-          next = 1;
-        } else {
-          G = cur;
-        }
-      }
-    } else {
-      G = cur;
+  for (int i0 = 0; i0 < c.N; i0 += kGroundRows) {
+    float4 pt[kGroundRows + 1];  // rows i0 .. i0 + kGroundRows, where a pair (i < g) reads them
+    float rg[kGroundRows];
+#pragma unroll
+    for (int u = 0; u <= kGroundRows; ++u) {
+      const int i = i0 + u;
+      pt[u] = i <= c.g && i < c.N ? bb.full[base + i * c.H + j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (u < kGroundRows) rg[u] = i < c.N ? bb.range[base + i * c.H + j] : 0.f;
     }
-    cur = next;
-    const size_t gp = base + i * c.H + j;
-    bb.ground[gp] = (int8_t)G;
-    bb.label[gp] = (G == 1 || bb.range[gp] == FLT_MAX) ? -1 : 0;     // :295-301
+#pragma unroll
+    for (int u = 0; u < kGroundRows; ++u) {
+      const int i = i0 + u;
+      if (i >= c.N) break;
+      int G;
+      int next = 0;
+      if (i < c.g) {
+        const float4 lo = pt[u], up = pt[u + 1];
+        if (lo.w == -1.0f || up.w == -1.0f) {
+          G = -1;
+        } else {
+          const float dX = up.x - lo.x, dY = up.y - lo.y, dZ = up.z - lo.z;
+          const float angle =
+              (float)((double)(lego_atan2f(dZ, __builtin_sqrtf(dX * dX + dY * dY)) * 180.0f) / M_PI);
+          if (lfabsf(angle - c.mount_angle) <= 10) {
+            G = 1;
+            next = 1;
+          } else {
+            G = cur;
+          }
+        }
+      } else {
+        G = cur;
+      }
+      cur = next;
+      const size_t gp = base + i * c.H + j;
+      bb.ground[gp] = (int8_t)G;
+      bb.label[gp] = (G == 1 || rg[u] == FLT_MAX) ? -1 : 0;     // :295-301
+    }
   }
 }
 
@@ -405,11 +422,11 @@ __device__ __forceinline__ Scan3 block_scan3_bits(bool f0, bool f1, bool f2, Sca
 //               valid root, valid, in a segment) into edges[] (free after the
 //               unions), and the chunk's three counts into parent[] (free
 //               after the roots: 3 ints per chunk at the scan's base);
-//  k_seg_scan   per scan the chunks' exclusive prefixes, in place, and the
-//               scan's totals (segmented / outlier counts, the last ring's end,
-//               findStartEndAngle);
-//  k_seg_write  each chunk's outputs at their ordered positions, and a valid
-//               root's label, negated, into root[] at the root;
+//  k_seg_write  each chunk's exclusive prefixes (wave 0 sums the earlier
+//               chunks' counts: a few hundred L2-resident words at most, in
+//               place of a per-scan scan launch), the chunk's outputs at their
+//               ordered positions, a valid root's label, negated, into root[]
+//               at the root; the last chunk the scan's totals (seg_totals);
 //  k_seg_labels (labels wanted) the final labelMat.
 // The results equal the single-workgroup walk of round 1 and k_seg_lds.
 enum { SF_KEEP = 1, SF_OUTL = 2, SF_VROOT = 4, SF_VALID = 8, SF_INSEG = 16 };
@@ -458,49 +475,52 @@ __global__ void __launch_bounds__(1024) k_seg_flags(BatchBufs bb, DevCfg c) {
   block_counts3(keep, outl, vroot, lds, bb.parent + base + 3 * ch);
 }
 
-__global__ void __launch_bounds__(1024) k_seg_scan(BatchBufs bb, DevCfg c) {
-  __shared__ int lds[64];
-  const int b = blockIdx.x;
-  const size_t base = (size_t)b * c.P;
-  const int nCh = (c.P + 1023) / 1024;
-  int* cnt = bb.parent + base;
-  int run[3] = {0, 0, 0};
-  for (int c0 = 0; c0 < nCh; c0 += blockDim.x) {
-    const int ch = c0 + threadIdx.x;
-    Scan3 in{{0, 0, 0}}, tot;
-    if (ch < nCh) in = Scan3{{cnt[3 * ch], cnt[3 * ch + 1], cnt[3 * ch + 2]}};
-    const Scan3 ex = block_scan3(in, &tot, lds);
-    if (ch < nCh)
-      for (int f = 0; f < 3; ++f) cnt[3 * ch + f] = run[f] + ex.v[f];
-    for (int f = 0; f < 3; ++f) run[f] += tot.v[f];
-  }
-  if (threadIdx.x == 0) {
-    const int segc = run[0], outc = run[1];
-    bb.ns[b] = segc;
-    bb.nout[b] = outc;
-    bb.eri[b * c.N + c.N - 1] = segc - 1 - 5;
-    // findStartEndAngle :199-209
-    const float so = bb.rawang[2 * b];
-    float eo = (float)((double)bb.rawang[2 * b + 1] + 2 * M_PI);
-    if ((double)(eo - so) > 3 * M_PI) eo = (float)((double)eo - 2 * M_PI);
-    else if ((double)(eo - so) < M_PI) eo = (float)((double)eo + 2 * M_PI);
-    bb.orient[3 * b] = so;
-    bb.orient[3 * b + 1] = eo;
-    bb.orient[3 * b + 2] = eo - so;
-  }
+// The scan's totals (segmented / outlier counts, the last ring's end) and
+// findStartEndAngle (:199-209); k_seg_write's last chunk.
+__device__ void seg_totals(const BatchBufs& bb, const DevCfg& c, int b, int segc, int outc) {
+  bb.ns[b] = segc;
+  bb.nout[b] = outc;
+  bb.eri[b * c.N + c.N - 1] = segc - 1 - 5;
+  const float so = bb.rawang[2 * b];
+  float eo = (float)((double)bb.rawang[2 * b + 1] + 2 * M_PI);
+  if ((double)(eo - so) > 3 * M_PI) eo = (float)((double)eo - 2 * M_PI);
+  else if ((double)(eo - so) < M_PI) eo = (float)((double)eo + 2 * M_PI);
+  bb.orient[3 * b] = so;
+  bb.orient[3 * b + 1] = eo;
+  bb.orient[3 * b + 2] = eo - so;
 }
 
 __global__ void __launch_bounds__(1024) k_seg_write(BatchBufs bb, DevCfg c) {
   __shared__ int lds[64];
+  __shared__ int off[3];  // the kept / outlier / valid-root pixels of the chunks before this one
   const int b = blockIdx.y, ch = blockIdx.x;
   const int p = ch * blockDim.x + threadIdx.x;
   const size_t base = (size_t)b * c.P;
+  if (threadIdx.x < 64) {  // the earlier chunks' counts (k_seg_flags), summed by wave 0
+    const int* cnt = bb.parent + base;
+    int s0 = 0, s1 = 0, s2 = 0;
+    for (int q = threadIdx.x; q < ch; q += 64) {
+      s0 += cnt[3 * q];
+      s1 += cnt[3 * q + 1];
+      s2 += cnt[3 * q + 2];
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      s0 += __shfl_xor(s0, o, 64);
+      s1 += __shfl_xor(s1, o, 64);
+      s2 += __shfl_xor(s2, o, 64);
+    }
+    if (threadIdx.x == 0) {
+      off[0] = s0;
+      off[1] = s1;
+      off[2] = s2;
+    }
+  }
   const int f = p < c.P ? bb.edges[base + p] : 0;
   const bool keep = f & SF_KEEP, outl = f & SF_OUTL, vroot = f & SF_VROOT;
   Scan3 tot;
-  const Scan3 ex = block_scan3_bits(keep, outl, vroot, &tot, lds);
+  const Scan3 ex = block_scan3_bits(keep, outl, vroot, &tot, lds);  // its barriers publish off[]
+  if (threadIdx.x == 0 && ch == (int)gridDim.x - 1) seg_totals(bb, c, b, off[0] + tot.v[0], off[1] + tot.v[1]);
   if (p >= c.P) return;
-  const int* off = bb.parent + base + 3 * ch;
   const int row = p / c.H, col = p - row * c.H;
   const int pos = off[0] + ex.v[0];  // kept pixels before p
   if (col == 0) {  // ring boundaries (:323, :354)
@@ -843,7 +863,6 @@ void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hip
   tm->mark("ip.compact", s);
   const dim3 gch((P + 1023) / 1024, B);
   k_seg_flags<<<gch, 1024, 0, s>>>(bb, c);
-  k_seg_scan<<<B, 1024, 0, s>>>(bb, c);
   k_seg_write<<<gch, 1024, 0, s>>>(bb, c);
   if (want_labels) k_seg_labels<<<gpix, 256, 0, s>>>(bb, c);
 }
