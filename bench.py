@@ -259,13 +259,13 @@ def mapping_bench(L, steps: int, cpu: bool):
 
     # a throwaway context's first step loads the mapping kernels' code: the
     # timed contexts then time steps 1..steps, the same steps the CPU leg runs
-    warm = L.Lego(L.sensor_cfg(sensor, L.hip_lib()), max_points=cap)
+    warm = L.Lego(L.sensor_cfg(sensor, L.hip_lib()), max_points=cap, opts=L.opts_from_env())
     run(warm, True, 1)
     warm.close()
-    gpu = L.Lego(L.sensor_cfg(sensor, L.hip_lib()), max_points=cap)
+    gpu = L.Lego(L.sensor_cfg(sensor, L.hip_lib()), max_points=cap, opts=L.opts_from_env())
     dts, outs = run(gpu, True, steps)
     gpu.close()
-    gpu = L.Lego(L.sensor_cfg(sensor, L.hip_lib()), max_points=cap)
+    gpu = L.Lego(L.sensor_cfg(sensor, L.hip_lib()), max_points=cap, opts=L.opts_from_env())
     dts1, _ = run(gpu, False, steps)
     gpu.close()
     its = [o["iterations"] for o in outs]
@@ -308,7 +308,7 @@ def loop_bench(L, nscans: int, calls: int, cpu: bool):
     sc = L.synth_cfg("VLP-16", 6, yaw_rate_dps=15.0, speed_mps=1.0)
     cap = L.synth_lib().lego_synth_max_points(L.C.byref(sc))
     scans = [L.synth_scan(sc, k) for k in range(nscans)]
-    gpu = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=cap)
+    gpu = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=cap, opts=L.opts_from_env())
     for pts, stamp in scans:
         gpu.ip(pts, stamp)
         gpu.fa()
@@ -392,10 +392,10 @@ def node_path_bench(L, nscans: int, cpu: bool, cpu_scans: int = 40, sensor: str 
                 "mapping_step_ms_max": max(t_map) if t_map else None}
 
     lib = L.hip_lib()
-    warm = L.Lego(L.sensor_cfg(sensor, lib), max_points=cap)
+    warm = L.Lego(L.sensor_cfg(sensor, lib), max_points=cap, opts=L.opts_from_env())
     run(lib, warm.h, lib.lego_ip_process, lib.lego_fa_process, lib.lego_mo_process, 8)
     warm.close()
-    gpu = L.Lego(L.sensor_cfg(sensor, lib), max_points=cap)
+    gpu = L.Lego(L.sensor_cfg(sensor, lib), max_points=cap, opts=L.opts_from_env())
     name = "C2 stream (VLP-16 seed 1)" if (sensor, seed) == ("VLP-16", 1) else f"{sensor} seed {seed} stream"
     res = {"workload": f"{name} one scan at a time from host buffers through the node API: "
                        f"lego_ip_process -> lego_fa_process -> lego_mo_process (keyframe map), {nscans} scans"}
@@ -429,7 +429,7 @@ def dense_bench(L, nscans: int, batch: int, device: int, cpu: bool = False, budg
     nb = nscans // batch
     d_pts = torch.from_numpy(pts.view(np.uint8)).to(device)
     d_off = [torch.from_numpy(off[i * batch:(i + 1) * batch + 1].astype(np.int64)).to(device) for i in range(nb)]
-    g = L.Lego(cfg, device=device, max_points=maxn + 16, max_batch=batch)
+    g = L.Lego(cfg, device=device, max_points=maxn + 16, max_batch=batch, opts=L.opts_from_env())
     recs = (L.PoseRec * batch)()
     sub = lambda j: g.submit_device(d_pts.data_ptr(), d_off[j].data_ptr(), stamps[j * batch:(j + 1) * batch],  # noqa: E731
                                     batch)
@@ -528,7 +528,7 @@ def fleet_bench(L, streams: int, k: int, steps: int, device: int, check: bool = 
         st = np.concatenate([np.arange(w * k, (w + 1) * k) * 0.1] * streams)
         wins.append((torch.from_numpy(np.concatenate(scans).view(np.uint8)).to(device),
                      torch.from_numpy(off).to(device), st))
-    fl = L.Lego(cfg, device=device, max_points=maxn + 16, max_batch=k, streams=streams)
+    fl = L.Lego(cfg, device=device, max_points=maxn + 16, max_batch=k, streams=streams, opts=L.opts_from_env())
     recs = (L.PoseRec * (streams * k))()
     sub = lambda w: fl.submit_device(w[0].data_ptr(), w[1].data_ptr(), w[2], streams * k)  # noqa: E731
     sub(wins[0])  # warm-up (initialises every stream)
@@ -624,7 +624,8 @@ def main():
     # (LEGO_BENCH_PG_TIMEOUT_S) and a per-rank watchdog (LEGO_BENCH_WATCHDOG_S)
     # that ends a rank making no progress with a message naming the step and
     # phase (multistream.Watchdog: os._exit, never a re-exec).  The native
-    # gather's own waits are bounded by LEGO_COMM_TIMEOUT_MS (lego_comm_create).
+    # gather's own waits are bounded by lego_comm_set_timeout (LEGO_COMM_TIMEOUT_MS
+    # in the environment, multistream.native_comm).
     wd = None
     pg_timeout = datetime.timedelta(seconds=float(os.environ.get("LEGO_BENCH_PG_TIMEOUT_S", "300")))
     if world > 1:
@@ -654,7 +655,7 @@ def main():
     d_off = [torch.from_numpy((off[i * B:(i + 1) * B + 1] - 0).astype(np.int64)).to(dev)
              for i in range(nb)]
     torch.cuda.synchronize()
-    gpu = L.Lego(cfg, device=local, max_points=maxn + 16, max_batch=B)
+    gpu = L.Lego(cfg, device=local, max_points=maxn + 16, max_batch=B, opts=L.opts_from_env())
     n_en = C.c_int32()
     on = (C.c_float * 1)()
     lib.lego_stage_times(gpu.h, None, on, 0, C.byref(n_en))  # enable the stage timer

@@ -232,8 +232,54 @@ int lego_create(const lego_sensor_cfg* cfg, int device, int32_t max_points,
  * No reference counterpart: the reference runs one stream per process. */
 int lego_fleet_create(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
                       int32_t max_points, int32_t scans_per_stream, lego_ctx** out);
+
+/* Per-context options, fixed at creation (lego_create_ex /
+ * lego_fleet_create_ex; lego_create and lego_fleet_create use the defaults).
+ * Scheduling and diagnostic switches: none of them changes a result, which
+ * the tests check by running both settings against the oracle.  Nothing in
+ * the library reads the environment.  No reference counterpart (the
+ * reference's schedule is fixed by its ROS nodes). */
+typedef struct lego_ctx_opts {
+  int32_t size;            /* sizeof(lego_ctx_opts); lego_ctx_opts_init sets it */
+  int32_t node_overlap;    /* 1 (default): lego_fa_process runs the per-ring less-flat VoxelGrid on a
+                              second stream beside the LM; 0: one stream */
+  int32_t front_parts;     /* a fleet batch's projection + extraction in this many parts of whole
+                              streams on their own HIP streams (default 2; reduced to a divisor) */
+  int32_t lfv_wave;        /* 1 (default): small rings' VoxelGrids by one wave each; 0: by workgroups */
+  int32_t lfv_block_rings; /* large rings per VoxelGrid workgroup; 0 (default): by the launch size */
+  int32_t lfv_wide;        /* 1: every ring's VoxelGrid by a 1024-thread workgroup, 0: 256 threads,
+                              -1 (default): 1024 for launches of <= 128 rings */
+  int32_t ccl_tiles;       /* 1 (default): the HBM union-find in LDS column tiles + seams; 0: per edge in HBM */
+  int32_t seg_hbm;         /* 1: every image through the HBM union-find (diagnostic; default 0) */
+  int32_t odom_workgroups; /* odometry workgroups per stream; 0 (default): by the sensor and the CUs */
+  int32_t odom_gridless;   /* 1 / 0: NN without / with grids; -1 (default): by the workgroup count */
+  int32_t odom_integ;      /* 1 / 0: the integration on its own workgroup or the lead's;
+                              -1 (default): its own when there are >= 2 workgroups */
+  int32_t odom_silent_wg;  /* diagnostic: this workgroup publishes into private exchange copies
+                              (the others steal its work); -1 (default): none */
+  int32_t odom_late_wg;    /* diagnostic: this workgroup starts after the lead ends; -1: none */
+  int32_t lf_wait_ms;      /* the node hand-off's bound on waiting for the VoxelGrid's stream
+                              (default 2000; 0: never waits, i.e. a forced LEGO_E_DEVICE, for tests) */
+  int32_t mo_cand_cache;   /* 1 (default): mapping keeps a candidate cache of map points */
+  int32_t kf_cap;          /* keyframe store capacity cap; 0 (default): sized from the arena */
+  int32_t vg_rounds;       /* mapping VoxelGrids' partition rounds; -1 (default): by the cloud size */
+  int32_t fa_synccheck;    /* diagnostic: synchronise after every extraction launch and name the
+                              kernel that failed (stderr); default 0 */
+  int32_t mo_hostprof;     /* diagnostic: the mapping step's host enqueue times (stderr); default 0 */
+  int32_t mo_evprof;       /* diagnostic: the mapping step's chain times (stderr); default 0 */
+  int32_t reserved[12];
+} lego_ctx_opts;
+void lego_ctx_opts_init(lego_ctx_opts* opts);
+/* lego_create / lego_fleet_create with options (NULL: the defaults). */
+int lego_create_ex(const lego_sensor_cfg* cfg, int device, int32_t max_points, int32_t max_batch,
+                   const lego_ctx_opts* opts, lego_ctx** out);
+int lego_fleet_create_ex(const lego_sensor_cfg* cfg, int device, int32_t n_streams, int32_t max_points,
+                         int32_t scans_per_stream, const lego_ctx_opts* opts, lego_ctx** out);
 int lego_destroy(lego_ctx* ctx);
-/* Resets the per-stream state (odometry, residues) to construction values. */
+/* Resets the per-stream state (odometry, residues) to construction values.
+ * Needed after a LEGO_E_DEVICE of the odometry's hand-off wait (the stream's
+ * state is then not advanced; lego_fa_process and the batch calls return
+ * LEGO_E_STATE until the reset). */
 int lego_reset(lego_ctx* ctx);
 
 int lego_ip_process(lego_ctx* ctx, const lego_point_xyzir* pts, int32_t n,
@@ -441,12 +487,13 @@ int lego_handoff_unpack(const void* packet, uint64_t bytes, int32_t k, lego_pose
  * (the caller broadcasts the 128 bytes, e.g. over MPI or torch.distributed). */
 typedef struct lego_comm lego_comm;
 int lego_comm_unique_id(uint8_t id[128]);
-/* Every wait a call makes on the communicator's stream is bounded by the
- * LEGO_COMM_TIMEOUT_MS environment value read here (default 60000): a peer
- * that never joins a collective makes the waiting call abort the
- * communicator and return LEGO_E_DEVICE with the wait named in
- * lego_last_error, instead of blocking the process. */
+/* Every wait a call makes on the communicator's stream is bounded (default
+ * 60000 ms, lego_comm_set_timeout): a peer that never joins a collective
+ * makes the waiting call abort the communicator and return LEGO_E_DEVICE with
+ * the wait named in lego_last_error, instead of blocking the process. */
 int lego_comm_create(const uint8_t id[128], int32_t nranks, int32_t rank, int32_t device, lego_comm** out);
+/* The bound of every later wait on the communicator's stream, ms >= 1. */
+int lego_comm_set_timeout(lego_comm* comm, int32_t timeout_ms);
 int lego_comm_destroy(lego_comm* comm);
 /* The communicator's rank count as RCCL reports it (ncclCommCount). */
 int lego_comm_count(lego_comm* comm, int32_t* nranks);
@@ -483,7 +530,7 @@ int lego_comm_gather_handoff(lego_comm* comm, lego_ctx* ctx, int32_t root);
 #define LEGO_COMM_DEVICE_RESULT 1u
 int lego_comm_gather_handoff_ex(lego_comm* comm, lego_ctx* ctx, int32_t root, uint32_t flags);
 /* Blocks until the last gather on the communicator has completed (within the
- * LEGO_COMM_TIMEOUT_MS bound, see lego_comm_create). */
+ * lego_comm_set_timeout bound, see lego_comm_create). */
 int lego_comm_wait(lego_comm* comm);
 /* On root after lego_comm_gather_handoff: rank r's packet in host memory,
  * valid until the next gather on the communicator. */

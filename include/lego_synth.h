@@ -31,7 +31,8 @@ typedef struct lego_synth_cfg {
   uint64_t seed;
 } lego_synth_cfg;
 
-/* "VLP-16", "HDL-64E", "VLS-128" (SURVEY.md §8d C1-C5). */
+/* "VLP-16", "HDL-64E", "VLS-128" (SURVEY.md §8d C1-C5), and the reference's
+ * other presets "HDL-32E", "OS1-16", "OS1-64" (utility.h:70-102). */
 int lego_synth_preset(const char* name, uint64_t seed, lego_synth_cfg* out);
 /* Upper bound on the points of one scan. */
 int32_t lego_synth_max_points(const lego_synth_cfg* cfg);

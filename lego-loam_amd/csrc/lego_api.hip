@@ -85,9 +85,16 @@ constexpr size_t kMoResBytes = ((sizeof(MoState) + 15) & ~(size_t)15) + ((sizeof
 struct lego_ctx {
   lego_sensor_cfg cfg;
   DevCfg dc;
+  lego_ctx_opts opts;  // fixed at creation (lego_create_ex)
+  LaunchOpts lo;       // its launch-shape part, as launch_ip / launch_fa take it
+  // a node call's hand-off gave up waiting for the VoxelGrid (kBadLfLate):
+  // the stream's state was not advanced and the odometry calls refuse to run
+  // until lego_reset
+  bool needReset = false;
   int device = 0;
   int maxPoints = 0, maxBatch = 0;  // maxBatch: scans per call over all streams
   int nStreams = 1;                   // a fleet context carries nStreams independent streams
+  int cus = 1;                        // the device's CUs (hipDeviceAttributeMultiprocessorCount)
   hipStream_t stream = nullptr;   // image projection + feature extraction (and everything else)
   hipStream_t ostream = nullptr;  // the odometry chain (overlaps the next batch's extraction)
   // Two batch slots: the per-scan buffers hold 2 x maxBatch scans; batch n
@@ -249,11 +256,12 @@ struct lego_ctx {
   }
 };
 
-static int make_devcfg(const lego_sensor_cfg* c, DevCfg* d) {
+static int make_devcfg(const lego_sensor_cfg* c, const lego_ctx_opts& o, DevCfg* d) {
   if (c->n_scan <= 0 || c->n_scan > kMaxRings || c->horizon_scan <= 0 ||
-      c->horizon_scan > kMaxHorizon || c->ground_scan_ind < 0 || c->ground_scan_ind >= c->n_scan ||
-      !c->use_cloud_ring)
+      c->horizon_scan > kMaxHorizon || c->ground_scan_ind < 0 || c->ground_scan_ind >= c->n_scan)
     return LEGO_E_ARG;
+  if (!c->use_cloud_ring && !(c->ang_res_y > 0.0f && std::isfinite(c->ang_bottom)))
+    return LEGO_E_ARG;  // the vertical-angle row needs a positive resolution
   d->N = c->n_scan;
   d->H = c->horizon_scan;
   d->P = c->n_scan * c->horizon_scan;
@@ -266,7 +274,7 @@ static int make_devcfg(const lego_sensor_cfg* c, DevCfg* d) {
   d->tanLo = tb.lo;
   d->tanHi = tb.hi;
   d->quad1 = tb.quad1 ? 1 : 0;
-  d->segHbm = std::getenv("LEGO_SEG_HBM") ? 1 : 0;  // diagnostic: the k_seg_lds cross-check
+  d->segHbm = o.seg_hbm ? 1 : 0;  // diagnostic: the k_seg_lds cross-check
   // labelComponents re-evaluates sin/cos(alpha) per edge (imageProjection.cpp:421);
   // they are per-sensor constants, evaluated with the same libm restatement.
   d->sinAX = lego_sinf(c->segment_alpha_x);
@@ -280,6 +288,9 @@ static int make_devcfg(const lego_sensor_cfg* c, DevCfg* d) {
   d->nn_sq = c->nearest_feature_search_sq_dist;
   d->scan_period = c->scan_period;
   d->skip = c->skip_frame_num;
+  d->ringRow = c->use_cloud_ring ? 1 : 0;
+  d->ang_res_y = c->ang_res_y;
+  d->ang_bottom = c->ang_bottom;
   return LEGO_OK;
 }
 
@@ -289,6 +300,7 @@ static int make_devcfg(const lego_sensor_cfg* c, DevCfg* d) {
 // next one starts fresh (from a constant pinned image).
 static int ctx_reset(lego_ctx* x) {
   ++x->devGen;
+  x->needReset = false;
   HIPCHK(hipMemcpyAsync(x->ob.st, x->h_resetSt, sizeof(OdomState) * x->nStreams, hipMemcpyHostToDevice,
                         x->ostream));
   // the hand-off tags restart with the state: no granule of the old stream may match
@@ -327,6 +339,28 @@ static int ctx_reset(lego_ctx* x) {
 extern "C" {
 
 const char* lego_last_error(void) { return g_err; }
+
+void lego_ctx_opts_init(lego_ctx_opts* o) {
+  if (!o) return;
+  std::memset(o, 0, sizeof(*o));
+  o->size = (int32_t)sizeof(*o);
+  o->node_overlap = 1;
+  o->front_parts = 2;  // profiles/r05_ab_front_parts.txt
+  o->lfv_wave = 1;
+  o->lfv_block_rings = 0;
+  o->lfv_wide = -1;
+  o->ccl_tiles = 1;
+  o->seg_hbm = 0;
+  o->odom_workgroups = 0;
+  o->odom_gridless = -1;
+  o->odom_integ = -1;
+  o->odom_silent_wg = -1;
+  o->odom_late_wg = -1;
+  o->lf_wait_ms = 2000;
+  o->mo_cand_cache = 1;
+  o->kf_cap = 0;
+  o->vg_rounds = -1;
+}
 
 int lego_sensor_preset(const char* name, lego_sensor_cfg* o) {
   if (!name || !o) return LEGO_E_ARG;
@@ -374,10 +408,23 @@ int lego_sensor_preset(const char* name, lego_sensor_cfg* o) {
 }
 
 static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams, int32_t max_points,
-                      int32_t max_batch, lego_ctx** out) {
+                      int32_t max_batch, const lego_ctx_opts* optsIn, lego_ctx** out) {
   if (!cfg || !out || max_points <= 0 || max_batch <= 0 || n_streams <= 0) return LEGO_E_ARG;
+  lego_ctx_opts opts;
+  lego_ctx_opts_init(&opts);
+  if (optsIn) {
+    if (optsIn->size != (int32_t)sizeof(lego_ctx_opts)) {
+      set_err("lego_ctx_opts.size %d != %d (lego_ctx_opts_init first)", optsIn->size, (int)sizeof(lego_ctx_opts));
+      return LEGO_E_ARG;
+    }
+    opts = *optsIn;
+  }
+  if (opts.front_parts < 1 || opts.lf_wait_ms < 0) {
+    set_err("lego_ctx_opts: front_parts >= 1 and lf_wait_ms >= 0");
+    return LEGO_E_ARG;
+  }
   DevCfg dc;
-  if (make_devcfg(cfg, &dc) != LEGO_OK) {
+  if (make_devcfg(cfg, opts, &dc) != LEGO_OK) {
     set_err("unsupported sensor configuration");
     return LEGO_E_ARG;
   }
@@ -390,6 +437,16 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
   if (!x) return LEGO_E_CAPACITY;
   x->cfg = *cfg;
   x->dc = dc;
+  x->opts = opts;
+  x->lo.cclTiles = opts.ccl_tiles;
+  x->lo.lfvWave = opts.lfv_wave;
+  x->lo.lfvBlockRings = opts.lfv_block_rings;
+  x->lo.lfvWide = opts.lfv_wide;
+  x->lo.faSyncCheck = opts.fa_synccheck;
+  x->vgApi.rounds = opts.vg_rounds;
+  x->mo.hostprof = opts.mo_hostprof != 0;
+  x->mo.evprof = opts.mo_evprof != 0;
+  for (VgScratch* v : {&x->mo.vg, &x->mo.vgMap2, &x->mo.vgScan1, &x->mo.vgScan2}) v->rounds = opts.vg_rounds;
   x->device = device;
   x->maxPoints = max_points;
   x->maxBatch = max_batch;
@@ -492,24 +549,20 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
     // workgroups of the odometry launch
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 1;
+    x->cus = cus;
     ob.G = odom_workgroups((int)N, cus);
     // a fleet's streams share the device: S x G workgroups, all resident
     if (n_streams > 1) ob.G = std::max(1, std::min(ob.G, cus / n_streams));
-    // diagnostic override (profiling / scaling studies); at most one
-    // workgroup per CU over the fleet's streams
-    if (const char* e = std::getenv("LEGO_ODOM_WORKGROUPS")) {
-      const int g = std::atoi(e);
-      if (g >= 1 && (long)g * (long)n_streams <= (long)cus) ob.G = g;
-    }
+    // override (profiling / scaling studies); at most one workgroup per CU
+    // over the fleet's streams
+    if (const int g = opts.odom_workgroups; g >= 1 && (long)g * (long)n_streams <= (long)cus) ob.G = g;
     // without grids an NN round's wave searches its query's whole LDS cloud:
     // worth it when that is about one query per wave (the grids' build is on
     // every scan's chain); a fleet's few workgroups per stream keep them
     ob.gridless = ob.G >= kGridlessMinWG ? 1 : 0;
-    if (const char* e = std::getenv("LEGO_ODOM_GRIDLESS")) ob.gridless = std::atoi(e) ? 1 : 0;  // diagnostic
-    ob.wg = -1;
-    if (const char* e = std::getenv("LEGO_ODOM_SILENT_WG"); e && S == 1) ob.wg = std::atoi(e);
-    ob.late = -1;
-    if (const char* e = std::getenv("LEGO_ODOM_LATE_WG"); e && S == 1) ob.late = std::atoi(e);
+    if (opts.odom_gridless >= 0) ob.gridless = opts.odom_gridless ? 1 : 0;  // diagnostic
+    ob.wg = S == 1 && opts.odom_silent_wg >= 0 ? opts.odom_silent_wg : -1;
+    ob.late = S == 1 && opts.odom_late_wg >= 0 ? opts.odom_late_wg : -1;
     const int copies = ob.wg >= 0 ? 2 : 1;  // exchange copies (OdomBufs::wg)
     const size_t G = S * ob.G;  // private copies over all streams' workgroups
     for (int k = 0; k < 2; ++k) {
@@ -567,7 +620,7 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
   A(ob.sumOut, B * 6);
   A(ob.intX, B * 6);
   ob.integ = ob.G > 1 ? 1 : 0;  // integration on its own workgroup per stream (OdomBufs::integ)
-  if (const char* e = std::getenv("LEGO_ODOM_INTEG")) ob.integ = ob.G > 1 && std::atoi(e) != 0;  // diagnostic A/B
+  if (opts.odom_integ >= 0) ob.integ = ob.G > 1 && opts.odom_integ != 0;  // diagnostic A/B
   A(ob.curOut, B * 6);
   A(ob.validOut, B);
   A(ob.pubOut, B);
@@ -618,16 +671,26 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
   return LEGO_OK;
 }
 
+int lego_create_ex(const lego_sensor_cfg* cfg, int device, int32_t max_points, int32_t max_batch,
+                   const lego_ctx_opts* opts, lego_ctx** out) {
+  return create_ctx(cfg, device, 1, max_points, max_batch, opts, out);
+}
+
 int lego_create(const lego_sensor_cfg* cfg, int device, int32_t max_points, int32_t max_batch,
                 lego_ctx** out) {
-  return create_ctx(cfg, device, 1, max_points, max_batch, out);
+  return create_ctx(cfg, device, 1, max_points, max_batch, nullptr, out);
+}
+
+int lego_fleet_create_ex(const lego_sensor_cfg* cfg, int device, int32_t n_streams, int32_t max_points,
+                         int32_t scans_per_stream, const lego_ctx_opts* opts, lego_ctx** out) {
+  if (n_streams <= 0 || scans_per_stream <= 0 || (int64_t)n_streams * scans_per_stream > (1 << 24))
+    return LEGO_E_ARG;
+  return create_ctx(cfg, device, n_streams, max_points, n_streams * scans_per_stream, opts, out);
 }
 
 int lego_fleet_create(const lego_sensor_cfg* cfg, int device, int32_t n_streams, int32_t max_points,
                       int32_t scans_per_stream, lego_ctx** out) {
-  if (n_streams <= 0 || scans_per_stream <= 0 || (int64_t)n_streams * scans_per_stream > (1 << 24))
-    return LEGO_E_ARG;
-  return create_ctx(cfg, device, n_streams, max_points, n_streams * scans_per_stream, out);
+  return lego_fleet_create_ex(cfg, device, n_streams, max_points, scans_per_stream, nullptr, out);
 }
 
 int lego_destroy(lego_ctx* x) {
@@ -783,18 +846,19 @@ static int fetch_ip(lego_ctx* x, int k, bool images, lego_ip_out* o, bool gated 
 static int run_ip(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offsets, int B, int on_device,
                   bool images, lego_ip_out* out, bool gated = false) {
   const int want_labels = images ? 1 : 0;
-  // every projection launch writes slot 0 (the outlier cloud among it): a
-  // resident hand-off of an earlier lego_fa_process is stale from here on
-  // (lego_ip_process and lego_ip_process_pc2 alike)
-  ++x->devGen;
   if (x->inflight) {
     set_err("node-shaped call while batches are in flight (lego_odom_batch_wait first)");
     return LEGO_E_STATE;
   }
   BatchBufs bb = x->bb;
-  x->lastBatch = false;
   int st = stage_inputs(x, pts, offsets, B, on_device, bb, true);
   if (st != LEGO_OK) return st;
+  // this launch writes slot 0 (the outlier cloud among it): a resident
+  // hand-off of an earlier lego_fa_process is stale from here on
+  // (lego_ip_process and lego_ip_process_pc2 alike).  A call
+  // rejected above launched nothing and leaves it valid.
+  ++x->devGen;
+  x->lastBatch = false;
   HIPCHK(hipMemsetAsync(bb.bad, 0, sizeof(int) * B, x->stream));
   if (gated && !x->gb.n) {
     const size_t P = x->dc.P;
@@ -804,7 +868,7 @@ static int run_ip(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offse
 #undef MA
   }
   x->tm.begin();
-  launch_ip(bb, x->dc, B, want_labels || gated ? 1 : 0, x->stream, &x->tm);
+  launch_ip(bb, x->dc, B, want_labels || gated ? 1 : 0, x->stream, &x->tm, x->lo);
   if (gated) {
     x->tm.mark("ip.gated", x->stream);
     launch_gated(bb, x->dc, x->gb, x->stream);
@@ -822,21 +886,19 @@ static int run_ip(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offse
   for (int k = 0; k < B; ++k)
     if (x->h_bad[k] & kBadNotDense) {
       x->lastB = 0;
-      set_err("scan %d of the batch has non-finite xyz (the cloud must be dense)", k);
+      set_err(x->dc.ringRow ? "scan %d of the batch has non-finite xyz (the cloud must be dense)"
+                            : "scan %d of the batch has no finite point", k);
       return LEGO_E_NOT_DENSE;
     }
   return LEGO_OK;
 }
 
-// Parts of a fleet batch's front end (submit_batch): LEGO_FRONT_PARTS (read
-// per call; A/B knob), else kFrontPartsDefault; at most kFrontPartsMax,
+// Parts of a fleet batch's front end (submit_batch): lego_ctx_opts::front_parts
+// (default 2, profiles/r05_ab_front_parts.txt), at most kFrontPartsMax,
 // reduced until it divides the streams.  A single stream is one part (its
 // scans chain through the extraction's carry).
-constexpr int kFrontPartsDefault = 2;  // profiles/r05_ab_front_parts.txt
-static int front_parts(int S) {
-  int p = kFrontPartsDefault;
-  if (const char* e = std::getenv("LEGO_FRONT_PARTS")) p = std::atoi(e);
-  p = std::max(1, std::min(p, lego_ctx::kFrontPartsMax));
+static int front_parts(const lego_ctx* x, int S) {
+  int p = std::max(1, std::min(x->opts.front_parts, lego_ctx::kFrontPartsMax));
   while (S % p) --p;
   return p;
 }
@@ -856,6 +918,10 @@ static int front_streams(lego_ctx* x, int parts) {
 // x->ostream after them, so they overlap the previous batch's odometry.
 static int submit_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offsets, int B, int on_device,
                         const lego_imu_msg* imu, int n_imu, const int32_t* imu_before) {
+  if (x->needReset) {
+    set_err("an earlier odometry call failed on the device: lego_reset first");
+    return LEGO_E_STATE;
+  }
   ++x->devGen;
   if (x->inflight >= 2) {
     set_err("two batches in flight: lego_odom_batch_wait before submitting another");
@@ -881,7 +947,7 @@ static int submit_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t*
   // and extraction in parts of whole streams (the batch is stream-major), on
   // HIP streams of their own, so that one part's LDS-bound kernels
   // (segmentation, VoxelGrids) share the CUs with another's HBM-bound ones
-  const int parts = front_parts(S);
+  const int parts = front_parts(x, S);
   if (parts > 1) {
     st = front_streams(x, parts);
     if (st != LEGO_OK) return st;
@@ -894,8 +960,8 @@ static int submit_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t*
     StageTimer* t = p ? &x->ftm : &tm;  // the stage times are part 0's
     BatchBufs q = parts > 1 ? bb_slice(bb, x->dc, p * Bp, Bp) : bb;
     if (p) q.xprof = nullptr;
-    launch_ip(q, x->dc, Bp, 0, s, t);
-    launch_fa(q, x->dc, Bp, Sp, x->d_carry + p * Sp, s, t);
+    launch_ip(q, x->dc, Bp, 0, s, t, x->lo);
+    launch_fa(q, x->dc, Bp, Sp, x->d_carry + p * Sp, s, t, x->lo);
   }
   for (int p = 1; p < parts; ++p) {
     HIPCHK(hipEventRecord(x->fJoin[p - 1], x->fstream[p - 1]));
@@ -952,7 +1018,8 @@ static int wait_batch(lego_ctx* x, lego_pose_rec* recs, int cap, int* nOut) {
   }
   for (int k = 0; k < B; ++k)
     if (pk[k].bad & kBadNotDense) {
-      set_err("scan %d of the batch has non-finite xyz (the cloud must be dense)", k);
+      set_err(x->dc.ringRow ? "scan %d of the batch has non-finite xyz (the cloud must be dense)"
+                            : "scan %d of the batch has no finite point", k);
       return LEGO_E_NOT_DENSE;
     }
   for (int k = 0; k < B; ++k)
@@ -1168,8 +1235,9 @@ int lego_ip_process(lego_ctx* x, const lego_point_xyzir* pts, int32_t n, double 
                     uint32_t flags, lego_ip_out* out) {
   if (!x || !pts || !out || n <= 0) return LEGO_E_ARG;
   if (n > x->maxPoints) return LEGO_E_CAPACITY;
-  {  // dense check (imageProjection.cpp:174): an all-ones exponent is inf / nan;
-     // accumulated without branches so the loop vectorises
+  if (x->dc.ringRow) {  // dense check (imageProjection.cpp:174): an all-ones exponent is inf / nan;
+                         // accumulated without branches so the loop vectorises.  Without
+                         // useCloudRing k_project drops such points (:170).
     uint32_t nonfinite = 0;
     for (int i = 0; i < n; ++i) {
       uint32_t u[3];
@@ -1177,7 +1245,10 @@ int lego_ip_process(lego_ctx* x, const lego_point_xyzir* pts, int32_t n, double 
       nonfinite |= (uint32_t)((u[0] & 0x7f800000u) == 0x7f800000u) | (uint32_t)((u[1] & 0x7f800000u) == 0x7f800000u) |
                    (uint32_t)((u[2] & 0x7f800000u) == 0x7f800000u);
     }
-    if (nonfinite) return LEGO_E_NOT_DENSE;
+    if (nonfinite) {
+      set_err("the cloud has non-finite xyz (it must be dense with use_cloud_ring)");
+      return LEGO_E_NOT_DENSE;
+    }
   }
   int64_t off[2] = {0, n};
   x->stamps.assign(1, stamp);
@@ -1226,6 +1297,10 @@ int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
     set_err("lego_fa_process needs a single-stream context");
     return LEGO_E_ARG;
   }
+  if (x->needReset) {
+    set_err("an earlier odometry call failed on the device: lego_reset first");
+    return LEGO_E_STATE;
+  }
   HIPCHK(hipSetDevice(x->device));
   ++x->devGen;
   const bool resident = x->lastIpDevice && in->segmented_cloud == x->h_seg &&
@@ -1248,14 +1323,19 @@ int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
   // the per-ring less-flat VoxelGrid (featureAssociation.cpp:778-782) feeds
   // only the hand-off (publishCloudsLast, :1759-1815): it runs on ostream
   // beside the LM, and the hand-off waits for it (OdomBufs::lfWait)
-  // (LEGO_NODE_OVERLAP=0: everything on one stream, A/B knob, read per call)
-  const char* ovS = std::getenv("LEGO_NODE_OVERLAP");
-  const bool overlap = !ovS || std::atoi(ovS) != 0;
-  launch_fa(bb, x->dc, 1, 1, x->d_carry, x->stream, &x->tm, overlap ? x->ostream : nullptr, x->lfFork,
+  // (lego_ctx_opts::node_overlap = 0: everything on one stream).  Only
+  // while the odometry's workgroups, each holding a CU's registers, leave
+  // room for the VoxelGrid's rings (a partitioned device with as many CUs as
+  // workgroups would starve it until the hand-off's wait gives up)
+  const int odomWGs = x->ob.G + (x->ob.integ ? 1 : 0);
+  const bool overlap = x->opts.node_overlap != 0 && odomWGs <= x->cus - x->dc.N / 2;
+  launch_fa(bb, x->dc, 1, 1, x->d_carry, x->stream, &x->tm, x->lo, overlap ? x->ostream : nullptr, x->lfFork,
             x->d_lfReady);
-  // launch_odom's prep zeroes *ob.xerr
+  // launch_odom's prep zeroes *ob.xerr; the hand-off's wait bound in ticks of
+  // the 100 MHz wall clock (s_memrealtime)
+  const unsigned long long lfTicks = (unsigned long long)x->opts.lf_wait_ms * 100000ull;
   if (launch_odom(bb, x->ob, x->dc, 1, x->stream, &x->tm, x->profOn ? x->d_prof : nullptr,
-                  overlap ? x->d_lfReady : nullptr) != 0) {
+                  overlap ? x->d_lfReady : nullptr, lfTicks) != 0) {
     set_err("odometry launch failed (%d workgroups)", x->ob.G);
     return LEGO_E_DEVICE;
   }
@@ -1290,7 +1370,9 @@ int lego_fa_process(lego_ctx* x, const lego_ip_out* in, lego_fa_out* out) {
   }
   if (x->h_hdr[FH_BAD] & kBadLfLate) {
     x->faK = -1;
-    set_err("the hand-off waited more than 2 s for the per-ring VoxelGrid on the side stream");
+    x->needReset = true;
+    set_err("the hand-off waited more than %d ms for the per-ring VoxelGrid on the side stream "
+            "(the stream state was not advanced: lego_reset to go on)", x->opts.lf_wait_ms);
     return LEGO_E_DEVICE;
   }
   return LEGO_OK;
@@ -1395,7 +1477,7 @@ static int mo_alloc(lego_ctx* x, int nc, int ns) {
     m.rowCap = N * kLessSharpPerRing + 2 * P;
     MA(m.rows, (size_t)m.rowCap * 8);
     m.candQ = std::min(m.rowCap, kCandQueries);
-    if (const char* e = std::getenv("LEGO_MO_CAND"); e && std::atoi(e) == 0) m.candQ = 0;  // no cache (device memory)
+    if (!x->opts.mo_cand_cache) m.candQ = 0;  // no cache (device memory)
     MA(m.cand, (size_t)m.candQ * kCand);
     MA(m.candRef, (size_t)m.candQ);
     m.partCap = 4096;  // k_mo_rows' grid cap (grid_for)
@@ -1450,7 +1532,7 @@ static int mo_alloc_keyframes(lego_ctx* x) {
   if (st != LEGO_OK) return st;
   MoKeyframes& kf = m.kf;
   int kcap = 16384, acap = 16 << 20;
-  if (const char* e = std::getenv("LEGO_KF_CAP")) kcap = std::max(1, std::min(kcap, std::atoi(e)));  // diagnostic
+  if (x->opts.kf_cap > 0) kcap = std::min(kcap, x->opts.kf_cap);  // diagnostic
 #define MA(ptr, n) \
   if (x->alloc(&(ptr), (size_t)(n)) != hipSuccess) { set_err("hipMalloc failed for %s", #ptr); return LEGO_E_DEVICE; }
   MA(kf.pos3, kcap); MA(kf.pose6, kcap * 6); MA(kf.time, kcap); MA(kf.seg, kcap * 6); MA(kf.arena, acap);
@@ -1573,7 +1655,7 @@ int lego_voxel_grid(lego_ctx* x, const lego_point_xyzi* in, int32_t n, float lea
   HIPCHK(hipMemcpy(out, x->vgOut, sizeof(float4) * nOut, hipMemcpyDeviceToHost));
   *n_out = nOut;
   // ctl: C_M 0, C_NLOC 4, C_NONFIN 5, C_NOUT 6, C_SLOW 7, C_HEAP 8, C_NLOCB 9 (lego_vg.hip)
-  const int st[8] = {ctl[0], ctl[6], vg_rounds_for(n), ctl[4] + ctl[9], ctl[7], ctl[8], ctl[5], (int)(ms * 1000.f)};
+  const int st[8] = {ctl[0], ctl[6], vg_rounds_for(n, x->vgApi.rounds), ctl[4] + ctl[9], ctl[7], ctl[8], ctl[5], (int)(ms * 1000.f)};
   std::copy(st, st + 8, x->vgStats);
   return LEGO_OK;
 }
@@ -1980,7 +2062,9 @@ static int pc2_stage(lego_ctx* x, const lego_pc2_msg* msgs, int K, bool onDevice
       set_err("PointCloud2 %d: bad layout (big-endian, point_step, row_step or a field past point_step)", k);
       return LEGO_E_ARG;
     }
-    if (!msgs[k].is_dense) {  // imageProjection.cpp:173-176
+    // imageProjection.cpp:172-176: with useCloudRing a non-dense message is an
+    // error; without it removeNaNFromPointCloud (:170) drops its NaN points
+    if (!msgs[k].is_dense && x->dc.ringRow) {
       set_err("PointCloud2 %d is not dense (is_dense = false)", k);
       return LEGO_E_NOT_DENSE;
     }
@@ -2039,6 +2123,10 @@ int lego_pc2_decode(lego_ctx* x, const lego_pc2_msg* msg, lego_point_xyzir* out,
 
 int lego_ip_process_pc2(lego_ctx* x, const lego_pc2_msg* msg, uint32_t flags, lego_ip_out* out) {
   if (!x || !msg || !out) return LEGO_E_ARG;
+  if (x->inflight) {  // before the decode, which writes the staging points a batch in flight may read
+    set_err("node-shaped call while batches are in flight (lego_odom_batch_wait first)");
+    return LEGO_E_STATE;
+  }
   HIPCHK(hipSetDevice(x->device));
   std::vector<int64_t> off;
   int st = pc2_stage(x, msg, 1, false, off);

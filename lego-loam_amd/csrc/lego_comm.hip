@@ -17,7 +17,7 @@
 // in use closes any open group and aborts the communicator (ncclCommAbort),
 // and the communicator is dead from then on.  Only root sizes buffers after
 // the size exchange; it aborts if that fails.  Every wait on the
-// communicator's stream is bounded (LEGO_COMM_TIMEOUT_MS, default 60 s): a
+// communicator's stream is bounded (lego_comm_set_timeout, default 60 s): a
 // peer that never joins a collective makes the call abort the communicator
 // and return LEGO_E_DEVICE naming the wait, instead of blocking the rank.
 #include <hip/hip_runtime.h>
@@ -52,7 +52,7 @@ struct lego_comm {
   std::vector<uint64_t> sizes, offs;
   bool haveResult = false, haveHost = false;
   bool dead = false;
-  int timeoutMs = 60000;  // bound of every wait on s (LEGO_COMM_TIMEOUT_MS)
+  int timeoutMs = 60000;  // bound of every wait on s (lego_comm_set_timeout)
   ~lego_comm() {
     if (device >= 0) (void)hipSetDevice(device);
     if (s) (void)hipStreamSynchronize(s);
@@ -124,8 +124,13 @@ int lego_comm_create(const uint8_t id[128], int32_t nranks, int32_t rank, int32_
   }
   c->sizes.assign(nranks, 0);
   c->offs.assign(nranks + 1, 0);
-  if (const char* e = std::getenv("LEGO_COMM_TIMEOUT_MS")) c->timeoutMs = std::max(1, std::atoi(e));
   *out = c;
+  return LEGO_OK;
+}
+
+int lego_comm_set_timeout(lego_comm* c, int32_t timeout_ms) {
+  if (!c || timeout_ms < 1) return LEGO_E_ARG;
+  c->timeoutMs = timeout_ms;
   return LEGO_OK;
 }
 

@@ -38,6 +38,12 @@ struct DevCfg {
   double tanLo, tanHi;
   int quad1;
   int segHbm;  // diagnostic (LEGO_SEG_HBM): the HBM union-find for every image size
+  // useCloudRing (utility.h:60): 1 = the row is the point's ring channel; 0 =
+  // the row from the vertical angle, (angle + ang_bottom) / ang_res_y
+  // (imageProjection.cpp:228-231), and non-finite points are removed first
+  // (pcl::removeNaNFromPointCloud, :170) instead of rejecting the scan
+  int ringRow;
+  float ang_res_y, ang_bottom;
 };
 
 // ---- IMU (featureAssociation.cpp:84-159, 317-459, 525-614)

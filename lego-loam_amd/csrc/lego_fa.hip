@@ -1230,71 +1230,68 @@ __global__ void k_fa_init(BatchBufs bb, int B, unsigned* lfReady) {
   }
 }
 
-// LEGO_FA_SYNCCHECK (diagnostic, host only): synchronise after every launch
-// of launch_fa and name the kernel whose execution returned an error.
-static void fa_synccheck(hipStream_t s, const char* what) {
-  static const bool on = std::getenv("LEGO_FA_SYNCCHECK") != nullptr;
-  if (!on) return;
+// lego_ctx_opts::fa_synccheck (diagnostic, host only): synchronise after
+// every launch of launch_fa and name the kernel whose execution returned an
+// error.
+static void fa_synccheck(const LaunchOpts& lo, hipStream_t s, const char* what) {
+  if (!lo.faSyncCheck) return;
   const hipError_t e = hipStreamSynchronize(s);
-  std::fprintf(stderr, "LEGO_FA_SYNCCHECK %s: %s\n", what, hipGetErrorString(e));
+  std::fprintf(stderr, "fa_synccheck %s: %s\n", what, hipGetErrorString(e));
 }
 
 void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_carry, hipStream_t s,
-               StageTimer* tm, hipStream_t side, hipEvent_t fork, unsigned* lfReady) {
+               StageTimer* tm, const LaunchOpts& lo, hipStream_t side, hipEvent_t fork, unsigned* lfReady) {
   tm->mark("fa.deskew", s);
   k_fa_init<<<(B + 255) / 256, 256, 0, s>>>(bb, B, side ? lfReady : nullptr);
-  fa_synccheck(s, "k_fa_init");
+  fa_synccheck(lo, s, "k_fa_init");
   dim3 gpts((c.P + 255) / 256, B);
   k_fa_half<<<gpts, 256, 0, s>>>(bb, c);
-  fa_synccheck(s, "k_fa_half");
+  fa_synccheck(lo, s, "k_fa_half");
   if (bb.imu) k_fa_imu_start<<<(B + 63) / 64, 64, 0, s>>>(bb, c);
   k_fa_point<<<gpts, 256, 0, s>>>(bb, c);
-  fa_synccheck(s, "k_fa_point");
+  fa_synccheck(lo, s, "k_fa_point");
   tm->mark("fa.extract", s);
   const size_t lds = extract_lds_bytes(c.H);
   k_extract<<<dim3(c.N, B), kExtractThreads, lds, s>>>(bb, c);
-  fa_synccheck(s, "k_extract");
+  fa_synccheck(lo, s, "k_extract");
   tm->mark("fa.fixup", s);
   k_fa_fixup<<<S, kExtractThreads, lds, s>>>(bb, c, B / S, d_carry);
-  fa_synccheck(s, "k_fa_fixup");
+  fa_synccheck(lo, s, "k_fa_fixup");
   if (side) {  // a node call: the LM's clouds now, the less-flat VoxelGrid beside the odometry
     tm->mark("fa.compact", s);
     k_fa_compact<1><<<dim3(c.N, B), 256, 0, s>>>(bb, c, nullptr);
-    fa_synccheck(s, "k_fa_compact<1>");
+    fa_synccheck(lo, s, "k_fa_compact<1>");
     (void)hipEventRecord(fork, s);
     (void)hipStreamWaitEvent(side, fork, 0);
     s = side;
   } else {
     tm->mark("fa.voxel", s);
   }
-  static const bool waveOn = !std::getenv("LEGO_LFV_WAVE") || std::atoi(std::getenv("LEGO_LFV_WAVE")) != 0;
+  const bool waveOn = lo.lfvWave != 0;
   const int g4 = waveOn ? (c.N + 3) / 4 : 0;
-  // rings per large-ring workgroup (LEGO_LFV_BLOCK_RINGS, A/B knob; 1 = one
+  // rings per large-ring workgroup (lego_ctx_opts::lfv_block_rings; 1 = one
   // workgroup per ring)
-  static const int rpbEnv = std::getenv("LEGO_LFV_BLOCK_RINGS") ? std::max(1, std::atoi(std::getenv("LEGO_LFV_BLOCK_RINGS"))) : 0;
-  const int rpb = rpbEnv ? rpbEnv : (waveOn && B * c.N > kLfvSmallLaunchRings ? kLfvBlockRings : 1);
+  const int rpb = lo.lfvBlockRings > 0 ? lo.lfvBlockRings
+                                       : (waveOn && B * c.N > kLfvSmallLaunchRings ? kLfvBlockRings : 1);
   const int gb = (c.N + rpb - 1) / rpb;
   // a launch that leaves the device idle but for itself (a node call): every
   // ring by a 1024-thread workgroup, the sort's levels over four times the
-  // lanes (LEGO_LFV_WIDE, A/B knob)
-  // (read per launch, so a test can switch it)
-  const char* wideS = std::getenv("LEGO_LFV_WIDE");
-  const int wideEnv = wideS ? std::atoi(wideS) : -1;
-  const bool wide = wideEnv >= 0 ? wideEnv != 0 : B * c.N <= kLfvWideLaunchRings;
+  // lanes (lego_ctx_opts::lfv_wide overrides)
+  const bool wide = lo.lfvWide >= 0 ? lo.lfvWide != 0 : B * c.N <= kLfvWideLaunchRings;
   if (wide)
     k_lf_voxel<1024><<<dim3(c.N, B), 1024, lfvox_lds_bytes(c.H), s>>>(bb, c, 0, c.N);
   else
     k_lf_voxel<kExtractThreads>
         <<<dim3(g4 + gb, B), kExtractThreads, std::max(kLfvWaveLds, lfvox_lds_bytes(c.H)), s>>>(bb, c, g4, gb);
-  fa_synccheck(s, wide ? "k_lf_voxel<1024>" : "k_lf_voxel<256>");
+  fa_synccheck(lo, s, wide ? "k_lf_voxel<1024>" : "k_lf_voxel<256>");
   if (side) {
     k_fa_compact<2><<<dim3(c.N, B), 256, 0, s>>>(bb, c, lfReady);
-    fa_synccheck(s, "k_fa_compact<2>");
+    fa_synccheck(lo, s, "k_fa_compact<2>");
     return;
   }
   tm->mark("fa.compact", s);
   k_fa_compact<0><<<dim3(c.N, B), 256, 0, s>>>(bb, c, nullptr);
-  fa_synccheck(s, "k_fa_compact");
+  fa_synccheck(lo, s, "k_fa_compact");
 }
 
 }  // namespace lego

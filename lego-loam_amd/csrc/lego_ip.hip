@@ -30,23 +30,67 @@
 
 namespace lego {
 
+__device__ __forceinline__ bool xyz_finite(const float4& p) {
+  return __builtin_isfinite(p.x) && __builtin_isfinite(p.y) && __builtin_isfinite(p.z);
+}
+
 __global__ void k_project(BatchBufs bb, DevCfg c) {
   const int b = blockIdx.y;
   const int n = scan_npts(bb, b);
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const lego_point_xyzir* pp = (const lego_point_xyzir*)bb.pts + bb.off[b] + i;
+  const lego_point_xyzir* p0 = (const lego_point_xyzir*)bb.pts + bb.off[b];
+  const lego_point_xyzir* pp = p0 + i;
   const float4 xyz = *(const float4*)pp;
   const uint16_t ring = pp->ring;
   const float x = xyz.x, y = xyz.y, z = xyz.z;
-  if (!__builtin_isfinite(x) || !__builtin_isfinite(y) || !__builtin_isfinite(z)) {
-    bb.bad[b] = kBadNotDense;  // the host rejects the batch with LEGO_E_NOT_DENSE
+  if (!xyz_finite(xyz)) {
+    if (c.ringRow) {
+      bb.bad[b] = kBadNotDense;  // the host rejects the batch with LEGO_E_NOT_DENSE
+      return;
+    }
+    // useCloudRing = false: removeNaNFromPointCloud (:170) drops the point,
+    // and points[0] / points[size - 1] of findStartEndAngle (:201-202) are
+    // the first / last finite ones.  One lane walks inwards from each end
+    // (the walk is as long as the run of non-finite points at that end).
+    if (i == 0) {
+      int k = 1;
+      while (k < n && !xyz_finite(*(const float4*)(p0 + k))) ++k;
+      if (k == n) {
+        bb.bad[b] = kBadNotDense;  // no finite point: points[0] of an empty cloud (UB upstream)
+        return;
+      }
+      const float4 q = *(const float4*)(p0 + k);
+      bb.rawang[2 * b] = -lego_atan2f(q.y, q.x);
+    }
+    if (i == n - 1) {
+      int k = n - 2;
+      while (k >= 0 && !xyz_finite(*(const float4*)(p0 + k))) --k;
+      if (k >= 0) {
+        const float4 q = *(const float4*)(p0 + k);
+        bb.rawang[2 * b + 1] = -lego_atan2f(q.y, q.x);
+      }
+    }
     return;
   }
   if (i == 0) bb.rawang[2 * b] = -lego_atan2f(y, x);                   // :201
   if (i == n - 1) bb.rawang[2 * b + 1] = -lego_atan2f(y, x);           // :202
-  const int row = ring;
-  if (row >= c.N) return;
+  int row;
+  if (c.ringRow) {
+    row = ring;  // :226
+    if (row >= c.N) return;
+  } else {
+    // :229-230: float atan2 / sqrt (utility.h's `using namespace std`), the
+    // product with 180 in float, the division by M_PI in double, stored to
+    // the float verticalAngle; then (float + float) / float
+    const float va = (float)((double)(lego_atan2f(z, __builtin_sqrtf(x * x + y * y)) * 180.0f) / M_PI);
+    const float v = (va + c.ang_bottom) / c.ang_res_y;
+    // rowIdn is size_t: x86-64 converts a float below 2^63 by truncation
+    // toward zero through int64, so (-1, 0) gives row 0 and v <= -1 an index
+    // past N_SCAN (skipped by :232, where `rowIdn < 0` is always false)
+    if (!(v > -1.0f && v < (float)c.N)) return;
+    row = (int)v;
+  }
   const float h = (float)((double)(lego_atan2f(x, y) * 180.0f) / M_PI);  // :235
   const double cd = -round(((double)h - 90.0) / (double)c.ang_res_x) + (double)(c.H / 2);
   if (cd < 0) return;
@@ -825,7 +869,7 @@ void launch_gated(const BatchBufs& bb, const DevCfg& c, const GatedBufs& gb, hip
 }
 
 void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hipStream_t s,
-               StageTimer* tm) {
+               StageTimer* tm, const LaunchOpts& lo) {
   const int P = c.P;
   tm->mark("ip.memset", s);
   // launch-path errors are sticky: the caller checks hipGetLastError() after the batch
@@ -848,10 +892,9 @@ void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hip
     return;
   }
   tm->mark("ip.ccl", s);
-  // the union-find: in LDS column tiles plus the seams (LEGO_CCL_TILES=0,
-  // diagnostic: every edge in HBM, k_ccl_init / k_ccl_union)
-  static const bool tiles = !std::getenv("LEGO_CCL_TILES") || std::atoi(std::getenv("LEGO_CCL_TILES")) != 0;
-  if (tiles) {
+  // the union-find: in LDS column tiles plus the seams (lego_ctx_opts::ccl_tiles
+  // = 0, diagnostic: every edge in HBM, k_ccl_init / k_ccl_union)
+  if (lo.cclTiles) {
     const int TW = ccl_tile_width(c, B), nT = (c.H + TW - 1) / TW;
     k_ccl_tile<<<dim3(nT, B), 1024, (size_t)c.N * TW * sizeof(int), s>>>(bb, c, TW);
     if (nT > 1) k_ccl_seam<<<dim3((nT * c.N + 255) / 256, B), 256, 0, s>>>(bb, c, TW, nT);

@@ -198,9 +198,19 @@ __host__ __device__ inline size_t ring_stride(int G, int gTS, int gTC, int capH)
 // the snapshot's slot and the launch's first current slot are never rewritten.
 __host__ __device__ inline int ring_slots(int K) { return K + 3; }
 
+// The launch-shape switches of a context (lego_ctx_opts, fixed at creation):
+// host only, never a kernel argument.
+struct LaunchOpts {
+  int cclTiles = 1;       // lego_ctx_opts::ccl_tiles
+  int lfvWave = 1;        // ::lfv_wave
+  int lfvBlockRings = 0;  // ::lfv_block_rings
+  int lfvWide = -1;       // ::lfv_wide
+  int faSyncCheck = 0;    // ::fa_synccheck
+};
+
 void launch_gated(const BatchBufs& bb, const DevCfg& c, const GatedBufs& gb, hipStream_t s);
 void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hipStream_t s,
-               StageTimer* tm);
+               StageTimer* tm, const LaunchOpts& lo);
 // B = S x K scans, stream-major (scans [s*K, s*K + K) are stream s's, in
 // order); d_carry[S].
 // side (node calls, B = 1): the per-ring less-flat VoxelGrid and its
@@ -209,16 +219,21 @@ void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hip
 // zeroed here first); the caller passes lfReady to launch_odom and joins side
 // into s before reading f_lflat.  null: everything on s.
 void launch_fa(const BatchBufs& bb, const DevCfg& c, int B, int S, FaCarry* d_carry, hipStream_t s,
-               StageTimer* tm, hipStream_t side = nullptr, hipEvent_t fork = nullptr, unsigned* lfReady = nullptr);
+               StageTimer* tm, const LaunchOpts& lo, hipStream_t side = nullptr, hipEvent_t fork = nullptr,
+               unsigned* lfReady = nullptr);
 // K scans per stream over ob.S streams (the caller zeroes *ob.xerr once per
 // batch).  Returns 0 on a successful launch.  lfReady (a node call, launch_fa
 // with a side stream): the scan's less-flat VoxelGrid is still running when
 // the LM starts; the hand-off, its only reader (publishCloudsLast,
 // featureAssociation.cpp:1759-1815), first waits until lfReady[b] counts
-// every ring (bounded: kLfWaitTicks, then bad[b] |= kBadLfLate and no
-// less-flat points).
+// every ring (bounded: lfTicks of the 100 MHz wall clock, 0 = none, then
+// bad[b] |= kBadLfLate and no less-flat points; the host then fails the call
+// and requires lego_reset).  The lead workgroup decides and publishes the
+// decision in lfReady[b]'s flag bits (kLfDecided*), which every other
+// workgroup follows.
 int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int K, hipStream_t s,
-                StageTimer* tm, unsigned long long* prof, unsigned* lfReady = nullptr);
+                StageTimer* tm, unsigned long long* prof, unsigned* lfReady = nullptr,
+                unsigned long long lfTicks = 0);
 int odom_workgroups(int N, int cusAvailable);
 // sensors whose last clouds never fit LDS: the stream keeps one ring copy (OdomBufs::ring)
 bool odom_ring_sensor(int N);

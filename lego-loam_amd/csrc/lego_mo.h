@@ -52,6 +52,7 @@ struct VgScratch {
   // points its scratches at MoCounts::derr (read after every step).
   int* err;
   int cap, capBig, capTiles, capLoc, capScanTiles;
+  int rounds = -1;  // host only: lego_ctx_opts::vg_rounds (-1: by the cloud's size)
 };
 
 // 1 m cells of the mapping NN index, hashed into T buckets
@@ -142,8 +143,9 @@ struct MoDev {
   // Each chain has its own VoxelGrid scratch.
   hipStream_t fork[2];
   hipEvent_t ev[6];
-  hipEvent_t prof[6] = {};  // LEGO_MO_EVPROF (diagnostic): the step's chain ends, timed
+  hipEvent_t prof[6] = {};  // lego_ctx_opts::mo_evprof (diagnostic): the step's chain ends, timed
   VgScratch vgMap2, vgScan1, vgScan2;
+  bool hostprof = false, evprof = false;  // lego_ctx_opts::mo_hostprof / mo_evprof (host only)
 };
 
 struct MoStepArgs {
@@ -194,7 +196,8 @@ int voxel_grid_device(const float4* in, int n, const int* nDev, float leaf, floa
                       const VgScratch& v, hipStream_t s);
 // partition rounds voxel_grid_device launches for a cloud of n points
 // (LEGO_VG_ROUNDS overrides: diagnostic)
-int vg_rounds_for(int n);
+// partition rounds for a cloud of n points; forced >= 0 (lego_ctx_opts::vg_rounds) overrides
+int vg_rounds_for(int n, int forced = -1);
 void mo_evprof_print(MoDev& m);  // after the step's stream is synchronised
 // the VgScratch counters of the last voxel_grid_device on s (16 ints, synchronous)
 int vg_read_ctl(const VgScratch& v, int* ctl16, hipStream_t s);

@@ -881,11 +881,10 @@ static int kf_map_recent(MoDev& m, const MoStepArgs& a, hipStream_t s) {
   return kf_map_filter(m, a.nCM, a.nSM, s);
 }
 
-// LEGO_MO_HOSTPROF (diagnostic): the host's enqueue time of the step's parts
-// to stderr (map, scan VoxelGrids, LM).
-static const bool g_hostprof = std::getenv("LEGO_MO_HOSTPROF") != nullptr;
+// lego_ctx_opts::mo_hostprof (diagnostic): the host's enqueue time of the
+// step's parts to stderr (map, scan VoxelGrids, LM).
 #define MO_HOSTPROF(k)                                                                                  \
-  if (g_hostprof) {                                                                                     \
+  if (m.hostprof) {                                                                                     \
     hp[k] = std::chrono::steady_clock::now();                                                           \
     if (k == 3)                                                                                         \
       std::fprintf(stderr, "mo enqueue us: map %.0f scan %.0f lm %.0f\n",                              \
@@ -894,18 +893,17 @@ static const bool g_hostprof = std::getenv("LEGO_MO_HOSTPROF") != nullptr;
                    std::chrono::duration<double, std::micro>(hp[3] - hp[2]).count());                   \
   }
 
-// LEGO_MO_EVPROF (diagnostic): timing events at the step's start and at the
-// end of each chain (s: the map's surf cloud; fork[1]: surf, map corner;
-// fork[0]: outlier, surf + outlier, corner), after the join and after the LM;
-// mo_evprof_print writes their offsets (us) to stderr.
-static const bool g_evprof = std::getenv("LEGO_MO_EVPROF") != nullptr;
+// lego_ctx_opts::mo_evprof (diagnostic): timing events at the step's start
+// and at the end of each chain (s: the map's surf cloud; fork[1]: surf, map
+// corner; fork[0]: outlier, surf + outlier, corner), after the join and after
+// the LM; mo_evprof_print writes their offsets (us) to stderr.
 static void evprof(MoDev& m, int k, hipStream_t st) {
-  if (!g_evprof) return;
+  if (!m.evprof) return;
   if (!m.prof[k] && hipEventCreate(&m.prof[k]) != hipSuccess) return;
   (void)hipEventRecord(m.prof[k], st);
 }
 void mo_evprof_print(MoDev& m) {
-  if (!g_evprof || !m.prof[0]) return;
+  if (!m.evprof || !m.prof[0]) return;
   static const char* names[6] = {"start", "s_map_surf", "f1_surf_mapcorner", "f0_outlier_total_corner", "join", "lm"};
   std::fprintf(stderr, "mo evprof us:");
   for (int k = 1; k < 6; ++k) {

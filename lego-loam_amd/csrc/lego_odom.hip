@@ -1296,7 +1296,13 @@ constexpr unsigned long long kLateTicks = 200000000;  // 2 s: the diagnostic lat
 // odom_integrate's polls of one scan's granules before it gives up (each
 // s_sleep 2 = 128 clocks; ~20 M polls, seconds)
 constexpr unsigned kIntegPolls = 20000000u;
-constexpr unsigned long long kLfWaitTicks = 200000000;  // 2 s: a node call's hand-off waiting for the less-flat cloud
+// A node call's hand-off waits for the less-flat cloud (launch_odom's
+// lfTicks, lego_ctx_opts::lf_wait_ms).  lfReady[b] counts the rings in its
+// low bits; the lead workgroup decides (ready, or late after lfTicks) and
+// ORs one of these flags in, and every other workgroup follows that decision
+// (bounded by lfTicks + kLfFollowTicks), so all take the same cloud size.
+constexpr unsigned kLfCountMask = 0xffffu, kLfDecidedOk = 1u << 30, kLfDecidedLate = 1u << 29;
+constexpr unsigned long long kLfFollowTicks = 100000000;  // 1 s past the lead's own bound
 __device__ __forceinline__ void x_publish(unsigned long long* p, unsigned long long v) {
   __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1842,7 +1848,8 @@ __device__ __forceinline__ void odom_integrate(const BatchBufs& bb, const OdomBu
 // offsets); also separate, so the batch kernels keep their registers.
 template <bool RING, bool LFW>
 __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs obShared, DevCfg c, int K,
-                                                      unsigned long long* prof, const unsigned* lfReady) {
+                                                      unsigned long long* prof, unsigned* lfReady,
+                                                      unsigned long long lfTicks) {
   // Claim the whole register file of the SIMD (2 waves x 256): no other
   // kernel's waves share a SIMD with the latency-bound chain while the next
   // chunk's extraction runs beside it.
@@ -1968,12 +1975,26 @@ __global__ void __launch_bounds__(kOdomThreads) k_odom(BatchBufs bb, OdomBufs ob
     if (LFW) {  // a node call: the less-flat cloud comes from the side stream (launch_fa)
       if (tid == 0) {
         const unsigned long long t0 = wall_clock64();
-        bool ok;
-        while (!(ok = __hip_atomic_load(lfReady + b, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)c.N) &&
-               wall_clock64() - t0 < kLfWaitTicks)
-          __builtin_amdgcn_s_sleep(2);
+        bool ok = false;
+        if (lead) {  // decides for the launch (kLfDecided*)
+          if (lfTicks)
+            while (!(ok = (__hip_atomic_load(lfReady + b, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) &
+                           kLfCountMask) >= (unsigned)c.N) &&
+                   wall_clock64() - t0 < lfTicks)
+              __builtin_amdgcn_s_sleep(2);
+          __hip_atomic_fetch_or(lfReady + b, ok ? kLfDecidedOk : kLfDecidedLate, __ATOMIC_RELEASE,
+                                __HIP_MEMORY_SCOPE_AGENT);
+        } else {  // follows the lead's decision
+          unsigned v;
+          while (!((v = __hip_atomic_load(lfReady + b, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) &
+                   (kLfDecidedOk | kLfDecidedLate)) &&
+                 wall_clock64() - t0 < lfTicks + kLfFollowTicks)
+            __builtin_amdgcn_s_sleep(2);
+          ok = (v & kLfDecidedOk) != 0;
+        }
         L.n[N_LF] = ok ? __hip_atomic_load(bb.f_cnt + b * 4 + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-        if (!ok && lead) atomicOr(bb.bad + b, kBadLfLate);
+        // the host fails the call and the context until lego_reset (never a silent empty cloud)
+        if (!ok) atomicOr(bb.bad + b, kBadLfLate);
       }
       __syncthreads();
       F.nLF = __builtin_amdgcn_readfirstlane(L.n[N_LF]);
@@ -2509,7 +2530,7 @@ __global__ void k_ring_prep(OdomBufs ob, int K) {
 bool odom_ring_sensor(int N) { return !(N * kFlatPerRing <= kLdsQ && N * kSharpPerRing <= kLdsQ / 2); }
 
 int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int K, hipStream_t s, StageTimer* tm,
-                unsigned long long* prof, unsigned* lfReady) {
+                unsigned long long* prof, unsigned* lfReady, unsigned long long lfTicks) {
   tm->mark("odom.lm", s);
   if (ob.ring) {
     const int gx = (int)std::min<size_t>(64, (ob.ringCtl / 16 + 255) / 256);
@@ -2535,11 +2556,11 @@ int launch_odom(const BatchBufs& bb, const OdomBufs& ob, const DevCfg& c, int K,
   const int blocks = ob.S * ob.G + (ob.integ ? ob.S : 0);  // the chains, then one integrating workgroup per stream
   const size_t lds = odom_lds_bytes();
   if (lfReady) {
-    if (ob.ring) k_odom<true, true><<<blocks, kOdomThreads, lds, s>>>(bb, ob, c, K, prof, lfReady);
-    else k_odom<false, true><<<blocks, kOdomThreads, lds, s>>>(bb, ob, c, K, prof, lfReady);
+    if (ob.ring) k_odom<true, true><<<blocks, kOdomThreads, lds, s>>>(bb, ob, c, K, prof, lfReady, lfTicks);
+    else k_odom<false, true><<<blocks, kOdomThreads, lds, s>>>(bb, ob, c, K, prof, lfReady, lfTicks);
   } else {
-    if (ob.ring) k_odom<true, false><<<blocks, kOdomThreads, lds, s>>>(bb, ob, c, K, prof, nullptr);
-    else k_odom<false, false><<<blocks, kOdomThreads, lds, s>>>(bb, ob, c, K, prof, nullptr);
+    if (ob.ring) k_odom<true, false><<<blocks, kOdomThreads, lds, s>>>(bb, ob, c, K, prof, nullptr, 0ull);
+    else k_odom<false, false><<<blocks, kOdomThreads, lds, s>>>(bb, ob, c, K, prof, nullptr, 0ull);
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

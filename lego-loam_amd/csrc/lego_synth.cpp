@@ -182,6 +182,18 @@ extern "C" int lego_synth_preset(const char* name, uint64_t seed, lego_synth_cfg
   } else if (!std::strcmp(name, "VLS-128")) {
     o->n_scan = 128; o->horizon_scan = 1800; o->vert_min_deg = -25.f;
     o->vert_max_deg = -25.f + 0.3f * 127; o->mount_height = 1.2f;
+  } else if (!std::strcmp(name, "HDL-32E")) {
+    // utility.h:71-76: 41.33 deg over 32 rings from -30.67; the beams sit
+    // 0.1 deg above the reference's row edges (as VLP-16's ang_bottom of
+    // 15 + 0.1 does for its own), so the vertical-angle row of the
+    // useCloudRing = false branch is the ring, not a float rounding away
+    o->n_scan = 32; o->horizon_scan = 1800; o->vert_min_deg = -30.67f + 0.1f;
+    o->vert_max_deg = -30.67f + 0.1f + 41.33f; o->mount_height = 1.5f;
+  } else if (!std::strcmp(name, "OS1-16")) {  // utility.h:89-94: +-16.6 deg
+    o->n_scan = 16; o->horizon_scan = 1024; o->vert_min_deg = -16.6f; o->vert_max_deg = 16.6f;
+  } else if (!std::strcmp(name, "OS1-64")) {  // utility.h:97-102
+    o->n_scan = 64; o->horizon_scan = 1024; o->vert_min_deg = -16.6f; o->vert_max_deg = 16.6f;
+    o->mount_height = 1.2f;
   } else {
     return LEGO_E_ARG;
   }

@@ -709,8 +709,7 @@ __global__ void __launch_bounds__(kHeadTile) k_vg_emit(const float4* in, int n, 
 // kVgSplit, so that their thousand leftovers sort in many small workgroups.
 constexpr int kVgSmallCloud = 65536;
 int vg_split_for(int n) { return n <= kVgSmallCloud ? kVgLocal : kVgSplit; }
-int vg_rounds_for(int n) {
-  static const int forced = std::getenv("LEGO_VG_ROUNDS") ? std::atoi(std::getenv("LEGO_VG_ROUNDS")) : -1;
+int vg_rounds_for(int n, int forced) {
   if (forced >= 0) return std::min(forced, kVgRoundsMax);
   const int split = vg_split_for(n);
   if (n <= split) return 0;
@@ -736,7 +735,7 @@ int voxel_grid_device(const float4* in, int n, const int* nDev, float leaf, floa
   k_vg_init<<<1, 64, 0, s>>>(v);
   k_vg_minmax<<<std::min(grid_for(n), 512), 256, 0, s>>>(in, n, nDev, v);
   k_vg_keys<<<grid_for(n), 256, 0, s>>>(in, n, nDev, leaf, v);
-  const int R = vg_rounds_for(n), split = vg_split_for(n);
+  const int R = vg_rounds_for(n, v.rounds), split = vg_split_for(n);
   k_vg_plan0<<<1, kVgPlanThreads, 0, s>>>(n, nDev, v, R, split);
   // grids sized by this cloud's bound n, not the scratch's capacity: a round's
   // tiles <= n / kVgTile + its segments (each > split keys)

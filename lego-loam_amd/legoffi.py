@@ -268,7 +268,43 @@ def oracle_lib() -> C.CDLL:
     return lib
 
 
+class CtxOpts(C.Structure):
+    """lego_ctx_opts (include/lego_loam.h): a context's scheduling and
+    diagnostic switches, fixed at creation."""
+    _fields_ = [(n, C.c_int32) for n in (
+        "size", "node_overlap", "front_parts", "lfv_wave", "lfv_block_rings", "lfv_wide", "ccl_tiles",
+        "seg_hbm", "odom_workgroups", "odom_gridless", "odom_integ", "odom_silent_wg", "odom_late_wg",
+        "lf_wait_ms", "mo_cand_cache", "kf_cap", "vg_rounds", "fa_synccheck", "mo_hostprof", "mo_evprof")] + [
+        ("reserved", C.c_int32 * 12)]
+
+
+# Tooling only (bench.py, scripts/): the A/B scripts switch a context's
+# options through the environment; the library itself reads none.
+ENV_OPTS = {"LEGO_NODE_OVERLAP": "node_overlap", "LEGO_FRONT_PARTS": "front_parts", "LEGO_LFV_WAVE": "lfv_wave",
+            "LEGO_LFV_BLOCK_RINGS": "lfv_block_rings", "LEGO_LFV_WIDE": "lfv_wide", "LEGO_CCL_TILES": "ccl_tiles",
+            "LEGO_SEG_HBM": "seg_hbm", "LEGO_ODOM_WORKGROUPS": "odom_workgroups",
+            "LEGO_ODOM_GRIDLESS": "odom_gridless", "LEGO_ODOM_INTEG": "odom_integ",
+            "LEGO_ODOM_SILENT_WG": "odom_silent_wg", "LEGO_ODOM_LATE_WG": "odom_late_wg",
+            "LEGO_MO_CAND": "mo_cand_cache", "LEGO_KF_CAP": "kf_cap", "LEGO_VG_ROUNDS": "vg_rounds",
+            "LEGO_FA_SYNCCHECK": "fa_synccheck", "LEGO_MO_HOSTPROF": "mo_hostprof", "LEGO_MO_EVPROF": "mo_evprof"}
+
+
+def opts_from_env() -> dict:
+    """The LEGO_* A/B variables of the tooling's environment as option values."""
+    return {f: int(os.environ[e]) for e, f in ENV_OPTS.items() if os.environ.get(e, "") != ""}
+
+
+def ctx_opts(lib: C.CDLL | None = None, **over) -> CtxOpts:
+    lib = lib or hip_lib()
+    o = CtxOpts()
+    lib.lego_ctx_opts_init(C.byref(o))
+    for k, v in over.items():
+        setattr(o, k, int(v))
+    return o
+
+
 HIP_EXPORTS = ["lego_sensor_preset", "lego_create", "lego_fleet_create", "lego_destroy", "lego_reset",
+               "lego_ctx_opts_init", "lego_create_ex", "lego_fleet_create_ex", "lego_comm_set_timeout",
                "lego_ip_process", "lego_fa_process", "lego_odom_batch", "lego_odom_batch_imu",
                "lego_imu_push", "lego_odom_batch_submit", "lego_odom_batch_wait", "lego_batch_fetch", "lego_pc2_decode", "lego_ip_process_pc2",
                "lego_odom_batch_pc2", "lego_pc2_encode_xyzi", "lego_cloud_info_serialize",
@@ -288,6 +324,13 @@ def hip_lib() -> C.CDLL:
                                 C.POINTER(C.c_void_p)]
     lib.lego_fleet_create.argtypes = [C.POINTER(SensorCfg), C.c_int, C.c_int32, C.c_int32, C.c_int32,
                                       C.POINTER(C.c_void_p)]
+    lib.lego_ctx_opts_init.argtypes = [C.POINTER(CtxOpts)]
+    lib.lego_ctx_opts_init.restype = None
+    lib.lego_create_ex.argtypes = [C.POINTER(SensorCfg), C.c_int, C.c_int32, C.c_int32, C.POINTER(CtxOpts),
+                                   C.POINTER(C.c_void_p)]
+    lib.lego_fleet_create_ex.argtypes = [C.POINTER(SensorCfg), C.c_int, C.c_int32, C.c_int32, C.c_int32,
+                                         C.POINTER(CtxOpts), C.POINTER(C.c_void_p)]
+    lib.lego_comm_set_timeout.argtypes = [C.c_void_p, C.c_int32]
     lib.lego_destroy.argtypes = [C.c_void_p]
     lib.lego_reset.argtypes = [C.c_void_p]
     lib.lego_ip_process.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_double, C.c_uint32,
@@ -590,17 +633,19 @@ class Lego:
     """The product pipeline (HIP) behind the C-ABI, one stream per context."""
 
     def __init__(self, cfg: SensorCfg, device: int = 0, max_points: int = 300000,
-                 max_batch: int = 1, streams: int = 0):
+                 max_batch: int = 1, streams: int = 0, opts: dict | None = None):
         """streams > 0: a fleet context (lego_fleet_create) of that many
-        streams, max_batch scans per stream; batches are stream-major."""
+        streams, max_batch scans per stream; batches are stream-major.
+        opts: lego_ctx_opts fields over the library defaults (lego_create_ex)."""
         self.lib = hip_lib()
         self.cfg = cfg
         self.h = C.c_void_p()
+        o = C.byref(ctx_opts(self.lib, **opts)) if opts else None
         if streams > 0:
-            check(self.lib.lego_fleet_create(C.byref(cfg), device, streams, max_points, max_batch,
-                                             C.byref(self.h)), "lego_fleet_create", self.lib)
+            check(self.lib.lego_fleet_create_ex(C.byref(cfg), device, streams, max_points, max_batch, o,
+                                                C.byref(self.h)), "lego_fleet_create", self.lib)
         else:
-            check(self.lib.lego_create(C.byref(cfg), device, max_points, max_batch, C.byref(self.h)),
+            check(self.lib.lego_create_ex(C.byref(cfg), device, max_points, max_batch, o, C.byref(self.h)),
                   "lego_create", self.lib)
         self._ip = IpOut()
         self._fa = FaOut()

@@ -111,6 +111,11 @@ def native_comm(L, dist, device: int):
     comm = C.c_void_p()
     L.check(lib.lego_comm_create(uid, dist.get_world_size(), dist.get_rank(), device, C.byref(comm)),
             "lego_comm_create", lib)
+    # the bound of the native gather's waits: the tooling's environment
+    # (LEGO_COMM_TIMEOUT_MS), handed to the library explicitly
+    if os.environ.get("LEGO_COMM_TIMEOUT_MS"):
+        L.check(lib.lego_comm_set_timeout(comm, max(1, int(os.environ["LEGO_COMM_TIMEOUT_MS"]))),
+                "lego_comm_set_timeout", lib)
     return comm
 
 

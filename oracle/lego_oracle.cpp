@@ -280,11 +280,28 @@ struct ImageProjection {
     orientationDiff = endOrientation - startOrientation;
   }
 
-  // projectPointCloud :211-257 (useCloudRing branch)
+  // The (size_t) conversion of :230.  Out of range it is UB in C++; the
+  // reference's x86-64 build converts a float below 2^63 by truncation toward
+  // zero through int64 (cvttss2si), so (-1, 0) gives row 0 and v <= -1 wraps
+  // to an index past N_SCAN.  Stated explicitly so this build cannot differ.
+  static size_t row_of(float v) {
+    if (!(v < 9.2233720e18f)) return ~(size_t)0;  // NaN or >= 2^63: never a row
+    return (size_t)(int64_t)v;
+  }
+
+  // projectPointCloud :211-257, both branches of useCloudRing (:225-231)
   void project(const lego_point_xyzir* in, int n) {
     for (int i = 0; i < n; ++i) {
       const float x = in[i].x, y = in[i].y, z = in[i].z;
-      size_t row = in[i].ring;
+      size_t row;
+      if (c.use_cloud_ring) {
+        row = in[i].ring;
+      } else {
+        // float atan2 / sqrt (utility.h's `using namespace std`), * 180 in
+        // float, / M_PI in double, stored to the float verticalAngle
+        const float va = (float)((double)(lego_atan2f(z, std::sqrt(x * x + y * y)) * 180.0f) / M_PI);
+        row = row_of((va + c.ang_bottom) / c.ang_res_y);
+      }
       if (row >= (size_t)N) continue;
       float h = (float)((double)(lego_atan2f(x, y) * 180.0f) / M_PI);
       double cd = -std::round(((double)h - 90.0) / (double)c.ang_res_x) + (double)(H / 2);
@@ -414,11 +431,31 @@ struct ImageProjection {
         }
   }
 
+  std::vector<lego_point_xyzir> finite;
+
   int process(const lego_point_xyzir* in, int n, bool images, bool gated = false) {
     if (n <= 0 || !in) return LEGO_E_ARG;
-    for (int i = 0; i < n; ++i)
-      if (!std::isfinite(in[i].x) || !std::isfinite(in[i].y) || !std::isfinite(in[i].z))
-        return LEGO_E_NOT_DENSE;
+    auto ok = [](const lego_point_xyzir& p) {
+      return std::isfinite(p.x) && std::isfinite(p.y) && std::isfinite(p.z);
+    };
+    if (c.use_cloud_ring) {
+      for (int i = 0; i < n; ++i)
+        if (!ok(in[i])) return LEGO_E_NOT_DENSE;  // :173-176
+    } else {
+      // pcl::removeNaNFromPointCloud (:170) of a non-dense cloud: the finite
+      // points in order (a dense-flagged cloud is projected unchanged upstream;
+      // here non-finite points are always removed, DESIGN.md §2 deviation 4)
+      bool all = true;
+      for (int i = 0; i < n && all; ++i) all = ok(in[i]);
+      if (!all) {
+        finite.clear();
+        for (int i = 0; i < n; ++i)
+          if (ok(in[i])) finite.push_back(in[i]);
+        if (finite.empty()) return LEGO_E_NOT_DENSE;  // points[0] of an empty cloud: UB upstream
+        in = finite.data();
+        n = (int)finite.size();
+      }
+    }
     reset();
     findStartEndAngle(in, n);
     project(in, n);

@@ -20,7 +20,7 @@ out = {"alone": b.dense_bench(L, 200, 20, 0)["scans_per_s"]}
 pts, off, stamps, maxn = b.make_stream(L, "VLP-16", 1, 100)
 d_pts = torch.from_numpy(pts.view(np.uint8)).to(0)
 d_off = torch.from_numpy(off.astype(np.int64)).to(0)
-g = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), device=0, max_points=maxn + 16, max_batch=100)
+g = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), device=0, max_points=maxn + 16, max_batch=100, opts=L.opts_from_env())
 out["vlp_ctx_idle"] = b.dense_bench(L, 200, 20, 0)["scans_per_s"]
 recs = (L.PoseRec * 100)()
 g.submit_device(d_pts.data_ptr(), d_off.data_ptr(), stamps, 100)

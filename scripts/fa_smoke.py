@@ -9,14 +9,14 @@ import legoffi as L  # noqa: E402
 
 sc = L.synth_cfg("VLS-128", 3)
 cap = L.synth_lib().lego_synth_max_points(L.C.byref(sc)) + 16
-g = L.Lego(L.sensor_cfg("VLS-128", L.hip_lib()), max_points=cap)
+g = L.Lego(L.sensor_cfg("VLS-128", L.hip_lib()), max_points=cap, opts=L.opts_from_env())
 for k in range(3):
     g.ip(*L.synth_scan(sc, k))
     fa = g.fa()
     print("front end scan", k, "ok", len(fa["surf_last"]), flush=True)
 g.close()
 surf, corner = L.synth_map(3, 50.0, 1_000_000, 200_000)
-g = L.Lego(L.sensor_cfg("VLS-128", L.hip_lib()), max_points=cap)
+g = L.Lego(L.sensor_cfg("VLS-128", L.hip_lib()), max_points=cap, opts=L.opts_from_env())
 g.mo_set_map(corner, surf)
 print("map installed", flush=True)
 for k in range(3):

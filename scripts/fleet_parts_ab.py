@@ -52,7 +52,7 @@ def main():
         wins.append((torch.from_numpy(np.concatenate(scans).view(np.uint8)).to("cuda:0"),
                      torch.from_numpy(off).to("cuda:0"), st))
     del src
-    fl = L.Lego(cfg, device=0, max_points=maxn + 16, max_batch=K, streams=S)
+    fl = L.Lego(cfg, device=0, max_points=maxn + 16, max_batch=K, streams=S, opts=L.opts_from_env())
     recs = (L.PoseRec * (S * K))()
     n = [0]
 

@@ -55,7 +55,7 @@ def main():
             st = np.concatenate([stamps_one[w * K:(w + 1) * K]] * S)
             wins.append((d_pts, d_off, st))
         torch.cuda.synchronize()
-        fl = L.Lego(cfg, device=0, max_points=maxn + 16, max_batch=K, streams=S)
+        fl = L.Lego(cfg, device=0, max_points=maxn + 16, max_batch=K, streams=S, opts=L.opts_from_env())
         n_en = C.c_int32()
         lib.lego_stage_times(fl.h, None, (C.c_float * 1)(), 0, C.byref(n_en))  # enable the stage timer
         recs = (L.PoseRec * (S * K))()

@@ -23,7 +23,7 @@ for sensor in os.environ.get("SENSORS", "VLP-16,HDL-64E,VLS-128").split(","):
     seed = SENS[sensor]
     sc = L.synth_cfg(sensor, seed)
     scans = [L.synth_scan(sc, k) for k in range(n)]
-    g = L.Lego(L.sensor_cfg(sensor, lib), max_points=max(len(p) for p, _ in scans) + 16)
+    g = L.Lego(L.sensor_cfg(sensor, lib), max_points=max(len(p) for p, _ in scans) + 16, opts=L.opts_from_env())
     on = (C.c_float * 1)()
     nn = C.c_int32()
     lib.lego_stage_times(g.h, None, on, 0, C.byref(nn))  # stage events on

@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.join(R, "lego-loam_amd"))
 import legoffi as L  # noqa: E402
 
 d = np.load(os.path.join(R, "tests/golden/dense_ring_keys.npz"))
-g = L.Lego(L.sensor_cfg("VLS-128", L.hip_lib()), max_points=4096)
+g = L.Lego(L.sensor_cfg("VLS-128", L.hip_lib()), max_points=4096, opts=L.opts_from_env())
 
 
 def t(keys, mode):

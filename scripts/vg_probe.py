@@ -13,7 +13,7 @@ sensor = "VLS-128"
 sc = L.synth_cfg(sensor, 3)
 surf, corner = L.synth_map(3, 50.0, 1_000_000, 200_000)
 cap = L.synth_lib().lego_synth_max_points(L.C.byref(sc)) + 16  # as bench.py's mapping line
-eng = L.Lego(L.sensor_cfg(sensor, L.hip_lib()), max_points=cap)
+eng = L.Lego(L.sensor_cfg(sensor, L.hip_lib()), max_points=cap, opts=L.opts_from_env())
 reps = int(os.environ.get("REPS", "5"))
 
 

@@ -21,5 +21,6 @@ int main(void) {
   O(lego_loop_out, between_translation);
   S(lego_mo_opts); O(lego_mo_opts, loop_closure_enable); O(lego_mo_opts, surrounding_keyframe_search_num);
   S(lego_synth_cfg); O(lego_synth_cfg, seed);
+  S(lego_ctx_opts); O(lego_ctx_opts, lf_wait_ms); O(lego_ctx_opts, mo_evprof); O(lego_ctx_opts, reserved);
   return 0;
 }

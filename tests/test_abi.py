@@ -48,7 +48,7 @@ def test_struct_layouts_match_ctypes(L, tmp_path):
     m = {"lego_point_xyzir": L.PointXYZIR, "lego_point_xyzi": L.PointXYZI, "lego_sensor_cfg": L.SensorCfg,
          "lego_cloud_info": L.CloudInfo, "lego_ip_out": L.IpOut, "lego_fa_out": L.FaOut,
          "lego_mo_out": L.MoOut, "lego_pose_rec": L.PoseRec, "lego_synth_cfg": L.SynthCfg,
-         "lego_loop_out": L.LoopOut, "lego_mo_opts": L.MoOpts}
+         "lego_loop_out": L.LoopOut, "lego_mo_opts": L.MoOpts, "lego_ctx_opts": L.CtxOpts}
     for key, val in out.items():
         if "." in key:
             t, f = key.split(".")
@@ -75,3 +75,32 @@ def test_bad_inputs_rejected_without_device(L):
     bad = L.SensorCfg.from_buffer_copy(bytes(good))
     bad.n_scan = 4096  # > kMaxRings
     assert lib.lego_create(C.byref(bad), 0, 10, 1, C.byref(h)) == L.LEGO_E_ARG
+
+
+def test_ctx_opts_defaults_and_validation(L):
+    """lego_ctx_opts_init's defaults (host only, no device needed) and the
+    size check of lego_create_ex."""
+    lib = L.hip_lib()
+    o = L.ctx_opts(lib)
+    assert o.size == C.sizeof(L.CtxOpts)
+    assert (o.node_overlap, o.front_parts, o.lfv_wave, o.lfv_wide, o.ccl_tiles, o.seg_hbm) == (1, 2, 1, -1, 1, 0)
+    assert (o.odom_workgroups, o.odom_gridless, o.odom_integ, o.odom_silent_wg, o.odom_late_wg) == (0, -1, -1, -1, -1)
+    assert (o.lf_wait_ms, o.mo_cand_cache, o.kf_cap, o.vg_rounds) == (2000, 1, 0, -1)
+    bad = L.ctx_opts(lib)
+    bad.size = 8
+    h = C.c_void_p()
+    cfg = L.sensor_cfg("VLP-16", lib)
+    assert lib.lego_create_ex(C.byref(cfg), 0, 1000, 1, C.byref(bad), C.byref(h)) == L.LEGO_E_ARG
+    neg = L.ctx_opts(lib, lf_wait_ms=-1)
+    assert lib.lego_create_ex(C.byref(cfg), 0, 1000, 1, C.byref(neg), C.byref(h)) == L.LEGO_E_ARG
+
+
+def test_no_environment_reads_in_the_library():
+    """The shipped library's schedule is fixed by lego_ctx_opts at creation:
+    no getenv anywhere in its sources."""
+    import re
+    src = REPO / "lego-loam_amd" / "csrc"
+    hits = [f"{p.name}:{i + 1}" for p in sorted(src.iterdir()) if p.suffix in (".hip", ".h", ".cpp")
+            and p.name != "lego_synth.cpp"
+            for i, line in enumerate(p.read_text().splitlines()) if re.search(r"\bgetenv\b", line)]
+    assert not hits, hits

@@ -1,12 +1,11 @@
 """A fleet batch's front end in parts (submit_batch: projection + extraction of
-whole streams per part, each part on its own HIP stream, LEGO_FRONT_PARTS read
-per call) is a scheduling change only: every stream's records equal, byte for
+whole streams per part, each part on its own HIP stream; lego_ctx_opts::front_parts)
+is a scheduling change only: every stream's records equal, byte for
 byte, the one-part order's, and the one-part records equal the oracle's (the
 C4 test checks the default split against the oracle scan by scan).
 Reference: featureAssociation.cpp:1817-1860 (runFeatureAssociation, per
 stream), imageProjection.cpp:300-460."""
 import ctypes as C
-import os
 import sys
 from pathlib import Path
 
@@ -31,22 +30,14 @@ def _pack(scans):
 
 
 def _run(L, cfg, cap, scans, parts):
-    old = os.environ.get("LEGO_FRONT_PARTS")
-    os.environ["LEGO_FRONT_PARTS"] = str(parts)
-    try:
-        h = K // 2
-        fl = L.Lego(cfg, max_points=cap, max_batch=h, streams=STREAMS)
-        got = []
-        for part in (slice(0, h), slice(h, K)):
-            recs = fl.odom_batch(*_pack([x for s in range(STREAMS) for x in scans[s][part]]))  # stream-major
-            got.append([bytes(C.string_at(C.addressof(r), C.sizeof(r))) for r in recs])
-        fl.close()
-        return got
-    finally:
-        if old is None:
-            os.environ.pop("LEGO_FRONT_PARTS", None)
-        else:
-            os.environ["LEGO_FRONT_PARTS"] = old
+    h = K // 2
+    fl = L.Lego(cfg, max_points=cap, max_batch=h, streams=STREAMS, opts={"front_parts": parts})
+    got = []
+    for part in (slice(0, h), slice(h, K)):
+        recs = fl.odom_batch(*_pack([x for s in range(STREAMS) for x in scans[s][part]]))  # stream-major
+        got.append([bytes(C.string_at(C.addressof(r), C.sizeof(r))) for r in recs])
+    fl.close()
+    return got
 
 
 def test_front_parts_are_only_scheduling(L):

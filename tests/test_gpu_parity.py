@@ -278,39 +278,34 @@ def test_scan_to_map_keyframe_parity(L):
 
 
 def test_keyframe_store_full_is_reported(L):
-    """The keyframe store's capacity (LEGO_KF_CAP shrinks it, diagnostic):
-    the step whose keyframe does not fit returns LEGO_E_CAPACITY itself (not
-    a later one), every later step does too (the history is incomplete), and
-    lego_reset recovers the context: the stream then matches a fresh one."""
-    import os
-
+    """The keyframe store's capacity (lego_ctx_opts::kf_cap shrinks it,
+    diagnostic): the step whose keyframe does not fit returns LEGO_E_CAPACITY
+    itself (not a later one), every later step does too (the history is
+    incomplete), and lego_reset recovers the context: the stream then matches
+    a fresh one."""
     sc = L.synth_cfg("VLP-16", 6)
     scans = [L.synth_scan(sc, k) for k in range(30)]
-    os.environ["LEGO_KF_CAP"] = "3"
-    try:
-        gpu = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=40000)
-        saved_ok, failed_at, msgs = 0, None, []
-        for k, (pts, stamp) in enumerate(scans):
-            gpu.ip(pts, stamp)
-            gpu.fa()
-            try:
-                saved_ok += gpu.mo()["processed"]
-            except RuntimeError as e:
-                msgs.append(str(e))
-                if failed_at is None:
-                    failed_at = k
-        assert failed_at is not None and "keyframe store is full" in msgs[0], msgs[:1]
-        assert "was not saved" in msgs[0] and len(msgs) >= 2, msgs  # reported at its own step, then sticky
-        assert f"status {L.LEGO_E_CAPACITY}" in msgs[0]
-        gpu.reset()
-        got = []
-        for pts, stamp in scans[:10]:
-            gpu.ip(pts, stamp)
-            gpu.fa()
-            got.append(gpu.mo()["transform_aft_mapped"])
-        gpu.close()
-    finally:
-        os.environ.pop("LEGO_KF_CAP", None)
+    gpu = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=40000, opts={"kf_cap": 3})
+    saved_ok, failed_at, msgs = 0, None, []
+    for k, (pts, stamp) in enumerate(scans):
+        gpu.ip(pts, stamp)
+        gpu.fa()
+        try:
+            saved_ok += gpu.mo()["processed"]
+        except RuntimeError as e:
+            msgs.append(str(e))
+            if failed_at is None:
+                failed_at = k
+    assert failed_at is not None and "keyframe store is full" in msgs[0], msgs[:1]
+    assert "was not saved" in msgs[0] and len(msgs) >= 2, msgs  # reported at its own step, then sticky
+    assert f"status {L.LEGO_E_CAPACITY}" in msgs[0]
+    gpu.reset()
+    got = []
+    for pts, stamp in scans[:10]:
+        gpu.ip(pts, stamp)
+        gpu.fa()
+        got.append(gpu.mo()["transform_aft_mapped"])
+    gpu.close()
     fresh = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=40000)
     for (pts, stamp), g in zip(scans[:10], got):
         fresh.ip(pts, stamp)
@@ -324,7 +319,6 @@ def test_concurrent_streams_identical(L):
     stream each) give the same pose records, byte for byte, as one context at
     a time — also with fewer odometry workgroups than the default (the
     redundant per-workgroup solve makes the count invisible)."""
-    import os
     import threading
 
     cfg = L.sensor_cfg("VLP-16", L.hip_lib())
@@ -352,13 +346,8 @@ def test_concurrent_streams_identical(L):
         ref.append(run(g, st))
         g.close()
     ctxs = []
-    for wg in (None, "16", "4", "1"):
-        if wg:
-            os.environ["LEGO_ODOM_WORKGROUPS"] = wg
-        try:
-            ctxs.append(L.Lego(cfg, max_points=40000, max_batch=K))
-        finally:
-            os.environ.pop("LEGO_ODOM_WORKGROUPS", None)
+    for wg in (None, 16, 4, 1):
+        ctxs.append(L.Lego(cfg, max_points=40000, max_batch=K, opts={"odom_workgroups": wg} if wg else None))
     got = [None] * len(ctxs)
     errs = []
 
@@ -381,7 +370,7 @@ def test_concurrent_streams_identical(L):
 
 
 @pytest.mark.parametrize("sensor,seeds,K,cap,workgroups", [
-    ("VLP-16", (4, 8, 9), 8, 40000, None), ("VLP-16", (4, 8, 9), 8, 40000, "1"),
+    ("VLP-16", (4, 8, 9), 8, 40000, None), ("VLP-16", (4, 8, 9), 8, 40000, 1),
     ("HDL-64E", (2, 5), 4, 140000, None)])
 def test_fleet_equals_single_streams(L, sensor, seeds, K, cap, workgroups):
     """A fleet context (lego_fleet_create: S streams, one launch per stage for
@@ -389,8 +378,6 @@ def test_fleet_equals_single_streams(L, sensor, seeds, K, cap, workgroups):
     the stream's own context, across two stream-major batches (the states
     and the FA carries cross the launch boundary per stream).  HDL-64E: the
     HBM-resident odometry with its per-stream hand-off exchange."""
-    import os
-
     cfg = L.sensor_cfg(sensor, L.hip_lib())
     S = len(seeds)
     streams = []
@@ -410,12 +397,8 @@ def test_fleet_equals_single_streams(L, sensor, seeds, K, cap, workgroups):
         raw = bytes(g.odom_batch(*pack(scans[:K // 2]))) + bytes(g.odom_batch(*pack(scans[K // 2:])))
         g.close()
         ref.append([raw[64 * k:64 * k + 60] for k in range(K)])
-    if workgroups:
-        os.environ["LEGO_ODOM_WORKGROUPS"] = workgroups
-    try:
-        fl = L.Lego(cfg, max_points=cap, max_batch=K // 2, streams=S)
-    finally:
-        os.environ.pop("LEGO_ODOM_WORKGROUPS", None)
+    fl = L.Lego(cfg, max_points=cap, max_batch=K // 2, streams=S,
+                opts={"odom_workgroups": workgroups} if workgroups else None)
     got = [[] for _ in range(S)]
     for h in (slice(0, K // 2), slice(K // 2, K)):
         batch = [sc for scans in streams for sc in scans[h]]  # stream-major
@@ -540,12 +523,11 @@ def test_reset_in_flight(L):
 @pytest.mark.parametrize("seed,extra", [(0, {}), (1, {}), (2, {"dup_frac": 0.05})])
 def test_seg_lds_equals_hbm_union_find(L, seed, extra):
     """VLP-16 batches of more than kSegHbmMaxScans (8) scans are segmented in
-    LDS (k_seg_lds); node calls (one scan) and LEGO_SEG_HBM (diagnostic) go
+    LDS (k_seg_lds); node calls (one scan) and the seg_hbm option (diagnostic) go
     through the HBM union-find (k_ccl_* + k_compact) that the larger sensors
-    use.  All equal the oracle, clouds and cloud_info byte for byte on 12
-    consecutive scans (and labels / images through the node calls)."""
-    import os
-
+    use (lego_ctx_opts::seg_hbm, diagnostic).  All equal the oracle, clouds and
+    cloud_info byte for byte on 12 consecutive scans (and labels / images
+    through the node calls)."""
     sc = L.synth_cfg("VLP-16", seed, **extra)
     scans = [L.synth_scan(sc, k) for k in range(12)]
     ora = L.Oracle(L.sensor_cfg("VLP-16"))
@@ -556,15 +538,11 @@ def test_seg_lds_equals_hbm_union_find(L, seed, extra):
     stamps = np.array([s for _, s in scans], dtype=np.float64)
     outs = {}
     for mode in ("lds", "hbm"):
-        if mode == "hbm":
-            os.environ["LEGO_SEG_HBM"] = "1"
-        try:
-            gpu = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=cap, max_batch=len(scans))
-            gpu.odom_batch(pts, offs, stamps)
-            outs[mode] = [gpu.batch_fetch(k)[0] for k in range(len(scans))]
-            gpu.close()
-        finally:
-            os.environ.pop("LEGO_SEG_HBM", None)
+        gpu = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=cap, max_batch=len(scans),
+                     opts={"seg_hbm": int(mode == "hbm")})
+        gpu.odom_batch(pts, offs, stamps)
+        outs[mode] = [gpu.batch_fetch(k)[0] for k in range(len(scans))]
+        gpu.close()
     node = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=cap)
     outs["node"] = [node.ip(p, s, images=True) for p, s in scans]
     node.close()

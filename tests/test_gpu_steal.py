@@ -1,12 +1,11 @@
 """The exchanges' steal-on-timeout paths (lego_odom.hip, "exchange" and the
 hand-off exchange): nothing assumes the workgroups of an odometry launch are
-resident together, so a workgroup that never publishes (LEGO_ODOM_SILENT_WG,
+resident together, so a workgroup that never publishes (lego_ctx_opts::odom_silent_wg,
 a diagnostic read at context creation) must only cost time: the others wait
 kStealTicks, then compute its NN queries and its share of TransformToEnd
 themselves.  The records must equal a normal context's byte for byte:
 VLP-16 (LDS-resident: NN exchange) and HDL-64E (HBM-resident: NN and
 hand-off exchanges)."""
-import os
 
 import numpy as np
 import pytest
@@ -29,11 +28,7 @@ def test_silent_workgroup_is_stolen(L, sensor, seed, n, cap):
     g = L.Lego(cfg, max_points=cap, max_batch=n)
     want = bytes(g.odom_batch(*_pack(scans)))
     g.close()
-    os.environ["LEGO_ODOM_SILENT_WG"] = "3"
-    try:
-        s = L.Lego(cfg, max_points=cap, max_batch=n)
-    finally:
-        os.environ.pop("LEGO_ODOM_SILENT_WG", None)
+    s = L.Lego(cfg, max_points=cap, max_batch=n, opts={"odom_silent_wg": 3})
     got = bytes(s.odom_batch(*_pack(scans)))
     s.close()
     assert [got[64 * k:64 * k + 60] for k in range(n)] == [want[64 * k:64 * k + 60] for k in range(n)]
@@ -43,7 +38,7 @@ def test_silent_workgroup_is_stolen(L, sensor, seed, n, cap):
 def test_late_workgroup_reads_input_state(L, sensor, seed, n, cap):
     """A workgroup dispatched after its stream's lead has finished (and written
     the launch's final OdomState) must still start from the launch's input
-    state (OdomBufs::stIn): LEGO_ODOM_LATE_WG holds one workgroup until the
+    state (OdomBufs::stIn): lego_ctx_opts::odom_late_wg holds one workgroup until the
     lead is done.  Three launches, so the late workgroup's private last clouds
     of launch k feed the NN results it publishes in launch k+1."""
     cfg = L.sensor_cfg(sensor, L.hip_lib())
@@ -60,11 +55,7 @@ def test_late_workgroup_reads_input_state(L, sensor, seed, n, cap):
     g = L.Lego(cfg, max_points=cap, max_batch=per)
     want = run(g)
     g.close()
-    os.environ["LEGO_ODOM_LATE_WG"] = "5"
-    try:
-        s = L.Lego(cfg, max_points=cap, max_batch=per)
-    finally:
-        os.environ.pop("LEGO_ODOM_LATE_WG", None)
+    s = L.Lego(cfg, max_points=cap, max_batch=per, opts={"odom_late_wg": 5})
     got = run(s)
     s.close()
     assert got == want

@@ -104,18 +104,13 @@ def test_vlp16_grid_and_gridless_odometry(L, gridless):
     """Both closest-point searches of the LDS-resident odometry against the
     oracle: the hashed 0.5 m grids (what a fleet with few workgroups per stream
     runs) and the gridless mode (exhaustive pass over the LDS cloud, key tables
-    only; what a single stream's 24 workgroups run).  LEGO_ODOM_GRIDLESS
+    only; what a single stream's 24 workgroups run).  lego_ctx_opts::odom_gridless
     overrides the host's choice (OdomBufs::gridless)."""
-    import os
-
     n, B = 40, 20
     scans, pts, off, stamps = _stream(L, "VLP-16", 4, n)
     ref = _oracle_recs(L, "VLP-16", scans)
-    os.environ["LEGO_ODOM_GRIDLESS"] = gridless
-    try:
-        g = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=int(np.max(np.diff(off))) + 16, max_batch=B)
-    finally:
-        os.environ.pop("LEGO_ODOM_GRIDLESS", None)
+    g = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=int(np.max(np.diff(off))) + 16, max_batch=B,
+               opts={"odom_gridless": int(gridless)})
     recs = []
     for i in range(n // B):
         a, b = off[i * B], off[(i + 1) * B]

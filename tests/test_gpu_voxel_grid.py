@@ -9,9 +9,6 @@ The adversarial keys (tests/golden/vg_killer.npz) come from McIlroy's
 adversary run against libstdc++'s std::sort (tests/golden/make_vg_killer.py);
 they become clouds with leaf 1: the point of key k lies in voxel k."""
 import ctypes as C
-import os
-import subprocess
-import sys
 from pathlib import Path
 
 import numpy as np
@@ -127,31 +124,16 @@ def test_leaf_overflow_copies_input(L, gpu):
     _same(got, p, "overflow is a copy")
 
 
-_FORCED = r"""
-import sys, numpy as np
-sys.path.insert(0, sys.argv[1])
-from conftest import _load_ffi
-import test_gpu_voxel_grid as T
-L = _load_ffi()
-g = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=40000, max_batch=1)
-keys = np.load(T.REPO / "tests/golden/vg_killer.npz")["n20000_div1"]
-for name, p, leaf in (("random", T.cloud(np.random.default_rng(3), 150000, 20.0, L.XYZI_DTYPE), 0.4),
-                      ("killer", T.keyed_cloud(keys, L.XYZI_DTYPE), 1.0)):
-    got, st = g.voxel_grid(p, leaf)
-    T._same(got, T.oracle_vg(L, p, leaf), name)
-    print(name, st)
-    assert st["rounds"] == 0 and st["slow_segments"] > 0, st
-g.close()
-print("ok")
-"""
-
-
-def test_forced_single_workgroup_partition():
-    """LEGO_VG_ROUNDS=0 (diagnostic): no multi-workgroup rounds, so clouds
-    above the workgroup size are partitioned by one workgroup in global memory
-    (the path for segments the rounds leave too large), heap sort included."""
-    env = dict(os.environ, LEGO_VG_ROUNDS="0")
-    r = subprocess.run([sys.executable, "-c", _FORCED, str(REPO / "tests")], env=env, capture_output=True,
-                       text=True, timeout=240)
-    print(r.stdout[-2000:], r.stderr[-2000:])
-    assert r.returncode == 0 and r.stdout.strip().endswith("ok")
+def test_forced_single_workgroup_partition(L):
+    """lego_ctx_opts::vg_rounds = 0 (diagnostic): no multi-workgroup rounds,
+    so clouds above the workgroup size are partitioned by one workgroup in
+    global memory (the path for segments the rounds leave too large), heap
+    sort included."""
+    g = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=40000, max_batch=1, opts={"vg_rounds": 0})
+    keys = np.load(REPO / "tests/golden/vg_killer.npz")["n20000_div1"]
+    for name, p, leaf in (("random", cloud(np.random.default_rng(3), 150000, 20.0, L.XYZI_DTYPE), 0.4),
+                          ("killer", keyed_cloud(keys, L.XYZI_DTYPE), 1.0)):
+        got, st = g.voxel_grid(p, leaf)
+        _same(got, oracle_vg(L, p, leaf), name)
+        assert st["rounds"] == 0 and st["slow_segments"] > 0, (name, st)
+    g.close()
