@@ -267,7 +267,10 @@ typedef struct lego_ctx_opts {
                               kernel that failed (stderr); default 0 */
   int32_t mo_hostprof;     /* diagnostic: the mapping step's host enqueue times (stderr); default 0 */
   int32_t mo_evprof;       /* diagnostic: the mapping step's chain times (stderr); default 0 */
-  int32_t reserved[12];
+  int32_t ip_fused;        /* 1 (default): a batch of VLP-16-class scans is projected, ground-walked
+                              and segmented by one kernel, a workgroup per scan (k_ip_lds);
+                              0: four kernels (k_project, k_pixels, k_ground, k_seg_lds) */
+  int32_t reserved[11];
 } lego_ctx_opts;
 void lego_ctx_opts_init(lego_ctx_opts* opts);
 /* lego_create / lego_fleet_create with options (NULL: the defaults). */

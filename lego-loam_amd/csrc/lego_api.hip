@@ -360,6 +360,7 @@ void lego_ctx_opts_init(lego_ctx_opts* o) {
   o->mo_cand_cache = 1;
   o->kf_cap = 0;
   o->vg_rounds = -1;
+  o->ip_fused = 1;
 }
 
 int lego_sensor_preset(const char* name, lego_sensor_cfg* o) {
@@ -443,6 +444,7 @@ static int create_ctx(const lego_sensor_cfg* cfg, int device, int32_t n_streams,
   x->lo.lfvBlockRings = opts.lfv_block_rings;
   x->lo.lfvWide = opts.lfv_wide;
   x->lo.faSyncCheck = opts.fa_synccheck;
+  x->lo.ipFused = opts.ip_fused;
   x->vgApi.rounds = opts.vg_rounds;
   x->mo.hostprof = opts.mo_hostprof != 0;
   x->mo.evprof = opts.mo_evprof != 0;

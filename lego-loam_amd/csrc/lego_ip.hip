@@ -34,11 +34,12 @@ __device__ __forceinline__ bool xyz_finite(const float4& p) {
   return __builtin_isfinite(p.x) && __builtin_isfinite(p.y) && __builtin_isfinite(p.z);
 }
 
-__global__ void k_project(BatchBufs bb, DevCfg c) {
-  const int b = blockIdx.y;
-  const int n = scan_npts(bb, b);
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+// projectPointCloud for point i of scan b (:219-256): its pixel, or -1 when
+// it is dropped; findStartEndAngle's two raw angles (:201-202) from the
+// scan's first / last point, and the non-dense flag.  k_project (one lane per
+// point, the owner image in HBM) and k_ip_lds (one workgroup per scan, the
+// owner image in LDS) share it.
+__device__ __forceinline__ int project_point(const BatchBufs& bb, const DevCfg& c, int b, int n, int i) {
   const lego_point_xyzir* p0 = (const lego_point_xyzir*)bb.pts + bb.off[b];
   const lego_point_xyzir* pp = p0 + i;
   const float4 xyz = *(const float4*)pp;
@@ -47,7 +48,7 @@ __global__ void k_project(BatchBufs bb, DevCfg c) {
   if (!xyz_finite(xyz)) {
     if (c.ringRow) {
       bb.bad[b] = kBadNotDense;  // the host rejects the batch with LEGO_E_NOT_DENSE
-      return;
+      return -1;
     }
     // useCloudRing = false: removeNaNFromPointCloud (:170) drops the point,
     // and points[0] / points[size - 1] of findStartEndAngle (:201-202) are
@@ -58,7 +59,7 @@ __global__ void k_project(BatchBufs bb, DevCfg c) {
       while (k < n && !xyz_finite(*(const float4*)(p0 + k))) ++k;
       if (k == n) {
         bb.bad[b] = kBadNotDense;  // no finite point: points[0] of an empty cloud (UB upstream)
-        return;
+        return -1;
       }
       const float4 q = *(const float4*)(p0 + k);
       bb.rawang[2 * b] = -lego_atan2f(q.y, q.x);
@@ -71,14 +72,14 @@ __global__ void k_project(BatchBufs bb, DevCfg c) {
         bb.rawang[2 * b + 1] = -lego_atan2f(q.y, q.x);
       }
     }
-    return;
+    return -1;
   }
   if (i == 0) bb.rawang[2 * b] = -lego_atan2f(y, x);                   // :201
   if (i == n - 1) bb.rawang[2 * b + 1] = -lego_atan2f(y, x);           // :202
   int row;
   if (c.ringRow) {
     row = ring;  // :226
-    if (row >= c.N) return;
+    if (row >= c.N) return -1;
   } else {
     // :229-230: float atan2 / sqrt (utility.h's `using namespace std`), the
     // product with 180 in float, the division by M_PI in double, stored to
@@ -88,18 +89,44 @@ __global__ void k_project(BatchBufs bb, DevCfg c) {
     // rowIdn is size_t: x86-64 converts a float below 2^63 by truncation
     // toward zero through int64, so (-1, 0) gives row 0 and v <= -1 an index
     // past N_SCAN (skipped by :232, where `rowIdn < 0` is always false)
-    if (!(v > -1.0f && v < (float)c.N)) return;
+    if (!(v > -1.0f && v < (float)c.N)) return -1;
     row = (int)v;
   }
   const float h = (float)((double)(lego_atan2f(x, y) * 180.0f) / M_PI);  // :235
   const double cd = -round(((double)h - 90.0) / (double)c.ang_res_x) + (double)(c.H / 2);
-  if (cd < 0) return;
+  if (cd < 0) return -1;
   long col = (long)cd;
   if (col >= c.H) col -= c.H;
-  if (col >= c.H) return;
+  if (col >= c.H) return -1;
   const float range = __builtin_sqrtf(x * x + y * y + z * z);          // :244
-  if (range < c.min_range) return;
-  atomicMax(&bb.owner[(size_t)b * c.P + row * c.H + col], i);
+  if (range < c.min_range) return -1;
+  return row * c.H + (int)col;
+}
+
+__global__ void k_project(BatchBufs bb, DevCfg c) {
+  const int b = blockIdx.y;
+  const int n = scan_npts(bb, b);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int pix = project_point(bb, c, b, n, i);
+  if (pix >= 0) atomicMax(&bb.owner[(size_t)b * c.P + pix], i);  // last writer wins (:248-255)
+}
+
+// A pixel of the range image and the full cloud (:248-255) from its owner
+// point o (-1: none).
+__device__ __forceinline__ void pixel_out(const BatchBufs& bb, const DevCfg& c, int b, int row, int col, int o) {
+  const size_t gp = (size_t)b * c.P + row * c.H + col;
+  if (o < 0) {
+    bb.range[gp] = FLT_MAX;
+    const float qn = __builtin_nanf("");
+    bb.full[gp] = make_float4(qn, qn, qn, -1.0f);
+    return;
+  }
+  const float4 xyz = *(const float4*)((const lego_point_xyzir*)bb.pts + bb.off[b] + o);
+  const float range = __builtin_sqrtf(xyz.x * xyz.x + xyz.y * xyz.y + xyz.z * xyz.z);
+  const float inten = (float)((double)(float)row + (double)(float)col / 10000.0);  // :250
+  bb.range[gp] = range;
+  bb.full[gp] = make_float4(xyz.x, xyz.y, xyz.z, inten);
 }
 
 // One workgroup per 4 rows x 64 columns (a wave per row): the stores stay
@@ -119,17 +146,7 @@ __global__ void __launch_bounds__(256) k_pixels(BatchBufs bb, DevCfg c) {
   // place of a separate fill of the whole image before every batch (a fleet
   // call's 590 MB fill took ~1.4 ms of a ~20 ms call)
   if (o >= 0) bb.owner[gp] = -1;
-  if (o < 0) {
-    bb.range[gp] = FLT_MAX;
-    const float qn = __builtin_nanf("");
-    bb.full[gp] = make_float4(qn, qn, qn, -1.0f);
-    return;
-  }
-  const float4 xyz = *(const float4*)((const lego_point_xyzir*)bb.pts + bb.off[b] + o);
-  const float range = __builtin_sqrtf(xyz.x * xyz.x + xyz.y * xyz.y + xyz.z * xyz.z);
-  const float inten = (float)((double)(float)row + (double)(float)col / 10000.0);  // :250
-  bb.range[gp] = range;
-  bb.full[gp] = make_float4(xyz.x, xyz.y, xyz.z, inten);
+  pixel_out(bb, c, b, row, col, o);
 }
 
 // groundMat column walk.  Carry form of the overwrite semantics:
@@ -139,10 +156,9 @@ __global__ void __launch_bounds__(256) k_pixels(BatchBufs bb, DevCfg c) {
 // the per-row form's loads behind the previous row's stores: ~13.5 us for a
 // single VLP-16 scan, 16 dependent rows).
 constexpr int kGroundRows = 8;
-__global__ void k_ground(BatchBufs bb, DevCfg c) {
-  const int b = blockIdx.y;
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= c.H) return;
+// Column j of scan b; par (k_ip_lds): the union-find's initial parents of
+// the column's pixels in LDS as well (p for an unlabelled pixel, else -1).
+__device__ __forceinline__ void ground_column(const BatchBufs& bb, const DevCfg& c, int b, int j, int* par) {
   const size_t base = (size_t)b * c.P;
   int cur = 0;  // value G[i] holds before pair i is examined
   for (int i0 = 0; i0 < c.N; i0 += kGroundRows) {
@@ -180,10 +196,17 @@ __global__ void k_ground(BatchBufs bb, DevCfg c) {
       }
       cur = next;
       const size_t gp = base + i * c.H + j;
+      const bool lab = G == 1 || rg[u] == FLT_MAX;
       bb.ground[gp] = (int8_t)G;
-      bb.label[gp] = (G == 1 || rg[u] == FLT_MAX) ? -1 : 0;     // :295-301
+      bb.label[gp] = lab ? -1 : 0;     // :295-301
+      if (par) par[i * c.H + j] = lab ? -1 : i * c.H + j;
     }
   }
+}
+
+__global__ void k_ground(BatchBufs bb, DevCfg c) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < c.H) ground_column(bb, c, blockIdx.y, j, nullptr);
 }
 
 __device__ __forceinline__ TanBand seg_tan_band(const DevCfg& c) {  // computed on the host
@@ -687,20 +710,25 @@ constexpr int kSegHbmMaxScans = 8;  // launches of up to this many scans segment
 bool seg_lds_ok(const DevCfg& c) { return c.N <= kSegLdsMaxN && c.P <= kSegLdsMaxP && !c.segHbm; }
 
 
-__global__ void __launch_bounds__(1024) k_seg_lds(BatchBufs bb, DevCfg c, int want_labels) {
-  extern __shared__ int par[];          // [P]
+// Scan b's segmentation and compaction by the calling 1024-thread workgroup,
+// par[P] its LDS parents; parReady: par already holds the initial parents
+// (k_ip_lds writes them with the ground image), else they come from bb.label.
+__device__ __forceinline__ void seg_lds(const BatchBufs& bb, const DevCfg& c, int b, int want_labels, int* par,
+                                        bool parReady) {
   __shared__ int wpre[kSegK][3][16];    // per chunk and flag: the waves' exclusive prefixes
   __shared__ int cpre[kSegK + 1][3];    // per chunk and flag: the chunks' exclusive prefixes
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const size_t base = (size_t)b * c.P;
   const int P = c.P, H = c.H, K = (P + 1023) >> 10;
   volatile int* vpar = par;
   const TanBand tb = seg_tan_band(c);
   // pixel k * 1024 + tid of chunk k: loads coalesced, chunk-ordered
+  if (!parReady) {
 #pragma unroll
-  for (int k = 0; k < kSegK; ++k) {
-    const int p = (k << 10) + tid;
-    if (k < K && p < P) par[p] = bb.label[base + p] == 0 ? p : -1;
+    for (int k = 0; k < kSegK; ++k) {
+      const int p = (k << 10) + tid;
+      if (k < K && p < P) par[p] = bb.label[base + p] == 0 ? p : -1;
+    }
   }
   __syncthreads();
   // unions over the right (wrapping) and down neighbours, four chunks' ranges in flight
@@ -861,6 +889,48 @@ __global__ void __launch_bounds__(1024) k_seg_lds(BatchBufs bb, DevCfg c, int wa
   }
 }
 
+__global__ void __launch_bounds__(1024) k_seg_lds(BatchBufs bb, DevCfg c, int want_labels) {
+  extern __shared__ int par[];  // [P]
+  seg_lds(bb, c, blockIdx.x, want_labels, par, false);
+}
+
+// The whole projection of a VLP-16-class scan (P <= kSegLdsMaxP) by one
+// 1024-thread workgroup, for batches (the launch's other workgroups fill the
+// device): the owner image in LDS (last writer wins by LDS atomicMax, :248),
+// the range image and full cloud (:248-255), the ground walk of each column
+// with the union-find's initial parents (:260-301), then k_seg_lds's
+// segmentation and compaction over the same LDS (:312-367).  Replaces
+// k_project + k_pixels + k_ground + k_seg_lds: no owner image in HBM, three
+// launches fewer, and the later phases read what the earlier ones wrote from
+// the CU's caches.
+constexpr int kIpLdsU = 4;  // points per thread in flight (the projection)
+__global__ void __launch_bounds__(1024) k_ip_lds(BatchBufs bb, DevCfg c, int want_labels) {
+  extern __shared__ int par[];  // [P]: the owner image, then the parents
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int P = c.P, H = c.H, n = scan_npts(bb, b);
+  for (int p = tid; p < P; p += 1024) par[p] = -1;
+  __syncthreads();
+  for (int i0 = tid; i0 < n; i0 += kIpLdsU * 1024) {
+    int pix[kIpLdsU];
+#pragma unroll
+    for (int u = 0; u < kIpLdsU; ++u) {
+      const int i = i0 + u * 1024;
+      pix[u] = i < n ? project_point(bb, c, b, n, i) : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < kIpLdsU; ++u)
+      if (pix[u] >= 0) atomicMax(&par[pix[u]], i0 + u * 1024);
+  }
+  __syncthreads();
+  for (int p = tid; p < P; p += 1024) {
+    const int row = p / H;
+    pixel_out(bb, c, b, row, p - row * H, par[p]);
+  }
+  __syncthreads();  // the pixels' stores are visible to the workgroup: the ground walk reads them
+  for (int j = tid; j < H; j += 1024) ground_column(bb, c, b, j, par);
+  seg_lds(bb, c, b, want_labels, par, true);  // (its first barrier orders the parents)
+}
+
 void launch_gated(const BatchBufs& bb, const DevCfg& c, const GatedBufs& gb, hipStream_t s) {
   const int nCh = (c.P + 1023) / 1024;
   k_gated_flags<<<nCh, 1024, 0, s>>>(bb, c, gb);
@@ -878,6 +948,11 @@ void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hip
   // 0.20 -> 0.16 ms, profiles/r04_ab_node_seg.txt; the same labels, pinned by
   // test_seg_lds_equals_hbm_union_find)
   const bool segLds = seg_lds_ok(c) && B > kSegHbmMaxScans;
+  if (segLds && lo.ipFused) {  // one workgroup per scan, everything in its LDS
+    tm->mark("ip.fused", s);
+    k_ip_lds<<<B, 1024, (size_t)P * sizeof(int), s>>>(bb, c, want_labels);
+    return;
+  }
   // bb.owner is all -1 here: filled at creation, and k_pixels clears what k_project set
   tm->mark("ip.project", s);
   dim3 gpts((bb.Nmax + 255) / 256, B), gpix((P + 255) / 256, B), gcol((c.H + 255) / 256, B);

@@ -206,6 +206,7 @@ struct LaunchOpts {
   int lfvBlockRings = 0;  // ::lfv_block_rings
   int lfvWide = -1;       // ::lfv_wide
   int faSyncCheck = 0;    // ::fa_synccheck
+  int ipFused = 1;        // ::ip_fused
 };
 
 void launch_gated(const BatchBufs& bb, const DevCfg& c, const GatedBufs& gb, hipStream_t s);

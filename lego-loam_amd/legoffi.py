@@ -274,8 +274,8 @@ class CtxOpts(C.Structure):
     _fields_ = [(n, C.c_int32) for n in (
         "size", "node_overlap", "front_parts", "lfv_wave", "lfv_block_rings", "lfv_wide", "ccl_tiles",
         "seg_hbm", "odom_workgroups", "odom_gridless", "odom_integ", "odom_silent_wg", "odom_late_wg",
-        "lf_wait_ms", "mo_cand_cache", "kf_cap", "vg_rounds", "fa_synccheck", "mo_hostprof", "mo_evprof")] + [
-        ("reserved", C.c_int32 * 12)]
+        "lf_wait_ms", "mo_cand_cache", "kf_cap", "vg_rounds", "fa_synccheck", "mo_hostprof", "mo_evprof",
+        "ip_fused")] + [("reserved", C.c_int32 * 11)]
 
 
 # Tooling only (bench.py, scripts/): the A/B scripts switch a context's
@@ -286,7 +286,8 @@ ENV_OPTS = {"LEGO_NODE_OVERLAP": "node_overlap", "LEGO_FRONT_PARTS": "front_part
             "LEGO_ODOM_GRIDLESS": "odom_gridless", "LEGO_ODOM_INTEG": "odom_integ",
             "LEGO_ODOM_SILENT_WG": "odom_silent_wg", "LEGO_ODOM_LATE_WG": "odom_late_wg",
             "LEGO_MO_CAND": "mo_cand_cache", "LEGO_KF_CAP": "kf_cap", "LEGO_VG_ROUNDS": "vg_rounds",
-            "LEGO_FA_SYNCCHECK": "fa_synccheck", "LEGO_MO_HOSTPROF": "mo_hostprof", "LEGO_MO_EVPROF": "mo_evprof"}
+            "LEGO_FA_SYNCCHECK": "fa_synccheck", "LEGO_MO_HOSTPROF": "mo_hostprof", "LEGO_MO_EVPROF": "mo_evprof",
+            "LEGO_IP_FUSED": "ip_fused"}
 
 
 def opts_from_env() -> dict:

@@ -1,14 +1,17 @@
 #!/usr/bin/env python3
-"""Fleet A/B over LEGO_FRONT_PARTS (the front end of a fleet batch in parts of
-whole streams, each on its own HIP stream): one fleet context (bench.py's
-fleet line: 256 VLP-16 streams, seeds 10.., 20 scans per stream per call, two
-calls in flight), the settings alternating in rounds of CALLS calls.  Prints
-scans/s per setting and round.  Diagnostic."""
+"""Fleet A/B over lego_ctx_opts settings: bench.py's fleet line (256 VLP-16
+streams, seeds 10.., 20 scans per stream per call, two calls in flight), one
+context per setting and round (created, warmed by one call, CALLS calls
+timed, closed: two open contexts would share the process's hardware queues),
+the settings alternating over ROUNDS rounds.  Prints scans/s per setting and
+round.  Diagnostic.
+
+  python scripts/fleet_opts_ab.py --settings "ip_fused=1;ip_fused=0"
+"""
 from __future__ import annotations
 
 import argparse
 import json
-import os
 import sys
 import time
 from concurrent.futures import ThreadPoolExecutor
@@ -21,6 +24,10 @@ sys.path.insert(0, str(REPO))
 import bench  # noqa: E402
 
 
+def parse(setting: str) -> dict:
+    return {k: int(v) for k, v in (kv.split("=") for kv in setting.split(",") if kv)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--streams", type=int, default=256)
@@ -28,7 +35,7 @@ def main():
     ap.add_argument("--windows", type=int, default=3)
     ap.add_argument("--calls", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--parts", default="1,2,4")
+    ap.add_argument("--settings", default="ip_fused=1;ip_fused=0")
     args = ap.parse_args()
     import torch
 
@@ -52,22 +59,18 @@ def main():
         wins.append((torch.from_numpy(np.concatenate(scans).view(np.uint8)).to("cuda:0"),
                      torch.from_numpy(off).to("cuda:0"), st))
     del src
-    fl = L.Lego(cfg, device=0, max_points=maxn + 16, max_batch=K, streams=S, opts=L.opts_from_env())
     recs = (L.PoseRec * (S * K))()
-    n = [0]
-
-    def sub():
-        w = wins[n[0] % len(wins)]
-        n[0] += 1
-        fl.submit_device(w[0].data_ptr(), w[1].data_ptr(), w[2], S * K)
-
-    sub()
-    fl.wait(recs)
-    torch.cuda.synchronize()
     for r in range(args.rounds):
-        for p in args.parts.split(","):
-            os.environ["LEGO_FRONT_PARTS"] = p
-            sub()  # the setting's first call, untimed
+        for setting in args.settings.split(";"):
+            fl = L.Lego(cfg, device=0, max_points=maxn + 16, max_batch=K, streams=S, opts=parse(setting))
+            n = [0]
+
+            def sub():
+                w = wins[n[0] % len(wins)]
+                n[0] += 1
+                fl.submit_device(w[0].data_ptr(), w[1].data_ptr(), w[2], S * K)
+
+            sub()  # untimed
             fl.wait(recs)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -78,10 +81,10 @@ def main():
             fl.wait(recs)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
-            print(json.dumps({"round": r, "parts": p, "scans_per_s": round(S * K * args.calls / dt),
+            print(json.dumps({"round": r, "setting": setting, "scans_per_s": round(S * K * args.calls / dt),
                               "ms_per_call": round(dt / args.calls * 1e3, 3),
                               "valid": sum(x.odom_valid for x in recs)}), flush=True)
-    fl.close()
+            fl.close()
 
 
 if __name__ == "__main__":

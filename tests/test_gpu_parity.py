@@ -522,12 +522,13 @@ def test_reset_in_flight(L):
 
 @pytest.mark.parametrize("seed,extra", [(0, {}), (1, {}), (2, {"dup_frac": 0.05})])
 def test_seg_lds_equals_hbm_union_find(L, seed, extra):
-    """VLP-16 batches of more than kSegHbmMaxScans (8) scans are segmented in
-    LDS (k_seg_lds); node calls (one scan) and the seg_hbm option (diagnostic) go
-    through the HBM union-find (k_ccl_* + k_compact) that the larger sensors
-    use (lego_ctx_opts::seg_hbm, diagnostic).  All equal the oracle, clouds and
-    cloud_info byte for byte on 12 consecutive scans (and labels / images
-    through the node calls)."""
+    """VLP-16 batches of more than kSegHbmMaxScans (8) scans are projected and
+    segmented in LDS, by default in one kernel per scan (k_ip_lds), with
+    lego_ctx_opts::ip_fused = 0 by k_project / k_pixels / k_ground + k_seg_lds;
+    node calls (one scan) and the seg_hbm option (diagnostic) go through the
+    HBM union-find (k_ccl_* + k_compact) that the larger sensors use.  All
+    equal the oracle, clouds and cloud_info byte for byte on 12 consecutive
+    scans (and labels / images through the node calls)."""
     sc = L.synth_cfg("VLP-16", seed, **extra)
     scans = [L.synth_scan(sc, k) for k in range(12)]
     ora = L.Oracle(L.sensor_cfg("VLP-16"))
@@ -537,9 +538,9 @@ def test_seg_lds_equals_hbm_union_find(L, seed, extra):
     offs = np.concatenate([[0], np.cumsum([len(p) for p, _ in scans])]).astype(np.int64)
     stamps = np.array([s for _, s in scans], dtype=np.float64)
     outs = {}
-    for mode in ("lds", "hbm"):
+    for mode in ("lds", "lds4", "hbm"):
         gpu = L.Lego(L.sensor_cfg("VLP-16", L.hip_lib()), max_points=cap, max_batch=len(scans),
-                     opts={"seg_hbm": int(mode == "hbm")})
+                     opts={"seg_hbm": int(mode == "hbm"), "ip_fused": int(mode == "lds")})
         gpu.odom_batch(pts, offs, stamps)
         outs[mode] = [gpu.batch_fetch(k)[0] for k in range(len(scans))]
         gpu.close()
@@ -548,5 +549,6 @@ def test_seg_lds_equals_hbm_union_find(L, seed, extra):
     node.close()
     for k in range(len(scans)):
         assert_ip_equal(outs["lds"][k], ref[k], images=False)
+        assert_ip_equal(outs["lds4"][k], ref[k], images=False)
         assert_ip_equal(outs["hbm"][k], ref[k], images=False)
         assert_ip_equal(outs["node"][k], ref[k])
