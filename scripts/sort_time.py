@@ -1,7 +1,8 @@
 """Per-ring time of the device's VoxelGrid block sort (GPU box): every ring of
 tests/golden/dense_ring_keys.npz (VLS-128 seed 3 scan 0, HDL-64E seed 2 scan 0)
-through lego_sort_permutation in the mode k_lf_voxel's node form runs (8: the
-LDS-id form, 1024 threads, sum order) and mode 7 (the same, exact order), host
+and C2 scan 465's rings (c2_ring_keys.npz) through lego_sort_permutation in
+the modes given (default 8,7: the LDS-id form, 1024 threads, sum order / exact,
+k_lf_voxel's node form), host
 wall clock per call minus the call's floor (a 2-key sort), min of 5.  Prints
 the slowest rings with their heap-sorted piece counts.  Diagnostic."""
 import os
@@ -14,7 +15,9 @@ R = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path.insert(0, os.path.join(R, "lego-loam_amd"))
 import legoffi as L  # noqa: E402
 
-d = np.load(os.path.join(R, "tests/golden/dense_ring_keys.npz"))
+MODES = [int(m) for m in (sys.argv[1] if len(sys.argv) > 1 else "8,7").split(",")]
+d = dict(np.load(os.path.join(R, "tests/golden/dense_ring_keys.npz")))
+d.update({"c2:" + k: v for k, v in np.load(os.path.join(R, "tests/golden/c2_ring_keys.npz")).items()})
 g = L.Lego(L.sensor_cfg("VLS-128", L.hip_lib()), max_points=4096, opts=L.opts_from_env())
 
 
@@ -27,11 +30,11 @@ def t(keys, mode):
     return best * 1e6, heap
 
 
-floor = min(t(np.array([2, 1], np.uint32), m)[0] for m in (7, 8))
+floor = min(t(np.array([2, 1], np.uint32), m)[0] for m in MODES)
 print(f"call floor {floor:.1f} us")
-for mode in (8, 7):
+for mode in MODES:
     rows = []
-    for k in d.files:
+    for k in d:
         us, heap = t(d[k], mode)
         rows.append((us - floor, k, len(d[k]), heap))
     rows.sort(reverse=True)
