@@ -861,7 +861,7 @@ static int run_ip(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offse
   // rejected above launched nothing and leaves it valid.
   ++x->devGen;
   x->lastBatch = false;
-  HIPCHK(hipMemsetAsync(bb.bad, 0, sizeof(int) * B, x->stream));
+  if (!ip_clears_bad(x->dc, B, x->lo)) HIPCHK(hipMemsetAsync(bb.bad, 0, sizeof(int) * B, x->stream));
   if (gated && !x->gb.n) {
     const size_t P = x->dc.P;
 #define MA(ptr, n) \
@@ -941,7 +941,10 @@ static int submit_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t*
   StageTimer& tm = x->stm[h];
   StageTimer& otm = x->sotm[h];
   tm.enabled = otm.enabled = x->tm.enabled;
-  HIPCHK(hipMemsetAsync(bb.bad, 0, sizeof(int) * B, x->stream));
+  const int parts = front_parts(x, S);
+  // k_ip_lds clears its scans' words itself: no fill queued behind the
+  // previous batch's odometry, whose workgroups hold every CU's registers
+  if (!ip_clears_bad(x->dc, B / parts, x->lo)) HIPCHK(hipMemsetAsync(bb.bad, 0, sizeof(int) * B, x->stream));
   bb.xprof = x->profOn ? x->d_prof + 32 : nullptr;
   tm.begin();
   otm.begin();
@@ -949,7 +952,6 @@ static int submit_batch(lego_ctx* x, const lego_point_xyzir* pts, const int64_t*
   // and extraction in parts of whole streams (the batch is stream-major), on
   // HIP streams of their own, so that one part's LDS-bound kernels
   // (segmentation, VoxelGrids) share the CUs with another's HBM-bound ones
-  const int parts = front_parts(x, S);
   if (parts > 1) {
     st = front_streams(x, parts);
     if (st != LEGO_OK) return st;

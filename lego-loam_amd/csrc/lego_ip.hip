@@ -908,6 +908,7 @@ __global__ void __launch_bounds__(1024) k_ip_lds(BatchBufs bb, DevCfg c, int wan
   extern __shared__ int par[];  // [P]: the owner image, then the parents
   const int b = blockIdx.x, tid = threadIdx.x;
   const int P = c.P, H = c.H, n = scan_npts(bb, b);
+  if (tid == 0) bb.bad[b] = 0;  // before the barrier: the projection may set kBadNotDense (ip_clears_bad)
   for (int p = tid; p < P; p += 1024) par[p] = -1;
   __syncthreads();
   for (int i0 = tid; i0 < n; i0 += kIpLdsU * 1024) {
@@ -922,9 +923,16 @@ __global__ void __launch_bounds__(1024) k_ip_lds(BatchBufs bb, DevCfg c, int wan
       if (pix[u] >= 0) atomicMax(&par[pix[u]], i0 + u * 1024);
   }
   __syncthreads();
-  for (int p = tid; p < P; p += 1024) {
-    const int row = p / H;
-    pixel_out(bb, c, b, row, p - row * H, par[p]);
+  // the pixels by (64-column block, row), a wave per pair: the waves of rows
+  // 4q .. 4q + 3 at the same columns gather the owners from the same 128-B
+  // lines of the firing-ordered input (k_pixels' mapping), instead of a wave
+  // per 64 row-major pixels touching 64 lines for one record each
+  {
+    const int N = c.N, nq = N * ((H + 63) >> 6);
+    for (int q = tid >> 6; q < nq; q += 16) {
+      const int row = q % N, col = (q / N) * 64 + (tid & 63);
+      if (col < H) pixel_out(bb, c, b, row, col, par[row * H + col]);
+    }
   }
   __syncthreads();  // the pixels' stores are visible to the workgroup: the ground walk reads them
   for (int j = tid; j < H; j += 1024) ground_column(bb, c, b, j, par);
@@ -938,6 +946,10 @@ void launch_gated(const BatchBufs& bb, const DevCfg& c, const GatedBufs& gb, hip
   k_gated_write<<<nCh, 1024, 0, s>>>(bb, c, gb);
 }
 
+bool ip_clears_bad(const DevCfg& c, int B, const LaunchOpts& lo) {
+  return seg_lds_ok(c) && B > kSegHbmMaxScans && lo.ipFused;
+}
+
 void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hipStream_t s,
                StageTimer* tm, const LaunchOpts& lo) {
   const int P = c.P;
@@ -948,7 +960,7 @@ void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hip
   // 0.20 -> 0.16 ms, profiles/r04_ab_node_seg.txt; the same labels, pinned by
   // test_seg_lds_equals_hbm_union_find)
   const bool segLds = seg_lds_ok(c) && B > kSegHbmMaxScans;
-  if (segLds && lo.ipFused) {  // one workgroup per scan, everything in its LDS
+  if (ip_clears_bad(c, B, lo)) {  // one workgroup per scan, everything in its LDS
     tm->mark("ip.fused", s);
     k_ip_lds<<<B, 1024, (size_t)P * sizeof(int), s>>>(bb, c, want_labels);
     return;

@@ -212,6 +212,9 @@ struct LaunchOpts {
 void launch_gated(const BatchBufs& bb, const DevCfg& c, const GatedBufs& gb, hipStream_t s);
 void launch_ip(const BatchBufs& bb, const DevCfg& c, int B, int want_labels, hipStream_t s,
                StageTimer* tm, const LaunchOpts& lo);
+// launch_ip of B scans takes k_ip_lds, which clears each scan's bb.bad word
+// itself (the caller's fill of bb.bad is then redundant)
+bool ip_clears_bad(const DevCfg& c, int B, const LaunchOpts& lo);
 // B = S x K scans, stream-major (scans [s*K, s*K + K) are stream s's, in
 // order); d_carry[S].
 // side (node calls, B = 1): the per-ring less-flat VoxelGrid and its

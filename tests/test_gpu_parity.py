@@ -191,6 +191,48 @@ def test_batch_argument_checks(L):
     gpu.close()
 
 
+def test_fused_batch_not_dense_word(L):
+    """Batches of more than 8 VLP-16 scans take k_ip_lds, which clears each
+    scan's error word itself (no fill before the batch): a non-finite point in
+    scan 10 is LEGO_E_NOT_DENSE naming that scan, and after lego_reset clean
+    batches through both slots succeed and equal a fresh context's records."""
+    import torch
+
+    cfg = L.sensor_cfg("VLP-16", L.hip_lib())
+    sc = L.synth_cfg("VLP-16", 4)
+    K = 12
+    scans = [L.synth_scan(sc, j) for j in range(3 * K)]
+    maxn = max(len(p) for p, _ in scans) + 16
+
+    def batch(lo):
+        pts = np.concatenate([p for p, _ in scans[lo:lo + K]])
+        off = np.zeros(K + 1, np.int64)
+        off[1:] = np.cumsum([len(p) for p, _ in scans[lo:lo + K]])
+        return pts, off, np.array([s for _, s in scans[lo:lo + K]])
+
+    def call(g, pts, off, st, recs):
+        dp = torch.from_numpy(pts.view(np.uint8)).cuda()
+        do = torch.from_numpy(off).cuda()
+        return g.lib.lego_odom_batch(g.h, dp.data_ptr(), do.data_ptr(), st.ctypes.data, K, 1, recs)
+
+    gpu = L.Lego(cfg, max_points=maxn, max_batch=K)
+    ref = L.Lego(cfg, max_points=maxn, max_batch=K)
+    recs, rref = (L.PoseRec * K)(), (L.PoseRec * K)()
+    pts, off, st = batch(0)
+    bad = pts.copy()
+    bad["x"][off[10] + 5] = np.nan
+    assert call(gpu, bad, off, st, recs) == L.LEGO_E_NOT_DENSE
+    assert "scan 10" in gpu.lib.lego_last_error().decode()
+    gpu.reset()
+    for w in range(3):
+        pts, off, st = batch(w * K)
+        assert call(gpu, pts, off, st, recs) == L.LEGO_OK, gpu.lib.lego_last_error()
+        assert call(ref, pts, off, st, rref) == L.LEGO_OK
+        assert bytes(recs) == bytes(rref), w
+    gpu.close()
+    ref.close()
+
+
 @pytest.mark.parametrize("sensor,seed,nscans,n_surf,n_corner", [
     ("VLP-16", 3, 14, 200000, 40000),
 ])
