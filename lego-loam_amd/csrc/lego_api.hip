@@ -169,6 +169,7 @@ struct lego_ctx {
   PackedRec* d_pack = nullptr;  // h_pack's device address: k_pack_recs writes the records there
   PackedRec* h_pack = nullptr;  // pinned
   int64_t* h_offp = nullptr;    // pinned [maxBatch + 1]: device offsets read back for validation
+  float4* h_stage = nullptr;  // pinned [maxPoints] packed points, created by the first host-buffer node call
   OdomState* h_resetSt = nullptr;   // pinned [S]: construction state (ctx_reset)
   FaCarry* h_resetCarry = nullptr;  // pinned [S]
   Fusion fusion;  // transformFusion state
@@ -229,6 +230,7 @@ struct lego_ctx {
     if (d_handoff) (void)hipFree(d_handoff);
     if (h_pack) (void)hipHostFree(h_pack);
     if (h_offp) (void)hipHostFree(h_offp);
+    if (h_stage) (void)hipHostFree(h_stage);
     if (h_resetSt) (void)hipHostFree(h_resetSt);
     if (h_resetCarry) (void)hipHostFree(h_resetCarry);
     if (hostBlock) (void)hipHostFree(hostBlock);
@@ -791,7 +793,7 @@ static OdomBufs ob_slice(const OdomBufs& a, const DevCfg& c, int c0, int s0, int
 // node: the caller synchronises before returning (run_ip), so the offsets may
 // go through the pinned h_offp
 static int stage_inputs(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offsets, int B,
-                        int on_device, BatchBufs& bb, bool node = false) {
+                        int on_device, BatchBufs& bb, bool node = false, bool staged = false) {
   HIPCHK(hipSetDevice(x->device));
   // Per-scan sizes are validated on the host in both modes: an empty scan is
   // undefined upstream (findStartEndAngle reads points[0] and points[size-1],
@@ -826,15 +828,17 @@ static int stage_inputs(lego_ctx* x, const lego_point_xyzir* pts, const int64_t*
     if (total > (int64_t)x->maxPoints * x->maxBatch) return LEGO_E_CAPACITY;
     const int64_t base = off[0];
     for (int k = 0; k <= B; ++k) off[k] -= base;
-    HIPCHK(hipMemcpyAsync(x->d_pts, pts + base, sizeof(lego_point_xyzir) * total,
-                          hipMemcpyHostToDevice, x->stream));
+    if (!staged)  // (staged: upload_checked already queued the points' copies on x->stream)
+      HIPCHK(hipMemcpyAsync(x->d_pts, pts + base, sizeof(lego_point_xyzir) * total,
+                            hipMemcpyHostToDevice, x->stream));
     if (node) {  // pinned: an asynchronous copy (a pageable source is a synchronous staged one)
       for (int k = 0; k <= B; ++k) x->h_offp[k] = off[k];
       HIPCHK(hipMemcpyAsync(x->d_off, x->h_offp, sizeof(int64_t) * (B + 1), hipMemcpyHostToDevice, x->stream));
     } else {
       HIPCHK(hipMemcpyAsync(x->d_off, off.data(), sizeof(int64_t) * (B + 1), hipMemcpyHostToDevice, x->stream));
     }
-    bb.pts = x->d_pts;
+    // staged: the packed form (bit 0 of the pointer, pts_view in lego_ip.hip)
+    bb.pts = staged ? (const void*)((uintptr_t)x->d_pts | 1) : (const void*)x->d_pts;
     bb.off = x->d_off;
   }
   bb.Nmax = mx;
@@ -846,14 +850,14 @@ static int fetch_ip(lego_ctx* x, int k, bool images, lego_ip_out* o, bool gated 
 // Image projection only (lego_ip_process*): slot 0, synchronous; scan 0's
 // outputs are fetched into *out with the batch's not-dense flags (one sync).
 static int run_ip(lego_ctx* x, const lego_point_xyzir* pts, const int64_t* offsets, int B, int on_device,
-                  bool images, lego_ip_out* out, bool gated = false) {
+                  bool images, lego_ip_out* out, bool gated = false, bool staged = false) {
   const int want_labels = images ? 1 : 0;
   if (x->inflight) {
     set_err("node-shaped call while batches are in flight (lego_odom_batch_wait first)");
     return LEGO_E_STATE;
   }
   BatchBufs bb = x->bb;
-  int st = stage_inputs(x, pts, offsets, B, on_device, bb, true);
+  int st = stage_inputs(x, pts, offsets, B, on_device, bb, true, staged);
   if (st != LEGO_OK) return st;
   // this launch writes slot 0 (the outlier cloud among it): a resident
   // hand-off of an earlier lego_fa_process is stale from here on
@@ -1235,29 +1239,64 @@ static int fetch_fa(lego_ctx* x, int k, lego_fa_out* o, bool withXerr = false) {
   return LEGO_OK;
 }
 
-int lego_ip_process(lego_ctx* x, const lego_point_xyzir* pts, int32_t n, double stamp,
-                    uint32_t flags, lego_ip_out* out) {
-  if (!x || !pts || !out || n <= 0) return LEGO_E_ARG;
-  if (n > x->maxPoints) return LEGO_E_CAPACITY;
-  if (x->dc.ringRow) {  // dense check (imageProjection.cpp:174): an all-ones exponent is inf / nan;
-                         // accumulated without branches so the loop vectorises.  Without
-                         // useCloudRing k_project drops such points (:170).
-    uint32_t nonfinite = 0;
-    for (int i = 0; i < n; ++i) {
+// The node call's upload of a host cloud (lego_ip_process): one pass over
+// the caller's records packs them (x, y, z, ring: the 16 bytes the
+// projection reads of each 32-byte record) into the context's pinned staging
+// buffer and accumulates the dense check (imageProjection.cpp:174; an all-ones
+// exponent is inf / nan, branch-free so the loop vectorises), chunk by chunk,
+// each chunk's DMA to x->d_pts queued as soon as it is staged, so the copy
+// engine works beside the next chunk's pass.  It replaces a separate check
+// pass plus the runtime's staged copy of pageable memory: VLS-128's 7.4 MB
+// were read twice and all of them crossed PCIe.  A non-dense cloud (with use_cloud_ring) is refused here,
+// before any kernel: nothing but d_pts has changed.  Without useCloudRing
+// k_project drops such points (:170).
+static int upload_checked(lego_ctx* x, const lego_point_xyzir* pts, int32_t n) {
+  HIPCHK(hipSetDevice(x->device));
+  static_assert(sizeof(float4) * 2 == sizeof(lego_point_xyzir), "the packed form fits d_pts");
+  if (!x->h_stage &&
+      hipHostMalloc((void**)&x->h_stage, sizeof(float4) * (size_t)x->maxPoints, hipHostMallocDefault) != hipSuccess) {
+    x->h_stage = nullptr;
+    set_err("hipHostMalloc failed for the node call's staging buffer");
+    return LEGO_E_DEVICE;
+  }
+  constexpr int kChunk = 32768;  // points (512 KB packed)
+  float4* d = (float4*)x->d_pts;
+  uint32_t nonfinite = 0;
+  for (int c0 = 0; c0 < n; c0 += kChunk) {
+    const int c1 = std::min(n, c0 + kChunk);
+    for (int i = c0; i < c1; ++i) {
       uint32_t u[3];
       std::memcpy(u, &pts[i].x, sizeof(u));
       nonfinite |= (uint32_t)((u[0] & 0x7f800000u) == 0x7f800000u) | (uint32_t)((u[1] & 0x7f800000u) == 0x7f800000u) |
                    (uint32_t)((u[2] & 0x7f800000u) == 0x7f800000u);
+      const uint32_t w[4] = {u[0], u[1], u[2], (uint32_t)pts[i].ring};
+      std::memcpy(&x->h_stage[i], w, sizeof(w));
     }
-    if (nonfinite) {
-      set_err("the cloud has non-finite xyz (it must be dense with use_cloud_ring)");
-      return LEGO_E_NOT_DENSE;
-    }
+    HIPCHK(hipMemcpyAsync(d + c0, x->h_stage + c0, sizeof(float4) * (size_t)(c1 - c0), hipMemcpyHostToDevice,
+                          x->stream));
   }
+  if (nonfinite && x->dc.ringRow) {
+    HIPCHK(hipStreamSynchronize(x->stream));  // the staging buffer is free again when this returns
+    set_err("the cloud has non-finite xyz (it must be dense with use_cloud_ring)");
+    return LEGO_E_NOT_DENSE;
+  }
+  return LEGO_OK;
+}
+
+int lego_ip_process(lego_ctx* x, const lego_point_xyzir* pts, int32_t n, double stamp,
+                    uint32_t flags, lego_ip_out* out) {
+  if (!x || !pts || !out || n <= 0) return LEGO_E_ARG;
+  if (n > x->maxPoints) return LEGO_E_CAPACITY;
+  if (x->inflight) {
+    set_err("node-shaped call while batches are in flight (lego_odom_batch_wait first)");
+    return LEGO_E_STATE;
+  }
+  const int up = upload_checked(x, pts, n);
+  if (up != LEGO_OK) return up;
   int64_t off[2] = {0, n};
   x->stamps.assign(1, stamp);
   const bool gated = (flags & LEGO_IP_GATED) != 0;
-  const int st = run_ip(x, pts, off, 1, 0, (flags & LEGO_IP_IMAGES) != 0, out, gated);
+  const int st = run_ip(x, pts, off, 1, 0, (flags & LEGO_IP_IMAGES) != 0, out, gated, true);
   if (st != LEGO_OK) return st;
   x->lastIp = *out;
   x->lastIpDevice = true;

@@ -116,7 +116,7 @@ struct BatchBufs {
   ImuScan* imuScan;          // [B]
   int Nmax;                  // max input points per scan
   // ---- image projection
-  const void* pts;           // lego_point_xyzir [*]
+  const void* pts;           // lego_point_xyzir [*], or with bit 0 set the node call's packed float4 [*] (pts_view)
   const int64_t* off;        // [B+1]
   int* owner;                // [B*P]
   float* range;              // [B*P]

@@ -39,11 +39,26 @@ __device__ __forceinline__ bool xyz_finite(const float4& p) {
 // scan's first / last point, and the non-dense flag.  k_project (one lane per
 // point, the owner image in HBM) and k_ip_lds (one workgroup per scan, the
 // owner image in LDS) share it.
+// Scan b's points: the caller's XYZIR records (32 B), or, with bit 0 of
+// bb.pts set, the node call's packed form (16 B: x, y, z and the ring's bits
+// in the fourth word; upload_checked in lego_api.hip).
+struct PtsView {
+  const unsigned char* base;
+  bool packed;
+  __device__ __forceinline__ float4 xyz(int i) const {
+    return *(const float4*)(base + (size_t)i * (packed ? 16 : 32));
+  }
+};
+__device__ __forceinline__ PtsView pts_view(const BatchBufs& bb, int b) {
+  const uintptr_t a = (uintptr_t)bb.pts;
+  const bool packed = (a & 1) != 0;
+  return PtsView{(const unsigned char*)(a & ~(uintptr_t)1) + (size_t)bb.off[b] * (packed ? 16 : 32), packed};
+}
+
 __device__ __forceinline__ int project_point(const BatchBufs& bb, const DevCfg& c, int b, int n, int i) {
-  const lego_point_xyzir* p0 = (const lego_point_xyzir*)bb.pts + bb.off[b];
-  const lego_point_xyzir* pp = p0 + i;
-  const float4 xyz = *(const float4*)pp;
-  const uint16_t ring = pp->ring;
+  const PtsView pv = pts_view(bb, b);
+  const float4 xyz = pv.xyz(i);
+  const uint16_t ring = pv.packed ? (uint16_t)__float_as_uint(xyz.w) : ((const lego_point_xyzir*)pv.base + i)->ring;
   const float x = xyz.x, y = xyz.y, z = xyz.z;
   if (!xyz_finite(xyz)) {
     if (c.ringRow) {
@@ -56,19 +71,19 @@ __device__ __forceinline__ int project_point(const BatchBufs& bb, const DevCfg& 
     // (the walk is as long as the run of non-finite points at that end).
     if (i == 0) {
       int k = 1;
-      while (k < n && !xyz_finite(*(const float4*)(p0 + k))) ++k;
+      while (k < n && !xyz_finite(pv.xyz(k))) ++k;
       if (k == n) {
         bb.bad[b] = kBadNotDense;  // no finite point: points[0] of an empty cloud (UB upstream)
         return -1;
       }
-      const float4 q = *(const float4*)(p0 + k);
+      const float4 q = pv.xyz(k);
       bb.rawang[2 * b] = -lego_atan2f(q.y, q.x);
     }
     if (i == n - 1) {
       int k = n - 2;
-      while (k >= 0 && !xyz_finite(*(const float4*)(p0 + k))) --k;
+      while (k >= 0 && !xyz_finite(pv.xyz(k))) --k;
       if (k >= 0) {
-        const float4 q = *(const float4*)(p0 + k);
+        const float4 q = pv.xyz(k);
         bb.rawang[2 * b + 1] = -lego_atan2f(q.y, q.x);
       }
     }
@@ -122,7 +137,7 @@ __device__ __forceinline__ void pixel_out(const BatchBufs& bb, const DevCfg& c, 
     bb.full[gp] = make_float4(qn, qn, qn, -1.0f);
     return;
   }
-  const float4 xyz = *(const float4*)((const lego_point_xyzir*)bb.pts + bb.off[b] + o);
+  const float4 xyz = pts_view(bb, b).xyz(o);
   const float range = __builtin_sqrtf(xyz.x * xyz.x + xyz.y * xyz.y + xyz.z * xyz.z);
   const float inten = (float)((double)(float)row + (double)(float)col / 10000.0);  // :250
   bb.range[gp] = range;
