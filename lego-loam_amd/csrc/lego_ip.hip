@@ -30,6 +30,29 @@
 
 namespace lego {
 
+// Diagnostic build (IP_PROF=1, scripts/ip_phase.sh): thread 0 of every
+// k_ip_lds workgroup adds the clock64 ticks between its phase barriers to
+// g_ipprof (lego_ip_profile reads and clears them).  No effect otherwise.
+#ifndef IP_PROF
+#define IP_PROF 0
+#endif
+#if IP_PROF
+constexpr int kIpProf = 12;  // [0, 10): phases, 11: workgroups
+__device__ unsigned long long g_ipprof[kIpProf];
+#define IP_T0() unsigned long long ipt_ = threadIdx.x == 0 ? (unsigned long long)clock64() : 0ull
+#define IP_STAMP(k)                                                      \
+  do {                                                                   \
+    if (threadIdx.x == 0) {                                              \
+      const unsigned long long n_ = clock64();                           \
+      atomicAdd(&g_ipprof[k], n_ - ipt_);                                \
+      ipt_ = n_;                                                         \
+    }                                                                    \
+  } while (0)
+#else
+#define IP_T0() (void)0
+#define IP_STAMP(k) (void)0
+#endif
+
 __device__ __forceinline__ bool xyz_finite(const float4& p) {
   return __builtin_isfinite(p.x) && __builtin_isfinite(p.y) && __builtin_isfinite(p.z);
 }
@@ -172,8 +195,11 @@ __global__ void __launch_bounds__(256) k_pixels(BatchBufs bb, DevCfg c) {
 // single VLP-16 scan, 16 dependent rows).
 constexpr int kGroundRows = 8;
 // Column j of scan b; par (k_ip_lds): the union-find's initial parents of
-// the column's pixels in LDS as well (p for an unlabelled pixel, else -1).
-__device__ __forceinline__ void ground_column(const BatchBufs& bb, const DevCfg& c, int b, int j, int* par) {
+// the column's pixels in LDS as well (p for an unlabelled pixel, else -1);
+// labels: also the label image's initial values (the HBM union-find reads
+// them; k_ip_lds needs them only when the label image is an output).
+__device__ __forceinline__ void ground_column(const BatchBufs& bb, const DevCfg& c, int b, int j, int* par,
+                                              bool labels = true) {
   const size_t base = (size_t)b * c.P;
   int cur = 0;  // value G[i] holds before pair i is examined
   for (int i0 = 0; i0 < c.N; i0 += kGroundRows) {
@@ -213,7 +239,7 @@ __device__ __forceinline__ void ground_column(const BatchBufs& bb, const DevCfg&
       const size_t gp = base + i * c.H + j;
       const bool lab = G == 1 || rg[u] == FLT_MAX;
       bb.ground[gp] = (int8_t)G;
-      bb.label[gp] = lab ? -1 : 0;     // :295-301
+      if (labels) bb.label[gp] = lab ? -1 : 0;  // :295-301
       if (par) par[i * c.H + j] = lab ? -1 : i * c.H + j;
     }
   }
@@ -737,6 +763,7 @@ __device__ __forceinline__ void seg_lds(const BatchBufs& bb, const DevCfg& c, in
   const int P = c.P, H = c.H, K = (P + 1023) >> 10;
   volatile int* vpar = par;
   const TanBand tb = seg_tan_band(c);
+  IP_T0();
   // pixel k * 1024 + tid of chunk k: loads coalesced, chunk-ordered
   if (!parReady) {
 #pragma unroll
@@ -746,6 +773,7 @@ __device__ __forceinline__ void seg_lds(const BatchBufs& bb, const DevCfg& c, in
     }
   }
   __syncthreads();
+  IP_STAMP(3);  // (k_ip_lds: the ground walk and the parents)
   // unions over the right (wrapping) and down neighbours, four chunks' ranges in flight
   for (int k0 = 0; k0 < K; k0 += 4) {
     float rp[4], rr_[4], rd[4];
@@ -774,6 +802,7 @@ __device__ __forceinline__ void seg_lds(const BatchBufs& bb, const DevCfg& c, in
     }
   }
   __syncthreads();
+  IP_STAMP(4);
   int rt[kSegK];  // each pixel's root (-1: not a candidate), in registers
 #pragma unroll
   for (int k = 0; k < kSegK; ++k) {
@@ -795,6 +824,7 @@ __device__ __forceinline__ void seg_lds(const BatchBufs& bb, const DevCfg& c, in
     if (rt[k] != p) atomicOr(&par[rt[k]], 1 << (15 + p / H));
   }
   __syncthreads();
+  IP_STAMP(5);
   // flags per chunk: kept in the segmented cloud, outlier, valid root; the
   // waves' counts per chunk into wpre
   unsigned mkeep = 0, mout = 0, mroot = 0;
@@ -837,6 +867,7 @@ __device__ __forceinline__ void seg_lds(const BatchBufs& bb, const DevCfg& c, in
     }
   }
   __syncthreads();
+  IP_STAMP(6);
   const int nw = blockDim.x >> 6;
   if (tid < 3 * K) {  // per (chunk, flag): the waves' exclusive prefix, the chunk's total
     const int k = tid / 3, f = tid - 3 * k;
@@ -858,6 +889,7 @@ __device__ __forceinline__ void seg_lds(const BatchBufs& bb, const DevCfg& c, in
     }
   }
   __syncthreads();
+  IP_STAMP(7);
   // outputs at their ordered positions (cloudSegmentation :318-357)
   const unsigned long long lt = (1ull << lane) - 1;
   for (int k = 0; k < K; ++k) {
@@ -902,6 +934,7 @@ __device__ __forceinline__ void seg_lds(const BatchBufs& bb, const DevCfg& c, in
     bb.orient[3 * b + 1] = eo;
     bb.orient[3 * b + 2] = eo - so;
   }
+  IP_STAMP(8);
 }
 
 __global__ void __launch_bounds__(1024) k_seg_lds(BatchBufs bb, DevCfg c, int want_labels) {
@@ -924,8 +957,10 @@ __global__ void __launch_bounds__(1024) k_ip_lds(BatchBufs bb, DevCfg c, int wan
   const int b = blockIdx.x, tid = threadIdx.x;
   const int P = c.P, H = c.H, n = scan_npts(bb, b);
   if (tid == 0) bb.bad[b] = 0;  // before the barrier: the projection may set kBadNotDense (ip_clears_bad)
+  IP_T0();
   for (int p = tid; p < P; p += 1024) par[p] = -1;
   __syncthreads();
+  IP_STAMP(0);
   for (int i0 = tid; i0 < n; i0 += kIpLdsU * 1024) {
     int pix[kIpLdsU];
 #pragma unroll
@@ -938,6 +973,7 @@ __global__ void __launch_bounds__(1024) k_ip_lds(BatchBufs bb, DevCfg c, int wan
       if (pix[u] >= 0) atomicMax(&par[pix[u]], i0 + u * 1024);
   }
   __syncthreads();
+  IP_STAMP(1);
   // the pixels by (64-column block, row), a wave per pair: the waves of rows
   // 4q .. 4q + 3 at the same columns gather the owners from the same 128-B
   // lines of the firing-ordered input (k_pixels' mapping), instead of a wave
@@ -950,9 +986,24 @@ __global__ void __launch_bounds__(1024) k_ip_lds(BatchBufs bb, DevCfg c, int wan
     }
   }
   __syncthreads();  // the pixels' stores are visible to the workgroup: the ground walk reads them
-  for (int j = tid; j < H; j += 1024) ground_column(bb, c, b, j, par);
+  IP_STAMP(2);
+#if IP_PROF
+  if (tid == 0) atomicAdd(&g_ipprof[11], 1ull);
+#endif
+  for (int j = tid; j < H; j += 1024) ground_column(bb, c, b, j, par, want_labels != 0);
   seg_lds(bb, c, b, want_labels, par, true);  // (its first barrier orders the parents)
 }
+
+#if IP_PROF
+}  // namespace lego
+extern "C" int lego_ip_profile(unsigned long long* out) {  // diagnostic build only: read and clear
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lego::g_ipprof), sizeof(unsigned long long) * lego::kIpProf) != hipSuccess)
+    return -1;
+  static const unsigned long long zero[lego::kIpProf] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(lego::g_ipprof), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+namespace lego {
+#endif
 
 void launch_gated(const BatchBufs& bb, const DevCfg& c, const GatedBufs& gb, hipStream_t s) {
   const int nCh = (c.P + 1023) / 1024;
