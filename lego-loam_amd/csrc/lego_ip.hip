@@ -151,8 +151,9 @@ __global__ void k_project(BatchBufs bb, DevCfg c) {
 }
 
 // A pixel of the range image and the full cloud (:248-255) from its owner
-// point o (-1: none).
-__device__ __forceinline__ void pixel_out(const BatchBufs& bb, const DevCfg& c, int b, int row, int col, int o) {
+// point o (-1: none) and that point's coordinates.
+__device__ __forceinline__ void pixel_store(const BatchBufs& bb, const DevCfg& c, int b, int row, int col, int o,
+                                            float4 xyz) {
   const size_t gp = (size_t)b * c.P + row * c.H + col;
   if (o < 0) {
     bb.range[gp] = FLT_MAX;
@@ -160,11 +161,13 @@ __device__ __forceinline__ void pixel_out(const BatchBufs& bb, const DevCfg& c, 
     bb.full[gp] = make_float4(qn, qn, qn, -1.0f);
     return;
   }
-  const float4 xyz = pts_view(bb, b).xyz(o);
   const float range = __builtin_sqrtf(xyz.x * xyz.x + xyz.y * xyz.y + xyz.z * xyz.z);
   const float inten = (float)((double)(float)row + (double)(float)col / 10000.0);  // :250
   bb.range[gp] = range;
   bb.full[gp] = make_float4(xyz.x, xyz.y, xyz.z, inten);
+}
+__device__ __forceinline__ void pixel_out(const BatchBufs& bb, const DevCfg& c, int b, int row, int col, int o) {
+  pixel_store(bb, c, b, row, col, o, o >= 0 ? pts_view(bb, b).xyz(o) : make_float4(0.f, 0.f, 0.f, 0.f));
 }
 
 // One workgroup per 4 rows x 64 columns (a wave per row): the stores stay
@@ -195,7 +198,8 @@ __global__ void __launch_bounds__(256) k_pixels(BatchBufs bb, DevCfg c) {
 // single VLP-16 scan, 16 dependent rows).
 constexpr int kGroundRows = 8;
 // Column j of scan b; par (k_ip_lds): the union-find's initial parents of
-// the column's pixels in LDS as well (p for an unlabelled pixel, else -1);
+// the column's pixels in LDS as well (p for an unlabelled pixel, -2 for a
+// ground one, else -1);
 // labels: also the label image's initial values (the HBM union-find reads
 // them; k_ip_lds needs them only when the label image is an output).
 __device__ __forceinline__ void ground_column(const BatchBufs& bb, const DevCfg& c, int b, int j, int* par,
@@ -240,7 +244,9 @@ __device__ __forceinline__ void ground_column(const BatchBufs& bb, const DevCfg&
       const bool lab = G == 1 || rg[u] == FLT_MAX;
       bb.ground[gp] = (int8_t)G;
       if (labels) bb.label[gp] = lab ? -1 : 0;  // :295-301
-      if (par) par[i * c.H + j] = lab ? -1 : i * c.H + j;
+      // k_ip_lds's parents: -2 for a ground pixel (G == 1), -1 for another
+      // labelled one, so the segmentation knows the ground without the image
+      if (par) par[i * c.H + j] = lab ? (G == 1 ? -2 : -1) : i * c.H + j;
     }
   }
 }
@@ -747,6 +753,7 @@ __global__ void __launch_bounds__(1024) k_gated_write(BatchBufs bb, DevCfg c, Ga
 constexpr int kSegLdsMaxP = 32767;  // counts fit 15 bits; 128 KB of parents
 constexpr int kSegLdsMaxN = 16;     // the row mask fits 16 bits
 constexpr int kSegK = (kSegLdsMaxP + 1023) / 1024;  // 1024-pixel chunks per scan
+constexpr int kSegOutU = 2;                          // chunks per round of the output pass
 constexpr int kSegHbmMaxScans = 8;  // launches of up to this many scans segment in HBM (launch_ip)
 bool seg_lds_ok(const DevCfg& c) { return c.N <= kSegLdsMaxN && c.P <= kSegLdsMaxP && !c.segHbm; }
 
@@ -807,7 +814,9 @@ __device__ __forceinline__ void seg_lds(const BatchBufs& bb, const DevCfg& c, in
 #pragma unroll
   for (int k = 0; k < kSegK; ++k) {
     const int p = (k << 10) + tid;
-    rt[k] = (k < K && p < P && vpar[p] >= 0) ? lds_find(vpar, p) : -1;
+    // parReady: a non-candidate keeps its mark (-2: ground, ground_column)
+    const int v = (k < K && p < P) ? vpar[p] : -1;
+    rt[k] = v >= 0 ? lds_find(vpar, p) : (parReady ? v : -1);
   }
   __syncthreads();  // every find done before the parents become words
 #pragma unroll
@@ -827,14 +836,15 @@ __device__ __forceinline__ void seg_lds(const BatchBufs& bb, const DevCfg& c, in
   IP_STAMP(5);
   // flags per chunk: kept in the segmented cloud, outlier, valid root; the
   // waves' counts per chunk into wpre
-  unsigned mkeep = 0, mout = 0, mroot = 0;
+  unsigned mkeep = 0, mout = 0, mroot = 0, mgnd = 0;  // mgnd: kept for being ground (the segmented cloud's ground flag)
 #pragma unroll
   for (int k0 = 0; k0 < kSegK; k0 += 8) {
     int8_t G[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int p = ((k0 + u) << 10) + tid;
-      G[u] = (k0 + u < K && p < P) ? bb.ground[base + p] : (int8_t)0;
+      if (parReady) G[u] = (k0 + u < K && rt[k0 + u] == -2) ? (int8_t)1 : (int8_t)0;  // no image read
+      else G[u] = (k0 + u < K && p < P) ? bb.ground[base + p] : (int8_t)0;
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -853,6 +863,7 @@ __device__ __forceinline__ void seg_lds(const BatchBufs& bb, const DevCfg& c, in
           outl = !valid && row > c.g && col % 5 == 0;                                // :328-334
         } else if (G[u] == 1) {
           keep = !(col % 5 != 0 && col > 5 && col < H - 5);                          // :337-340
+          mgnd |= (keep ? 1u : 0u) << k;
         }
       }
       mkeep |= (keep ? 1u : 0u) << k;
@@ -891,26 +902,44 @@ __device__ __forceinline__ void seg_lds(const BatchBufs& bb, const DevCfg& c, in
   __syncthreads();
   IP_STAMP(7);
   // outputs at their ordered positions (cloudSegmentation :318-357)
+  // kSegOutU chunks per round: their pixels' loads (full cloud, range) all in
+  // flight before the round's stores; the ground flag from the flags pass
   const unsigned long long lt = (1ull << lane) - 1;
-  for (int k = 0; k < K; ++k) {
-    const int p = (k << 10) + tid;
-    const bool keep = (mkeep >> k) & 1u, outl = (mout >> k) & 1u, vroot = (mroot >> k) & 1u;
-    const unsigned long long b0 = __ballot(keep), b1 = __ballot(outl), b2 = __ballot(vroot);
-    if (p >= P) continue;
-    const int row = p / H, col = p - row * H;
-    const int pos = cpre[k][0] + wpre[k][0][wave] + (int)__popcll(b0 & lt);  // kept pixels before p
-    if (col == 0) {  // ring boundaries (:323, :354)
-      bb.sri[b * c.N + row] = pos - 1 + 5;
-      if (row > 0) bb.eri[b * c.N + row - 1] = pos - 1 - 5;
+  for (int k0 = 0; k0 < K; k0 += kSegOutU) {
+    int pos[kSegOutU], opos[kSegOutU];
+    unsigned fl[kSegOutU];  // bit 0 keep, 1 outlier, 2 ground flag
+    float4 fv[kSegOutU];
+    float rv[kSegOutU];
+#pragma unroll
+    for (int u = 0; u < kSegOutU; ++u) {
+      const int k = k0 + u, p = (k << 10) + tid;
+      const bool in = k < K && p < P;
+      const bool keep = in && ((mkeep >> k) & 1u), outl = in && ((mout >> k) & 1u), vroot = in && ((mroot >> k) & 1u);
+      const unsigned long long b0 = __ballot(keep), b1 = __ballot(outl), b2 = __ballot(vroot);
+      pos[u] = k < K ? cpre[k][0] + wpre[k][0][wave] + (int)__popcll(b0 & lt) : 0;  // kept pixels before p
+      opos[u] = outl ? cpre[k][1] + wpre[k][1][wave] + (int)__popcll(b1 & lt) : 0;
+      if (vroot) par[p] = -(cpre[k][2] + wpre[k][2][wave] + (int)__popcll(b2 & lt) + 1);  // its label, negated
+      fl[u] = (keep ? 1u : 0u) | (outl ? 2u : 0u) | (in && ((mgnd >> k) & 1u) ? 4u : 0u);
+      fv[u] = keep || outl ? bb.full[base + p] : make_float4(0.f, 0.f, 0.f, 0.f);
+      rv[u] = keep ? bb.range[base + p] : 0.f;
     }
-    if (vroot) par[p] = -(cpre[k][2] + wpre[k][2][wave] + (int)__popcll(b2 & lt) + 1);  // its label, negated
-    if (keep) {
-      bb.seg[base + pos] = bb.full[base + p];
-      bb.gflag[base + pos] = (bb.ground[base + p] == 1) ? 1 : 0;
-      bb.col[base + pos] = (uint32_t)col;
-      bb.srange[base + pos] = bb.range[base + p];
+#pragma unroll
+    for (int u = 0; u < kSegOutU; ++u) {
+      const int k = k0 + u, p = (k << 10) + tid;
+      if (k >= K || p >= P) continue;
+      const int row = p / H, col = p - row * H;
+      if (col == 0) {  // ring boundaries (:323, :354)
+        bb.sri[b * c.N + row] = pos[u] - 1 + 5;
+        if (row > 0) bb.eri[b * c.N + row - 1] = pos[u] - 1 - 5;
+      }
+      if (fl[u] & 1u) {
+        bb.seg[base + pos[u]] = fv[u];
+        bb.gflag[base + pos[u]] = (fl[u] & 4u) ? 1 : 0;
+        bb.col[base + pos[u]] = (uint32_t)col;
+        bb.srange[base + pos[u]] = rv[u];
+      }
+      if (fl[u] & 2u) bb.outl[base + opos[u]] = fv[u];
     }
-    if (outl) bb.outl[base + cpre[k][1] + wpre[k][1][wave] + (int)__popcll(b1 & lt)] = bb.full[base + p];
   }
   if (want_labels) {  // the final labelMat: a valid segment's label, 999999 for the rest
     __syncthreads();
@@ -952,6 +981,7 @@ __global__ void __launch_bounds__(1024) k_seg_lds(BatchBufs bb, DevCfg c, int wa
 // launches fewer, and the later phases read what the earlier ones wrote from
 // the CU's caches.
 constexpr int kIpLdsU = 4;  // points per thread in flight (the projection)
+constexpr int kIpPixU = 4;  // pixels per thread in flight (the range image and full cloud)
 __global__ void __launch_bounds__(1024) k_ip_lds(BatchBufs bb, DevCfg c, int want_labels) {
   extern __shared__ int par[];  // [P]: the owner image, then the parents
   const int b = blockIdx.x, tid = threadIdx.x;
@@ -978,11 +1008,25 @@ __global__ void __launch_bounds__(1024) k_ip_lds(BatchBufs bb, DevCfg c, int wan
   // 4q .. 4q + 3 at the same columns gather the owners from the same 128-B
   // lines of the firing-ordered input (k_pixels' mapping), instead of a wave
   // per 64 row-major pixels touching 64 lines for one record each
+  // kIpPixU pairs per wave and round: their owners and gathers are all in
+  // flight before the first store (one memory latency per round)
   {
     const int N = c.N, nq = N * ((H + 63) >> 6);
-    for (int q = tid >> 6; q < nq; q += 16) {
-      const int row = q % N, col = (q / N) * 64 + (tid & 63);
-      if (col < H) pixel_out(bb, c, b, row, col, par[row * H + col]);
+    const PtsView pv = pts_view(bb, b);
+    for (int q0 = tid >> 6; q0 < nq; q0 += 16 * kIpPixU) {
+      int o[kIpPixU], row[kIpPixU], col[kIpPixU];
+      float4 xyz[kIpPixU];
+#pragma unroll
+      for (int u = 0; u < kIpPixU; ++u) {
+        const int q = q0 + 16 * u;
+        row[u] = q % N;
+        col[u] = q < nq ? (q / N) * 64 + (tid & 63) : H;
+        o[u] = col[u] < H ? par[row[u] * H + col[u]] : -1;
+        xyz[u] = o[u] >= 0 ? pv.xyz(o[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < kIpPixU; ++u)
+        if (col[u] < H) pixel_store(bb, c, b, row[u], col[u], o[u], xyz[u]);
     }
   }
   __syncthreads();  // the pixels' stores are visible to the workgroup: the ground walk reads them

@@ -594,3 +594,29 @@ def test_seg_lds_equals_hbm_union_find(L, seed, extra):
         assert_ip_equal(outs["lds4"][k], ref[k], images=False)
         assert_ip_equal(outs["hbm"][k], ref[k], images=False)
         assert_ip_equal(outs["node"][k], ref[k])
+
+
+def test_node_upload_capacity_and_chunks(L):
+    """The node call's staged upload (lego_ip_process): a cloud of exactly
+    max_points points, spanning several 32768-point chunks, projects like the
+    oracle; one point more is LEGO_E_CAPACITY before any upload; a cloud with
+    a non-finite point in its last chunk is refused and the context keeps
+    working."""
+    sc = L.synth_cfg("HDL-64E", 2)
+    pts, st = L.synth_scan(sc, 0)
+    n = len(pts)
+    assert n > 3 * 32768
+    cfg = L.sensor_cfg("HDL-64E", L.hip_lib())
+    gpu = L.Lego(cfg, max_points=n)
+    ora = L.Oracle(L.sensor_cfg("HDL-64E"))
+    assert_ip_equal(gpu.ip(pts, st, images=True), ora.ip(pts, st, images=True))
+    big = np.concatenate([pts, pts[:1]])
+    out = L.IpOut()
+    assert gpu.lib.lego_ip_process(gpu.h, big.ctypes.data, len(big), st, 0, L.C.byref(out)) == L.LEGO_E_CAPACITY
+    bad = pts.copy()
+    bad["y"][n - 3] = np.inf
+    assert gpu.lib.lego_ip_process(gpu.h, bad.ctypes.data, n, st, 0, L.C.byref(out)) == L.LEGO_E_NOT_DENSE
+    pts1, st1 = L.synth_scan(sc, 1)
+    if len(pts1) <= n:
+        assert_ip_equal(gpu.ip(pts1, st1, images=True), L.Oracle(L.sensor_cfg("HDL-64E")).ip(pts1, st1, images=True))
+    gpu.close()
