@@ -15,6 +15,7 @@ Prints ONE JSON line on rank 0 (contract in the task statement).
 from __future__ import annotations
 
 import argparse
+import contextlib
 import datetime
 import ctypes as C
 import importlib.util
@@ -584,6 +585,22 @@ def fleet_bench(L, streams: int, k: int, steps: int, device: int, check: bool = 
                                  "counts) x scans/s"}}
 
 
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """File descriptor 1 onto 2 for the block: gloo's connection messages
+    ("[Gloo] Rank r is connected to ...", printed to stdout by every rank)
+    stay out of the one JSON line rank 0 prints."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -634,7 +651,8 @@ def main():
         wd = ms.Watchdog(float(os.environ.get("LEGO_BENCH_WATCHDOG_S", "240")), rank)
         wd.mark(None, "init_process_group")
         torch.cuda.set_device(local)
-        dist.init_process_group(backend, timeout=pg_timeout)
+        with stdout_to_stderr():
+            dist.init_process_group(backend, timeout=pg_timeout)
     dev = torch.device("cuda", local)
 
     def mark(step, phase):
@@ -673,7 +691,8 @@ def main():
     comm_ranks = None
     if dist is not None:
         mark(None, "control group")
-        ctrl = dist.new_group(backend="gloo", timeout=pg_timeout) if backend != "gloo" else None
+        with stdout_to_stderr():
+            ctrl = dist.new_group(backend="gloo", timeout=pg_timeout) if backend != "gloo" else None
         want_native = backend == "nccl"
         create_error = None
         if want_native:
