@@ -199,3 +199,40 @@ def test_ringless_pc2_without_ring_field(L):
     gr = L.Lego(L.sensor_cfg("OS1-16", L.hip_lib()), max_points=maxpts(L, sc))
     assert gr.lib.lego_ip_process_pc2(gr.h, C.byref(m), 0, C.byref(out)) == L.LEGO_E_NOT_DENSE
     gr.close()
+
+
+@pytest.mark.parametrize("sensor,seed,ring", [("VLP-16", 7, False), ("OS1-16", 5, True), ("OS1-16", 8, False)])
+def test_fused_batch_presets(L, sensor, seed, ring):
+    """Batches of more than 8 VLP-16-class scans take k_ip_lds (the whole
+    projection and segmentation per scan in one workgroup), with the
+    ring-less branch's NaN removal and OS1-16's 1024 columns: 12 scans as one
+    device batch (non-finite points in every ring-less scan), every scan's
+    segmented cloud, cloud_info and features byte-equal and every pose
+    bit-exact against the oracle."""
+    K = 12
+    sc = L.synth_cfg(sensor, seed)
+    rng = np.random.default_rng(seed)
+    scans = []
+    for k in range(K):
+        p, s = L.synth_scan(sc, k)
+        if not ring:
+            p["x"][rng.choice(len(p), 40, replace=False)] = np.nan
+            p["ring"] = rng.integers(0, 1000, len(p))  # not read by this branch
+        scans.append((p, s))
+    gc, oc = cfgs(L, sensor, ring=ring)
+    ora = L.Oracle(oc)
+    want = []
+    for p, s in scans:
+        wi = ora.ip(p, s)
+        want.append((wi, ora.fa()))
+    pts = np.concatenate([p for p, _ in scans])
+    off = np.zeros(K + 1, np.int64)
+    off[1:] = np.cumsum([len(p) for p, _ in scans])
+    gb = L.Lego(gc, max_points=max(len(p) for p, _ in scans) + 16, max_batch=K)
+    recs = gb.odom_batch(pts, off, np.array([s for _, s in scans]))
+    for k in range(K):
+        gi, gf = gb.batch_fetch(k)
+        assert_ip_equal(gi, want[k][0], images=False)
+        assert_feat_equal(gf, want[k][1])
+        assert np.array_equal(u32(list(recs[k].transform_sum)), u32(want[k][1]["transform_sum"])), k
+    gb.close()
