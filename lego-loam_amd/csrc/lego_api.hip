@@ -1247,9 +1247,9 @@ static int fetch_fa(lego_ctx* x, int k, lego_fa_out* o, bool withXerr = false) {
 // each chunk's DMA to x->d_pts queued as soon as it is staged, so the copy
 // engine works beside the next chunk's pass.  It replaces a separate check
 // pass plus the runtime's staged copy of pageable memory: VLS-128's 7.4 MB
-// were read twice and all of them crossed PCIe.  A non-dense cloud (with use_cloud_ring) is refused here,
-// before any kernel: nothing but d_pts has changed.  Without useCloudRing
-// k_project drops such points (:170).
+// were read twice and all of them crossed PCIe.  A non-dense cloud (with
+// use_cloud_ring) is refused here, before any kernel: nothing but d_pts has
+// changed.  Without useCloudRing k_project drops such points (:170).
 static int upload_checked(lego_ctx* x, const lego_point_xyzir* pts, int32_t n) {
   HIPCHK(hipSetDevice(x->device));
   static_assert(sizeof(float4) * 2 == sizeof(lego_point_xyzir), "the packed form fits d_pts");
