@@ -200,8 +200,9 @@ constexpr int kGroundRows = 8;
 // Column j of scan b; par (k_ip_lds): the union-find's initial parents of
 // the column's pixels in LDS as well (p for an unlabelled pixel, -2 for a
 // ground one, else -1);
-// labels: also the label image's initial values (the HBM union-find reads
-// them; k_ip_lds needs them only when the label image is an output).
+// labels: also the ground image and the label image's initial values (the
+// HBM union-find and compaction read them; k_ip_lds needs them only when the
+// images are outputs: its segmentation takes the ground from the parents).
 __device__ __forceinline__ void ground_column(const BatchBufs& bb, const DevCfg& c, int b, int j, int* par,
                                               bool labels = true) {
   const size_t base = (size_t)b * c.P;
@@ -242,8 +243,10 @@ __device__ __forceinline__ void ground_column(const BatchBufs& bb, const DevCfg&
       cur = next;
       const size_t gp = base + i * c.H + j;
       const bool lab = G == 1 || rg[u] == FLT_MAX;
-      bb.ground[gp] = (int8_t)G;
-      if (labels) bb.label[gp] = lab ? -1 : 0;  // :295-301
+      if (labels) {  // the images (k_ip_lds reads neither unless they are outputs)
+        bb.ground[gp] = (int8_t)G;
+        bb.label[gp] = lab ? -1 : 0;  // :295-301
+      }
       // k_ip_lds's parents: -2 for a ground pixel (G == 1), -1 for another
       // labelled one, so the segmentation knows the ground without the image
       if (par) par[i * c.H + j] = lab ? (G == 1 ? -2 : -1) : i * c.H + j;
@@ -758,6 +761,22 @@ constexpr int kSegHbmMaxScans = 8;  // launches of up to this many scans segment
 bool seg_lds_ok(const DevCfg& c) { return c.N <= kSegLdsMaxN && c.P <= kSegLdsMaxP && !c.segHbm; }
 
 
+// p / H for a pixel index p < 2^15 (kSegLdsMaxP): the float product with
+// the reciprocal is within 2^-8 of the quotient, so one correction makes it
+// exact.  A few instructions where the integer division by the runtime width
+// is a ~25-instruction sequence (five per pixel in seg_lds).
+struct RowDiv {
+  int H;
+  float inv;
+  __device__ __forceinline__ int row(int p) const {
+    int r = (int)((float)p * inv);
+    const int m = r * H;
+    if (m > p) --r;
+    else if (m + H <= p) ++r;
+    return r;
+  }
+};
+
 // Scan b's segmentation and compaction by the calling 1024-thread workgroup,
 // par[P] its LDS parents; parReady: par already holds the initial parents
 // (k_ip_lds writes them with the ground image), else they come from bb.label.
@@ -768,6 +787,7 @@ __device__ __forceinline__ void seg_lds(const BatchBufs& bb, const DevCfg& c, in
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const size_t base = (size_t)b * c.P;
   const int P = c.P, H = c.H, K = (P + 1023) >> 10;
+  const RowDiv rdiv{H, 1.0f / (float)H};
   volatile int* vpar = par;
   const TanBand tb = seg_tan_band(c);
   IP_T0();
@@ -789,7 +809,7 @@ __device__ __forceinline__ void seg_lds(const BatchBufs& bb, const DevCfg& c, in
       const int p = ((k0 + u) << 10) + tid;
       rp[u] = rr_[u] = rd[u] = 0.f;
       if (k0 + u < K && p < P) {
-        const int row = p / H, col = p - row * H;
+        const int row = rdiv.row(p), col = p - row * H;
         rp[u] = bb.range[base + p];
         rr_[u] = bb.range[base + row * H + (col + 1 == H ? 0 : col + 1)];
         if (row + 1 < c.N) rd[u] = bb.range[base + p + H];
@@ -799,7 +819,7 @@ __device__ __forceinline__ void seg_lds(const BatchBufs& bb, const DevCfg& c, in
     for (int u = 0; u < 4; ++u) {
       const int p = ((k0 + u) << 10) + tid;
       if (k0 + u >= K || p >= P || vpar[p] < 0) continue;  // candidates keep a parent >= 0 throughout
-      const int row = p / H, col = p - row * H;
+      const int row = rdiv.row(p), col = p - row * H;
       const int qr = row * H + (col + 1 == H ? 0 : col + 1);  // column wrap :403-406
       if (vpar[qr] >= 0 && seg_edge_fast(rp[u], rr_[u], c.sinAX, c.cosAX, c.theta, tb)) lds_unite(par, p, qr);
       if (row + 1 < c.N) {
@@ -830,7 +850,7 @@ __device__ __forceinline__ void seg_lds(const BatchBufs& bb, const DevCfg& c, in
     const int p = (k << 10) + tid;
     if (rt[k] < 0) continue;
     atomicAdd(&par[rt[k]], 1);
-    if (rt[k] != p) atomicOr(&par[rt[k]], 1 << (15 + p / H));
+    if (rt[k] != p) atomicOr(&par[rt[k]], 1 << (15 + rdiv.row(p)));
   }
   __syncthreads();
   IP_STAMP(5);
@@ -852,7 +872,7 @@ __device__ __forceinline__ void seg_lds(const BatchBufs& bb, const DevCfg& c, in
       if (k >= K) break;
       bool keep = false, outl = false, vroot = false;
       if (p < P) {
-        const int row = p / H, col = p - row * H;
+        const int row = rdiv.row(p), col = p - row * H;
         if (rt[k] >= 0) {
           const int w = vpar[rt[k]];
           const int sz = w & 0x7fff;
@@ -927,7 +947,7 @@ __device__ __forceinline__ void seg_lds(const BatchBufs& bb, const DevCfg& c, in
     for (int u = 0; u < kSegOutU; ++u) {
       const int k = k0 + u, p = (k << 10) + tid;
       if (k >= K || p >= P) continue;
-      const int row = p / H, col = p - row * H;
+      const int row = rdiv.row(p), col = p - row * H;
       if (col == 0) {  // ring boundaries (:323, :354)
         bb.sri[b * c.N + row] = pos[u] - 1 + 5;
         if (row > 0) bb.eri[b * c.N + row - 1] = pos[u] - 1 - 5;
@@ -1013,14 +1033,16 @@ __global__ void __launch_bounds__(1024) k_ip_lds(BatchBufs bb, DevCfg c, int wan
   {
     const int N = c.N, nq = N * ((H + 63) >> 6);
     const PtsView pv = pts_view(bb, b);
+    const RowDiv ndiv{N, 1.0f / (float)N};
     for (int q0 = tid >> 6; q0 < nq; q0 += 16 * kIpPixU) {
       int o[kIpPixU], row[kIpPixU], col[kIpPixU];
       float4 xyz[kIpPixU];
 #pragma unroll
       for (int u = 0; u < kIpPixU; ++u) {
         const int q = q0 + 16 * u;
-        row[u] = q % N;
-        col[u] = q < nq ? (q / N) * 64 + (tid & 63) : H;
+        const int qb = ndiv.row(q);  // q / N
+        row[u] = q - qb * N;
+        col[u] = q < nq ? qb * 64 + (tid & 63) : H;
         o[u] = col[u] < H ? par[row[u] * H + col[u]] : -1;
         xyz[u] = o[u] >= 0 ? pv.xyz(o[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
