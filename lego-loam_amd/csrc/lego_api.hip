@@ -25,6 +25,7 @@
 #include "lego_kernels.h"
 #include "lego_mo.h"
 #include "lego_loam.h"
+#include "lego_pack_host.h"
 #include "lego_pgo_host.h"
 #include "lego_seg.h"
 #include "lego_wire.h"
@@ -170,6 +171,7 @@ struct lego_ctx {
   PackedRec* h_pack = nullptr;  // pinned
   int64_t* h_offp = nullptr;    // pinned [maxBatch + 1]: device offsets read back for validation
   float4* h_stage = nullptr;  // pinned [maxPoints] packed points, created by the first host-buffer node call
+  std::unique_ptr<lego::PackPool> pack;  // the upload pass's helper threads (clouds of more than two chunks)
   OdomState* h_resetSt = nullptr;   // pinned [S]: construction state (ctx_reset)
   FaCarry* h_resetCarry = nullptr;  // pinned [S]
   Fusion fusion;  // transformFusion state
@@ -1245,7 +1247,9 @@ static int fetch_fa(lego_ctx* x, int k, lego_fa_out* o, bool withXerr = false) {
 // buffer and accumulates the dense check (imageProjection.cpp:174; an all-ones
 // exponent is inf / nan, branch-free so the loop vectorises), chunk by chunk,
 // each chunk's DMA to x->d_pts queued as soon as it is staged, so the copy
-// engine works beside the next chunk's pass.  It replaces a separate check
+// engine works beside the next chunk's pass; clouds of more than two chunks
+// (dense sensors) are packed by three helper threads and the caller
+// (lego_pack_host.h).  It replaces a separate check
 // pass plus the runtime's staged copy of pageable memory: VLS-128's 7.4 MB
 // were read twice and all of them crossed PCIe.  A non-dense cloud (with
 // use_cloud_ring) is refused here, before any kernel: nothing but d_pts has
@@ -1259,21 +1263,25 @@ static int upload_checked(lego_ctx* x, const lego_point_xyzir* pts, int32_t n) {
     set_err("hipHostMalloc failed for the node call's staging buffer");
     return LEGO_E_DEVICE;
   }
-  constexpr int kChunk = 32768;  // points (512 KB packed)
   float4* d = (float4*)x->d_pts;
   uint32_t nonfinite = 0;
-  for (int c0 = 0; c0 < n; c0 += kChunk) {
-    const int c1 = std::min(n, c0 + kChunk);
-    for (int i = c0; i < c1; ++i) {
-      uint32_t u[3];
-      std::memcpy(u, &pts[i].x, sizeof(u));
-      nonfinite |= (uint32_t)((u[0] & 0x7f800000u) == 0x7f800000u) | (uint32_t)((u[1] & 0x7f800000u) == 0x7f800000u) |
-                   (uint32_t)((u[2] & 0x7f800000u) == 0x7f800000u);
-      const uint32_t w[4] = {u[0], u[1], u[2], (uint32_t)pts[i].ring};
-      std::memcpy(&x->h_stage[i], w, sizeof(w));
+  constexpr int kChunk = PackPool::kChunk;
+  if (n > 2 * kChunk) {  // a dense sensor's cloud: three helper threads beside the caller
+    if (!x->pack) x->pack.reset(new PackPool(3, x->maxPoints));
+    hipError_t err = hipSuccess;
+    nonfinite = x->pack->run(pts, (uint32_t*)x->h_stage, n, [&](int c0, int c1) {
+      if (err == hipSuccess)
+        err = hipMemcpyAsync(d + c0, x->h_stage + c0, sizeof(float4) * (size_t)(c1 - c0), hipMemcpyHostToDevice,
+                             x->stream);
+    });
+    HIPCHK(err);
+  } else {
+    for (int c0 = 0; c0 < n; c0 += kChunk) {
+      const int c1 = std::min(n, c0 + kChunk);
+      nonfinite |= pack_points(pts, (uint32_t*)x->h_stage, c0, c1);
+      HIPCHK(hipMemcpyAsync(d + c0, x->h_stage + c0, sizeof(float4) * (size_t)(c1 - c0), hipMemcpyHostToDevice,
+                            x->stream));
     }
-    HIPCHK(hipMemcpyAsync(d + c0, x->h_stage + c0, sizeof(float4) * (size_t)(c1 - c0), hipMemcpyHostToDevice,
-                          x->stream));
   }
   if (nonfinite && x->dc.ringRow) {
     HIPCHK(hipStreamSynchronize(x->stream));  // the staging buffer is free again when this returns

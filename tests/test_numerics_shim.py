@@ -118,3 +118,16 @@ def test_segmentation_alpha_constants(L):
     assert float(np.float32(sy)).hex() == "0x1.1de58c0000000p-5"
     assert float(np.float32(cy)).hex() == "0x1.ffb0280000000p-1"
     assert float(np.float32(cfg.segment_theta)).hex() == "0x1.0c15240000000p+0"  # 0x3f860a92
+
+
+def test_pack_pool_matches_one_thread(tmp_path):
+    """The node call's threaded upload pass (lego_pack_host.h): thousands of
+    back-to-back jobs of random sizes on one pool give the one-thread
+    packing's words and non-finite flag, with the DMA runs in order."""
+    exe = tmp_path / "pack_pool_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", "-I", str(REPO / "include"), "-I",
+                    str(REPO / "lego-loam_amd/csrc"), str(REPO / "tests/native/pack_pool_check.cpp"), "-o", str(exe)],
+                   check=True)
+    r = subprocess.run([str(exe), "3000"], capture_output=True, text=True, timeout=600)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout
